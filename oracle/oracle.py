@@ -1,0 +1,187 @@
+"""ctypes front-end of the CPU oracle (oracle/cc_oracle.c).
+
+TEST INFRASTRUCTURE ONLY.  The oracle is the checker and the CPU baseline; only
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import it.
+The product (cluster_tools_amd) never imports anything from oracle/.
+
+Build: `make -C oracle` (also done by __graft_entry__.build()).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, 'libcc_oracle.so')
+_lib = None
+
+MODES = {'greater': 0, 'less': 1, 'equal': 2}
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            raise RuntimeError('oracle library missing: run `make -C oracle`')
+        L = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.c_void_p
+        i64 = ctypes.c_int64
+        L.oracle_boundary_map.argtypes = [P, P, i64, i64, i64, i64, i64, i64, ctypes.c_uint64, ctypes.c_int]
+        L.oracle_boundary_map.restype = None
+        L.oracle_label_volume.argtypes = [P, P, P, P, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                          P, P, P, P, P, P, i64, P, ctypes.c_int, P]
+        L.oracle_label_volume.restype = ctypes.c_int
+        L.oracle_n_blocks.argtypes = [P, P]
+        L.oracle_n_blocks.restype = i64
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def boundary_map(shape, origin=(0, 0, 0), seed=0x5EED, n_threads=8, as_q=False):
+    """Synthetic boundary map (oracle/synth.py definition), float32 or uint8 q."""
+    shape = tuple(int(s) for s in shape)
+    out = np.empty(shape, dtype=np.uint8 if as_q else np.float32)
+    args = (None, out) if as_q else (out, None)
+    lib().oracle_boundary_map(_ptr(args[0]), _ptr(args[1]), *shape, *[int(o) for o in origin],
+                              ctypes.c_uint64(seed), int(n_threads))
+    return out
+
+
+def n_blocks(shape, block_shape):
+    s = np.ascontiguousarray(shape, dtype=np.int64)
+    b = np.ascontiguousarray(block_shape, dtype=np.int64)
+    return int(lib().oracle_n_blocks(_ptr(s), _ptr(b)))
+
+
+def label_volume(inp, block_shape, threshold, mode='greater', mask=None, n_threads=1,
+                 quirk_n_jobs=0, want_local=False, want_lut=True):
+    """Run the restated reference path.  Returns a dict of artefacts:
+    labels (final uint64), values (n_i+1 or 0), offsets, n_labels, lut, max_id,
+    empty_blocks, stage_seconds, and local (block-local labels) if want_local."""
+    inp = np.ascontiguousarray(inp, dtype=np.float32)
+    assert inp.ndim == 3
+    if mask is not None:
+        mask = np.ascontiguousarray(mask, dtype=np.uint8)
+        assert mask.shape == inp.shape
+    shape = np.array(inp.shape, dtype=np.int64)
+    bs = np.array(block_shape, dtype=np.int64)
+    nb = n_blocks(shape, bs)
+    labels = np.empty(inp.shape, dtype=np.uint64)
+    local = np.empty(inp.shape, dtype=np.uint64) if want_local else None
+    values = np.empty(nb, dtype=np.uint64)
+    offsets = np.empty(nb, dtype=np.uint64)
+    n_labels = np.zeros(1, dtype=np.uint64)
+    max_id = np.zeros(1, dtype=np.uint64)
+    stage_s = np.zeros(5, dtype=np.float64)
+    # n_labels <= n_blocks + voxels/1 ; size the LUT after a first cheap bound
+    lut_cap = int(inp.size + nb + 1) if want_lut else 0
+    lut = np.empty(lut_cap, dtype=np.uint64) if want_lut else None
+    rc = lib().oracle_label_volume(_ptr(inp), _ptr(mask), _ptr(shape), _ptr(bs), float(threshold),
+                                   MODES[mode], int(n_threads), _ptr(labels), _ptr(local),
+                                   _ptr(values), _ptr(offsets), _ptr(n_labels), _ptr(lut),
+                                   lut_cap, _ptr(max_id), int(quirk_n_jobs), _ptr(stage_s))
+    if rc != 0:
+        raise RuntimeError('oracle_label_volume failed: %d' % rc)
+    nl = int(n_labels[0])
+    out = dict(labels=labels, values=values, offsets=offsets, n_labels=nl,
+               lut=None if lut is None else lut[:nl].copy(), max_id=int(max_id[0]),
+               empty_blocks=np.nonzero(values == 0)[0], stage_seconds=stage_s)
+    if want_local:
+        out['local'] = local
+    return out
+
+
+def canon(labels):
+    """First-occurrence (C order) consecutive relabel; 0 stays 0 (parity contract)."""
+    flat = np.asarray(labels).ravel()
+    out = np.zeros(flat.shape, dtype=np.uint32)
+    nz = flat != 0
+    if nz.any():
+        vals = flat[nz]
+        uniq, first, inv = np.unique(vals, return_index=True, return_inverse=True)
+        order = np.argsort(first, kind='stable')
+        rank = np.empty(len(uniq), dtype=np.uint32)
+        rank[order] = np.arange(1, len(uniq) + 1, dtype=np.uint32)
+        out[nz] = rank[inv.ravel()]
+    return out.reshape(np.shape(labels))
+
+
+def face_pairs(local, block_shape, offsets, empty):
+    """Deduplicated (K,2) face pairs of block_faces.py:87-137 from block-local labels."""
+    shape = local.shape
+    nbz, nby, nbx = [-(-s // b) for s, b in zip(shape, block_shape)]
+    empty = set(int(e) for e in empty)
+    out = []
+    for b in range(nbz * nby * nbx):
+        if b in empty:
+            continue
+        c = np.unravel_index(b, (nbz, nby, nbx))
+        beg = [ci * bs for ci, bs in zip(c, block_shape)]
+        end = [min(bg + bs, s) for bg, bs, s in zip(beg, block_shape, shape)]
+        for axis in range(3):
+            cn = list(c)
+            cn[axis] += 1
+            if cn[axis] >= (nbz, nby, nbx)[axis]:
+                continue
+            nb = int(np.ravel_multi_index(cn, (nbz, nby, nbx)))
+            if nb in empty:
+                continue
+            sa = tuple(slice(bg, e) if d != axis else slice(e - 1, e)
+                       for d, (bg, e) in enumerate(zip(beg, end)))
+            sb = tuple(slice(bg, e) if d != axis else slice(e, e + 1)
+                       for d, (bg, e) in enumerate(zip(beg, end)))
+            la, lb = local[sa].ravel(), local[sb].ravel()
+            keep = (la != 0) & (lb != 0)
+            if keep.any():
+                out.append(np.stack([la[keep] + offsets[b], lb[keep] + offsets[nb]], axis=1))
+    if not out:
+        return np.zeros((0, 2), dtype=np.uint64)
+    return np.unique(np.concatenate(out, axis=0).astype(np.uint64), axis=0)
+
+
+def graph_components(inp_fg, block_shape):
+    """Independent restatement of the partition, via scipy:
+    26-connectivity inside blocks, 6-connectivity across block faces.  Returns
+    canonical labels.  Small inputs only."""
+    from scipy.sparse import coo_matrix
+    from scipy.sparse.csgraph import connected_components
+    fg = np.asarray(inp_fg, dtype=bool)
+    shape = fg.shape
+    idx = np.arange(fg.size).reshape(shape)
+    blk = [np.arange(s) // b for s, b in zip(shape, block_shape)]
+    rows, cols = [], []
+    for dz in (-1, 0, 1):
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                if (dz, dy, dx) <= (0, 0, 0):
+                    continue
+                d = (dz, dy, dx)
+                sl_a = tuple(slice(max(0, -o), s - max(0, o)) for o, s in zip(d, shape))
+                sl_b = tuple(slice(a.start + o, a.stop + o) for a, o in zip(sl_a, d))
+                ok = fg[sl_a] & fg[sl_b]
+                n_axes = sum(1 for o in d if o != 0)
+                same = np.ones(ok.shape, dtype=bool)
+                for ax, o in enumerate(d):
+                    if o == 0:
+                        continue
+                    ba = blk[ax][sl_a[ax]]
+                    bb = blk[ax][sl_b[ax]]
+                    shp = [1, 1, 1]
+                    shp[ax] = -1
+                    same &= (ba == bb).reshape(shp)
+                allowed = same if n_axes > 1 else np.ones_like(same)
+                ok &= allowed
+                rows.append(idx[sl_a][ok])
+                cols.append(idx[sl_b][ok])
+    r = np.concatenate(rows)
+    c = np.concatenate(cols)
+    n = fg.size
+    g = coo_matrix((np.ones(len(r), dtype=np.int8), (r, c)), shape=(n, n))
+    _, lab = connected_components(g, directed=False)
+    lab = (lab + 1).reshape(shape).astype(np.uint64)
+    lab[~fg] = 0
+    return canon(lab)
