@@ -1,0 +1,254 @@
+"""ctypes binding of libcc_mi355x.so (the C ABI in include/cc_mi355x.h).
+
+This is the only way the product reaches the GPU.  There is no CPU fallback: if the
+library is missing or no GPU is visible, every compute call raises.
+
+Arrays: host numpy arrays go through the *_host entry points; device buffers are
+torch CUDA tensors (ROCm) passed by data_ptr().
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'lib', 'libcc_mi355x.so')
+MODES = {'greater': 0, 'less': 1, 'equal': 2}
+
+# every symbol include/cc_mi355x.h declares (checked by tests/test_boundary.py)
+EXPORTS = (
+    'cc_create', 'cc_destroy', 'cc_last_error', 'cc_set_stream', 'cc_version',
+    'cc_label_volume', 'cc_label_volume_host', 'cc_get_block_values', 'cc_get_offsets',
+    'cc_get_lut', 'cc_block_components', 'cc_merge_offsets', 'cc_block_faces',
+    'cc_merge_assignments', 'cc_write', 'cc_generate_boundary_map', 'cc_set_profiling',
+    'cc_get_profile', 'cc_reset_profile',
+)
+
+
+class CCResult(ctypes.Structure):
+    _fields_ = [('n_blocks', ctypes.c_int64), ('n_labels', ctypes.c_uint64),
+                ('max_id', ctypes.c_uint64), ('n_components', ctypes.c_uint64),
+                ('n_block_components', ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def load():
+    """Load the shared library and declare signatures (no GPU needed)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError('libcc_mi355x.so not built (%s): run __graft_entry__.build()' % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    P, i64, u64, I = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int
+    sig = {
+        'cc_create': (I, [I, ctypes.POINTER(P)]),
+        'cc_destroy': (None, [P]),
+        'cc_last_error': (ctypes.c_char_p, []),
+        'cc_set_stream': (I, [P, P]),
+        'cc_version': (ctypes.c_char_p, []),
+        'cc_label_volume': (I, [P, P, P, P, P, ctypes.c_double, I, P, ctypes.POINTER(CCResult)]),
+        'cc_label_volume_host': (I, [P, P, P, P, P, ctypes.c_double, I, P, ctypes.POINTER(CCResult)]),
+        'cc_get_block_values': (i64, [P, P, i64]),
+        'cc_get_offsets': (i64, [P, P, i64]),
+        'cc_get_lut': (i64, [P, P, i64]),
+        'cc_block_components': (I, [P, P, P, P, P, ctypes.c_double, I, P, P, i64]),
+        'cc_merge_offsets': (I, [P, i64, P, P, P]),
+        'cc_block_faces': (i64, [P, P, P, P, P, P, i64]),
+        'cc_merge_assignments': (I, [P, P, i64, u64, P]),
+        'cc_write': (I, [P, P, P, P, P, P, u64]),
+        'cc_generate_boundary_map': (I, [P, P, P, P, u64]),
+        'cc_set_profiling': (I, [P, I]),
+        'cc_get_profile': (I, [P, ctypes.c_char_p, I, P, P, I]),
+        'cc_reset_profile': (I, [P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc < 0:
+        raise RuntimeError('libcc_mi355x: ' + load().cc_last_error().decode())
+    return rc
+
+
+def _i64(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.int64))
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if hasattr(a, 'data_ptr'):
+        return a.data_ptr()
+    return a.ctypes.data
+
+
+def mode_id(mode):
+    if isinstance(mode, int):
+        return mode
+    if mode not in MODES:
+        raise ValueError('threshold_mode must be one of %s' % (tuple(MODES),))
+    return MODES[mode]
+
+
+class Context:
+    """One cc_ctx (one GPU).  Not thread-safe."""
+
+    def __init__(self, device=0):
+        L = load()
+        h = ctypes.c_void_p()
+        _check(L.cc_create(int(device), ctypes.byref(h)))
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if self._h:
+            load().cc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_stream(self, stream_ptr):
+        _check(load().cc_set_stream(self._h, ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+
+    # ---- fused path ----
+    def label_volume(self, inp, block_shape, threshold, mode='greater', mask=None, out=None):
+        """Fused five-stage path.  `inp` is a float32 torch CUDA tensor (device path) or a
+        numpy array (host path).  Returns (labels, result dict)."""
+        L = load()
+        shape = _i64(inp.shape)
+        bs = _i64(block_shape)
+        assert len(shape) == 3 and len(bs) == 3
+        res = CCResult()
+        if hasattr(inp, 'data_ptr'):
+            import torch
+            assert inp.is_cuda and inp.dtype == torch.float32 and inp.is_contiguous()
+            if mask is not None:
+                assert mask.is_cuda and mask.dtype == torch.uint8 and mask.shape == inp.shape
+                mask = mask.contiguous()
+            if out is None:
+                out = torch.empty(tuple(inp.shape), dtype=torch.int64, device=inp.device)
+            _check(L.cc_label_volume(self._h, _ptr(inp), _ptr(mask), _ptr(shape), _ptr(bs),
+                                     float(threshold), mode_id(mode), _ptr(out), ctypes.byref(res)))
+        else:
+            inp = np.ascontiguousarray(inp, dtype=np.float32)
+            if mask is not None:
+                mask = np.ascontiguousarray(mask)
+                if mask.dtype != np.uint8:
+                    mask = (mask != 0).astype(np.uint8)
+                assert mask.shape == inp.shape
+            if out is None:
+                out = np.empty(inp.shape, dtype=np.uint64)
+            _check(L.cc_label_volume_host(self._h, _ptr(inp), _ptr(mask), _ptr(shape), _ptr(bs),
+                                          float(threshold), mode_id(mode), _ptr(out), ctypes.byref(res)))
+        return out, res.as_dict()
+
+    def block_values(self, n_blocks):
+        a = np.empty(n_blocks, dtype=np.uint64)
+        _check(load().cc_get_block_values(self._h, _ptr(a), n_blocks))
+        return a
+
+    def offsets(self, n_blocks):
+        a = np.empty(n_blocks, dtype=np.uint64)
+        _check(load().cc_get_offsets(self._h, _ptr(a), n_blocks))
+        return a
+
+    def lut(self, n_labels):
+        a = np.empty(n_labels, dtype=np.uint64)
+        _check(load().cc_get_lut(self._h, _ptr(a), n_labels))
+        return a
+
+    # ---- stage-level ----
+    def block_components(self, inp_dev, block_shape, threshold, mode='greater', mask_dev=None, out_dev=None):
+        import torch
+        shape = _i64(inp_dev.shape)
+        bs = _i64(block_shape)
+        nb = int(np.prod([-(-s // b) for s, b in zip(shape, bs)]))
+        values = np.empty(nb, dtype=np.uint64)
+        if out_dev is None:
+            out_dev = torch.empty(tuple(inp_dev.shape), dtype=torch.int64, device=inp_dev.device)
+        _check(load().cc_block_components(self._h, _ptr(inp_dev), _ptr(mask_dev), _ptr(shape), _ptr(bs),
+                                          float(threshold), mode_id(mode), _ptr(out_dev), _ptr(values), nb))
+        return out_dev, values
+
+    def block_faces(self, labels_dev, block_shape, offsets):
+        shape = _i64(labels_dev.shape)
+        bs = _i64(block_shape)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = _check(load().cc_block_faces(self._h, _ptr(labels_dev), _ptr(shape), _ptr(bs), _ptr(offsets),
+                                         None, 0))
+        pairs = np.empty((n, 2), dtype=np.uint64)
+        if n:
+            _check(load().cc_block_faces(self._h, _ptr(labels_dev), _ptr(shape), _ptr(bs), _ptr(offsets),
+                                         _ptr(pairs), n))
+        return pairs
+
+    def merge_assignments(self, pairs, n_labels):
+        pairs = np.ascontiguousarray(pairs, dtype=np.uint64).reshape(-1, 2)
+        lut = np.empty(int(n_labels), dtype=np.uint64)
+        _check(load().cc_merge_assignments(self._h, _ptr(pairs), len(pairs), int(n_labels), _ptr(lut)))
+        return lut
+
+    def write(self, labels_dev, block_shape, offsets, lut):
+        shape = _i64(labels_dev.shape)
+        bs = _i64(block_shape)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lut = np.ascontiguousarray(lut, dtype=np.uint64)
+        _check(load().cc_write(self._h, _ptr(labels_dev), _ptr(shape), _ptr(bs), _ptr(offsets), _ptr(lut),
+                               len(lut)))
+        return labels_dev
+
+    def generate_boundary_map(self, shape, origin=(0, 0, 0), seed=0x5EED, out_dev=None, device=None):
+        import torch
+        if out_dev is None:
+            out_dev = torch.empty(tuple(int(s) for s in shape), dtype=torch.float32,
+                                  device=device if device is not None else 'cuda:%d' % self.device)
+        shape_a, origin_a = _i64(shape), _i64(origin)   # keep alive across the call
+        _check(load().cc_generate_boundary_map(self._h, _ptr(out_dev), _ptr(shape_a), _ptr(origin_a), int(seed)))
+        return out_dev
+
+    # ---- profiling ----
+    def set_profiling(self, on=True):
+        _check(load().cc_set_profiling(self._h, 1 if on else 0))
+
+    def reset_profile(self):
+        _check(load().cc_reset_profile(self._h))
+
+    def profile(self):
+        cap = 64
+        names = ctypes.create_string_buffer(8192)
+        counts = np.zeros(cap, dtype=np.int64)
+        ms = np.zeros(cap, dtype=np.float64)
+        n = _check(load().cc_get_profile(self._h, names, 8192, _ptr(counts), _ptr(ms), cap))
+        keys = names.value.decode().split(',') if n else []
+        return {k: {'count': int(counts[i]), 'total_ms': float(ms[i])} for i, k in enumerate(keys)}
+
+
+def merge_offsets(values):
+    """merge_offsets.py:104-120 through the C ABI (host arithmetic)."""
+    values = np.ascontiguousarray(values, dtype=np.uint64)
+    offsets = np.empty_like(values)
+    empty = np.empty(len(values), dtype=np.uint8)
+    n_labels = np.zeros(1, dtype=np.uint64)
+    _check(load().cc_merge_offsets(_ptr(values), len(values), _ptr(offsets), _ptr(empty), _ptr(n_labels)))
+    return offsets, np.nonzero(empty)[0], int(n_labels[0])

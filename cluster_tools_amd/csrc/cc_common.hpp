@@ -1,0 +1,182 @@
+// cc_common.hpp -- shared device helpers for the MI355X thresholded-CCL library.
+//
+// Layout vocabulary:
+//   block  = reference block of the block grid (nifty.tools.blocking, C-order ids,
+//            cluster_tools/utils/volume_utils.py:31-77); normalisation and 26-connectivity
+//            are per block, block faces stitch with 6-connectivity.
+//   tile   = the unit one workgroup labels in LDS: TZ x TY x TX voxels, tiled from each
+//            block's origin (so no tile straddles a block), truncated at block ends.
+//   cube   = 2x2x2 voxels inside a tile (tile origin aligned); every foreground voxel of a
+//            cube is 26-adjacent to every other, so a cube is one union-find node in LDS.
+//   node   = a tile-local component; global id t*cap + k (k = its compact index in tile t).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cc {
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+typedef uint8_t u8;
+
+// Tile geometry.  TX = 64 so one tile row is one 64-bit ballot.
+constexpr int TZ = 16, TY = 32, TX = 64;
+constexpr int CZ = TZ / 2, CY = TY / 2, CX = TX / 2;
+constexpr int NC = CZ * CY * CX;           // cubes per full tile (4096)
+constexpr int NROWS = TZ * TY;             // bit rows per tile (512)
+constexpr int NTHREADS = 256;              // 4 waves of 64
+// face planes of a tile, in cubes; entry = k | (4 face-voxel bits << 16), 0 = no face voxel
+constexpr int F_Z = CY * CX, F_Y = CZ * CX, F_X = CZ * CY;
+constexpr int F_ZLO = 0, F_ZHI = F_Z, F_YLO = 2 * F_Z, F_YHI = 2 * F_Z + F_Y;
+constexpr int F_XLO = 2 * F_Z + 2 * F_Y, F_XHI = 2 * F_Z + 2 * F_Y + F_X;
+constexpr int FACE_STRIDE = 2 * (F_Z + F_Y + F_X);
+constexpr u32 NONE = 0xFFFFFFFFu;
+constexpr int KEY_BITS = 36;               // packed sort key: block << 36 | first-voxel index
+
+enum { MODE_GREATER = 0, MODE_LESS = 1, MODE_EQUAL = 2 };
+enum { BP_EMPTY = 0, BP_INTERVAL = 1, BP_EXACT = 2 };
+
+struct BlockParam {      // per reference block, from its min/max (volume_utils.py:98-105)
+    float mn, m;         // min and max(x - min) (NaN where numpy's would be NaN)
+    u32 lo, hi;          // foreground <=> lo <= ord(x) <= hi   (kind == BP_INTERVAL)
+    u32 kind;
+    u32 pad;
+};
+
+struct Geom {
+    int64_t Z, Y, X;          // volume (or z-slab) shape
+    int64_t zoff;             // global z of this volume's first plane (keys / multi-GPU)
+    int64_t gY, gX;           // global Y, X (== Y, X)
+    int32_t nb[3];            // blocks per axis
+    int32_t nt[3];            // tiles per axis
+    int64_t n_tiles;
+    int64_t n_blocks;
+    int32_t cap;              // node slots per tile (max cubes of any tile)
+    int32_t pad;
+    const int32_t* tstart[3]; // per-axis tile tables
+    const int32_t* tlen[3];
+    const int32_t* tblk[3];
+};
+
+struct TileInfo {
+    int iz, iy, ix;
+    int z0, y0, x0;
+    int lz, ly, lx;
+    int64_t block;
+};
+
+__device__ __forceinline__ TileInfo tile_info(const Geom& g, int64_t t) {
+    TileInfo ti;
+    ti.ix = (int)(t % g.nt[2]);
+    ti.iy = (int)((t / g.nt[2]) % g.nt[1]);
+    ti.iz = (int)(t / ((int64_t)g.nt[2] * g.nt[1]));
+    ti.z0 = g.tstart[0][ti.iz]; ti.lz = g.tlen[0][ti.iz];
+    ti.y0 = g.tstart[1][ti.iy]; ti.ly = g.tlen[1][ti.iy];
+    ti.x0 = g.tstart[2][ti.ix]; ti.lx = g.tlen[2][ti.ix];
+    ti.block = ((int64_t)g.tblk[0][ti.iz] * g.nb[1] + g.tblk[1][ti.iy]) * g.nb[2] + g.tblk[2][ti.ix];
+    return ti;
+}
+
+// IEEE-754 total order for non-NaN floats as unsigned ints (-0 < +0).
+__device__ __host__ __forceinline__ u32 f2ord(u32 u) { return (u & 0x80000000u) ? ~u : (u | 0x80000000u); }
+__device__ __host__ __forceinline__ u32 ord2f(u32 o) { return (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o; }
+
+// The reference's per-voxel predicate with block statistics (block_components.py:161,166-173).
+__device__ __forceinline__ bool exact_pred(float x, float mn, float m, float thr, int mode) {
+    float y = x - mn;
+    if (m > 0.0f) y = y / m;
+    return mode == MODE_GREATER ? (y > thr) : mode == MODE_LESS ? (y < thr) : (y == thr);
+}
+
+__device__ __forceinline__ bool voxel_pred(const BlockParam& p, float x, float thr, int mode) {
+    if (p.kind == BP_INTERVAL) {
+        u32 o = f2ord(__float_as_uint(x));
+        return o >= p.lo && o <= p.hi;
+    }
+    if (p.kind == BP_EXACT) return exact_pred(x, p.mn, p.m, thr, mode);
+    return false;
+}
+
+// ---- LDS union-find over cubes (root = smallest cube index of the component) ----
+__device__ __forceinline__ u32 lfind(volatile u32* par, u32 x) {
+    u32 p = par[x];
+    while (p != x) { x = p; p = par[x]; }
+    return x;
+}
+
+__device__ __forceinline__ void lunion(u32* par, u32 a, u32 b) {
+    volatile u32* vp = par;
+    bool done;
+    do {
+        a = lfind(vp, a);
+        b = lfind(vp, b);
+        if (a < b) {
+            u32 old = atomicMin(&par[b], a);
+            done = (old == b);
+            b = old;
+        } else if (b < a) {
+            u32 old = atomicMin(&par[a], b);
+            done = (old == a);
+            a = old;
+        } else {
+            done = true;
+        }
+    } while (!done);
+}
+
+// ---- global union-find over nodes, agent-coherent accesses ----
+__device__ __forceinline__ u32 gload(u32* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void gstore(u32* p, u32 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+__device__ __forceinline__ u32 gfind(u32* P, u32 x) {
+    while (true) {
+        u32 p = gload(P + x);
+        if (p == x) return x;
+        u32 gp = gload(P + p);
+        if (gp == p) return p;
+        gstore(P + x, gp);        // path halving: only ever points x at an ancestor
+        x = gp;
+    }
+}
+
+// Link the root with the larger key under the root with the smaller key.  Keys are
+// unique per root, so the final root of a set is its minimum-key node.
+__device__ __forceinline__ void gunion(u32* P, const u64* K, u32 a, u32 b) {
+    while (true) {
+        a = gfind(P, a);
+        b = gfind(P, b);
+        if (a == b) return;
+        if (K[a] < K[b]) { u32 t = a; a = b; b = t; }
+        u32 old = atomicCAS(P + a, a, b);
+        if (old == a) return;
+    }
+}
+
+// grid-stride loop for 1-D element kernels (grids are capped: a launch may not exceed 2^32 threads)
+#define CC_FOR(i, n) \
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)(n); i += (int64_t)gridDim.x * blockDim.x)
+
+// ---- block-wide exclusive scan (256 threads) ----
+__device__ __forceinline__ u32 block_excl_scan(u32 v, u32* scratch, u32* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u32 x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        u32 y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) scratch[wave] = x;
+    __syncthreads();
+    u32 base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NTHREADS / 64; ++w) {
+        u32 s = scratch[w];
+        if (w < wave) base += s;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+}  // namespace cc

@@ -1,0 +1,534 @@
+// cc_lib.hip -- host orchestration and the C ABI (include/cc_mi355x.h).
+// One translation unit: kernels (cc_kernels.hip, cc_stage_kernels.hip, cc_generate.hip) + hipcub.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/cc_mi355x.h"
+#include "cc_kernels.hip"
+#include "cc_stage_kernels.hip"
+#include "cc_generate.hip"
+
+using namespace cc;
+
+static thread_local std::string g_err;
+
+struct CCError {
+    std::string msg;
+};
+
+#define HIP_OK(expr)                                                                           \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            throw CCError{std::string(#expr) + ": " + hipGetErrorString(e_)};                  \
+    } while (0)
+
+#define CC_REQUIRE(cond, msg)                                                                  \
+    do {                                                                                       \
+        if (!(cond)) throw CCError{msg};                                                       \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    template <class T>
+    T* as() const { return (T*)p; }
+    void ensure(size_t need) {
+        if (need <= bytes && p) return;
+        if (p) HIP_OK(hipFree(p));
+        p = nullptr;
+        size_t nb = std::max<size_t>(need + need / 8, 256);
+        HIP_OK(hipMalloc(&p, nb));
+        bytes = nb;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+struct ProfEntry {
+    int64_t count = 0;
+    double ms = 0;
+};
+
+struct cc_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    // workspace
+    DevBuf tiles, bstat, bparam, bits, faces, count, P, KR, FIN, keys, keys2, vals, vals2, seg,
+        values, offsets, lut, cub_tmp, scalars, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2;
+    // last run
+    int64_t n_blocks = 0;
+    uint64_t n_labels = 0;
+    std::vector<uint64_t> h_values, h_offsets;
+    std::vector<int32_t> h_tab;
+    bool lut_valid = false;
+    // profiling
+    bool prof = false;
+    std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    std::vector<hipEvent_t> event_pool;
+    std::map<std::string, ProfEntry> prof_acc;
+};
+
+// ------------------------------------------------------------------------------------------
+// helpers
+// ------------------------------------------------------------------------------------------
+static hipEvent_t pool_event(cc_ctx* c) {
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    HIP_OK(hipEventCreate(&e));
+    return e;
+}
+
+template <class F>
+static void launch(cc_ctx* c, const char* name, F&& f) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (c->prof) {
+        a = pool_event(c);
+        b = pool_event(c);
+        HIP_OK(hipEventRecord(a, c->stream));
+    }
+    f();
+    HIP_OK(hipGetLastError());
+    if (c->prof) {
+        HIP_OK(hipEventRecord(b, c->stream));
+        c->pending.push_back({name, {a, b}});
+    }
+}
+
+static void resolve_profile(cc_ctx* c) {
+    for (auto& pe : c->pending) {
+        float ms = 0;
+        HIP_OK(hipEventElapsedTime(&ms, pe.second.first, pe.second.second));
+        auto& acc = c->prof_acc[pe.first];
+        acc.count += 1;
+        acc.ms += ms;
+        c->event_pool.push_back(pe.second.first);
+        c->event_pool.push_back(pe.second.second);
+    }
+    c->pending.clear();
+}
+
+static void sync(cc_ctx* c) {
+    HIP_OK(hipStreamSynchronize(c->stream));
+    if (c->prof) resolve_profile(c);
+}
+
+// 1-D grid; element kernels index one element per thread, so n must stay below 2^32 threads
+// (volume-sized kernels use CC_FOR with the grid capped by grid_stride()).
+static inline unsigned grid1d(int64_t n, int bs = 256) {
+    CC_REQUIRE(n < (1LL << 32) - bs, "1-D launch larger than 2^32 threads");
+    return (unsigned)std::max<int64_t>(1, (n + bs - 1) / bs);
+}
+static inline unsigned grid_stride(int64_t n, int bs = 256) { return (unsigned)std::min<int64_t>(1 << 20, std::max<int64_t>(1, (n + bs - 1) / bs)); }
+
+// Block grid + tile tables (tiles tiled from each block's origin).
+struct HostGeom {
+    Geom g;
+    std::vector<int32_t> tab;  // [3][3][nt] packed
+    int64_t nvox;
+};
+
+static HostGeom make_geom(const int64_t shape[3], const int64_t block_shape[3], int64_t zoff) {
+    HostGeom hg;
+    Geom& g = hg.g;
+    std::memset(&g, 0, sizeof(g));
+    const int T[3] = {TZ, TY, TX};
+    std::vector<int32_t> st[3], ln[3], bk[3];
+    int maxlen[3] = {0, 0, 0};
+    for (int a = 0; a < 3; ++a) {
+        CC_REQUIRE(shape[a] >= 1 && shape[a] < (1LL << 31), "shape must be in [1, 2^31)");
+        CC_REQUIRE(block_shape[a] >= 1, "block_shape must be >= 1");
+        const int64_t nb = (shape[a] + block_shape[a] - 1) / block_shape[a];
+        g.nb[a] = (int32_t)nb;
+        for (int64_t b = 0; b < nb; ++b) {
+            const int64_t b0 = b * block_shape[a], b1 = std::min(b0 + block_shape[a], shape[a]);
+            for (int64_t s = b0; s < b1; s += T[a]) {
+                const int l = (int)std::min<int64_t>(T[a], b1 - s);
+                st[a].push_back((int32_t)s);
+                ln[a].push_back(l);
+                bk[a].push_back((int32_t)b);
+                maxlen[a] = std::max(maxlen[a], l);
+            }
+        }
+        g.nt[a] = (int32_t)st[a].size();
+    }
+    g.Z = shape[0]; g.Y = shape[1]; g.X = shape[2];
+    g.gY = shape[1]; g.gX = shape[2];
+    g.zoff = zoff;
+    g.n_tiles = (int64_t)g.nt[0] * g.nt[1] * g.nt[2];
+    g.n_blocks = (int64_t)g.nb[0] * g.nb[1] * g.nb[2];
+    g.cap = ((maxlen[0] + 1) / 2) * ((maxlen[1] + 1) / 2) * ((maxlen[2] + 1) / 2);
+    hg.nvox = shape[0] * shape[1] * shape[2];
+    CC_REQUIRE((uint64_t)g.n_tiles * (uint64_t)g.cap < 0xFFFFFFF0ull,
+               "too many tiles x cubes for 32-bit node ids (block shape too small for this volume)");
+    CC_REQUIRE(g.n_blocks < (1LL << (64 - KEY_BITS)), "too many blocks");
+    CC_REQUIRE((uint64_t)(zoff + shape[0]) * (uint64_t)shape[1] * (uint64_t)shape[2] < (1ull << KEY_BITS),
+               "volume too large (>= 2^36 voxels)");
+    CC_REQUIRE(g.n_tiles < (1LL << 31), "too many tiles");
+    for (int a = 0; a < 3; ++a) {
+        hg.tab.insert(hg.tab.end(), st[a].begin(), st[a].end());
+        hg.tab.insert(hg.tab.end(), ln[a].begin(), ln[a].end());
+        hg.tab.insert(hg.tab.end(), bk[a].begin(), bk[a].end());
+    }
+    return hg;
+}
+
+static void upload_geom(cc_ctx* c, HostGeom& hg) {
+    c->h_tab = hg.tab;     // kept alive in the ctx until the stream has consumed it
+    c->tiles.ensure(c->h_tab.size() * sizeof(int32_t));
+    HIP_OK(hipMemcpyAsync(c->tiles.p, c->h_tab.data(), c->h_tab.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                          c->stream));
+    int32_t* base = c->tiles.as<int32_t>();
+    int64_t off = 0;
+    for (int a = 0; a < 3; ++a) {
+        const int n = hg.g.nt[a];
+        hg.g.tstart[a] = base + off;
+        hg.g.tlen[a] = base + off + n;
+        hg.g.tblk[a] = base + off + 2 * n;
+        off += 3 * n;
+    }
+}
+
+static int to_mode(int mode) {
+    CC_REQUIRE(mode >= 0 && mode <= 2, "mode must be 0 (greater), 1 (less) or 2 (equal)");
+    return mode;
+}
+
+// ------------------------------------------------------------------------------------------
+// the device pipeline
+// ------------------------------------------------------------------------------------------
+// local_only: stop after block-local components and write skimage-numbered local labels.
+static void run_pipeline(cc_ctx* c, const float* in, const uint8_t* mask, const int64_t shape[3],
+                         const int64_t block_shape[3], double threshold, int mode, uint64_t* out,
+                         bool local_only, cc_result* res) {
+    HostGeom hg = make_geom(shape, block_shape, 0);
+    upload_geom(c, hg);
+    Geom& g = hg.g;
+    const float thr = (float)threshold;                 // numpy: python float -> float32
+    const int64_t nt = g.n_tiles, nb = g.n_blocks;
+    const uint64_t nodes = (uint64_t)nt * g.cap;
+    hipStream_t s = c->stream;
+
+    c->bstat.ensure(nb * 3 * sizeof(u32));
+    c->bparam.ensure(nb * sizeof(BlockParam));
+    c->bits.ensure(nt * NROWS * sizeof(u64));
+    c->faces.ensure(nt * FACE_STRIDE * sizeof(u32));
+    c->count.ensure(nt * sizeof(u32));
+    c->P.ensure(nodes * sizeof(u32));
+    c->KR.ensure(nodes * sizeof(u64));
+    c->seg.ensure(nb * 2 * sizeof(u32));
+    c->values.ensure(nb * sizeof(u64));
+    c->offsets.ensure(nb * sizeof(u64));
+    c->scalars.ensure(4 * sizeof(u64));
+    c->counter.ensure(sizeof(u32));
+
+    u32* smin = c->bstat.as<u32>();
+    u32* smax = smin + nb;
+    u32* sflag = smax + nb;
+    HIP_OK(hipMemsetAsync(smin, 0xFF, nb * sizeof(u32), s));
+    HIP_OK(hipMemsetAsync(smax, 0x00, 2 * nb * sizeof(u32), s));
+    HIP_OK(hipMemsetAsync(c->scalars.p, 0, 4 * sizeof(u64), s));
+    HIP_OK(hipMemsetAsync(c->counter.p, 0, sizeof(u32), s));
+
+    BlockParam* bp = c->bparam.as<BlockParam>();
+    u64* BITS = c->bits.as<u64>();
+    u32* FACES = c->faces.as<u32>();
+    u32* COUNT = c->count.as<u32>();
+    u32* P = c->P.as<u32>();
+    u64* KR = c->KR.as<u64>();
+
+    launch(c, "k_block_stats", [&] { k_block_stats<<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, smin, smax, sflag); });
+    launch(c, "k_block_params", [&] { k_block_params<<<grid1d(nb), 256, 0, s>>>(nb, smin, smax, sflag, thr, mode, bp); });
+    if (mask)
+        launch(c, "k_pass1", [&] { k_pass1<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, mask, bp, thr, mode, BITS, FACES, COUNT, P, KR); });
+    else
+        launch(c, "k_pass1", [&] { k_pass1<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, nullptr, bp, thr, mode, BITS, FACES, COUNT, P, KR); });
+    launch(c, "k_stitch_intra", [&] { k_stitch<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, FACES, P, KR); });
+
+    // block-local roots: count them, read the count back (the one mid-run host sync), size the
+    // sort buffers, then collect (block, first voxel) keys
+    u32* counter = c->counter.as<u32>();
+    u32 n_roots_h = 0;
+    {
+        launch(c, "k_count_roots", [&] { k_count_roots<<<(unsigned)nt, NTHREADS, 0, s>>>(g, COUNT, P, counter); });
+        HIP_OK(hipMemcpyAsync(&n_roots_h, counter, sizeof(u32), hipMemcpyDeviceToHost, s));
+        sync(c);
+    }
+    const int64_t nr = n_roots_h;
+    c->keys.ensure(std::max<int64_t>(1, nr) * sizeof(u64));
+    c->keys2.ensure(std::max<int64_t>(1, nr) * sizeof(u64));
+    c->vals.ensure(std::max<int64_t>(1, nr) * sizeof(u32));
+    c->vals2.ensure(std::max<int64_t>(1, nr) * sizeof(u32));
+    u64* keys = c->keys.as<u64>();
+    u64* keys2 = c->keys2.as<u64>();
+    u32* vals = c->vals.as<u32>();
+    u32* vals2 = c->vals2.as<u32>();
+    u32* seg_start = c->seg.as<u32>();
+    u32* seg_end = seg_start + nb;
+    u64* values = c->values.as<u64>();
+    u64* offsets = c->offsets.as<u64>();
+    u64* scalars = c->scalars.as<u64>();
+    HIP_OK(hipMemsetAsync(seg_start, 0, 2 * nb * sizeof(u32), s));
+    if (nr > 0) {
+        HIP_OK(hipMemsetAsync(counter, 0, sizeof(u32), s));
+        launch(c, "k_collect_roots", [&] { k_collect_roots<<<(unsigned)nt, NTHREADS, 0, s>>>(g, COUNT, P, KR, keys, vals, counter); });
+        int end_bit = KEY_BITS;
+        while ((1LL << (end_bit - KEY_BITS)) < nb) ++end_bit;
+        size_t tmp_bytes = 0;
+        HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys2, vals, vals2, (int)nr, 0, end_bit, s));
+        c->cub_tmp.ensure(tmp_bytes);
+        launch(c, "radix_sort", [&] {
+            HIP_OK(hipcub::DeviceRadixSort::SortPairs(c->cub_tmp.p, tmp_bytes, keys, keys2, vals, vals2, (int)nr, 0, end_bit, s));
+        });
+        launch(c, "k_segments", [&] { k_segments<<<grid1d(nr), 256, 0, s>>>(nr, keys2, seg_start, seg_end); });
+    }
+    launch(c, "k_values", [&] { k_values<<<grid1d(nb), 256, 0, s>>>(nb, seg_start, seg_end, values); });
+    {
+        size_t tmp_bytes = 0;
+        HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, values, offsets, (int)nb, s));
+        c->cub_tmp.ensure(tmp_bytes);
+        launch(c, "scan_offsets", [&] {
+            HIP_OK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, values, offsets, (int)nb, s));
+        });
+    }
+    launch(c, "k_nlabels", [&] { k_nlabels<<<1, 1, 0, s>>>(nb, values, offsets, scalars); });
+    if (nr > 0)
+        launch(c, "k_assign_rid", [&] { k_assign_rid<<<grid1d(nr), 256, 0, s>>>(nr, keys2, vals2, seg_start, offsets, KR); });
+
+    u64* FIN = KR;
+    const uint64_t lut_cap = (uint64_t)nr + (uint64_t)nb + 1;
+    if (local_only) {
+        c->FIN.ensure(nodes * sizeof(u64));
+        FIN = c->FIN.as<u64>();
+        launch(c, "k_finalize", [&] { k_finalize<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, COUNT, P, KR, offsets, FIN); });
+        c->lut_valid = false;
+    } else {
+        launch(c, "k_stitch_inter", [&] { k_stitch<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, FACES, P, KR); });
+        c->lut.ensure(lut_cap * sizeof(u64));
+        u64* lut = c->lut.as<u64>();
+        launch(c, "k_lut_init", [&] { k_lut_init<<<grid1d(lut_cap), 256, 0, s>>>(lut_cap, scalars, lut); });
+        if (nr > 0)
+            launch(c, "k_lut", [&] { k_lut<<<grid1d(nr), 256, 0, s>>>(nr, vals2, P, KR, lut, scalars); });
+        launch(c, "k_finalize", [&] { k_finalize<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, COUNT, P, KR, offsets, KR); });
+        c->lut_valid = true;
+    }
+    launch(c, "k_pass2", [&] { k_pass2<<<(unsigned)nt, NTHREADS, 0, s>>>(g, BITS, COUNT, FIN, out); });
+
+    // small artefacts back to host
+    u64 sc[4] = {0, 0, 0, 0};
+    HIP_OK(hipMemcpyAsync(sc, scalars, 4 * sizeof(u64), hipMemcpyDeviceToHost, s));
+    c->h_values.resize(nb);
+    c->h_offsets.resize(nb);
+    HIP_OK(hipMemcpyAsync(c->h_values.data(), values, nb * sizeof(u64), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(c->h_offsets.data(), offsets, nb * sizeof(u64), hipMemcpyDeviceToHost, s));
+    sync(c);
+    c->n_blocks = nb;
+    c->n_labels = sc[0];
+    if (res) {
+        res->n_blocks = nb;
+        res->n_labels = sc[0];
+        res->max_id = sc[0] - 1;    // lut[n_labels-1] = n_labels-1 is never merged (write.py:283)
+        res->n_components = local_only ? 0 : sc[1];
+        res->n_block_components = (uint64_t)nr;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+#define CC_TRY(...)                                                                            \
+    try {                                                                                      \
+        __VA_ARGS__;                                                                           \
+        return 0;                                                                              \
+    } catch (const CCError& e) {                                                               \
+        g_err = e.msg;                                                                         \
+        return -1;                                                                             \
+    } catch (const std::exception& e) {                                                        \
+        g_err = e.what();                                                                      \
+        return -2;                                                                             \
+    }
+
+extern "C" {
+
+const char* cc_version(void) { return "cc_mi355x 0.1 gfx950"; }
+
+const char* cc_last_error(void) { return g_err.c_str(); }
+
+int cc_create(int device, cc_ctx** out) {
+    CC_TRY({
+        CC_REQUIRE(out != nullptr, "out is NULL");
+        int n = 0;
+        HIP_OK(hipGetDeviceCount(&n));
+        CC_REQUIRE(device >= 0 && device < n, "no such HIP device");
+        HIP_OK(hipSetDevice(device));
+        cc_ctx* c = new cc_ctx();
+        c->device = device;
+        HIP_OK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+        c->stream = c->own_stream;
+        *out = c;
+    })
+}
+
+void cc_destroy(cc_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    DevBuf* bufs[] = {&c->tiles, &c->bstat, &c->bparam, &c->bits, &c->faces, &c->count, &c->P, &c->KR,
+                      &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
+                      &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
+                      &c->out_tmp, &c->pairs, &c->pairs2};
+    for (DevBuf* b : bufs) b->release();
+    for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
+    for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+int cc_set_stream(cc_ctx* c, void* stream) {
+    CC_TRY({
+        CC_REQUIRE(c, "ctx is NULL");
+        c->stream = stream ? (hipStream_t)stream : c->own_stream;
+    })
+}
+
+int cc_label_volume(cc_ctx* c, const float* in, const uint8_t* mask, const int64_t shape[3],
+                    const int64_t block_shape[3], double threshold, int mode, uint64_t* labels,
+                    cc_result* res) {
+    CC_TRY({
+        CC_REQUIRE(c && in && labels && shape && block_shape, "NULL argument");
+        HIP_OK(hipSetDevice(c->device));
+        run_pipeline(c, in, mask, shape, block_shape, threshold, to_mode(mode), labels, false, res);
+    })
+}
+
+int cc_label_volume_host(cc_ctx* c, const float* in, const uint8_t* mask, const int64_t shape[3],
+                         const int64_t block_shape[3], double threshold, int mode, uint64_t* labels,
+                         cc_result* res) {
+    CC_TRY({
+        CC_REQUIRE(c && in && labels && shape && block_shape, "NULL argument");
+        HIP_OK(hipSetDevice(c->device));
+        const int64_t n = shape[0] * shape[1] * shape[2];
+        c->in_tmp.ensure(n * sizeof(float));
+        c->out_tmp.ensure(n * sizeof(u64));
+        HIP_OK(hipMemcpyAsync(c->in_tmp.p, in, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        const uint8_t* dmask = nullptr;
+        if (mask) {
+            c->mask_tmp.ensure(n);
+            HIP_OK(hipMemcpyAsync(c->mask_tmp.p, mask, n, hipMemcpyHostToDevice, c->stream));
+            dmask = c->mask_tmp.as<uint8_t>();
+        }
+        run_pipeline(c, c->in_tmp.as<float>(), dmask, shape, block_shape, threshold, to_mode(mode),
+                     c->out_tmp.as<uint64_t>(), false, res);
+        HIP_OK(hipMemcpyAsync(labels, c->out_tmp.p, n * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+        sync(c);
+    })
+}
+
+int64_t cc_get_block_values(cc_ctx* c, uint64_t* out, int64_t cap) {
+    if (!c || !out) { g_err = "NULL argument"; return -1; }
+    if (cap < (int64_t)c->h_values.size()) { g_err = "cap too small"; return -1; }
+    std::memcpy(out, c->h_values.data(), c->h_values.size() * sizeof(uint64_t));
+    return (int64_t)c->h_values.size();
+}
+
+int64_t cc_get_offsets(cc_ctx* c, uint64_t* out, int64_t cap) {
+    if (!c || !out) { g_err = "NULL argument"; return -1; }
+    if (cap < (int64_t)c->h_offsets.size()) { g_err = "cap too small"; return -1; }
+    std::memcpy(out, c->h_offsets.data(), c->h_offsets.size() * sizeof(uint64_t));
+    return (int64_t)c->h_offsets.size();
+}
+
+int64_t cc_get_lut(cc_ctx* c, uint64_t* out, int64_t cap) {
+    if (!c || !out) { g_err = "NULL argument"; return -1; }
+    if (!c->lut_valid) { g_err = "no LUT: run cc_label_volume first"; return -1; }
+    if (cap < (int64_t)c->n_labels) { g_err = "cap too small"; return -1; }
+    try {
+        HIP_OK(hipSetDevice(c->device));
+        HIP_OK(hipMemcpyAsync(out, c->lut.p, c->n_labels * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+        sync(c);
+    } catch (const CCError& e) {
+        g_err = e.msg;
+        return -1;
+    }
+    return (int64_t)c->n_labels;
+}
+
+int cc_block_components(cc_ctx* c, const float* in, const uint8_t* mask, const int64_t shape[3],
+                        const int64_t block_shape[3], double threshold, int mode, uint64_t* labels,
+                        uint64_t* values_host, int64_t n_blocks) {
+    CC_TRY({
+        CC_REQUIRE(c && in && labels && shape && block_shape, "NULL argument");
+        HIP_OK(hipSetDevice(c->device));
+        run_pipeline(c, in, mask, shape, block_shape, threshold, to_mode(mode), labels, true, nullptr);
+        if (values_host) {
+            CC_REQUIRE(n_blocks >= c->n_blocks, "values buffer too small");
+            std::memcpy(values_host, c->h_values.data(), c->n_blocks * sizeof(uint64_t));
+        }
+    })
+}
+
+int cc_merge_offsets(const uint64_t* values, int64_t n_blocks, uint64_t* offsets, uint8_t* empty,
+                     uint64_t* n_labels) {
+    CC_TRY({
+        CC_REQUIRE(values && n_blocks > 0, "bad arguments");
+        uint64_t acc = 0;
+        for (int64_t b = 0; b < n_blocks; ++b) {
+            if (offsets) offsets[b] = acc;
+            if (empty) empty[b] = values[b] == 0;
+            acc += values[b];
+        }
+        if (n_labels) *n_labels = acc + 1;   // offsets[-1] + values[-1] + 1
+    })
+}
+
+int cc_set_profiling(cc_ctx* c, int enable) {
+    CC_TRY({
+        CC_REQUIRE(c, "ctx is NULL");
+        c->prof = enable != 0;
+    })
+}
+
+int cc_reset_profile(cc_ctx* c) {
+    CC_TRY({
+        CC_REQUIRE(c, "ctx is NULL");
+        c->prof_acc.clear();
+    })
+}
+
+int cc_get_profile(cc_ctx* c, char* names, int names_cap, int64_t* counts, double* total_ms, int cap) {
+    if (!c) { g_err = "ctx is NULL"; return -1; }
+    std::string joined;
+    int i = 0;
+    for (auto& kv : c->prof_acc) {
+        if (i >= cap) break;
+        if (!joined.empty()) joined += ",";
+        joined += kv.first;
+        if (counts) counts[i] = kv.second.count;
+        if (total_ms) total_ms[i] = kv.second.ms;
+        ++i;
+    }
+    if (names && names_cap > 0) {
+        std::strncpy(names, joined.c_str(), names_cap - 1);
+        names[names_cap - 1] = 0;
+    }
+    return i;
+}
+
+}  // extern "C"
+
+#include "cc_stage_host.hip"

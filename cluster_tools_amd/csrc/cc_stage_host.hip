@@ -1,0 +1,161 @@
+// cc_stage_host.hip -- host side of the stage-level entry points and the generator (included at the
+// end of cc_lib.hip, same translation unit).
+
+extern "C" {
+
+int64_t cc_block_faces(cc_ctx* c, const uint64_t* labels, const int64_t shape[3], const int64_t block_shape[3],
+                       const uint64_t* offsets_host, uint64_t* pairs_host, int64_t cap) {
+    try {
+        CC_REQUIRE(c && labels && shape && block_shape && offsets_host, "NULL argument");
+        HIP_OK(hipSetDevice(c->device));
+        hipStream_t s = c->stream;
+        int64_t nb[3], n_face = 0;
+        for (int a = 0; a < 3; ++a) {
+            CC_REQUIRE(shape[a] >= 1 && block_shape[a] >= 1, "bad shape / block_shape");
+            nb[a] = (shape[a] + block_shape[a] - 1) / block_shape[a];
+        }
+        const int64_t n_blocks = nb[0] * nb[1] * nb[2];
+        for (int a = 0; a < 3; ++a)
+            n_face += ((shape[a] - 1) / block_shape[a]) * (shape[0] * shape[1] * shape[2] / shape[a]);
+        c->offsets.ensure(n_blocks * sizeof(u64));
+        HIP_OK(hipMemcpyAsync(c->offsets.p, offsets_host, n_blocks * sizeof(u64), hipMemcpyHostToDevice, s));
+        const int64_t capn = std::max<int64_t>(1, n_face);
+        c->pairs.ensure(2 * capn * sizeof(u64));
+        c->pairs2.ensure(2 * capn * sizeof(u64));
+        c->counter.ensure(sizeof(unsigned long long));
+        c->scalars.ensure(4 * sizeof(u64));
+        u64* pa = c->pairs.as<u64>();
+        u64* pb = pa + capn;
+        u64* qa = c->pairs2.as<u64>();
+        u64* qb = qa + capn;
+        unsigned long long* cnt = (unsigned long long*)c->counter.p;
+        HIP_OK(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), s));
+        for (int a = 0; a < 3; ++a) {
+            const int64_t nplanes = (shape[a] - 1) / block_shape[a];
+            const int64_t work = nplanes * (shape[0] * shape[1] * shape[2] / shape[a]);
+            if (work == 0) continue;
+            launch(c, "k_face_pairs", [&] {
+                k_face_pairs<<<grid1d(work), 256, 0, s>>>(a, shape[0], shape[1], shape[2], block_shape[0],
+                                                          block_shape[1], block_shape[2], nb[0], nb[1], nb[2],
+                                                          labels, c->offsets.as<u64>(), pa, pb, cnt, (u64)capn);
+            });
+        }
+        unsigned long long n_raw = 0;
+        HIP_OK(hipMemcpyAsync(&n_raw, cnt, sizeof(n_raw), hipMemcpyDeviceToHost, s));
+        sync(c);
+        const int64_t n = (int64_t)n_raw;
+        if (n == 0) return 0;
+        // lexicographic sort: by b, then stably by a (block_faces.py:112,132,172 np.unique(axis=0))
+        size_t tb = 0;
+        HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, pb, qb, pa, qa, (int)n, 0, 64, s));
+        c->cub_tmp.ensure(tb);
+        HIP_OK(hipcub::DeviceRadixSort::SortPairs(c->cub_tmp.p, tb, pb, qb, pa, qa, (int)n, 0, 64, s));
+        HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, qa, pa, qb, pb, (int)n, 0, 64, s));
+        c->cub_tmp.ensure(tb);
+        HIP_OK(hipcub::DeviceRadixSort::SortPairs(c->cub_tmp.p, tb, qa, pa, qb, pb, (int)n, 0, 64, s));
+        // pa, pb sorted lexicographically; unique
+        c->FIN.ensure(n * sizeof(u8) + 16);
+        u8* flags = c->FIN.as<u8>();
+        k_unique_flags<<<grid1d(n), 256, 0, s>>>(n, pa, pb, flags);
+        HIP_OK(hipGetLastError());
+        int* nsel = (int*)c->scalars.p;
+        HIP_OK(hipcub::DeviceSelect::Flagged(nullptr, tb, pa, flags, qa, nsel, (int)n, s));
+        c->cub_tmp.ensure(tb);
+        HIP_OK(hipcub::DeviceSelect::Flagged(c->cub_tmp.p, tb, pa, flags, qa, nsel, (int)n, s));
+        HIP_OK(hipcub::DeviceSelect::Flagged(c->cub_tmp.p, tb, pb, flags, qb, nsel, (int)n, s));
+        int nu = 0;
+        HIP_OK(hipMemcpyAsync(&nu, nsel, sizeof(int), hipMemcpyDeviceToHost, s));
+        sync(c);
+        if (pairs_host && cap > 0) {
+            const int64_t m = std::min<int64_t>(cap, nu);
+            std::vector<u64> ha(m), hb(m);
+            HIP_OK(hipMemcpyAsync(ha.data(), qa, m * sizeof(u64), hipMemcpyDeviceToHost, s));
+            HIP_OK(hipMemcpyAsync(hb.data(), qb, m * sizeof(u64), hipMemcpyDeviceToHost, s));
+            sync(c);
+            for (int64_t i = 0; i < m; ++i) { pairs_host[2 * i] = ha[i]; pairs_host[2 * i + 1] = hb[i]; }
+        }
+        return nu;
+    } catch (const CCError& e) {
+        g_err = e.msg;
+        return -1;
+    }
+}
+
+int cc_merge_assignments(cc_ctx* c, const uint64_t* pairs_host, int64_t n_pairs, uint64_t n_labels,
+                         uint64_t* lut_host) {
+    CC_TRY({
+        CC_REQUIRE(c && lut_host && n_labels >= 1 && n_pairs >= 0, "bad arguments");
+        CC_REQUIRE(n_pairs == 0 || pairs_host, "pairs is NULL");
+        HIP_OK(hipSetDevice(c->device));
+        hipStream_t s = c->stream;
+        c->lut.ensure(n_labels * sizeof(u64));
+        c->pairs.ensure(std::max<int64_t>(1, 2 * n_pairs) * sizeof(u64));
+        c->counter.ensure(sizeof(u32));
+        u64* P = c->lut.as<u64>();
+        u32* err = c->counter.as<u32>();
+        HIP_OK(hipMemsetAsync(err, 0, sizeof(u32), s));
+        launch(c, "k_iota64", [&] { k_iota64<<<grid1d(n_labels), 256, 0, s>>>(n_labels, P); });
+        if (n_pairs > 0) {
+            HIP_OK(hipMemcpyAsync(c->pairs.p, pairs_host, 2 * n_pairs * sizeof(u64), hipMemcpyHostToDevice, s));
+            launch(c, "k_union_pairs", [&] {
+                k_union_pairs<<<grid1d(n_pairs), 256, 0, s>>>(n_pairs, c->pairs.as<u64>(), n_labels, P, err);
+            });
+        }
+        launch(c, "k_resolve64", [&] { k_resolve64<<<grid1d(n_labels), 256, 0, s>>>(n_labels, P); });
+        u32 herr = 0;
+        HIP_OK(hipMemcpyAsync(&herr, err, sizeof(u32), hipMemcpyDeviceToHost, s));
+        HIP_OK(hipMemcpyAsync(lut_host, P, n_labels * sizeof(u64), hipMemcpyDeviceToHost, s));
+        sync(c);
+        c->n_labels = n_labels;
+        c->lut_valid = true;
+        CC_REQUIRE(herr == 0, "assignment id >= n_labels (merge_assignments.py:124)");
+    })
+}
+
+int cc_write(cc_ctx* c, uint64_t* labels, const int64_t shape[3], const int64_t block_shape[3],
+             const uint64_t* offsets_host, const uint64_t* lut_host, uint64_t n_labels) {
+    CC_TRY({
+        CC_REQUIRE(c && labels && shape && block_shape && offsets_host && lut_host && n_labels >= 1, "bad arguments");
+        HIP_OK(hipSetDevice(c->device));
+        hipStream_t s = c->stream;
+        int64_t nb[3];
+        for (int a = 0; a < 3; ++a) nb[a] = (shape[a] + block_shape[a] - 1) / block_shape[a];
+        const int64_t n_blocks = nb[0] * nb[1] * nb[2];
+        const int64_t n = shape[0] * shape[1] * shape[2];
+        c->offsets.ensure(n_blocks * sizeof(u64));
+        c->lut.ensure(n_labels * sizeof(u64));
+        c->counter.ensure(sizeof(u32));
+        HIP_OK(hipMemcpyAsync(c->offsets.p, offsets_host, n_blocks * sizeof(u64), hipMemcpyHostToDevice, s));
+        HIP_OK(hipMemcpyAsync(c->lut.p, lut_host, n_labels * sizeof(u64), hipMemcpyHostToDevice, s));
+        HIP_OK(hipMemsetAsync(c->counter.p, 0, sizeof(u32), s));
+        launch(c, "k_write_offsets", [&] {
+            k_write_offsets<<<grid_stride(n), 256, 0, s>>>(shape[0], shape[1], shape[2], block_shape[0], block_shape[1],
+                                                      block_shape[2], nb[1], nb[2], labels, c->offsets.as<u64>(),
+                                                      c->lut.as<u64>(), n_labels, c->counter.as<u32>());
+        });
+        u32 herr = 0;
+        HIP_OK(hipMemcpyAsync(&herr, c->counter.p, sizeof(u32), hipMemcpyDeviceToHost, s));
+        sync(c);
+        CC_REQUIRE(herr == 0, "label id exceeds number of node labels (write.py:164)");
+    })
+}
+
+int cc_generate_boundary_map(cc_ctx* c, float* out, const int64_t shape[3], const int64_t origin[3],
+                             uint64_t seed) {
+    CC_TRY({
+        CC_REQUIRE(c && out && shape, "NULL argument");
+        HIP_OK(hipSetDevice(c->device));
+        int64_t o[3] = {0, 0, 0};
+        if (origin) { o[0] = origin[0]; o[1] = origin[1]; o[2] = origin[2]; }
+        for (int a = 0; a < 3; ++a) CC_REQUIRE(shape[a] >= 1 && o[a] >= 0 && o[a] + shape[a] < (1LL << 21), "bad shape/origin");
+        const int64_t nxb = (shape[2] + 255) / 256;
+        CC_REQUIRE(shape[1] * nxb < (1LL << 24) && shape[0] < 65536, "volume too large for the generator grid");
+        const dim3 grid((unsigned)(shape[1] * nxb), (unsigned)shape[0]);
+        launch(c, "k_generate", [&] {
+            k_generate<<<grid, 256, 0, c->stream>>>(out, shape[0], shape[1], shape[2], o[0], o[1], o[2], seed);
+        });
+        sync(c);
+    })
+}
+
+}  // extern "C"

@@ -1,0 +1,139 @@
+/*
+ * cc_mi355x.h -- C ABI of the MI355X thresholded connected-components library
+ * (libcc_mi355x.so, built from the HIP sources in cluster_tools_amd/csrc for gfx950).
+ *
+ * Drop-in boundary for cluster_tools' ThresholdedComponentsWorkflow (reference v0.3.3).
+ * The reference has no native boundary of its own: its five stages are Python job
+ * functions run as `python <tmp>/<task>.py <tmp>/<task>_job_<i>.config`
+ * (cluster_tools/cluster_tasks.py:529-543).  Each entry point below replaces the
+ * compute of one of those job functions (or all five, fused); the Python host shell
+ * (package cluster_tools_amd.thresholded_components) keeps the task classes, configs,
+ * tmp artefacts and log tokens and calls these through ctypes.  See INTEGRATION.md.
+ *
+ * Conventions
+ *   - status: 0 = ok, < 0 = error; cc_last_error() returns the message of the last
+ *     failure on the calling thread.  The Python binding raises RuntimeError.
+ *   - volumes are C-order (Z, Y, X); shape/block_shape are int64[3] host arrays.
+ *   - the _dev pointers are device pointers (hipMalloc / torch CUDA tensors); the
+ *     _host entry points take host pointers and copy.
+ *   - mode: 0 = 'greater', 1 = 'less', 2 = 'equal'  (block_components.py:41,166-173).
+ *     threshold is cast to float32, as numpy does for `float32_array OP python_float`.
+ *   - one cc_ctx per GPU; a ctx is not thread-safe; all work is enqueued on the
+ *     ctx's stream (cc_set_stream) and the call returns when it is complete.
+ *   - output label semantics: the reference id space (block offset + skimage label,
+ *     merge_offsets.py:115-120, block_faces.py:108-109) with the union-find
+ *     representative = the smallest id of each component.  The reference uses
+ *     nifty's boost_ufd representative instead; the partition is identical and
+ *     maxId (= n_labels - 1) is identical.
+ */
+#ifndef CC_MI355X_H
+#define CC_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct cc_ctx cc_ctx;
+
+/* Results of one labelling run (host copy of the small artefacts). */
+typedef struct {
+    int64_t  n_blocks;      /* blocks_in_volume(shape, block_shape)           */
+    uint64_t n_labels;      /* merge_offsets.py:120                            */
+    uint64_t max_id;        /* write.py:281-289 (attrs['maxId'])               */
+    uint64_t n_components;  /* number of distinct non-zero output labels      */
+    uint64_t n_block_components; /* sum over blocks of n_i (block-local comps) */
+} cc_result;
+
+/* --- context ----------------------------------------------------------- */
+int         cc_create(int device, cc_ctx** out);
+void        cc_destroy(cc_ctx* ctx);
+const char* cc_last_error(void);
+/* use an existing hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL -> ctx's own */
+int         cc_set_stream(cc_ctx* ctx, void* hip_stream);
+/* library version string, e.g. "cc_mi355x 0.1 gfx950" */
+const char* cc_version(void);
+
+/* --- fused path: block_components -> merge_offsets -> block_faces ->
+ *     merge_assignments -> write, all on the device.
+ * Replaces: block_components  cluster_tools/thresholded_components/block_components.py:236-291
+ *           merge_offsets     cluster_tools/thresholded_components/merge_offsets.py:83-131
+ *           block_faces       cluster_tools/thresholded_components/block_faces.py:140-177
+ *           merge_assignments cluster_tools/thresholded_components/merge_assignments.py:88-141
+ *           write (offsets)   cluster_tools/write/write.py:185-220,292-387
+ * in_dev     float32 [Z*Y*X]
+ * mask_dev   uint8 [Z*Y*X] or NULL (nonzero = inside, block_components.py:194,225)
+ * labels_dev uint64 [Z*Y*X] final labels (0 = background)
+ * res        may be NULL
+ */
+int cc_label_volume(cc_ctx* ctx, const float* in_dev, const uint8_t* mask_dev,
+                    const int64_t shape[3], const int64_t block_shape[3],
+                    double threshold, int mode, uint64_t* labels_dev, cc_result* res);
+
+/* Same with host buffers (copies in and out; the PCIe-inclusive path). */
+int cc_label_volume_host(cc_ctx* ctx, const float* in_host, const uint8_t* mask_host,
+                         const int64_t shape[3], const int64_t block_shape[3],
+                         double threshold, int mode, uint64_t* labels_host, cc_result* res);
+
+/* Artefacts of the last cc_label_volume* call, copied to host:
+ *   block values v_i = n_i + 1 or 0   (connected_components_offsets_<job>.json values,
+ *                                      block_components.py:175-182,286-290)
+ *   offsets                           (cc_offsets.json 'offsets', merge_offsets.py:115-117)
+ *   lut[n_labels]                     (the 'assignments' dataset, merge_assignments.py:136-139)
+ * Each returns the number of elements written, or <0 (error / cap too small). */
+int64_t cc_get_block_values(cc_ctx* ctx, uint64_t* out_host, int64_t cap);
+int64_t cc_get_offsets(cc_ctx* ctx, uint64_t* out_host, int64_t cap);
+int64_t cc_get_lut(cc_ctx* ctx, uint64_t* out_host, int64_t cap);
+
+/* --- stage-level entry points (each a single reference job's compute) ---------- */
+
+/* block_components (block_components.py:143-291): block-local 26-connected labels in
+ * skimage numbering (1..n_i, raster first occurrence) written to labels_dev (0 outside),
+ * and values_host[n_blocks] = n_i + 1 or 0. */
+int cc_block_components(cc_ctx* ctx, const float* in_dev, const uint8_t* mask_dev,
+                        const int64_t shape[3], const int64_t block_shape[3],
+                        double threshold, int mode, uint64_t* labels_dev,
+                        uint64_t* values_host, int64_t n_blocks);
+
+/* merge_offsets (merge_offsets.py:104-120): exclusive scan of values; writes offsets
+ * and empty flags; returns n_labels through *n_labels. Host arrays. */
+int cc_merge_offsets(const uint64_t* values_host, int64_t n_blocks, uint64_t* offsets_host,
+                     uint8_t* empty_host, uint64_t* n_labels);
+
+/* block_faces (block_faces.py:87-177): from block-local labels (device) and offsets
+ * (host), the deduplicated face pairs (label_a + off_a, label_b + off_b), sorted
+ * lexicographically like np.unique(axis=0).  Writes at most cap pairs to pairs_host
+ * ([cap][2]); returns the number of pairs (may exceed cap: call again with a larger cap). */
+int64_t cc_block_faces(cc_ctx* ctx, const uint64_t* labels_dev, const int64_t shape[3],
+                       const int64_t block_shape[3], const uint64_t* offsets_host,
+                       uint64_t* pairs_host, int64_t cap);
+
+/* merge_assignments (merge_assignments.py:105-130): union-find over ids 0..n_labels-1
+ * merged by pairs (host, [n_pairs][2]); lut_host[n_labels] = min id of each set. */
+int cc_merge_assignments(cc_ctx* ctx, const uint64_t* pairs_host, int64_t n_pairs,
+                         uint64_t n_labels, uint64_t* lut_host);
+
+/* write with offsets (write.py:185-220): per non-empty block, seg[seg!=0] += off;
+ * seg = lut[seg], in place on labels_dev.  offsets/lut are host arrays. */
+int cc_write(cc_ctx* ctx, uint64_t* labels_dev, const int64_t shape[3],
+             const int64_t block_shape[3], const uint64_t* offsets_host,
+             const uint64_t* lut_host, uint64_t n_labels);
+
+/* --- synthetic benchmark input (oracle/synth.py is its restatement) --- */
+int cc_generate_boundary_map(cc_ctx* ctx, float* out_dev, const int64_t shape[3],
+                             const int64_t origin[3], uint64_t seed);
+
+/* --- instrumentation ---------------------------------------------------------- */
+/* Enable per-kernel HIP-event timing on the ctx stream (adds one event pair per launch). */
+int cc_set_profiling(cc_ctx* ctx, int enable);
+/* Accumulated per-kernel totals since the last reset: name list as "k1,k2,...",
+ * and for each: launch count and total milliseconds.  Returns number of kernels. */
+int cc_get_profile(cc_ctx* ctx, char* names, int names_cap, int64_t* counts, double* total_ms,
+                   int cap);
+int cc_reset_profile(cc_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CC_MI355X_H */

@@ -1,0 +1,40 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, 'tests', 'golden')
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an MI355X (HIP device)')
+    config.addinivalue_line('markers', 'slow: large-volume checks')
+
+
+def golden_index():
+    with open(os.path.join(GOLDEN, 'index.json')) as f:
+        return json.load(f)
+
+
+def load_golden(name):
+    d = np.load(os.path.join(GOLDEN, name + '.npz'))
+    out = {k: d[k] for k in d.files}
+    if 'input' not in out:
+        out['input'] = out['input_q'].astype(np.float32) / np.float32(256)
+    return out
+
+
+@pytest.fixture(scope='session')
+def ctx():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from cluster_tools_amd import _lib
+    c = _lib.Context(0)
+    yield c
+    c.close()

@@ -1,0 +1,63 @@
+"""The C-ABI boundary: the shared library loads without a GPU, exports every symbol the
+header declares, and host-only entry points work.  CPU only."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, 'include', 'cc_mi355x.h')).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(cc_[a-z0-9_]+)\s*\(', src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from cluster_tools_amd import _lib
+    L = _lib.load()
+    declared = header_functions()
+    assert len(declared) >= 19
+    for name in declared:
+        assert hasattr(L, name), name
+    assert set(declared) == set(_lib.EXPORTS)
+
+
+def test_version_and_error_channel():
+    from cluster_tools_amd import _lib
+    L = _lib.load()
+    assert b'gfx950' in L.cc_version()
+    assert isinstance(L.cc_last_error(), bytes)
+
+
+def test_merge_offsets_host_entry_matches_reference_rule():
+    # merge_offsets.py:109-120 on a hand example: values n_i + 1 or 0
+    from cluster_tools_amd import _lib
+    values = np.array([3, 0, 5, 1, 0], dtype=np.uint64)
+    offsets, empty, n_labels = _lib.merge_offsets(values)
+    np.testing.assert_array_equal(offsets, [0, 3, 3, 8, 9])
+    np.testing.assert_array_equal(empty, [1, 4])
+    assert n_labels == 0 + 9 + 0 + 1  # offsets[-1] + values[-1] + 1 = 9 + 0 + 1
+
+
+def test_no_silent_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('GPU present')
+    from cluster_tools_amd import _lib
+    with pytest.raises(RuntimeError):
+        _lib.Context(0)
+
+
+def test_product_never_imports_oracle():
+    pkg = os.path.join(ROOT, 'cluster_tools_amd')
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith('.py'):
+                txt = open(os.path.join(dirpath, f)).read()
+                for line in txt.splitlines():
+                    s = line.strip()
+                    if s.startswith('import') or s.startswith('from'):
+                        assert 'oracle' not in s, (f, s)

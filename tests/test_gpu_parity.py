@@ -1,0 +1,144 @@
+"""Parity of the HIP path with the oracle and with the reference's golden vectors.
+All tests here run on an MI355X through the C ABI (libcc_mi355x.so)."""
+import numpy as np
+import pytest
+
+from conftest import golden_index, load_golden
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+CASES = sorted((k, v) for k, v in golden_index().items() if not v['quirk'])
+IDS = [c[0] for c in CASES]
+
+
+def _check_against_oracle(ctx, inp, block_shape, thr, mode, mask=None, res=None, lab=None):
+    if lab is None:
+        lab, res = ctx.label_volume(inp, block_shape, thr, mode, mask)
+    r = O.label_volume(inp, block_shape, thr, mode, mask, n_threads=8)
+    nb = len(r['values'])
+    np.testing.assert_array_equal(lab, r['labels'])          # raw uint64, bit-exact
+    np.testing.assert_array_equal(ctx.block_values(nb), r['values'])
+    np.testing.assert_array_equal(ctx.offsets(nb), r['offsets'])
+    assert res['n_labels'] == r['n_labels']
+    assert res['max_id'] == r['max_id']
+    np.testing.assert_array_equal(ctx.lut(res['n_labels']), r['lut'])
+    return lab, res, r
+
+
+@pytest.mark.parametrize('name,meta', CASES, ids=IDS)
+def test_fused_path_golden(ctx, name, meta):
+    d = load_golden(name)
+    lab, res, r = _check_against_oracle(ctx, d['input'], meta['block_shape'], float(d['threshold']),
+                                        meta['mode'], d.get('mask'))
+    # against the reference itself (canonical relabel = the parity contract)
+    np.testing.assert_array_equal(O.canon(lab), d['labels_canon'])
+    np.testing.assert_array_equal(ctx.block_values(len(d['block_values'])), d['block_values'])
+    np.testing.assert_array_equal(ctx.offsets(len(d['offsets'])), d['offsets'])
+    assert res['n_labels'] == int(d['n_labels'])
+    assert res['max_id'] == int(d['max_id'])
+    np.testing.assert_array_equal(O.canon(ctx.lut(res['n_labels'])), d['lut_canon'])
+    assert res['n_components'] == int(d['labels_canon'].max())
+
+
+@pytest.mark.parametrize('name,meta', CASES, ids=IDS)
+def test_stage_level_golden(ctx, name, meta):
+    """block_components -> merge_offsets -> block_faces -> merge_assignments -> write, one
+    C-ABI entry per reference job, each artefact against the reference's."""
+    import torch
+    d = load_golden(name)
+    x = torch.from_numpy(d['input']).cuda()
+    m = torch.from_numpy(d['mask']).cuda() if 'mask' in d else None
+    local, values = ctx.block_components(x, meta['block_shape'], float(d['threshold']), meta['mode'], m)
+    np.testing.assert_array_equal(local.cpu().numpy().view(np.uint64), d['local_labels'].astype(np.uint64))
+    np.testing.assert_array_equal(values, d['block_values'])
+    from cluster_tools_amd import _lib
+    offsets, empty, n_labels = _lib.merge_offsets(values)
+    np.testing.assert_array_equal(offsets, d['offsets'])
+    np.testing.assert_array_equal(empty, d['empty_blocks'])
+    assert n_labels == int(d['n_labels'])
+    pairs = ctx.block_faces(local, meta['block_shape'], offsets)
+    np.testing.assert_array_equal(pairs, d['pairs'])
+    lut = ctx.merge_assignments(pairs, n_labels)
+    np.testing.assert_array_equal(O.canon(lut), d['lut_canon'])
+    ctx.write(local, meta['block_shape'], offsets, lut)
+    np.testing.assert_array_equal(O.canon(local.cpu().numpy()), d['labels_canon'])
+
+
+def test_device_and_host_paths_agree(ctx):
+    import torch
+    d = load_golden('bmap_big_less')
+    host, _ = ctx.label_volume(d['input'], (32, 64, 64), 0.5, 'less')
+    dev, _ = ctx.label_volume(torch.from_numpy(d['input']).cuda(), (32, 64, 64), 0.5, 'less')
+    np.testing.assert_array_equal(host, dev.cpu().numpy().view(np.uint64))
+
+
+SYNTH = [
+    ((64, 256, 256), (32, 128, 128), 'greater'),
+    ((64, 256, 256), (32, 128, 128), 'less'),
+    ((100, 300, 200), (50, 128, 100), 'less'),     # odd x extents, edge blocks
+    ((96, 200, 250), (25, 64, 64), 'greater'),     # odd block z (partial cubes at block ends)
+    ((70, 130, 190), (70, 130, 190), 'less'),      # one block, many tiles: 26-conn tile seams
+    ((33, 65, 129), (11, 13, 43), 'greater'),      # tiles smaller than TX, odd everything
+    ((128, 128, 128), (128, 128, 128), 'greater'),
+]
+
+
+@pytest.mark.parametrize('shape,bs,mode', SYNTH)
+def test_synthetic_vs_oracle(ctx, shape, bs, mode):
+    inp = O.boundary_map(shape, origin=(7, 3, 1))
+    _check_against_oracle(ctx, inp, bs, 0.5, mode)
+
+
+@pytest.mark.parametrize('density', [0.2, 0.45, 0.6])
+def test_white_noise_tile_seams(ctx, density):
+    """White noise hits every 26-neighbour configuration at every tile seam."""
+    rng = np.random.default_rng(int(density * 100))
+    inp = rng.random((40, 80, 150), dtype=np.float32)
+    _check_against_oracle(ctx, inp, (40, 80, 150), density, 'less')
+    _check_against_oracle(ctx, inp, (20, 40, 75), 1 - density, 'greater')
+
+
+def test_mask_vs_oracle(ctx):
+    from oracle.synth import ellipsoid_mask
+    shape = (64, 160, 192)
+    inp = O.boundary_map(shape)
+    mask = ellipsoid_mask(shape, 0.4)
+    _check_against_oracle(ctx, inp, (32, 64, 64), 0.5, 'greater', mask)
+    _check_against_oracle(ctx, inp, (32, 64, 64), 0.5, 'less', mask * 200)
+
+
+def test_normalisation_edge_cases(ctx):
+    rng = np.random.default_rng(5)
+    x = rng.random((32, 48, 64), dtype=np.float32)
+    x[:16, :24, :32] = x[:16, :24, :32] * np.float32(1e6) - np.float32(3e5)
+    x[16:, 24:, 32:] = np.float32(-2.5)                       # constant block
+    x[:16, 24:, 32:] = np.float32(np.nan)
+    x[20, 5, 7] = np.float32(np.inf)
+    x[3, 30, 3] = np.float32(-np.inf)
+    x[16:, :24, :32] = (x[16:, :24, :32] * np.float32(1e-40)).astype(np.float32)   # denormals
+    for mode, thr in [('greater', 0.5), ('less', 0.5), ('equal', 0.0), ('less', 0.1), ('greater', 1e-7)]:
+        _check_against_oracle(ctx, x, (16, 24, 32), thr, mode)
+
+
+def test_generator_matches_oracle(ctx):
+    for shape, origin in [((40, 70, 300), (3, 5, 7)), ((17, 33, 513), (64, 0, 1000))]:
+        g = ctx.generate_boundary_map(shape, origin=origin).cpu().numpy()
+        np.testing.assert_array_equal(g, O.boundary_map(shape, origin=origin))
+
+
+def test_repeat_runs_identical(ctx):
+    import torch
+    x = ctx.generate_boundary_map((128, 512, 512))
+    a, ra = ctx.label_volume(x, (64, 256, 256), 0.5, 'less')
+    b, rb = ctx.label_volume(x, (64, 256, 256), 0.5, 'less')
+    assert torch.equal(a, b) and ra == rb
+
+
+@pytest.mark.slow
+def test_c2_vs_oracle(ctx):
+    """BASELINE config 2 (512^3, block 128^3) bit-exact against the C oracle."""
+    x = ctx.generate_boundary_map((512, 512, 512))
+    lab, res = ctx.label_volume(x, (128, 128, 128), 0.5, 'greater')
+    inp = x.cpu().numpy()
+    _check_against_oracle(ctx, inp, (128, 128, 128), 0.5, 'greater', res=res,
+                          lab=lab.cpu().numpy().view(np.uint64))
