@@ -1,0 +1,188 @@
+"""Benchmark: Gvoxels/s of thresholded CCL end to end on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode greater|less] [--mask]
+
+One step = the full five-stage path (block_components -> merge_offsets -> block_faces ->
+merge_assignments -> write) over one synthetic volume that is already resident in HBM,
+ending with the final uint64 labels resident in HBM.
+
+Workloads:
+  N = 1  C3: (1024, 2048, 2048) float32, block (64, 512, 512), threshold 0.5 'greater'
+  N > 1  z-slab sharded, one process per GPU, weak scaling: each rank owns a
+         (256, 4096, 4096) slab of a (256 N, 4096, 4096) volume -- at N = 8 this is C5,
+         (2048, 4096, 4096).  Seams are stitched over RCCL (cluster_tools_amd/distributed.py).
+Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = 'Gvoxels/sec thresholded CCL end-to-end at 1/2/4/8 MI355X; % of HBM roofline'
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+B_ALG = 12.0                   # algorithmic bytes / voxel: f32 read + uint64 write (+1 with mask)
+# algorithmic bytes per voxel of each kernel
+KERNEL_BYTES = {'k_block_stats': 4.0, 'k_pass1': 4.0, 'k_pass2': 8.0}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=10)
+    p.add_argument('--warmup', type=int, default=3)
+    p.add_argument('--mode', default='greater')
+    p.add_argument('--threshold', type=float, default=0.5)
+    p.add_argument('--mask', action='store_true')
+    p.add_argument('--shape', default=None, help='override Z,Y,X (per-rank slab for N > 1)')
+    p.add_argument('--block-shape', default='64,512,512')
+    p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--cpu-sample-z', type=int, default=128)
+    p.add_argument('--traffic-json', default=None, help='rocprofv3 PMC summary to fill roofline.traffic')
+    return p.parse_args()
+
+
+def cpu_baseline(args, block_shape, shape_yx):
+    """Oracle C restatement of the reference target='local' path on host cores, on a bounded
+    sample: the first `cpu_sample_z` planes of the same synthetic volume."""
+    from oracle import oracle as O
+    threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, 64))
+    shape = (args.cpu_sample_z,) + tuple(shape_yx)
+    x = O.boundary_map(shape, n_threads=threads)
+    t0 = time.perf_counter()
+    r = O.label_volume(x, block_shape, args.threshold, args.mode, n_threads=threads, want_lut=False)
+    dt = time.perf_counter() - t0
+    nvox = x.size
+    del x, r
+    return {'value': round(nvox / dt / 1e9, 4), 'unit': 'Gvox/s', 'cores': threads, 'kind': 'port',
+            'sample': 'oracle/cc_oracle.c (C restatement of the 5 reference stages, n_jobs=%d threads, '
+                      'blocks strided as LocalTask) on shape %s block %s, %.2f s wall'
+                      % (threads, list(shape), list(block_shape), dt)}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from cluster_tools_amd import _lib
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    assert world == args.gpus, 'launch N > 1 with torch.distributed.run (WORLD_SIZE must equal --gpus)'
+    torch.cuda.set_device(local_rank)
+    dev = torch.device('cuda', local_rank)
+    if world > 1:
+        os.environ.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+        dist.init_process_group('nccl', device_id=dev)
+
+    block_shape = tuple(int(v) for v in args.block_shape.split(','))
+    if args.shape:
+        slab = tuple(int(v) for v in args.shape.split(','))
+    else:
+        slab = (1024, 2048, 2048) if world == 1 else (256, 4096, 4096)
+    gshape = (slab[0] * world,) + slab[1:]
+    workload = ('C3 (1024,2048,2048) f32, 1 GPU' if world == 1 and not args.shape else
+                'C5-style z-slabs (256N,4096,4096) f32' if not args.shape else 'custom %s' % (gshape,))
+
+    ctx = _lib.Context(local_rank)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    z0 = slab[0] * rank
+    x = ctx.generate_boundary_map(slab, origin=(z0, 0, 0), device=dev)
+    mask = None
+    if args.mask:
+        from cluster_tools_amd.synthetic import ellipsoid_mask_device
+        mask = ellipsoid_mask_device(gshape, z0, slab[0], dev)
+    out = torch.empty(slab, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+
+    if world == 1:
+        def step():
+            return ctx.label_volume(x, block_shape, args.threshold, args.mode, mask=mask, out=out)[1]
+    else:
+        from cluster_tools_amd.distributed import ShardedLabeler
+        lab = ShardedLabeler(ctx, gshape, block_shape, z0, slab[0], dev)
+
+        def step():
+            return lab.label(x, args.threshold, args.mode, mask=mask, out=out)
+
+    for _ in range(args.warmup):
+        res = step()
+    ctx.set_profiling(True)
+    ctx.reset_profile()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    prof = ctx.profile()
+    ctx.set_profiling(False)
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    nvox_rank = int(np.prod(slab))
+    nvox_all = nvox_rank * world
+    ms_per_step = dt / args.steps * 1e3
+    value = nvox_all * args.steps / dt / 1e9
+    b_alg = B_ALG + (1.0 if args.mask else 0.0)
+    # dominant kernel of this rank, timed by HIP events on the stream it runs on
+    kern = {k: v for k, v in prof.items() if v['count']}
+    dom = max(kern, key=lambda k: kern[k]['total_ms'])
+    avg_ms = kern[dom]['total_ms'] / kern[dom]['count']
+    kb = KERNEL_BYTES.get(dom)
+    if dom == 'k_pass1' and args.mask:
+        kb += 1.0
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        traffic = json.load(open(args.traffic_json)).get(dom)
+    roofline = None
+    if kb is not None:
+        achieved = kb * nvox_rank / (avg_ms * 1e-3) / 1e9
+        roofline = {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
+                    'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
+                    'alg_bytes_per_voxel': kb, 'avg_launch_ms': round(avg_ms, 4)}
+    e2e_gbs = b_alg * nvox_all * args.steps / dt / 1e9 / world
+
+    line = {
+        'metric': METRIC, 'value': round(value, 3), 'unit': 'Gvox/s', 'n_gpus': world,
+        'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3),
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'data': 'synthetic (integer-only jittered-Voronoi boundary map, SURVEY.md §8d, seed 0x5EED)',
+        'config': {'workload': workload, 'shape': list(gshape), 'slab': list(slab),
+                   'block_shape': list(block_shape), 'threshold': args.threshold,
+                   'threshold_mode': args.mode, 'mask': bool(args.mask),
+                   'parallelism': 'z-slab x%d' % world if world > 1 else 'single GPU'},
+        'roofline': roofline,
+        'e2e_roofline': {'alg_bytes_per_voxel': b_alg, 'achieved_gbs_per_gpu': round(e2e_gbs, 1),
+                         'frac': round(e2e_gbs / HBM_PEAK_GBS, 4)},
+        'kernels_ms_per_step': {k: round(v['total_ms'] / args.steps, 4) for k, v in
+                                sorted(kern.items(), key=lambda kv: -kv[1]['total_ms'])},
+        'result': res,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        del x, out
+        torch.cuda.empty_cache()
+        line['cpu_baseline'] = cpu_baseline(args, block_shape, slab[1:])
+    elif rank == 0:
+        line['cpu_baseline'] = None
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -21,7 +21,8 @@ EXPORTS = (
     'cc_label_volume', 'cc_label_volume_host', 'cc_get_block_values', 'cc_get_offsets',
     'cc_get_lut', 'cc_block_components', 'cc_merge_offsets', 'cc_block_faces',
     'cc_merge_assignments', 'cc_write', 'cc_generate_boundary_map', 'cc_set_profiling',
-    'cc_get_profile', 'cc_reset_profile',
+    'cc_get_profile', 'cc_reset_profile', 'cc_shard_begin', 'cc_shard_assign', 'cc_shard_planes',
+    'cc_seam_pairs', 'cc_shard_finish',
 )
 
 
@@ -66,6 +67,11 @@ def load():
         'cc_set_profiling': (I, [P, I]),
         'cc_get_profile': (I, [P, ctypes.c_char_p, I, P, P, I]),
         'cc_reset_profile': (I, [P]),
+        'cc_shard_begin': (I, [P, P, P, P, P, ctypes.c_double, I, i64, P]),
+        'cc_shard_assign': (I, [P, u64]),
+        'cc_shard_planes': (I, [P, P, P]),
+        'cc_seam_pairs': (i64, [P, P, P, i64, P, i64]),
+        'cc_shard_finish': (I, [P, P, i64, P, ctypes.POINTER(CCResult)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -226,6 +232,43 @@ class Context:
         shape_a, origin_a = _i64(shape), _i64(origin)   # keep alive across the call
         _check(load().cc_generate_boundary_map(self._h, _ptr(out_dev), _ptr(shape_a), _ptr(origin_a), int(seed)))
         return out_dev
+
+    # ---- z-slab shards (cluster_tools_amd/distributed.py drives these) ----
+    def shard_begin(self, x_dev, block_shape, threshold, mode, z_offset, mask_dev=None):
+        shape, bs = _i64(x_dev.shape), _i64(block_shape)
+        out = np.zeros(1, dtype=np.uint64)
+        _check(load().cc_shard_begin(self._h, _ptr(x_dev), _ptr(mask_dev), _ptr(shape), _ptr(bs),
+                                     float(threshold), mode_id(mode), int(z_offset), _ptr(out)))
+        return int(out[0])
+
+    def shard_assign(self, id_base):
+        _check(load().cc_shard_assign(self._h, int(id_base)))
+
+    def shard_planes(self, bottom_dev=None, top_dev=None):
+        _check(load().cc_shard_planes(self._h, _ptr(bottom_dev), _ptr(top_dev)))
+
+    def seam_pairs(self, upper_dev, lower_dev, pairs_dev=None):
+        n = upper_dev.numel()
+        cap = 0 if pairs_dev is None else pairs_dev.shape[0]
+        return _check(load().cc_seam_pairs(self._h, _ptr(upper_dev), _ptr(lower_dev), n, _ptr(pairs_dev), cap))
+
+    def shard_finish(self, pairs_dev, n_pairs, out_dev):
+        res = CCResult()
+        _check(load().cc_shard_finish(self._h, _ptr(pairs_dev) if n_pairs else None, int(n_pairs),
+                                      _ptr(out_dev), ctypes.byref(res)))
+        return res.as_dict()
+
+    def lut_local(self):
+        """The LUT of the last run on this ctx: for a shard, its ids id_base .. id_base + sum."""
+        n = 1 << 20
+        while True:
+            a = np.empty(n, dtype=np.uint64)
+            r = load().cc_get_lut(self._h, _ptr(a), n)
+            if r >= 0:
+                return a[:r]
+            if n > 1 << 40:
+                _check(r)
+            n *= 8
 
     # ---- profiling ----
     def set_profiling(self, on=True):

@@ -24,7 +24,7 @@ constexpr int TZ = 16, TY = 32, TX = 64;
 constexpr int CZ = TZ / 2, CY = TY / 2, CX = TX / 2;
 constexpr int NC = CZ * CY * CX;           // cubes per full tile (4096)
 constexpr int NROWS = TZ * TY;             // bit rows per tile (512)
-constexpr int NTHREADS = 256;              // 4 waves of 64
+constexpr int NTHREADS = 512;              // 8 waves of 64
 // face planes of a tile, in cubes; entry = k | (4 face-voxel bits << 16), 0 = no face voxel
 constexpr int F_Z = CY * CX, F_Y = CZ * CX, F_X = CZ * CY;
 constexpr int F_ZLO = 0, F_ZHI = F_Z, F_YLO = 2 * F_Z, F_YHI = 2 * F_Z + F_Y;
@@ -98,9 +98,17 @@ __device__ __forceinline__ bool voxel_pred(const BlockParam& p, float x, float t
 }
 
 // ---- LDS union-find over cubes (root = smallest cube index of the component) ----
+// find with path halving.  Only ever stores an ancestor of x into par[x] (same set,
+// smaller index), which keeps the concurrent atomicMin-based unions correct.
 __device__ __forceinline__ u32 lfind(volatile u32* par, u32 x) {
     u32 p = par[x];
-    while (p != x) { x = p; p = par[x]; }
+    while (p != x) {
+        const u32 gp = par[p];
+        if (gp == p) return p;
+        par[x] = gp;
+        x = gp;
+        p = par[x];
+    }
     return x;
 }
 
@@ -156,7 +164,7 @@ __device__ __forceinline__ void gunion(u32* P, const u64* K, u32 a, u32 b) {
 #define CC_FOR(i, n) \
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)(n); i += (int64_t)gridDim.x * blockDim.x)
 
-// ---- block-wide exclusive scan (256 threads) ----
+// ---- block-wide exclusive scan (NTHREADS threads) ----
 __device__ __forceinline__ u32 block_excl_scan(u32 v, u32* scratch, u32* total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     u32 x = v;

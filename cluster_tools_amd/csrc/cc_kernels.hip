@@ -45,40 +45,108 @@ __host__ __device__ constexpr u32 fsel(int sp, int sq) {
 #define CC_DIRS(X)                                                                            \
     X(-1, -1, -1) X(-1, -1, 0) X(-1, -1, 1) X(-1, 0, -1) X(-1, 0, 0) X(-1, 0, 1) X(-1, 1, -1) \
     X(-1, 1, 0) X(-1, 1, 1) X(0, -1, -1) X(0, -1, 0) X(0, -1, 1) X(0, 0, -1)
+// the same without (0, 0, -1), which the x-runs cover
+#define CC_DIRS12(X)                                                                          \
+    X(-1, -1, -1) X(-1, -1, 0) X(-1, -1, 1) X(-1, 0, -1) X(-1, 0, 0) X(-1, 0, 1) X(-1, 1, -1) \
+    X(-1, 1, 0) X(-1, 1, 1) X(0, -1, -1) X(0, -1, 0) X(0, -1, 1)
 
 // ------------------------------------------------------------------------------------------
 // tile CCL in LDS.  rows[NROWS] holds the tile's foreground bits (zero outside its extent).
 // After return (R = number of tile-local components): for every non-empty cube c,
 //   root = par[c] & 0xFFFF, k = par[root] >> 16 (k in [0, R), deterministic).
+//
+// Cube c = tid + NTHREADS*i, so lanes 0-31 / 32-63 of a wave hold cx = 0..31 of two cube rows:
+// the x-direction unions are done with two ballots (runs of x-linked cubes, root = run start)
+// and only the 12 other lex-negative directions go through the LDS union-find.
 // ------------------------------------------------------------------------------------------
-__device__ u32 tile_ccl(const u64* rows, u8* cm, u32* par, u32* scratch) {
-    const int tid = threadIdx.x;
+constexpr u32 XLO_BITS = sel_bits(2, 2, 0), XHI_BITS = sel_bits(2, 2, 1);
+constexpr u64 EVEN64 = 0x5555555555555555ull;
+constexpr int NCROW = CZ * CY;          // cube rows per tile
+constexpr int NDIR = 12;                // lex-negative directions other than (0,0,-1)
+// direction d = grp*3 + (dx+1), grp: (dz,dy) = (-1,-1), (-1,0), (-1,1), (0,-1)
+__host__ __device__ constexpr int dir_dz(int d) { return d / 3 == 3 ? 0 : -1; }
+__host__ __device__ constexpr int dir_dy(int d) { return d / 3 == 3 ? -1 : d / 3 - 1; }
+__host__ __device__ constexpr int dir_dx(int d) { return d % 3 - 1; }
+
+// OR of the voxel rows of a cube row whose (lz, ly) match selections (sz, sy); a[lz*2+ly]
+__device__ __forceinline__ u64 pick_rows(const u64 a[4], int sz, int sy) {
+    u64 u = 0;
+    if (sz != 1 && sy != 1) u |= a[0];
+    if (sz != 1 && sy != 0) u |= a[1];
+    if (sz != 0 && sy != 1) u |= a[2];
+    if (sz != 0 && sy != 0) u |= a[3];
+    return u;
+}
+// cube-level mask in "even" representation (cube cx <-> bit 2cx) of voxels with lx in sx
+__device__ __forceinline__ u64 xsel(u64 u, int sx) {
+    return sx == 0 ? (u & EVEN64) : sx == 1 ? ((u >> 1) & EVEN64) : ((u | (u >> 1)) & EVEN64);
+}
+__device__ __forceinline__ u64 shift_dx(u64 m, int dx) { return dx > 0 ? m >> 2 : dx < 0 ? m << 2 : m; }
+// x-links of a cube row, even repr: bit 2cx set iff cube cx is 26-linked to cube cx+1
+__device__ __forceinline__ u64 xlinks(const u64 a[4]) {
+    const u64 u = a[0] | a[1] | a[2] | a[3];
+    return ((u >> 1) & EVEN64) & ((u & EVEN64) >> 2);
+}
+
+// Per cube row and direction, the cube pairs whose union is NOT implied by the x-runs plus
+// the union of the pair one cube to the left (same A-run, same B-run, also connected).
+__device__ __forceinline__ void necessary_unions(const u64* rows, u64* nec) {
+    for (int w = threadIdx.x; w < NCROW * 4; w += NTHREADS) {
+        const int row = w >> 2, grp = w & 3;
+        const int cz = row / CY, cy = row % CY;
+        const int dz = grp == 3 ? 0 : -1, dy = grp == 3 ? -1 : grp - 1;
+        const int bz = cz + dz, by = cy + dy;
+        u64 a[4], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = rows[(2 * cz + (j >> 1)) * TY + 2 * cy + (j & 1)];
+        const bool okb = bz >= 0 && by >= 0 && by < CY;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = okb ? rows[(2 * bz + (j >> 1)) * TY + 2 * by + (j & 1)] : 0;
+        const int szs = dz < 0 ? 0 : 2, szn = dz < 0 ? 1 : 2;
+        const int sys = dy < 0 ? 0 : dy > 0 ? 1 : 2, syn = dy < 0 ? 1 : dy > 0 ? 0 : 2;
+        const u64 ua = pick_rows(a, szs, sys), ub = pick_rows(b, szn, syn);
+        const u64 ea_prev = xlinks(a) << 2, eb_prev = xlinks(b) << 2;
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+            const int sxs = dx < 0 ? 0 : dx > 0 ? 1 : 2, sxn = dx < 0 ? 1 : dx > 0 ? 0 : 2;
+            const u64 C = xsel(ua, sxs) & shift_dx(xsel(ub, sxn), dx);
+            const u64 red = (C << 2) & ea_prev & shift_dx(eb_prev, dx);
+            nec[row * NDIR + grp * 3 + dx + 1] = C & ~red;
+        }
+    }
+}
+
+__device__ u32 tile_ccl(const u64* rows, u8* cm, u32* par, u64* nec, u32* scratch) {
+    const int tid = threadIdx.x, lane = tid & 63;
     for (int c = tid; c < NC; c += NTHREADS) {
         const int cz = c / (CY * CX), cy = (c / CX) % CY, cx = c % CX;
         const int r = (2 * cz) * TY + 2 * cy;
         const int sh = 2 * cx;
         const u32 m = (u32)((rows[r] >> sh) & 3) | ((u32)((rows[r + 1] >> sh) & 3) << 2) |
                       ((u32)((rows[r + TY] >> sh) & 3) << 4) | ((u32)((rows[r + TY + 1] >> sh) & 3) << 6);
+        // x-runs: cube cx links to cx+1 iff it has a voxel at local x=1 and cx+1 one at local x=0
+        const u64 L = __ballot((m & XLO_BITS) != 0), Rr = __ballot((m & XHI_BITS) != 0);
+        const u64 E = Rr & (L >> 1) & 0x7FFFFFFF7FFFFFFFull;         // no link across the two cube rows
+        const u64 B = (L | Rr) & ~(E << 1);                           // run starts
+        const u64 below = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+        const int s0 = 63 - __builtin_clzll((B & below) | 1ull);
         cm[c] = (u8)m;
-        par[c] = m ? (u32)c : NONE;
+        par[c] = m ? (u32)(c - lane + s0) : NONE;
     }
+    necessary_unions(rows, nec);
     __syncthreads();
     for (int c = tid; c < NC; c += NTHREADS) {
-        const u32 m = cm[c];
-        if (!m) continue;
-        const int cz = c / (CY * CX), cy = (c / CX) % CY, cx = c % CX;
-#define CC_MERGE(DZ, DY, DX)                                                                   \
-    {                                                                                          \
-        const int nz = cz + (DZ), ny = cy + (DY), nx = cx + (DX);                              \
-        if (nz >= 0 && ny >= 0 && ny < CY && nx >= 0 && nx < CX) {                            \
-            const int n = c + (DZ) * (CY * CX) + (DY) * CX + (DX);                             \
-            constexpr u32 SC = sel_bits(self_sel(DZ), self_sel(DY), self_sel(DX));             \
-            constexpr u32 SN = sel_bits(nbr_sel(DZ), nbr_sel(DY), nbr_sel(DX));                \
-            if ((m & SC) && (cm[n] & SN)) lunion(par, (u32)c, (u32)n);                          \
-        }                                                                                      \
-    }
-        CC_DIRS(CC_MERGE)
-#undef CC_MERGE
+        if (!cm[c]) continue;
+        const int row = c / CX, sh = 2 * (c % CX);
+        const u64* nr = nec + row * NDIR;
+#pragma unroll
+        for (int d = 0; d < NDIR; ++d) {
+            if ((nr[d] >> sh) & 1) {
+                const int n = c + dir_dz(d) * (CY * CX) + dir_dy(d) * CX + dir_dx(d);
+                const u32 pc = par[c], pn = par[n];
+                if (pc != pn) lunion(par, pc, pn);
+            }
+        }
     }
     __syncthreads();
     for (int c = tid; c < NC; c += NTHREADS)
@@ -103,42 +171,91 @@ __device__ __forceinline__ u32 cube_k(const u32* par, int c) {
 // ------------------------------------------------------------------------------------------
 // k_block_stats: per-block ordered min / max and NaN flag.  One workgroup per tile, lane = x.
 // ------------------------------------------------------------------------------------------
-constexpr int UNR = 16;   // rows in flight per wave
+constexpr int UNR = 16;   // rows in flight per wave (scalar path)
+constexpr int G4 = 4;     // float4 row groups (4 rows each) in flight per wave
 
+// Can the tile's rows be read as float4 (16-B aligned, 16 lanes per row)?
+__device__ __forceinline__ bool vec4_ok(const Geom& g, const TileInfo& ti) {
+    return ((ti.x0 | ti.lx | (int)(g.X & 3)) & 3) == 0;
+}
+
+// Visit every voxel row of the tile with its values: f(row index r = lz*TY + ly, lane-held
+// values).  Vector path: lane = (row q = lane/16, float4 i = lane%16); scalar path: lane = x.
+template <bool HAS_MASK, class F4, class F1>
+__device__ __forceinline__ void for_tile_rows(const Geom& g, const TileInfo& ti, const float* __restrict__ in,
+                                              const u8* __restrict__ mask, F4&& f4, F1&& f1) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int NW = NTHREADS / 64;
+    if (vec4_ok(g, ti)) {
+        const int q = lane >> 4, i = lane & 15;
+        const bool xact = 4 * i < ti.lx;
+        for (int r0 = wave * 4 * G4; r0 < NROWS; r0 += NW * 4 * G4) {
+            float4 v[G4];
+            u32 mk[G4];
+            bool act[G4];
+#pragma unroll
+            for (int j = 0; j < G4; ++j) {
+                const int r = r0 + 4 * j + q, lz = r / TY, ly = r % TY;
+                act[j] = xact && lz < ti.lz && ly < ti.ly;
+                v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                mk[j] = 0;
+                if (act[j]) {
+                    const int64_t idx = ((int64_t)(ti.z0 + lz) * g.Y + ti.y0 + ly) * g.X + ti.x0 + 4 * i;
+                    v[j] = *reinterpret_cast<const float4*>(in + idx);
+                    if (HAS_MASK) mk[j] = *reinterpret_cast<const u32*>(mask + idx);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < G4; ++j) f4(r0 + 4 * j + q, i, act[j], v[j], mk[j]);
+        }
+    } else {
+        const bool act = lane < ti.lx;
+        const int nrows = ti.lz * ti.ly;
+        for (int r0 = wave * UNR; r0 < nrows; r0 += NW * UNR) {
+            float v[UNR];
+            u8 mk[UNR];
+#pragma unroll
+            for (int j = 0; j < UNR; ++j) {
+                const int r = r0 + j;
+                v[j] = 0.0f;
+                mk[j] = 0;
+                if (act && r < nrows) {
+                    const int64_t idx = ((int64_t)(ti.z0 + r / ti.ly) * g.Y + ti.y0 + r % ti.ly) * g.X + ti.x0 + lane;
+                    v[j] = in[idx];
+                    if (HAS_MASK) mk[j] = mask[idx];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < UNR; ++j) {
+                const int r = r0 + j;
+                f1((r / ti.ly) * TY + r % ti.ly, act && r < nrows, v[j], (u32)mk[j]);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_block_stats: per-block ordered min / max and NaN flag.  One workgroup per tile.
+// ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(NTHREADS) void k_block_stats(Geom g, const float* __restrict__ in,
                                                           u32* smin, u32* smax, u32* sflag) {
     __shared__ u32 red[3][NTHREADS / 64];
     const int64_t t = blockIdx.x;
     const TileInfo ti = tile_info(g, t);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int nrows = ti.lz * ti.ly;
     u32 mn = 0xFFFFFFFFu, mx = 0u;
     bool nan = false;
-    const bool act = lane < ti.lx;
-    for (int r0 = wave * UNR; r0 < nrows; r0 += (NTHREADS / 64) * UNR) {
-        float v[UNR];
-#pragma unroll
-        for (int j = 0; j < UNR; ++j) {
-            const int r = r0 + j;
-            v[j] = 0.0f;
-            if (act && r < nrows) {
-                const int z = ti.z0 + r / ti.ly, y = ti.y0 + r % ti.ly;
-                v[j] = in[((int64_t)z * g.Y + y) * g.X + ti.x0 + lane];
-            }
+    auto acc = [&](float x) {
+        if (x != x) nan = true;
+        else {
+            const u32 o = f2ord(__float_as_uint(x));
+            mn = o < mn ? o : mn;
+            mx = o > mx ? o : mx;
         }
-#pragma unroll
-        for (int j = 0; j < UNR; ++j) {
-            if (act && r0 + j < nrows) {
-                const float x = v[j];
-                if (x != x) nan = true;
-                else {
-                    const u32 o = f2ord(__float_as_uint(x));
-                    mn = o < mn ? o : mn;
-                    mx = o > mx ? o : mx;
-                }
-            }
-        }
-    }
+    };
+    for_tile_rows<false>(g, ti, in, nullptr,
+                  [&](int, int, bool act, float4 v, u32) { if (act) { acc(v.x); acc(v.y); acc(v.z); acc(v.w); } },
+                  [&](int, bool act, float v, u32) { if (act) acc(v); });
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const u32 a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
@@ -225,33 +342,30 @@ template <bool HAS_MASK>
 __device__ __forceinline__ void load_rows(const Geom& g, const TileInfo& ti, const float* __restrict__ in,
                                           const u8* __restrict__ mask, const BlockParam& p, float thr,
                                           int mode, u64* rows) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int nrows = ti.lz * ti.ly;
-    const bool act = lane < ti.lx;
-    for (int r0 = wave * UNR; r0 < nrows; r0 += (NTHREADS / 64) * UNR) {
-        float v[UNR];
-        u8 mk[UNR];
-#pragma unroll
-        for (int j = 0; j < UNR; ++j) {
-            const int r = r0 + j;
-            v[j] = 0.0f;
-            mk[j] = 0;
-            if (act && r < nrows) {
-                const int z = ti.z0 + r / ti.ly, y = ti.y0 + r % ti.ly;
-                const int64_t idx = ((int64_t)z * g.Y + y) * g.X + ti.x0 + lane;
-                v[j] = in[idx];
-                if (HAS_MASK) mk[j] = mask[idx];
+    const int lane = threadIdx.x & 63;
+    for_tile_rows<HAS_MASK>(g, ti, in, mask,
+        [&](int r, int i, bool act, float4 v, u32 mk) {
+            u32 nib = 0;
+            if (act) {
+                nib = (u32)voxel_pred(p, v.x, thr, mode) | ((u32)voxel_pred(p, v.y, thr, mode) << 1) |
+                      ((u32)voxel_pred(p, v.z, thr, mode) << 2) | ((u32)voxel_pred(p, v.w, thr, mode) << 3);
+                if (HAS_MASK)
+                    nib &= (u32)((mk & 0xFFu) != 0) | ((u32)((mk & 0xFF00u) != 0) << 1) |
+                           ((u32)((mk & 0xFF0000u) != 0) << 2) | ((u32)((mk & 0xFF000000u) != 0) << 3);
             }
-        }
-#pragma unroll
-        for (int j = 0; j < UNR; ++j) {
-            const int r = r0 + j;
-            bool fg = act && r < nrows && voxel_pred(p, v[j], thr, mode);
-            if (HAS_MASK) fg = fg && mk[j] != 0;
+            u64 w = (u64)nib << (4 * i);
+            w |= __shfl_xor(w, 1, 64);
+            w |= __shfl_xor(w, 2, 64);
+            w |= __shfl_xor(w, 4, 64);
+            w |= __shfl_xor(w, 8, 64);
+            if (i == 0 && r / TY < ti.lz && r % TY < ti.ly) rows[r] = w;
+        },
+        [&](int r, bool act, float v, u32 mk) {
+            bool fg = act && voxel_pred(p, v, thr, mode);
+            if (HAS_MASK) fg = fg && mk != 0;
             const u64 bal = __ballot(fg);
-            if (lane == 0 && r < nrows) rows[(r / ti.ly) * TY + (r % ti.ly)] = bal;
-        }
-    }
+            if (lane == 0 && act) rows[r] = bal;
+        });
 }
 
 // face plane entry i of a tile (see cc_common.hpp for the layout)
@@ -302,8 +416,10 @@ __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restr
     __shared__ u64 rows[NROWS];
     __shared__ u8 cm[NC];
     __shared__ u32 par[NC];
-    __shared__ u32 key[NC];
+    __shared__ u64 kn[NC / 2];          // nec masks during the CCL, then first-voxel keys
+    static_assert(NCROW * NDIR <= NC / 2, "nec does not fit the key buffer");
     __shared__ u32 scratch[8];
+    u32* key = reinterpret_cast<u32*>(kn);
     const int64_t t = blockIdx.x;
     const TileInfo ti = tile_info(g, t);
     const BlockParam p = bp[ti.block];
@@ -313,7 +429,7 @@ __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restr
     if (p.kind != BP_EMPTY) load_rows<HAS_MASK>(g, ti, in, mask, p, thr, mode, rows);
     __syncthreads();
     for (int i = tid; i < NROWS; i += NTHREADS) BITS[t * NROWS + i] = rows[i];
-    const u32 R = tile_ccl(rows, cm, par, scratch);
+    const u32 R = tile_ccl(rows, cm, par, kn, scratch);
     for (u32 k = tid; k < R; k += NTHREADS) key[k] = NONE;
     __syncthreads();
     for (int c = tid; c < NC; c += NTHREADS) {
@@ -344,9 +460,31 @@ __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restr
 //   INTER = true : seams on block faces, 6-connectivity (3 face directions).
 // Keys: first-voxel index (intra) or rid (inter); the union keeps the smaller key as root.
 // ------------------------------------------------------------------------------------------
+// LDS set of (node, node) pairs already sent to the global union-find by this workgroup: most
+// face-cube pairs of a seam connect the same two tile-local components.
+constexpr int HSET = 2048;
+
+__device__ __forceinline__ bool hset_insert(u64* hs, u64 key) {
+    u32 h = (u32)((key * 0x9E3779B97F4A7C15ull) >> 53) & (HSET - 1);
+#pragma unroll 1
+    for (int probe = 0; probe < 16; ++probe) {
+        const u64 old = atomicCAS((unsigned long long*)&hs[h], ~0ull, (unsigned long long)key);
+        if (old == ~0ull) return true;
+        if (old == key) return false;
+        h = (h + 1) & (HSET - 1);
+    }
+    return true;   // table crowded: do the (idempotent) union anyway
+}
+
 template <bool INTER>
 __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restrict__ FACES, u32* P,
                                                      const u64* __restrict__ K) {
+    __shared__ u64 hs[HSET];
+    for (int i = threadIdx.x; i < HSET; i += NTHREADS) hs[i] = ~0ull;
+    __syncthreads();
+    auto gunion = [&](u32* Pp, const u64* Kp, u32 a, u32 b) {
+        if (hset_insert(hs, ((u64)a << 32) | b)) cc::gunion(Pp, Kp, a, b);
+    };
     const int64_t t = blockIdx.x;
     const TileInfo ti = tile_info(g, t);
     const int tid = threadIdx.x;
@@ -558,31 +696,44 @@ __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restri
 // ------------------------------------------------------------------------------------------
 // block-local roots -> sort keys
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(NTHREADS) void k_collect_roots(Geom g, const u32* COUNT, u32* P, const u64* KEY,
-                                                            u64* keys, u32* vals, u32* counter) {
-    const int64_t t = blockIdx.x;
-    const u32 R = COUNT[t];
-    if (R == 0) return;
-    const TileInfo ti = tile_info(g, t);
-    const u32 base = (u32)(t * g.cap);
-    for (u32 k = threadIdx.x; k < R; k += NTHREADS) {
-        const u32 node = base + k;
-        if (P[node] == node) {
-            const u32 pos = atomicAdd(counter, 1u);
-            keys[pos] = ((u64)ti.block << KEY_BITS) | KEY[node];
-            vals[pos] = node;
-        }
-    }
-}
+// one wave per tile: tile t = blockIdx.x * WAVES + wave
+constexpr int WAVES = NTHREADS / 64;
 
-__global__ __launch_bounds__(NTHREADS) void k_count_roots(Geom g, const u32* COUNT, u32* P, u32* counter) {
-    const int64_t t = blockIdx.x;
+// block-local roots per tile (no atomics: counts, then an exclusive scan, then a collect that
+// writes each tile's roots at its scanned offset in node order)
+__global__ __launch_bounds__(NTHREADS) void k_count_roots(Geom g, const u32* COUNT, const u32* P, u32* RC) {
+    const int64_t t = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+    if (t >= g.n_tiles) return;
     const u32 R = COUNT[t];
-    if (R == 0) return;
     const u32 base = (u32)(t * g.cap);
     u32 n = 0;
-    for (u32 k = threadIdx.x; k < R; k += NTHREADS) n += (P[base + k] == base + k);
-    if (n) atomicAdd(counter, n);
+    for (u32 k = threadIdx.x & 63; k < R; k += 64) n += (P[base + k] == base + k);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+    if ((threadIdx.x & 63) == 0) RC[t] = n;
+}
+
+__global__ __launch_bounds__(NTHREADS) void k_collect_roots(Geom g, const u32* COUNT, const u32* P, const u64* KEY,
+                                                            const u32* ROFF, u64* keys, u32* vals) {
+    const int64_t t = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+    if (t >= g.n_tiles) return;
+    const u32 R = COUNT[t];
+    if (R == 0) return;
+    const int lane = threadIdx.x & 63;
+    const TileInfo ti = tile_info(g, t);
+    const u32 base = (u32)(t * g.cap);
+    u32 pos = ROFF[t];
+    for (u32 k0 = 0; k0 < R; k0 += 64) {
+        const u32 k = k0 + lane;
+        const bool is = k < R && P[base + k] == base + k;
+        const u64 bal = __ballot(is);
+        if (is) {
+            const u32 p = pos + (u32)__popcll(bal & ((1ull << lane) - 1));
+            keys[p] = ((u64)ti.block << KEY_BITS) | KEY[base + k];
+            vals[p] = base + k;
+        }
+        pos += (u32)__popcll(bal);
+    }
 }
 
 __global__ void k_segments(int64_t n, const u64* keys, u32* seg_start, u32* seg_end) {
@@ -600,8 +751,15 @@ __global__ void k_values(int64_t nb, const u32* seg_start, const u32* seg_end, u
     values[b] = n ? n + 1 : 0;                                // block_components.py:175-182
 }
 
+// scalars[0] = sum of block values (n_labels - 1 of this volume / slab), merge_offsets.py:120
 __global__ void k_nlabels(int64_t nb, const u64* values, const u64* offsets, u64* scalars) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) scalars[0] = offsets[nb - 1] + values[nb - 1] + 1;  // merge_offsets.py:120
+    if (threadIdx.x == 0 && blockIdx.x == 0) scalars[0] = offsets[nb - 1] + values[nb - 1];
+}
+
+// z-slab sharding: this slab's ids start at `base` (sum of the values of the slabs before it)
+__global__ void k_add_base(int64_t nb, u64* offsets, u64 base) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nb) offsets[b] += base;
 }
 
 __global__ void k_assign_rid(int64_t n, const u64* keys, const u32* vals, const u32* seg_start,
@@ -612,18 +770,33 @@ __global__ void k_assign_rid(int64_t n, const u64* keys, const u32* vals, const 
     KR[vals[i]] = offsets[b] + (u64)(i - seg_start[b]) + 1;   // skimage label = rank + 1
 }
 
-__global__ void k_lut_init(u64 cap, const u64* scalars, u64* lut) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < cap && i < scalars[0]) lut[i] = i;
+// Seam mapping (multi-GPU): sorted distinct ids U[m] and their merged representative V[m].
+__device__ __forceinline__ u64 apply_map(u64 v, const u64* U, const u64* V, int64_t m) {
+    if (m == 0) return v;
+    int64_t lo = 0, hi = m;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (U[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return (lo < m && U[lo] == v) ? V[lo] : v;
 }
 
-__global__ void k_lut(int64_t n, const u32* vals, u32* P, const u64* KR, u64* lut, u64* scalars) {
+// lut[i] = base + i for the ids of this volume (slab): i in [0, scalars[0]] (the last one is
+// the slack id n_labels - 1 on the last slab, merge_offsets.py:120)
+__global__ void k_lut_init(u64 cap, const u64* scalars, u64 base, u64* lut) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < cap && i <= scalars[0]) lut[i] = base + i;
+}
+
+__global__ void k_lut(int64_t n, const u32* vals, u32* P, const u64* KR, u64 base, const u64* U, const u64* V,
+                      int64_t m, u64* lut, u64* scalars) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u32 node = vals[i];
     const u32 r = gfind(P, node);
-    lut[KR[node]] = KR[r];
-    if (r == node) atomicAdd((unsigned long long*)&scalars[1], 1ull);   // distinct components
+    const u64 rep = apply_map(KR[r], U, V, m);
+    lut[KR[node] - base] = rep;
+    if (r == node && rep == KR[r]) atomicAdd((unsigned long long*)&scalars[1], 1ull);   // components owned here
 }
 
 // final label of every node.  FIN may alias KR when !LOCAL: roots keep their rid, so a
@@ -631,61 +804,148 @@ __global__ void k_lut(int64_t n, const u32* vals, u32* P, const u64* KR, u64* lu
 // block_components) writes the block-local skimage label rid - offset into a separate FIN.
 template <bool LOCAL>
 __global__ __launch_bounds__(NTHREADS) void k_finalize(Geom g, const u32* COUNT, u32* P, const u64* KR,
-                                                       const u64* offsets, u64* FIN) {
-    const int64_t t = blockIdx.x;
+                                                       const u64* offsets, const u64* U, const u64* V,
+                                                       int64_t m, u64* FIN) {
+    const int64_t t = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+    if (t >= g.n_tiles) return;
     const u32 R = COUNT[t];
     if (R == 0) return;
     const u32 base = (u32)(t * g.cap);
     u64 off = 0;
     if (LOCAL) off = offsets[tile_info(g, t).block];
-    for (u32 k = threadIdx.x; k < R; k += NTHREADS) {
+    for (u32 k = threadIdx.x & 63; k < R; k += 64) {
         const u32 node = base + k;
         const u64 v = KR[gfind(P, node)];
-        FIN[node] = LOCAL ? v - off : v;
+        FIN[node] = LOCAL ? v - off : apply_map(v, U, V, m);
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// z-slab seams (multi-GPU).  The bottom / top voxel plane of a slab as the current component
+// id of each voxel (0 = background), from the ZLO / ZHI face planes of the first / last tile
+// layer.  One workgroup per tile of that layer.
+// ------------------------------------------------------------------------------------------
+template <bool TOP>
+__global__ __launch_bounds__(NTHREADS) void k_plane_labels(Geom g, const u32* __restrict__ FACES, u32* P,
+                                                           const u64* __restrict__ KR, u64* plane) {
+    const int64_t t = (TOP ? (int64_t)(g.nt[0] - 1) * g.nt[1] * g.nt[2] : 0) + blockIdx.x;
+    const TileInfo ti = tile_info(g, t);
+    const u32* F = FACES + t * FACE_STRIDE + (TOP ? F_ZHI : F_ZLO);
+    const u32 base = (u32)(t * g.cap);
+    const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2;
+    for (int e = threadIdx.x; e < ncy * CX; e += NTHREADS) {
+        const int cy = e / CX, cx = e % CX;
+        if (cx >= ncx) continue;
+        const u32 a = F[e];
+        const u64 v = a ? KR[gfind(P, base + (a & 0xFFFFu))] : 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int y = 2 * cy + j, x = 2 * cx + i;
+                if (y < ti.ly && x < ti.lx)
+                    plane[(int64_t)(ti.y0 + y) * g.X + ti.x0 + x] = ((a >> (16 + j * 2 + i)) & 1) ? v : 0;
+            }
+    }
+}
+
+// pairs of ids facing each other across a seam (6-connectivity, block_faces.py:99-111)
+__global__ void k_seam_pairs(int64_t n, const u64* upper, const u64* lower, u64* pa, u64* pb,
+                             unsigned long long* counter, u64 cap) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u64 a = upper[i], b = lower[i];
+    if (!a || !b) return;
+    const unsigned long long pos = atomicAdd(counter, 1ull);
+    if (pos < cap) { pa[pos] = a; pb[pos] = b; }
+}
+
+// seam union-find over compact indices: pairs of ids -> indices into the sorted distinct ids
+__global__ void k_pairs_to_index(int64_t n, const u64* pairs, const u64* U, int64_t m, u64* ip) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 2 * n) return;
+    const u64 v = pairs[i];
+    int64_t lo = 0, hi = m;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (U[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    ip[i] = (u64)lo;
+}
+
+__global__ void k_map_values(int64_t m, const u64* U, const u64* root, u64* V) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) V[i] = U[root[i]];
 }
 
 // ------------------------------------------------------------------------------------------
 // k_pass2: recompute the tile CCL from the bit rows and write the uint64 labels
 // ------------------------------------------------------------------------------------------
-constexpr int LABCAP = 1024;
+constexpr int LABCAP = NCROW * NDIR;   // lab[] aliases the nec masks (used before it)
+
+// store the two voxels (x, x+1) of one cube row segment; 16-B store when aligned
+__device__ __forceinline__ void store2(u64* __restrict__ out, int64_t idx, u64 v0, u64 v1, bool two, bool vec) {
+    if (two && vec) {
+        *reinterpret_cast<ulonglong2*>(out + idx) = make_ulonglong2(v0, v1);
+    } else {
+        out[idx] = v0;
+        if (two) out[idx + 1] = v1;
+    }
+}
 
 __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restrict__ BITS, const u32* COUNT,
                                                     const u64* __restrict__ FIN, u64* __restrict__ out) {
     __shared__ u64 rows[NROWS];
     __shared__ u8 cm[NC];
     __shared__ u32 par[NC];
-    __shared__ u64 lab[LABCAP];
+    __shared__ u64 lab[LABCAP];          // nec masks during the CCL, then final labels
     __shared__ u32 scratch[8];
+    u64* nec = lab;
     const int64_t t = blockIdx.x;
     const TileInfo ti = tile_info(g, t);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x;
     const u32 R = COUNT[t];
-    const int nrows = ti.lz * ti.ly;
-    const bool act = lane < ti.lx;
+    const bool vec = ((ti.x0 | (int)(g.X & 1)) & 1) == 0;    // 16-B aligned pairs
+    const int ncz = (ti.lz + 1) / 2, ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2;
     if (R == 0) {
-        for (int r = wave; r < nrows; r += NTHREADS / 64) {
-            const int z = ti.z0 + r / ti.ly, y = ti.y0 + r % ti.ly;
-            if (act) out[((int64_t)z * g.Y + y) * g.X + ti.x0 + lane] = 0;
+        for (int c = tid; c < NC; c += NTHREADS) {
+            const int cz = c / (CY * CX), cy = (c / CX) % CY, cx = c % CX;
+            if (cz >= ncz || cy >= ncy || cx >= ncx) continue;
+            const bool two = 2 * cx + 1 < ti.lx;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const int z = 2 * cz + (d >> 1), y = 2 * cy + (d & 1);
+                if (z < ti.lz && y < ti.ly)
+                    store2(out, ((int64_t)(ti.z0 + z) * g.Y + ti.y0 + y) * g.X + ti.x0 + 2 * cx, 0, 0, two, vec);
+            }
         }
         return;
     }
     for (int i = tid; i < NROWS; i += NTHREADS) rows[i] = BITS[t * NROWS + i];
     __syncthreads();
-    tile_ccl(rows, cm, par, scratch);
+    tile_ccl(rows, cm, par, nec, scratch);
     const u32 base = (u32)(t * g.cap);
     for (u32 k = tid; k < R && k < LABCAP; k += NTHREADS) lab[k] = FIN[base + k];
     __syncthreads();
-    for (int r = wave; r < nrows; r += NTHREADS / 64) {
-        const int lzz = r / ti.ly, lyy = r % ti.ly;
-        const u64 bits = rows[lzz * TY + lyy];
-        if (!act) continue;
+    for (int c = tid; c < NC; c += NTHREADS) {
+        const int cz = c / (CY * CX), cy = (c / CX) % CY, cx = c % CX;
+        if (cz >= ncz || cy >= ncy || cx >= ncx) continue;
+        const u32 m = cm[c];
         u64 v = 0;
-        if ((bits >> lane) & 1) {
-            const u32 k = cube_k(par, ((lzz >> 1) * CY + (lyy >> 1)) * CX + (lane >> 1));
+        if (m) {
+            const u32 k = cube_k(par, c);
             v = k < LABCAP ? lab[k] : FIN[base + k];
         }
-        out[((int64_t)(ti.z0 + lzz) * g.Y + ti.y0 + lyy) * g.X + ti.x0 + lane] = v;
+        const bool two = 2 * cx + 1 < ti.lx;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {                 // (dz, dy) = (d >> 1, d & 1); bits 4dz + 2dy + dx
+            const int z = 2 * cz + (d >> 1), y = 2 * cy + (d & 1);
+            if (z < ti.lz && y < ti.ly) {
+                const u32 b = m >> (2 * d);
+                store2(out, ((int64_t)(ti.z0 + z) * g.Y + ti.y0 + y) * g.X + ti.x0 + 2 * cx,
+                       (b & 1) ? v : 0, (b & 2) ? v : 0, two, vec);
+            }
+        }
     }
 }
 
@@ -694,7 +954,9 @@ template __global__ void k_pass1<false>(Geom, const float*, const u8*, const Blo
 template __global__ void k_pass1<true>(Geom, const float*, const u8*, const BlockParam*, float, int, u64*, u32*, u32*, u32*, u64*);
 template __global__ void k_stitch<false>(Geom, const u32*, u32*, const u64*);
 template __global__ void k_stitch<true>(Geom, const u32*, u32*, const u64*);
-template __global__ void k_finalize<false>(Geom, const u32*, u32*, const u64*, const u64*, u64*);
-template __global__ void k_finalize<true>(Geom, const u32*, u32*, const u64*, const u64*, u64*);
+template __global__ void k_finalize<false>(Geom, const u32*, u32*, const u64*, const u64*, const u64*, const u64*, int64_t, u64*);
+template __global__ void k_finalize<true>(Geom, const u32*, u32*, const u64*, const u64*, const u64*, const u64*, int64_t, u64*);
+template __global__ void k_plane_labels<false>(Geom, const u32*, u32*, const u64*, u64*);
+template __global__ void k_plane_labels<true>(Geom, const u32*, u32*, const u64*, u64*);
 
 }  // namespace cc

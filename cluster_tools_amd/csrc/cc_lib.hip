@@ -65,8 +65,9 @@ struct cc_ctx {
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     // workspace
-    DevBuf tiles, bstat, bparam, bits, faces, count, P, KR, FIN, keys, keys2, vals, vals2, seg,
-        values, offsets, lut, cub_tmp, scalars, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2;
+    DevBuf tiles, bstat, bparam, bits, faces, count, rc, roff, P, KR, FIN, keys, keys2, vals, vals2, seg,
+        values, offsets, lut, cub_tmp, scalars, scalars2, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2,
+        flags, map_ids, map_ids2, map_vals, map_par;
     // last run
     int64_t n_blocks = 0;
     uint64_t n_labels = 0;
@@ -78,6 +79,7 @@ struct cc_ctx {
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, ProfEntry> prof_acc;
+    void* run = nullptr;     // RunState of the current labelling run
 };
 
 // ------------------------------------------------------------------------------------------
@@ -210,16 +212,38 @@ static int to_mode(int mode) {
 }
 
 // ------------------------------------------------------------------------------------------
-// the device pipeline
+// the device pipeline, in phases (single GPU: local -> rid(0) -> final; z-slab shards:
+// local -> [allgather of sums] -> rid(base) -> planes -> [seam exchange] -> map -> final)
 // ------------------------------------------------------------------------------------------
-// local_only: stop after block-local components and write skimage-numbered local labels.
-static void run_pipeline(cc_ctx* c, const float* in, const uint8_t* mask, const int64_t shape[3],
-                         const int64_t block_shape[3], double threshold, int mode, uint64_t* out,
-                         bool local_only, cc_result* res) {
-    HostGeom hg = make_geom(shape, block_shape, 0);
-    upload_geom(c, hg);
-    Geom& g = hg.g;
-    const float thr = (float)threshold;                 // numpy: python float -> float32
+struct RunState {
+    HostGeom hg;
+    float thr = 0.f;
+    int mode = 0;
+    int64_t nr = 0;            // block-local roots
+    uint64_t sum_v = 0;        // sum of block values of this volume / slab
+    uint64_t base = 0;         // global id base of this slab
+    int64_t n_map = 0;         // seam mapping size
+    bool local_only = false;
+    int stage = 0;             // 1 local done, 2 rid done, 3 final done
+};
+
+static RunState& state(cc_ctx* c) {
+    if (!c->run) c->run = new RunState();
+    return *(RunState*)c->run;
+}
+
+// stats -> params -> pass1 -> intra-block stitch -> roots -> sort -> offsets (local)
+static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const int64_t shape[3],
+                        const int64_t block_shape[3], double threshold, int mode, int64_t zoff,
+                        bool local_only) {
+    RunState& st = state(c);
+    st = RunState();
+    st.hg = make_geom(shape, block_shape, zoff);
+    upload_geom(c, st.hg);
+    Geom& g = st.hg.g;
+    st.thr = (float)threshold;                // numpy: python float -> float32
+    st.mode = mode;
+    st.local_only = local_only;
     const int64_t nt = g.n_tiles, nb = g.n_blocks;
     const uint64_t nodes = (uint64_t)nt * g.cap;
     hipStream_t s = c->stream;
@@ -235,7 +259,6 @@ static void run_pipeline(cc_ctx* c, const float* in, const uint8_t* mask, const 
     c->values.ensure(nb * sizeof(u64));
     c->offsets.ensure(nb * sizeof(u64));
     c->scalars.ensure(4 * sizeof(u64));
-    c->counter.ensure(sizeof(u32));
 
     u32* smin = c->bstat.as<u32>();
     u32* smax = smin + nb;
@@ -243,7 +266,6 @@ static void run_pipeline(cc_ctx* c, const float* in, const uint8_t* mask, const 
     HIP_OK(hipMemsetAsync(smin, 0xFF, nb * sizeof(u32), s));
     HIP_OK(hipMemsetAsync(smax, 0x00, 2 * nb * sizeof(u32), s));
     HIP_OK(hipMemsetAsync(c->scalars.p, 0, 4 * sizeof(u64), s));
-    HIP_OK(hipMemsetAsync(c->counter.p, 0, sizeof(u32), s));
 
     BlockParam* bp = c->bparam.as<BlockParam>();
     u64* BITS = c->bits.as<u64>();
@@ -251,6 +273,7 @@ static void run_pipeline(cc_ctx* c, const float* in, const uint8_t* mask, const 
     u32* COUNT = c->count.as<u32>();
     u32* P = c->P.as<u32>();
     u64* KR = c->KR.as<u64>();
+    const float thr = st.thr;
 
     launch(c, "k_block_stats", [&] { k_block_stats<<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, smin, smax, sflag); });
     launch(c, "k_block_params", [&] { k_block_params<<<grid1d(nb), 256, 0, s>>>(nb, smin, smax, sflag, thr, mode, bp); });
@@ -260,16 +283,27 @@ static void run_pipeline(cc_ctx* c, const float* in, const uint8_t* mask, const 
         launch(c, "k_pass1", [&] { k_pass1<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, nullptr, bp, thr, mode, BITS, FACES, COUNT, P, KR); });
     launch(c, "k_stitch_intra", [&] { k_stitch<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, FACES, P, KR); });
 
-    // block-local roots: count them, read the count back (the one mid-run host sync), size the
-    // sort buffers, then collect (block, first voxel) keys
-    u32* counter = c->counter.as<u32>();
-    u32 n_roots_h = 0;
+    // block-local roots: per-tile counts -> exclusive scan -> one host read of the total (the one
+    // mid-run host sync; it sizes the radix sort)
+    c->rc.ensure((nt + 1) * sizeof(u32));
+    c->roff.ensure((nt + 1) * sizeof(u32));
+    u32* RC = c->rc.as<u32>();
+    u32* ROFF = c->roff.as<u32>();
+    launch(c, "k_count_roots", [&] { k_count_roots<<<grid1d(nt, WAVES), NTHREADS, 0, s>>>(g, COUNT, P, RC); });
     {
-        launch(c, "k_count_roots", [&] { k_count_roots<<<(unsigned)nt, NTHREADS, 0, s>>>(g, COUNT, P, counter); });
-        HIP_OK(hipMemcpyAsync(&n_roots_h, counter, sizeof(u32), hipMemcpyDeviceToHost, s));
-        sync(c);
+        size_t tmp_bytes = 0;
+        HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, RC, ROFF, (int)nt + 1, s));
+        c->cub_tmp.ensure(tmp_bytes);
+        HIP_OK(hipMemsetAsync(RC + nt, 0, sizeof(u32), s));
+        launch(c, "scan_roots", [&] {
+            HIP_OK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, RC, ROFF, (int)nt + 1, s));
+        });
     }
+    u32 n_roots_h = 0;
+    HIP_OK(hipMemcpyAsync(&n_roots_h, ROFF + nt, sizeof(u32), hipMemcpyDeviceToHost, s));
+    sync(c);
     const int64_t nr = n_roots_h;
+    st.nr = nr;
     c->keys.ensure(std::max<int64_t>(1, nr) * sizeof(u64));
     c->keys2.ensure(std::max<int64_t>(1, nr) * sizeof(u64));
     c->vals.ensure(std::max<int64_t>(1, nr) * sizeof(u32));
@@ -285,8 +319,7 @@ static void run_pipeline(cc_ctx* c, const float* in, const uint8_t* mask, const 
     u64* scalars = c->scalars.as<u64>();
     HIP_OK(hipMemsetAsync(seg_start, 0, 2 * nb * sizeof(u32), s));
     if (nr > 0) {
-        HIP_OK(hipMemsetAsync(counter, 0, sizeof(u32), s));
-        launch(c, "k_collect_roots", [&] { k_collect_roots<<<(unsigned)nt, NTHREADS, 0, s>>>(g, COUNT, P, KR, keys, vals, counter); });
+        launch(c, "k_collect_roots", [&] { k_collect_roots<<<grid1d(nt, WAVES), NTHREADS, 0, s>>>(g, COUNT, P, KR, ROFF, keys, vals); });
         int end_bit = KEY_BITS;
         while ((1LL << (end_bit - KEY_BITS)) < nb) ++end_bit;
         size_t tmp_bytes = 0;
@@ -307,45 +340,180 @@ static void run_pipeline(cc_ctx* c, const float* in, const uint8_t* mask, const 
         });
     }
     launch(c, "k_nlabels", [&] { k_nlabels<<<1, 1, 0, s>>>(nb, values, offsets, scalars); });
-    if (nr > 0)
-        launch(c, "k_assign_rid", [&] { k_assign_rid<<<grid1d(nr), 256, 0, s>>>(nr, keys2, vals2, seg_start, offsets, KR); });
+    st.stage = 1;
+}
 
+static uint64_t read_sum_v(cc_ctx* c) {
+    u64 v = 0;
+    HIP_OK(hipMemcpyAsync(&v, c->scalars.p, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    state(c).sum_v = v;
+    return v;
+}
+
+// global ids: offsets += base; rank -> rid; 6-connected unions across block faces
+static void phase_rid(cc_ctx* c, uint64_t base) {
+    RunState& st = state(c);
+    CC_REQUIRE(st.stage == 1, "phase order: call begin first");
+    Geom& g = st.hg.g;
+    hipStream_t s = c->stream;
+    const int64_t nb = g.n_blocks, nr = st.nr, nt = g.n_tiles;
+    st.base = base;
+    u64* offsets = c->offsets.as<u64>();
+    if (base) launch(c, "k_add_base", [&] { k_add_base<<<grid1d(nb), 256, 0, s>>>(nb, offsets, base); });
+    if (nr > 0)
+        launch(c, "k_assign_rid", [&] {
+            k_assign_rid<<<grid1d(nr), 256, 0, s>>>(nr, c->keys2.as<u64>(), c->vals2.as<u32>(), c->seg.as<u32>(),
+                                                    offsets, c->KR.as<u64>());
+        });
+    if (!st.local_only)
+        launch(c, "k_stitch_inter", [&] { k_stitch<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->faces.as<u32>(), c->P.as<u32>(), c->KR.as<u64>()); });
+    st.n_map = 0;
+    st.stage = 2;
+}
+
+// seam planes of a slab (bottom: first voxel plane, top: last), Y*X ids each
+static void phase_planes(cc_ctx* c, uint64_t* bottom, uint64_t* top) {
+    RunState& st = state(c);
+    CC_REQUIRE(st.stage == 2 && !st.local_only, "phase order: call assign first");
+    Geom& g = st.hg.g;
+    hipStream_t s = c->stream;
+    const unsigned nlayer = (unsigned)((int64_t)g.nt[1] * g.nt[2]);
+    if (bottom)
+        launch(c, "k_plane_labels", [&] { k_plane_labels<false><<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<u32>(), c->P.as<u32>(), c->KR.as<u64>(), bottom); });
+    if (top)
+        launch(c, "k_plane_labels", [&] { k_plane_labels<true><<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<u32>(), c->P.as<u32>(), c->KR.as<u64>(), top); });
+}
+
+// sort (a, b) pairs lexicographically and drop duplicates; pa/pb are inputs (clobbered),
+// results in qa/qb; returns the number of unique pairs (host sync)
+static int64_t dedup_pairs(cc_ctx* c, u64* pa, u64* pb, u64* qa, u64* qb, int64_t n) {
+    hipStream_t s = c->stream;
+    if (n == 0) return 0;
+    size_t tb = 0;
+    HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, pb, qb, pa, qa, (int)n, 0, 64, s));
+    c->cub_tmp.ensure(tb);
+    HIP_OK(hipcub::DeviceRadixSort::SortPairs(c->cub_tmp.p, tb, pb, qb, pa, qa, (int)n, 0, 64, s));
+    HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, qa, pa, qb, pb, (int)n, 0, 64, s));
+    c->cub_tmp.ensure(tb);
+    HIP_OK(hipcub::DeviceRadixSort::SortPairs(c->cub_tmp.p, tb, qa, pa, qb, pb, (int)n, 0, 64, s));
+    c->flags.ensure(n + 16);
+    u8* flags = c->flags.as<u8>();
+    k_unique_flags<<<grid1d(n), 256, 0, s>>>(n, pa, pb, flags);
+    HIP_OK(hipGetLastError());
+    c->scalars2.ensure(16);
+    int* nsel = (int*)c->scalars2.p;
+    HIP_OK(hipcub::DeviceSelect::Flagged(nullptr, tb, pa, flags, qa, nsel, (int)n, s));
+    c->cub_tmp.ensure(tb);
+    HIP_OK(hipcub::DeviceSelect::Flagged(c->cub_tmp.p, tb, pa, flags, qa, nsel, (int)n, s));
+    HIP_OK(hipcub::DeviceSelect::Flagged(c->cub_tmp.p, tb, pb, flags, qb, nsel, (int)n, s));
+    int nu = 0;
+    HIP_OK(hipMemcpyAsync(&nu, nsel, sizeof(int), hipMemcpyDeviceToHost, s));
+    sync(c);
+    return nu;
+}
+
+// replicated union-find over the seam pairs of all slabs -> sorted id -> representative map
+static void phase_map(cc_ctx* c, const u64* pairs, int64_t n) {
+    RunState& st = state(c);
+    CC_REQUIRE(st.stage == 2, "phase order");
+    hipStream_t s = c->stream;
+    st.n_map = 0;
+    if (n <= 0) return;
+    // distinct ids
+    c->map_ids.ensure(2 * n * sizeof(u64));
+    c->map_ids2.ensure(2 * n * sizeof(u64));
+    u64* ids = c->map_ids.as<u64>();
+    u64* ids2 = c->map_ids2.as<u64>();
+    HIP_OK(hipMemcpyAsync(ids, pairs, 2 * n * sizeof(u64), hipMemcpyDeviceToDevice, s));
+    size_t tb = 0;
+    HIP_OK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, ids, ids2, (int)(2 * n), 0, 64, s));
+    c->cub_tmp.ensure(tb);
+    HIP_OK(hipcub::DeviceRadixSort::SortKeys(c->cub_tmp.p, tb, ids, ids2, (int)(2 * n), 0, 64, s));
+    c->scalars2.ensure(16);
+    int* nsel = (int*)c->scalars2.p;
+    HIP_OK(hipcub::DeviceSelect::Unique(nullptr, tb, ids2, ids, nsel, (int)(2 * n), s));
+    c->cub_tmp.ensure(tb);
+    HIP_OK(hipcub::DeviceSelect::Unique(c->cub_tmp.p, tb, ids2, ids, nsel, (int)(2 * n), s));
+    int m = 0;
+    HIP_OK(hipMemcpyAsync(&m, nsel, sizeof(int), hipMemcpyDeviceToHost, s));
+    sync(c);
+    // U = ids[0:m]; index pairs; union-find (smallest index = smallest id) -> V
+    c->map_vals.ensure(std::max<int64_t>(1, m) * sizeof(u64));
+    u64* ip = ids2;    // 2n indices
+    launch(c, "k_pairs_to_index", [&] { k_pairs_to_index<<<grid1d(2 * n), 256, 0, s>>>(n, pairs, ids, m, ip); });
+    c->map_par.ensure(std::max<int64_t>(1, m) * sizeof(u64));
+    u64* par = c->map_par.as<u64>();
+    c->counter.ensure(sizeof(u32));
+    HIP_OK(hipMemsetAsync(c->counter.p, 0, sizeof(u32), s));
+    launch(c, "k_iota64", [&] { k_iota64<<<grid1d(m), 256, 0, s>>>((u64)m, par); });
+    launch(c, "k_union_pairs", [&] { k_union_pairs<<<grid1d(n), 256, 0, s>>>(n, ip, (u64)m, par, c->counter.as<u32>()); });
+    launch(c, "k_resolve64", [&] { k_resolve64<<<grid1d(m), 256, 0, s>>>((u64)m, par); });
+    launch(c, "k_map_values", [&] { k_map_values<<<grid1d(m), 256, 0, s>>>(m, ids, par, c->map_vals.as<u64>()); });
+    st.n_map = m;
+}
+
+// LUT, final label per node, bit rows -> uint64 labels; small artefacts to host
+static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
+    RunState& st = state(c);
+    CC_REQUIRE(st.stage == 2, "phase order: call assign first");
+    Geom& g = st.hg.g;
+    hipStream_t s = c->stream;
+    const int64_t nt = g.n_tiles, nb = g.n_blocks, nr = st.nr;
+    const uint64_t nodes = (uint64_t)nt * g.cap;
+    u32* P = c->P.as<u32>();
+    u64* KR = c->KR.as<u64>();
+    u32* COUNT = c->count.as<u32>();
+    u64* offsets = c->offsets.as<u64>();
+    u64* scalars = c->scalars.as<u64>();
+    const u64* U = st.n_map ? c->map_ids.as<u64>() : nullptr;
+    const u64* V = st.n_map ? c->map_vals.as<u64>() : nullptr;
+    const int64_t m = st.n_map;
     u64* FIN = KR;
     const uint64_t lut_cap = (uint64_t)nr + (uint64_t)nb + 1;
-    if (local_only) {
+    if (st.local_only) {
         c->FIN.ensure(nodes * sizeof(u64));
         FIN = c->FIN.as<u64>();
-        launch(c, "k_finalize", [&] { k_finalize<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, COUNT, P, KR, offsets, FIN); });
+        launch(c, "k_finalize", [&] { k_finalize<true><<<grid1d(nt, WAVES), NTHREADS, 0, s>>>(g, COUNT, P, KR, offsets, U, V, m, FIN); });
         c->lut_valid = false;
     } else {
-        launch(c, "k_stitch_inter", [&] { k_stitch<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, FACES, P, KR); });
         c->lut.ensure(lut_cap * sizeof(u64));
         u64* lut = c->lut.as<u64>();
-        launch(c, "k_lut_init", [&] { k_lut_init<<<grid1d(lut_cap), 256, 0, s>>>(lut_cap, scalars, lut); });
+        const u64 base = st.base;
+        launch(c, "k_lut_init", [&] { k_lut_init<<<grid1d(lut_cap), 256, 0, s>>>(lut_cap, scalars, base, lut); });
         if (nr > 0)
-            launch(c, "k_lut", [&] { k_lut<<<grid1d(nr), 256, 0, s>>>(nr, vals2, P, KR, lut, scalars); });
-        launch(c, "k_finalize", [&] { k_finalize<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, COUNT, P, KR, offsets, KR); });
+            launch(c, "k_lut", [&] { k_lut<<<grid1d(nr), 256, 0, s>>>(nr, c->vals2.as<u32>(), P, KR, base, U, V, m, lut, scalars); });
+        launch(c, "k_finalize", [&] { k_finalize<false><<<grid1d(nt, WAVES), NTHREADS, 0, s>>>(g, COUNT, P, KR, offsets, U, V, m, KR); });
         c->lut_valid = true;
     }
-    launch(c, "k_pass2", [&] { k_pass2<<<(unsigned)nt, NTHREADS, 0, s>>>(g, BITS, COUNT, FIN, out); });
+    launch(c, "k_pass2", [&] { k_pass2<<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, FIN, out); });
 
-    // small artefacts back to host
     u64 sc[4] = {0, 0, 0, 0};
     HIP_OK(hipMemcpyAsync(sc, scalars, 4 * sizeof(u64), hipMemcpyDeviceToHost, s));
     c->h_values.resize(nb);
     c->h_offsets.resize(nb);
-    HIP_OK(hipMemcpyAsync(c->h_values.data(), values, nb * sizeof(u64), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(c->h_values.data(), c->values.p, nb * sizeof(u64), hipMemcpyDeviceToHost, s));
     HIP_OK(hipMemcpyAsync(c->h_offsets.data(), offsets, nb * sizeof(u64), hipMemcpyDeviceToHost, s));
     sync(c);
+    st.sum_v = sc[0];
+    st.stage = 3;
     c->n_blocks = nb;
-    c->n_labels = sc[0];
+    c->n_labels = sc[0] + 1;        // LUT length of this volume (slab): ids base .. base + sum_v
     if (res) {
         res->n_blocks = nb;
-        res->n_labels = sc[0];
-        res->max_id = sc[0] - 1;    // lut[n_labels-1] = n_labels-1 is never merged (write.py:283)
-        res->n_components = local_only ? 0 : sc[1];
+        res->n_labels = st.base + sc[0] + 1;   // global on the last slab / single GPU
+        res->max_id = res->n_labels - 1;       // lut[n_labels-1] = n_labels-1 is never merged
+        res->n_components = st.local_only ? 0 : sc[1];
         res->n_block_components = (uint64_t)nr;
     }
+}
+
+static void run_pipeline(cc_ctx* c, const float* in, const uint8_t* mask, const int64_t shape[3],
+                         const int64_t block_shape[3], double threshold, int mode, uint64_t* out,
+                         bool local_only, cc_result* res) {
+    phase_local(c, in, mask, shape, block_shape, threshold, mode, 0, local_only);
+    phase_rid(c, 0);
+    phase_final(c, out, res);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -388,14 +556,16 @@ void cc_destroy(cc_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->tiles, &c->bstat, &c->bparam, &c->bits, &c->faces, &c->count, &c->P, &c->KR,
+    DevBuf* bufs[] = {&c->tiles, &c->bstat, &c->bparam, &c->bits, &c->faces, &c->count, &c->rc, &c->roff, &c->P, &c->KR,
                       &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
                       &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
-                      &c->out_tmp, &c->pairs, &c->pairs2};
+                      &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
+                      &c->map_ids2, &c->map_vals, &c->map_par};
     for (DevBuf* b : bufs) b->release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete (RunState*)c->run;
     delete c;
 }
 

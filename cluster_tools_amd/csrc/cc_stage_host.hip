@@ -45,27 +45,8 @@ int64_t cc_block_faces(cc_ctx* c, const uint64_t* labels, const int64_t shape[3]
         sync(c);
         const int64_t n = (int64_t)n_raw;
         if (n == 0) return 0;
-        // lexicographic sort: by b, then stably by a (block_faces.py:112,132,172 np.unique(axis=0))
-        size_t tb = 0;
-        HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, pb, qb, pa, qa, (int)n, 0, 64, s));
-        c->cub_tmp.ensure(tb);
-        HIP_OK(hipcub::DeviceRadixSort::SortPairs(c->cub_tmp.p, tb, pb, qb, pa, qa, (int)n, 0, 64, s));
-        HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, qa, pa, qb, pb, (int)n, 0, 64, s));
-        c->cub_tmp.ensure(tb);
-        HIP_OK(hipcub::DeviceRadixSort::SortPairs(c->cub_tmp.p, tb, qa, pa, qb, pb, (int)n, 0, 64, s));
-        // pa, pb sorted lexicographically; unique
-        c->FIN.ensure(n * sizeof(u8) + 16);
-        u8* flags = c->FIN.as<u8>();
-        k_unique_flags<<<grid1d(n), 256, 0, s>>>(n, pa, pb, flags);
-        HIP_OK(hipGetLastError());
-        int* nsel = (int*)c->scalars.p;
-        HIP_OK(hipcub::DeviceSelect::Flagged(nullptr, tb, pa, flags, qa, nsel, (int)n, s));
-        c->cub_tmp.ensure(tb);
-        HIP_OK(hipcub::DeviceSelect::Flagged(c->cub_tmp.p, tb, pa, flags, qa, nsel, (int)n, s));
-        HIP_OK(hipcub::DeviceSelect::Flagged(c->cub_tmp.p, tb, pb, flags, qb, nsel, (int)n, s));
-        int nu = 0;
-        HIP_OK(hipMemcpyAsync(&nu, nsel, sizeof(int), hipMemcpyDeviceToHost, s));
-        sync(c);
+        // lexicographic sort + unique (block_faces.py:112,132,172 np.unique(axis=0))
+        const int64_t nu = dedup_pairs(c, pa, pb, qa, qb, n);
         if (pairs_host && cap > 0) {
             const int64_t m = std::min<int64_t>(cap, nu);
             std::vector<u64> ha(m), hb(m);
@@ -155,6 +136,85 @@ int cc_generate_boundary_map(cc_ctx* c, float* out, const int64_t shape[3], cons
             k_generate<<<grid, 256, 0, c->stream>>>(out, shape[0], shape[1], shape[2], o[0], o[1], o[2], seed);
         });
         sync(c);
+    })
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// z-slab sharding (multi-GPU): see cluster_tools_amd/distributed.py for the collective schedule
+// ---------------------------------------------------------------------------------------------
+extern "C" {
+
+int cc_shard_begin(cc_ctx* c, const float* in, const uint8_t* mask, const int64_t slab_shape[3],
+                   const int64_t block_shape[3], double threshold, int mode, int64_t z_offset,
+                   uint64_t* sum_values) {
+    CC_TRY({
+        CC_REQUIRE(c && in && slab_shape && block_shape && sum_values, "NULL argument");
+        CC_REQUIRE(z_offset >= 0 && z_offset % block_shape[0] == 0,
+                   "slab z offset must be a multiple of block_shape[0] (seams on block faces)");
+        HIP_OK(hipSetDevice(c->device));
+        phase_local(c, in, mask, slab_shape, block_shape, threshold, to_mode(mode), z_offset, false);
+        *sum_values = read_sum_v(c);
+    })
+}
+
+int cc_shard_assign(cc_ctx* c, uint64_t id_base) {
+    CC_TRY({
+        CC_REQUIRE(c, "NULL ctx");
+        HIP_OK(hipSetDevice(c->device));
+        phase_rid(c, id_base);
+    })
+}
+
+int cc_shard_planes(cc_ctx* c, uint64_t* bottom, uint64_t* top) {
+    CC_TRY({
+        CC_REQUIRE(c, "NULL ctx");
+        HIP_OK(hipSetDevice(c->device));
+        phase_planes(c, bottom, top);
+        sync(c);
+    })
+}
+
+int64_t cc_seam_pairs(cc_ctx* c, const uint64_t* upper, const uint64_t* lower, int64_t n, uint64_t* pairs,
+                      int64_t cap) {
+    try {
+        CC_REQUIRE(c && upper && lower && n >= 0, "bad arguments");
+        HIP_OK(hipSetDevice(c->device));
+        hipStream_t s = c->stream;
+        const int64_t capn = std::max<int64_t>(1, n);
+        c->pairs.ensure(2 * capn * sizeof(u64));
+        c->pairs2.ensure(2 * capn * sizeof(u64));
+        c->counter.ensure(sizeof(unsigned long long));
+        u64* pa = c->pairs.as<u64>();
+        u64* pb = pa + capn;
+        u64* qa = c->pairs2.as<u64>();
+        u64* qb = qa + capn;
+        unsigned long long* cnt = (unsigned long long*)c->counter.p;
+        HIP_OK(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), s));
+        launch(c, "k_seam_pairs", [&] { k_seam_pairs<<<grid1d(n), 256, 0, s>>>(n, upper, lower, pa, pb, cnt, (u64)capn); });
+        unsigned long long n_raw = 0;
+        HIP_OK(hipMemcpyAsync(&n_raw, cnt, sizeof(n_raw), hipMemcpyDeviceToHost, s));
+        sync(c);
+        const int64_t nu = dedup_pairs(c, pa, pb, qa, qb, (int64_t)n_raw);
+        if (pairs && cap > 0 && nu > 0) {
+            const int64_t m = std::min<int64_t>(cap, nu);
+            launch(c, "k_interleave", [&] { k_interleave<<<grid1d(m), 256, 0, s>>>(m, qa, qb, pairs); });
+            sync(c);
+        }
+        return nu;
+    } catch (const CCError& e) {
+        g_err = e.msg;
+        return -1;
+    }
+}
+
+int cc_shard_finish(cc_ctx* c, const uint64_t* pairs, int64_t n_pairs, uint64_t* labels, cc_result* res) {
+    CC_TRY({
+        CC_REQUIRE(c && labels && n_pairs >= 0 && (n_pairs == 0 || pairs), "bad arguments");
+        HIP_OK(hipSetDevice(c->device));
+        phase_map(c, pairs, n_pairs);
+        phase_final(c, labels, res);
     })
 }
 

@@ -36,6 +36,13 @@ __global__ void k_face_pairs(int axis, int64_t Z, int64_t Y, int64_t X, int64_t 
     (void)nbz;
 }
 
+__global__ void k_interleave(int64_t n, const u64* a, const u64* b, u64* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[2 * i] = a[i];
+    out[2 * i + 1] = b[i];
+}
+
 __global__ void k_unique_flags(int64_t n, const u64* a, const u64* b, u8* flags) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;

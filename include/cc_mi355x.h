@@ -120,6 +120,30 @@ int cc_write(cc_ctx* ctx, uint64_t* labels_dev, const int64_t shape[3],
              const int64_t block_shape[3], const uint64_t* offsets_host,
              const uint64_t* lut_host, uint64_t n_labels);
 
+/* --- z-slab sharding (multi-GPU, one process and one cc_ctx per GPU) ----------------------
+ * The volume is split along z at block faces; rank r labels slab r.  Collective schedule
+ * (cluster_tools_amd/distributed.py, RCCL over xGMI):
+ *   cc_shard_begin   local stages up to the per-slab block offsets; returns the slab's sum of
+ *                    block values (merge_offsets.py:115-120 restricted to the slab)
+ *   [allgather of the sums -> id_base = sum over the slabs below]
+ *   cc_shard_assign  global ids (offsets + id_base) and the slab's 6-connected block-face unions
+ *   cc_shard_planes  bottom / top voxel planes as component ids (Y*X uint64 each, NULL = skip)
+ *   [send top plane to rank r+1; rank r+1 forms the seam pairs with cc_seam_pairs;
+ *    allgather of all seam pairs]
+ *   cc_shard_finish  replicated union-find over all seam pairs, LUT, final labels.
+ * cc_get_lut then returns the slab's part of the LUT (ids id_base .. id_base + sum). */
+int cc_shard_begin(cc_ctx* ctx, const float* in_dev, const uint8_t* mask_dev,
+                   const int64_t slab_shape[3], const int64_t block_shape[3], double threshold,
+                   int mode, int64_t z_offset, uint64_t* sum_values);
+int cc_shard_assign(cc_ctx* ctx, uint64_t id_base);
+int cc_shard_planes(cc_ctx* ctx, uint64_t* bottom_dev, uint64_t* top_dev);
+/* unique (upper[i], lower[i]) pairs with both non-zero, sorted; writes min(cap, count) pairs
+ * ([n][2] uint64, device) and returns the count */
+int64_t cc_seam_pairs(cc_ctx* ctx, const uint64_t* upper_dev, const uint64_t* lower_dev, int64_t n,
+                      uint64_t* pairs_dev, int64_t cap);
+int cc_shard_finish(cc_ctx* ctx, const uint64_t* pairs_dev, int64_t n_pairs, uint64_t* labels_dev,
+                    cc_result* res);
+
 /* --- synthetic benchmark input (oracle/synth.py is its restatement) --- */
 int cc_generate_boundary_map(cc_ctx* ctx, float* out_dev, const int64_t shape[3],
                              const int64_t origin[3], uint64_t seed);

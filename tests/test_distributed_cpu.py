@@ -1,0 +1,111 @@
+"""The z-slab schedule of cluster_tools_amd/distributed.py (collectives, id bases, seam exchange,
+pair padding) over torch.distributed 'gloo' with world_size 2 and 3, on CPU.
+
+The per-slab device work is stood in for by an oracle-backed fake context with the same
+shard_* interface (the GPU implementation of those entry points is tested in
+tests/test_gpu_sharded.py); the final labels must equal the oracle on the whole volume."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import oracle as O
+
+
+class FakeShardCtx:
+    def shard_begin(self, x, block_shape, threshold, mode, z0, mask=None):
+        r = O.label_volume(x.numpy(), block_shape, threshold, mode,
+                           None if mask is None else mask.numpy())
+        self.lab = r['labels'].astype(np.int64)
+        return r['n_labels'] - 1
+
+    def shard_assign(self, base):
+        self.lab[self.lab != 0] += base
+
+    def shard_planes(self, bottom=None, top=None):
+        if bottom is not None:
+            bottom.copy_(torch.from_numpy(self.lab[0]))
+        if top is not None:
+            top.copy_(torch.from_numpy(self.lab[-1]))
+
+    def seam_pairs(self, upper, lower, pairs):
+        a, b = upper.numpy().ravel(), lower.numpy().ravel()
+        keep = (a != 0) & (b != 0)
+        p = np.unique(np.stack([a[keep], b[keep]], axis=1), axis=0) if keep.any() else np.zeros((0, 2), np.int64)
+        pairs[:len(p)] = torch.from_numpy(p)
+        return len(p)
+
+    def shard_finish(self, allp, n, out):
+        mapping = {}
+        if n:
+            p = allp[:n].numpy()
+            ids = np.unique(p)
+            par = {int(i): int(i) for i in ids}
+
+            def find(v):
+                while par[v] != v:
+                    par[v] = par[par[v]]
+                    v = par[v]
+                return v
+            for a, b in p:
+                ra, rb = find(int(a)), find(int(b))
+                if ra != rb:
+                    par[max(ra, rb)] = min(ra, rb)
+            mapping = {i: find(i) for i in par}
+        flat = self.lab.ravel()
+        res = np.array([mapping.get(int(v), int(v)) for v in flat], dtype=np.int64).reshape(self.lab.shape)
+        out.copy_(torch.from_numpy(res))
+        return {'n_components': 0}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, shape, block_shape, thr, mode, result_dir):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from cluster_tools_amd.distributed import ShardedLabeler, TorchComm, slab_bounds
+    x = O.boundary_map(shape, n_threads=1)
+    z0, zs = slab_bounds(shape[0], block_shape[0], world)[rank]
+    lab = ShardedLabeler(FakeShardCtx(), shape, block_shape, z0, zs, device=None,
+                         comm=TorchComm(device=None))
+    out = torch.empty((zs,) + tuple(shape[1:]), dtype=torch.int64)
+    res = lab.label(torch.from_numpy(x[z0:z0 + zs].copy()), thr, mode, out=out)
+    np.save(os.path.join(result_dir, 'slab_%d.npy' % rank), out.numpy())
+    np.save(os.path.join(result_dir, 'nl_%d.npy' % rank), np.array([res['n_labels'], res['id_base']]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,shape,block_shape,mode', [
+    (2, (32, 70, 90), (16, 32, 32), 'greater'),
+    (2, (32, 70, 90), (8, 40, 48), 'less'),
+    (3, (40, 64, 64), (8, 32, 32), 'less'),
+])
+def test_gloo_sharded_schedule_matches_oracle(tmp_path, world, shape, block_shape, mode):
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, shape, block_shape, 0.5, mode, str(tmp_path)), nprocs=world, join=True)
+    got = np.concatenate([np.load(str(tmp_path / ('slab_%d.npy' % r))) for r in range(world)]).astype(np.uint64)
+    ref = O.label_volume(O.boundary_map(shape, n_threads=1), block_shape, 0.5, mode)
+    np.testing.assert_array_equal(got, ref['labels'])
+    for r in range(world):
+        assert int(np.load(str(tmp_path / ('nl_%d.npy' % r)))[0]) == ref['n_labels']
+
+
+def test_slab_bounds():
+    from cluster_tools_amd.distributed import slab_bounds, check_slabs
+    b = slab_bounds(1024, 64, 8)
+    assert b == [(128 * r, 128) for r in range(8)]
+    b = slab_bounds(125, 50, 2)
+    assert b == [(0, 100), (100, 25)]
+    for z0, zs in b:
+        check_slabs((125, 10, 10), (50, 10, 10), z0, zs)
+    with pytest.raises(ValueError):
+        check_slabs((128, 4, 4), (64, 4, 4), 32, 64)
