@@ -1,0 +1,81 @@
+"""Volume helpers of the hot path (cluster_tools/utils/volume_utils.py:21-77,187-236).
+
+file_reader opens N5 containers with cluster_tools_amd.n5 (the reference uses elf/z5py)."""
+import json
+import os
+
+import numpy as np
+
+from .. import n5
+
+
+def file_reader(path, mode='a'):
+    return n5.open_file(path, mode)
+
+
+def get_shape(path, key):
+    with file_reader(path, 'r') as f:
+        return f[key].shape
+
+
+class Block:
+    def __init__(self, begin, end):
+        self.begin = list(begin)
+        self.end = list(end)
+        self.shape = [e - b for b, e in zip(begin, end)]
+
+
+class Blocking:
+    """nifty.tools.blocking: regular grid from roiBegin, C-order block ids, edge blocks cut."""
+
+    def __init__(self, roi_begin, roi_end, block_shape):
+        self.roiBegin, self.roiEnd = list(roi_begin), list(roi_end)
+        self.blockShape = list(block_shape)
+        self.blocksPerAxis = [-(-(e - b) // s) for b, e, s in zip(self.roiBegin, self.roiEnd, self.blockShape)]
+        self.numberOfBlocks = int(np.prod(self.blocksPerAxis))
+
+    def getBlock(self, block_id):
+        c = np.unravel_index(block_id, self.blocksPerAxis)
+        beg = [rb + int(ci) * s for rb, ci, s in zip(self.roiBegin, c, self.blockShape)]
+        end = [min(b + s, re) for b, s, re in zip(beg, self.blockShape, self.roiEnd)]
+        return Block(beg, end)
+
+    def getNeighborId(self, block_id, axis, lower):
+        c = list(np.unravel_index(block_id, self.blocksPerAxis))
+        c[axis] += -1 if lower else 1
+        if c[axis] < 0 or c[axis] >= self.blocksPerAxis[axis]:
+            return -1
+        return int(np.ravel_multi_index(c, self.blocksPerAxis))
+
+
+def blocking(roi_begin, roi_end, block_shape):
+    return Blocking(roi_begin, roi_end, block_shape)
+
+
+def blocks_in_volume(shape, block_shape, roi_begin=None, roi_end=None, block_list_path=None,
+                     return_blocking=False):
+    """cluster_tools/utils/volume_utils.py:31-73.  A ROI is rejected: the reference's
+    merge_offsets indexes offsets by rank but block_faces/write index them by block id, so
+    ROI runs are inconsistent upstream."""
+    assert len(shape) == len(block_shape)
+    if roi_begin is not None or roi_end is not None:
+        raise NotImplementedError('roi_begin/roi_end are not supported on the thresholded-components path')
+    b = Blocking([0] * len(shape), list(shape), list(block_shape))
+    block_list = list(range(b.numberOfBlocks))
+    if block_list_path is not None:
+        with open(block_list_path) as f:
+            block_list = json.load(f)
+    return (block_list, b) if return_blocking else block_list
+
+
+def block_to_bb(block):
+    return tuple(slice(beg, end) for beg, end in zip(block.begin, block.end))
+
+
+def load_mask(mask_path, mask_key, shape):
+    """volume_utils.py:174-184 for a full-resolution mask (resized masks are rejected)."""
+    ds = file_reader(mask_path, 'r')[mask_key]
+    if tuple(ds.shape) != tuple(shape):
+        raise NotImplementedError('mask shape %s != volume shape %s (ResizedVolume not supported)'
+                                  % (ds.shape, shape))
+    return ds

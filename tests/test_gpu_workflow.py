@@ -1,0 +1,99 @@
+"""ThresholdedComponentsWorkflow end to end through the task API on N5 (the drop-in path), and
+the five stage tasks run one by one (like test/thresholded_components/thresholded_components.py
+of the reference), against the golden vectors made by the reference's own job functions."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(tmp_path, name, block_shape):
+    from cluster_tools_amd import n5
+    from cluster_tools_amd.cluster_tasks import BaseClusterTask
+    d = load_golden(name)
+    data = str(tmp_path / 'data.n5')
+    with n5.open_file(data) as f:
+        f.create_dataset('volumes/boundaries', data=d['input'], chunks=(8, 32, 32), compression='gzip')
+        if 'mask' in d:
+            f.create_dataset('volumes/mask', data=d['mask'], chunks=(8, 32, 32), compression='gzip')
+    cfg = str(tmp_path / 'config')
+    os.makedirs(cfg)
+    g = BaseClusterTask.default_global_config()
+    g['block_shape'] = list(block_shape)
+    with open(os.path.join(cfg, 'global.config'), 'w') as f:
+        json.dump(g, f)
+    return d, data, cfg
+
+
+@pytest.mark.parametrize('name', ['bmap_greater', 'bmap_less', 'bmap_mask', 'noise_tiny_blocks'])
+def test_workflow_fused(tmp_path, name):
+    from cluster_tools_amd import luigi_compat as luigi, n5
+    from cluster_tools_amd.thresholded_components import ThresholdedComponentsWorkflow
+    from conftest import golden_index
+    meta = golden_index()[name]
+    d, data, cfg = _setup(tmp_path, name, meta['block_shape'])
+    kw = {}
+    if 'mask' in d:
+        kw = dict(mask_path=data, mask_key='volumes/mask')
+    t = ThresholdedComponentsWorkflow(tmp_folder=str(tmp_path / 'tmp'), config_dir=cfg, target='local', max_jobs=4,
+                                      input_path=data, input_key='volumes/boundaries', output_path=data,
+                                      output_key='data', assignment_key='assignments',
+                                      threshold=float(d['threshold']), threshold_mode=meta['mode'], **kw)
+    assert luigi.build([t], local_scheduler=True)
+    with n5.open_file(data, 'r') as f:
+        seg = f['data'][:]
+        lut = f['assignments'][:]
+        max_id = f['data'].attrs['maxId']
+    np.testing.assert_array_equal(O.canon(seg), d['labels_canon'])
+    np.testing.assert_array_equal(O.canon(lut), d['lut_canon'])
+    assert max_id == int(d['max_id'])
+    off = json.load(open(str(tmp_path / 'tmp' / 'cc_offsets.json')))
+    np.testing.assert_array_equal(np.array(off['offsets'], dtype=np.uint64), d['offsets'])
+    np.testing.assert_array_equal(off['empty_blocks'], d['empty_blocks'])
+    assert off['n_labels'] == int(d['n_labels'])
+    for task in ('block_components', 'merge_offsets', 'block_faces', 'merge_assignments',
+                 'write_thresholded_components'):
+        assert (tmp_path / 'tmp' / (task + '.log')).exists(), task
+
+
+def test_stage_by_stage(tmp_path):
+    """Each stage task on its own (fused=False): BlockComponents writes the reference's
+    block-local labels, BlockFaces / MergeAssignments / Write do the real work."""
+    from cluster_tools_amd import luigi_compat as luigi, n5
+    from cluster_tools_amd.cluster_tasks import DummyTask
+    from cluster_tools_amd.thresholded_components.block_components import BlockComponentsLocal
+    from cluster_tools_amd.thresholded_components.merge_offsets import MergeOffsetsLocal
+    from cluster_tools_amd.thresholded_components.block_faces import BlockFacesLocal
+    from cluster_tools_amd.thresholded_components.merge_assignments import MergeAssignmentsLocal
+    from cluster_tools_amd.write import WriteLocal
+    name = 'bmap_less'
+    bs = (16, 32, 32)
+    d, data, cfg = _setup(tmp_path, name, bs)
+    tmp = str(tmp_path / 'tmp')
+    common = dict(tmp_folder=tmp, config_dir=cfg, max_jobs=4)
+    t1 = BlockComponentsLocal(input_path=data, input_key='volumes/boundaries', output_path=data, output_key='data',
+                              threshold=0.5, threshold_mode='less', dependency=DummyTask(), **common)
+    assert luigi.build([t1], local_scheduler=True)
+    with n5.open_file(data, 'r') as f:
+        np.testing.assert_array_equal(f['data'][:], d['local_labels'].astype(np.uint64))
+    off_path = os.path.join(tmp, 'cc_offsets.json')
+    shape = list(d['input'].shape)
+    t2 = MergeOffsetsLocal(shape=shape, save_path=off_path, dependency=t1, **common)
+    t3 = BlockFacesLocal(input_path=data, input_key='data', offsets_path=off_path, dependency=t2, **common)
+    t4 = MergeAssignmentsLocal(output_path=data, output_key='assignments', shape=shape, offset_path=off_path,
+                               dependency=t3, **common)
+    t5 = WriteLocal(input_path=data, input_key='data', output_path=data, output_key='data',
+                    assignment_path=data, assignment_key='assignments', identifier='thresholded_components',
+                    offset_path=off_path, dependency=t4, **common)
+    assert luigi.build([t5], local_scheduler=True)
+    np.testing.assert_array_equal(np.load(os.path.join(tmp, 'cc_assignments_0.npy')), d['pairs'])
+    with n5.open_file(data, 'r') as f:
+        np.testing.assert_array_equal(O.canon(f['data'][:]), d['labels_canon'])
+        np.testing.assert_array_equal(O.canon(f['assignments'][:]), d['lut_canon'])
+        assert f['data'].attrs['maxId'] == int(d['max_id'])
