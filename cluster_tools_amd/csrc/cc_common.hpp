@@ -98,9 +98,14 @@ __device__ __forceinline__ bool voxel_pred(const BlockParam& p, float x, float t
 }
 
 // ---- LDS union-find over cubes (root = smallest cube index of the component) ----
+// LDS pointers with an explicit address space: volatile accesses through a generic pointer
+// are not narrowed to LDS by the compiler and would become flat_load / flat_store.
+typedef __attribute__((address_space(3))) u32 lds_u32;
+__device__ __forceinline__ lds_u32* as_lds(u32* p) { return (lds_u32*)p; }
+
 // find with path halving.  Only ever stores an ancestor of x into par[x] (same set,
 // smaller index), which keeps the concurrent atomicMin-based unions correct.
-__device__ __forceinline__ u32 lfind(volatile u32* par, u32 x) {
+__device__ __forceinline__ u32 lfind(volatile lds_u32* par, u32 x) {
     u32 p = par[x];
     while (p != x) {
         const u32 gp = par[p];
@@ -112,18 +117,19 @@ __device__ __forceinline__ u32 lfind(volatile u32* par, u32 x) {
     return x;
 }
 
-__device__ __forceinline__ void lunion(u32* par, u32 a, u32 b) {
-    volatile u32* vp = par;
+__device__ __forceinline__ void lunion(u32* par_, u32 a, u32 b) {
+    lds_u32* par = as_lds(par_);
+    volatile lds_u32* vp = par;
     bool done;
     do {
         a = lfind(vp, a);
         b = lfind(vp, b);
         if (a < b) {
-            u32 old = atomicMin(&par[b], a);
+            u32 old = __hip_atomic_fetch_min(&par[b], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             done = (old == b);
             b = old;
         } else if (b < a) {
-            u32 old = atomicMin(&par[a], b);
+            u32 old = __hip_atomic_fetch_min(&par[a], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             done = (old == a);
             a = old;
         } else {

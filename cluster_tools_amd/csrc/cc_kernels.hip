@@ -88,85 +88,134 @@ __device__ __forceinline__ u64 xlinks(const u64 a[4]) {
     return ((u >> 1) & EVEN64) & ((u & EVEN64) >> 2);
 }
 
-// Per cube row and direction, the cube pairs whose union is NOT implied by the x-runs plus
-// the union of the pair one cube to the left (same A-run, same B-run, also connected).
-__device__ __forceinline__ void necessary_unions(const u64* rows, u64* nec) {
-    for (int w = threadIdx.x; w < NCROW * 4; w += NTHREADS) {
-        const int row = w >> 2, grp = w & 3;
+// ------------------------------------------------------------------------------------------
+// Run-based tile CCL.
+//
+// A cube row (fixed cz, cy) holds 32 cubes; consecutive cubes are 26-linked along x iff the left
+// one has a voxel at local x=1 and the right one a voxel at local x=0.  Maximal x-linked
+// sequences ("runs") are the union-find nodes; a run is named by its first cube index, so the
+// root of a component is its smallest cube index (deterministic).  Per cube row, 64-bit masks in
+// "even" representation (cube cx <-> bit 2cx) give the runs and, for each of the 12 other
+// lex-negative directions, the cube pairs whose union is not already implied by the runs and by
+// the pair one cube to the left.  Only those pairs reach the LDS union-find.
+//
+// After tile_ccl every run start s holds par[s] = root | (k << 16), k in [0, R) the component's
+// compact index (deterministic: roots in cube order).
+// ------------------------------------------------------------------------------------------
+struct TileCCL {
+    u64 rstart[NCROW];     // run starts of each cube row (even representation)
+    u32 par[NC];           // union-find, entries at run starts only
+    u32 rcnt[NCROW];       // roots per cube row
+    u32 scratch[8];
+};
+
+__device__ __forceinline__ void load_row4(const u64* rows, int row, u64 a[4]) {
+    const int cz = row / CY, cy = row % CY;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = rows[(2 * cz + (j >> 1)) * TY + 2 * cy + (j & 1)];
+}
+
+// highest set bit of m at or below bit position b
+__device__ __forceinline__ int hibit_le(u64 m, int b) {
+    const u64 below = b >= 63 ? ~0ull : ((2ull << b) - 1);
+    return 63 - __builtin_clzll((m & below) | 1ull);
+}
+
+// run start (cube index) of occupied cube (row, cx)
+__device__ __forceinline__ u32 run_of(const TileCCL& T, int row, int cx) {
+    return (u32)(row * CX + (hibit_le(T.rstart[row], 2 * cx) >> 1));
+}
+
+__device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T) {
+    const int tid = threadIdx.x;
+    u32* par = T.par;
+    // 1. runs per cube row; every run start is its own parent
+    for (int row = tid; row < NCROW; row += NTHREADS) {
+        u64 a[4];
+        load_row4(rows, row, a);
+        const u64 E = xlinks(a);
+        const u64 u = a[0] | a[1] | a[2] | a[3];
+        const u64 B = (u | (u >> 1)) & EVEN64 & ~(E << 2);
+        T.rstart[row] = B;
+        for (u64 m = B; m; m &= m - 1) {
+            const u32 s0 = (u32)(row * CX + (__builtin_ctzll(m) >> 1));
+            par[s0] = s0;
+        }
+    }
+    __syncthreads();
+    // 2. unions between runs of neighbouring cube rows: thread = (row, direction group)
+    for (int w = tid; w < NCROW * 4; w += NTHREADS) {
+        const int row = w % NCROW, grp = w / NCROW;          // grp is uniform per 2 waves
         const int cz = row / CY, cy = row % CY;
         const int dz = grp == 3 ? 0 : -1, dy = grp == 3 ? -1 : grp - 1;
         const int bz = cz + dz, by = cy + dy;
+        if (bz < 0 || by < 0 || by >= CY) continue;
+        const int rowb = bz * CY + by;
         u64 a[4], b[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] = rows[(2 * cz + (j >> 1)) * TY + 2 * cy + (j & 1)];
-        const bool okb = bz >= 0 && by >= 0 && by < CY;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) b[j] = okb ? rows[(2 * bz + (j >> 1)) * TY + 2 * by + (j & 1)] : 0;
+        load_row4(rows, row, a);
+        load_row4(rows, rowb, b);
         const int szs = dz < 0 ? 0 : 2, szn = dz < 0 ? 1 : 2;
         const int sys = dy < 0 ? 0 : dy > 0 ? 1 : 2, syn = dy < 0 ? 1 : dy > 0 ? 0 : 2;
         const u64 ua = pick_rows(a, szs, sys), ub = pick_rows(b, szn, syn);
         const u64 ea_prev = xlinks(a) << 2, eb_prev = xlinks(b) << 2;
+        const u64 BA = T.rstart[row], BB = T.rstart[rowb];
 #pragma unroll
         for (int dx = -1; dx <= 1; ++dx) {
             const int sxs = dx < 0 ? 0 : dx > 0 ? 1 : 2, sxn = dx < 0 ? 1 : dx > 0 ? 0 : 2;
             const u64 C = xsel(ua, sxs) & shift_dx(xsel(ub, sxn), dx);
             const u64 red = (C << 2) & ea_prev & shift_dx(eb_prev, dx);
-            nec[row * NDIR + grp * 3 + dx + 1] = C & ~red;
-        }
-    }
-}
-
-__device__ u32 tile_ccl(const u64* rows, u8* cm, u32* par, u64* nec, u32* scratch) {
-    const int tid = threadIdx.x, lane = tid & 63;
-    for (int c = tid; c < NC; c += NTHREADS) {
-        const int cz = c / (CY * CX), cy = (c / CX) % CY, cx = c % CX;
-        const int r = (2 * cz) * TY + 2 * cy;
-        const int sh = 2 * cx;
-        const u32 m = (u32)((rows[r] >> sh) & 3) | ((u32)((rows[r + 1] >> sh) & 3) << 2) |
-                      ((u32)((rows[r + TY] >> sh) & 3) << 4) | ((u32)((rows[r + TY + 1] >> sh) & 3) << 6);
-        // x-runs: cube cx links to cx+1 iff it has a voxel at local x=1 and cx+1 one at local x=0
-        const u64 L = __ballot((m & XLO_BITS) != 0), Rr = __ballot((m & XHI_BITS) != 0);
-        const u64 E = Rr & (L >> 1) & 0x7FFFFFFF7FFFFFFFull;         // no link across the two cube rows
-        const u64 B = (L | Rr) & ~(E << 1);                           // run starts
-        const u64 below = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-        const int s0 = 63 - __builtin_clzll((B & below) | 1ull);
-        cm[c] = (u8)m;
-        par[c] = m ? (u32)(c - lane + s0) : NONE;
-    }
-    necessary_unions(rows, nec);
-    __syncthreads();
-    for (int c = tid; c < NC; c += NTHREADS) {
-        if (!cm[c]) continue;
-        const int row = c / CX, sh = 2 * (c % CX);
-        const u64* nr = nec + row * NDIR;
-#pragma unroll
-        for (int d = 0; d < NDIR; ++d) {
-            if ((nr[d] >> sh) & 1) {
-                const int n = c + dir_dz(d) * (CY * CX) + dir_dy(d) * CX + dir_dx(d);
-                const u32 pc = par[c], pn = par[n];
-                if (pc != pn) lunion(par, pc, pn);
+            for (u64 m = C & ~red; m; m &= m - 1) {
+                const int bit = __builtin_ctzll(m);           // 2 cx
+                const u32 ra = (u32)(row * CX + (hibit_le(BA, bit) >> 1));
+                const u32 rb = (u32)(rowb * CX + (hibit_le(BB, bit + 2 * dx) >> 1));
+                lunion(par, ra, rb);
             }
         }
     }
     __syncthreads();
-    for (int c = tid; c < NC; c += NTHREADS)
-        if (cm[c]) par[c] = lfind(par, (u32)c);
+    // 3. compress run starts; count the roots of each cube row
+    for (int row = tid; row < NCROW; row += NTHREADS) {
+        u32 n = 0;
+        for (u64 m = T.rstart[row]; m; m &= m - 1) {
+            const u32 s0 = (u32)(row * CX + (__builtin_ctzll(m) >> 1));
+            const u32 r = lfind(as_lds(par), s0);
+            par[s0] = r;
+            n += (r == s0);
+        }
+        T.rcnt[row] = n;
+    }
     __syncthreads();
-    u32 cnt = 0;
-    for (int c = tid; c < NC; c += NTHREADS)
-        cnt += (cm[c] && par[c] == (u32)c);
-    u32 total;
-    u32 k = block_excl_scan(cnt, scratch, &total);
-    for (int c = tid; c < NC; c += NTHREADS)
-        if (cm[c] && par[c] == (u32)c) par[c] = (u32)c | (k++ << 16);
+    // 4. compact index k of every root, in cube order
+    u32 total = 0;
+    {
+        const u32 v = tid < NCROW ? T.rcnt[tid] : 0;
+        const u32 base = block_excl_scan(v, T.scratch, &total);
+        if (tid < NCROW) {
+            u32 k = base;
+            for (u64 m = T.rstart[tid]; m; m &= m - 1) {
+                const u32 s0 = (u32)(tid * CX + (__builtin_ctzll(m) >> 1));
+                if (par[s0] == s0) par[s0] = s0 | (k++ << 16);
+            }
+        }
+    }
+    __syncthreads();
+    // 5. every run start carries its component's k
+    for (int row = tid; row < NCROW; row += NTHREADS) {
+        for (u64 m = T.rstart[row]; m; m &= m - 1) {
+            const u32 s0 = (u32)(row * CX + (__builtin_ctzll(m) >> 1));
+            const u32 r = par[s0] & 0xFFFFu;
+            if (r != s0) par[s0] = r | (par[r] & 0xFFFF0000u);
+        }
+    }
     __syncthreads();
     return total;
 }
 
-__device__ __forceinline__ u32 cube_k(const u32* par, int c) {
-    const u32 root = par[c] & 0xFFFFu;
-    return par[root] >> 16;
+// component index k of an occupied cube
+__device__ __forceinline__ u32 cube_k(const TileCCL& T, int row, int cx) {
+    return T.par[run_of(T, row, cx)] >> 16;
 }
+__device__ __forceinline__ u32 cube_k(const TileCCL& T, int c) { return cube_k(T, c / CX, c % CX); }
 
 // ------------------------------------------------------------------------------------------
 // k_block_stats: per-block ordered min / max and NaN flag.  One workgroup per tile, lane = x.
@@ -369,7 +418,7 @@ __device__ __forceinline__ void load_rows(const Geom& g, const TileInfo& ti, con
 }
 
 // face plane entry i of a tile (see cc_common.hpp for the layout)
-__device__ __forceinline__ u32 face_entry(int i, const u64* rows, const u32* par, const TileInfo& ti) {
+__device__ __forceinline__ u32 face_entry(int i, const u64* rows, const TileCCL& T, const TileInfo& ti) {
     u32 bits = 0;
     int c = 0;
     if (i < F_YLO) {                       // z faces: (cy, cx), bits (y-local j)*2 + (x-local i)
@@ -402,7 +451,7 @@ __device__ __forceinline__ u32 face_entry(int i, const u64* rows, const u32* par
         c = (cz * CY + cy) * CX + (x >> 1);
     }
     if (!bits) return 0;
-    return cube_k(par, c) | (bits << 16);
+    return cube_k(T, c) | (bits << 16);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -414,12 +463,8 @@ __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restr
                                                     float thr, int mode, u64* BITS, u32* FACES,
                                                     u32* COUNT, u32* P, u64* KEY) {
     __shared__ u64 rows[NROWS];
-    __shared__ u8 cm[NC];
-    __shared__ u32 par[NC];
-    __shared__ u64 kn[NC / 2];          // nec masks during the CCL, then first-voxel keys
-    static_assert(NCROW * NDIR <= NC / 2, "nec does not fit the key buffer");
-    __shared__ u32 scratch[8];
-    u32* key = reinterpret_cast<u32*>(kn);
+    __shared__ TileCCL T;
+    __shared__ u32 key[NC];              // first voxel (tile raster index) of each component
     const int64_t t = blockIdx.x;
     const TileInfo ti = tile_info(g, t);
     const BlockParam p = bp[ti.block];
@@ -429,16 +474,30 @@ __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restr
     if (p.kind != BP_EMPTY) load_rows<HAS_MASK>(g, ti, in, mask, p, thr, mode, rows);
     __syncthreads();
     for (int i = tid; i < NROWS; i += NTHREADS) BITS[t * NROWS + i] = rows[i];
-    const u32 R = tile_ccl(rows, cm, par, kn, scratch);
+    const u32 R = tile_ccl(rows, T);
     for (u32 k = tid; k < R; k += NTHREADS) key[k] = NONE;
     __syncthreads();
-    for (int c = tid; c < NC; c += NTHREADS) {
-        const u32 m = cm[c];
-        if (!m) continue;
-        const int cz = c / (CY * CX), cy = (c / CX) % CY, cx = c % CX;
-        const int bi = __builtin_ctz(m);
-        const int lz = 2 * cz + (bi >> 2), ly = 2 * cy + ((bi >> 1) & 1), lx = 2 * cx + (bi & 1);
-        atomicMin(&key[cube_k(par, c)], (u32)((lz * TY + ly) * TX + lx));
+    // first voxel of each run: voxel order inside a run is (dz, dy) first, then x
+    for (int row = tid; row < NCROW; row += NTHREADS) {
+        const int cz = row / CY, cy = row % CY;
+        u64 a[4];
+        load_row4(rows, row, a);
+        const u64 B = T.rstart[row];
+        const u64 E = xlinks(a);
+        for (u64 m = B; m; m &= m - 1) {
+            const int b0 = __builtin_ctzll(m);                              // 2 * start cube
+            const u64 tail = ~(E >> b0) & EVEN64;                           // first unlinked cube
+            const int b1 = b0 + __builtin_ctzll(tail | (1ull << 62));       // 2 * end cube
+            const u64 hi = b1 + 1 >= 63 ? ~0ull : ((2ull << (b1 + 1)) - 1);
+            const u64 xr = hi & ~((1ull << b0) - 1);
+            u32 idx = NONE;
+#pragma unroll
+            for (int j = 3; j >= 0; --j) {
+                const u64 r = a[j] & xr;
+                if (r) idx = (u32)(((2 * cz + (j >> 1)) * TY + 2 * cy + (j & 1)) * TX + __builtin_ctzll(r));
+            }
+            atomicMin(&key[T.par[row * CX + (b0 >> 1)] >> 16], idx);
+        }
     }
     __syncthreads();
     if (tid == 0) COUNT[t] = R;
@@ -451,7 +510,7 @@ __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restr
         KEY[node] = ((u64)(g.zoff + ti.z0 + lz) * (u64)g.Y + (u64)(ti.y0 + ly)) * (u64)g.X + (u64)(ti.x0 + lx);
     }
     u32* F = FACES + t * FACE_STRIDE;
-    for (int i = tid; i < FACE_STRIDE; i += NTHREADS) F[i] = face_entry(i, rows, par, ti);
+    for (int i = tid; i < FACE_STRIDE; i += NTHREADS) F[i] = face_entry(i, rows, T, ti);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -881,7 +940,7 @@ __global__ void k_map_values(int64_t m, const u64* U, const u64* root, u64* V) {
 // ------------------------------------------------------------------------------------------
 // k_pass2: recompute the tile CCL from the bit rows and write the uint64 labels
 // ------------------------------------------------------------------------------------------
-constexpr int LABCAP = NCROW * NDIR;   // lab[] aliases the nec masks (used before it)
+constexpr int LABCAP = 2048;          // component labels cached in LDS
 
 // store the two voxels (x, x+1) of one cube row segment; 16-B store when aligned
 __device__ __forceinline__ void store2(u64* __restrict__ out, int64_t idx, u64 v0, u64 v1, bool two, bool vec) {
@@ -896,11 +955,8 @@ __device__ __forceinline__ void store2(u64* __restrict__ out, int64_t idx, u64 v
 __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restrict__ BITS, const u32* COUNT,
                                                     const u64* __restrict__ FIN, u64* __restrict__ out) {
     __shared__ u64 rows[NROWS];
-    __shared__ u8 cm[NC];
-    __shared__ u32 par[NC];
-    __shared__ u64 lab[LABCAP];          // nec masks during the CCL, then final labels
-    __shared__ u32 scratch[8];
-    u64* nec = lab;
+    __shared__ TileCCL T;
+    __shared__ u64 lab[LABCAP];
     const int64_t t = blockIdx.x;
     const TileInfo ti = tile_info(g, t);
     const int tid = threadIdx.x;
@@ -923,18 +979,21 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
     }
     for (int i = tid; i < NROWS; i += NTHREADS) rows[i] = BITS[t * NROWS + i];
     __syncthreads();
-    tile_ccl(rows, cm, par, nec, scratch);
+    tile_ccl(rows, T);
     const u32 base = (u32)(t * g.cap);
     for (u32 k = tid; k < R && k < LABCAP; k += NTHREADS) lab[k] = FIN[base + k];
     __syncthreads();
     for (int c = tid; c < NC; c += NTHREADS) {
         const int cz = c / (CY * CX), cy = (c / CX) % CY, cx = c % CX;
         if (cz >= ncz || cy >= ncy || cx >= ncx) continue;
-        const u32 m = cm[c];
+        const int r = (2 * cz) * TY + 2 * cy, sh = 2 * cx;
+        const u32 m = (u32)((rows[r] >> sh) & 3) | ((u32)((rows[r + 1] >> sh) & 3) << 2) |
+                      ((u32)((rows[r + TY] >> sh) & 3) << 4) | ((u32)((rows[r + TY + 1] >> sh) & 3) << 6);
         u64 v = 0;
         if (m) {
-            const u32 k = cube_k(par, c);
-            v = k < LABCAP ? lab[k] : FIN[base + k];
+            const u32 k = cube_k(T, c);
+            if (k < LABCAP) v = lab[k];
+            else v = __builtin_nontemporal_load(FIN + base + k);
         }
         const bool two = 2 * cx + 1 < ti.lx;
 #pragma unroll
