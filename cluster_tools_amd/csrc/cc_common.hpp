@@ -56,6 +56,8 @@ struct Geom {
     const int32_t* tstart[3]; // per-axis tile tables
     const int32_t* tlen[3];
     const int32_t* tblk[3];
+    const int32_t* bt0[3];    // per-axis block tables: first tile index and tile count of a block
+    const int32_t* btn[3];
 };
 
 struct TileInfo {

@@ -535,24 +535,16 @@ __device__ __forceinline__ bool hset_insert(u64* hs, u64 key) {
     return true;   // table crowded: do the (idempotent) union anyway
 }
 
-template <bool INTER>
-__global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restrict__ FACES, u32* P,
-                                                     const u64* __restrict__ K) {
-    __shared__ u64 hs[HSET];
-    for (int i = threadIdx.x; i < HSET; i += NTHREADS) hs[i] = ~0ull;
-    __syncthreads();
-    auto gunion = [&](u32* Pp, const u64* Kp, u32 a, u32 b) {
-        if (hset_insert(hs, ((u64)a << 32) | b)) cc::gunion(Pp, Kp, a, b);
-    };
-    const int64_t t = blockIdx.x;
-    const TileInfo ti = tile_info(g, t);
-    const int tid = threadIdx.x;
-    const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
-    const u32 capu = (u32)g.cap;
+// Unions across the lower seams of tile t: calls U(t, entry, t_nbr, entry_nbr) for every pair of
+// face cubes that are connected (face entry = k | bits << 16).
+//   INTER = false: seams inside one block, 26-connectivity (13 tile directions).
+//   INTER = true : seams on block faces, 6-connectivity (3 face directions).
+template <bool INTER, class UF>
+__device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict__ FACES, int64_t t,
+                                            const TileInfo& ti, int tid, int nthr, UF&& U) {
     const u32* F = FACES + t * FACE_STRIDE;
     const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2, ncz = (ti.lz + 1) / 2;
-    const u32 base = (u32)(t * g.cap);
-    auto node_of = [&](int64_t tt, u32 e) -> u32 { return (u32)(tt * capu) + (e & 0xFFFFu); };
+    const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
 
     // ---------------- z-lower seam ----------------
     if (ti.iz > 0) {
@@ -561,18 +553,18 @@ __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restri
         const u32* FN = FACES + tn * FACE_STRIDE;
         if (INTER) {
             if (!same_z)
-                for (int e = tid; e < ncy * CX; e += NTHREADS) {
+                for (int e = tid; e < ncy * CX; e += nthr) {
                     const int cy = e / CX, cx = e % CX;
                     if (cx >= ncx) continue;
                     const u32 a = F[F_ZLO + e];
                     if (!a) continue;
                     const u32 b = FN[F_ZHI + e];
-                    if ((a >> 16) & (b >> 16)) gunion(P, K, base + (a & 0xFFFFu), node_of(tn, b));
+                    if ((a >> 16) & (b >> 16)) U(t, a, tn, b);
                     (void)cy;
                 }
         } else if (same_z) {
             // face (-1, 0, 0): 9 cube offsets in (dy, dx)
-            for (int e = tid; e < ncy * CX; e += NTHREADS) {
+            for (int e = tid; e < ncy * CX; e += nthr) {
                 const int cy = e / CX, cx = e % CX;
                 if (cx >= ncx) continue;
                 const u32 a = F[F_ZLO + e];
@@ -587,7 +579,7 @@ __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restri
                         const u32 b = FN[F_ZHI + ny * CX + nx];
                         if (!b) continue;
                         if ((ab & fsel(self_sel(dy), self_sel(dx))) && ((b >> 16) & fsel(nbr_sel(dy), nbr_sel(dx))))
-                            gunion(P, K, base + (a & 0xFFFFu), node_of(tn, b));
+                            U(t, a, tn, b);
                     }
                 }
             }
@@ -600,7 +592,7 @@ __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restri
                 const int cyo = s < 0 ? 0 : ncy - 1, cyn = s < 0 ? (lyn - 1) / 2 : 0;
                 const int jo = s < 0 ? 0 : (ti.ly - 1) & 1, jn = s < 0 ? (lyn - 1) & 1 : 0;
                 const u32* FE = FACES + te * FACE_STRIDE;
-                for (int cx = tid; cx < ncx; cx += NTHREADS) {
+                for (int cx = tid; cx < ncx; cx += nthr) {
                     const u32 a = F[F_ZLO + cyo * CX + cx];
                     if (!a) continue;
                     for (int dx = -1; dx <= 1; ++dx) {
@@ -609,7 +601,7 @@ __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restri
                         const u32 b = FE[F_ZHI + cyn * CX + nx];
                         if (!b) continue;
                         if (((a >> 16) & fsel(jo, self_sel(dx))) && ((b >> 16) & fsel(jn, nbr_sel(dx))))
-                            gunion(P, K, base + (a & 0xFFFFu), node_of(te, b));
+                            U(t, a, te, b);
                     }
                 }
             }
@@ -622,7 +614,7 @@ __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restri
                 const int cxo = s < 0 ? 0 : ncx - 1, cxn = s < 0 ? (lxn - 1) / 2 : 0;
                 const int io = s < 0 ? 0 : (ti.lx - 1) & 1, in_ = s < 0 ? (lxn - 1) & 1 : 0;
                 const u32* FE = FACES + te * FACE_STRIDE;
-                for (int cy = tid; cy < ncy; cy += NTHREADS) {
+                for (int cy = tid; cy < ncy; cy += nthr) {
                     const u32 a = F[F_ZLO + cy * CX + cxo];
                     if (!a) continue;
                     for (int dy = -1; dy <= 1; ++dy) {
@@ -631,7 +623,7 @@ __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restri
                         const u32 b = FE[F_ZHI + ny * CX + cxn];
                         if (!b) continue;
                         if (((a >> 16) & fsel(self_sel(dy), io)) && ((b >> 16) & fsel(nbr_sel(dy), in_)))
-                            gunion(P, K, base + (a & 0xFFFFu), node_of(te, b));
+                            U(t, a, te, b);
                     }
                 }
             }
@@ -650,7 +642,7 @@ __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restri
                     const u32 a = F[F_ZLO + cyo * CX + cxo];
                     const u32 b = FACES[tc * FACE_STRIDE + F_ZHI + cyn * CX + cxn];
                     if (a && b && ((a >> 16) & fsel(jo, io)) && ((b >> 16) & fsel(jn, in_)))
-                        gunion(P, K, base + (a & 0xFFFFu), node_of(tc, b));
+                        U(t, a, tc, b);
                 }
             }
         }
@@ -662,17 +654,17 @@ __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restri
         const u32* FN = FACES + tn * FACE_STRIDE;
         if (INTER) {
             if (!same_y)
-                for (int e = tid; e < ncz * CX; e += NTHREADS) {
+                for (int e = tid; e < ncz * CX; e += nthr) {
                     const int cx = e % CX;
                     if (cx >= ncx) continue;
                     const u32 a = F[F_YLO + e];
                     if (!a) continue;
                     const u32 b = FN[F_YHI + e];
-                    if ((a >> 16) & (b >> 16)) gunion(P, K, base + (a & 0xFFFFu), node_of(tn, b));
+                    if ((a >> 16) & (b >> 16)) U(t, a, tn, b);
                 }
         } else if (same_y) {
             // face (0, -1, 0): offsets (dz, dx)
-            for (int e = tid; e < ncz * CX; e += NTHREADS) {
+            for (int e = tid; e < ncz * CX; e += nthr) {
                 const int cz = e / CX, cx = e % CX;
                 if (cx >= ncx) continue;
                 const u32 a = F[F_YLO + e];
@@ -686,7 +678,7 @@ __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restri
                         const u32 b = FN[F_YHI + nz * CX + nx];
                         if (!b) continue;
                         if (((a >> 16) & fsel(self_sel(dz), self_sel(dx))) && ((b >> 16) & fsel(nbr_sel(dz), nbr_sel(dx))))
-                            gunion(P, K, base + (a & 0xFFFFu), node_of(tn, b));
+                            U(t, a, tn, b);
                     }
                 }
             }
@@ -699,7 +691,7 @@ __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restri
                 const int cxo = s < 0 ? 0 : ncx - 1, cxn = s < 0 ? (lxn - 1) / 2 : 0;
                 const int io = s < 0 ? 0 : (ti.lx - 1) & 1, in_ = s < 0 ? (lxn - 1) & 1 : 0;
                 const u32* FE = FACES + te * FACE_STRIDE;
-                for (int cz = tid; cz < ncz; cz += NTHREADS) {
+                for (int cz = tid; cz < ncz; cz += nthr) {
                     const u32 a = F[F_YLO + cz * CX + cxo];
                     if (!a) continue;
                     for (int dz = -1; dz <= 1; ++dz) {
@@ -708,7 +700,7 @@ __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restri
                         const u32 b = FE[F_YHI + nz * CX + cxn];
                         if (!b) continue;
                         if (((a >> 16) & fsel(self_sel(dz), io)) && ((b >> 16) & fsel(nbr_sel(dz), in_)))
-                            gunion(P, K, base + (a & 0xFFFFu), node_of(te, b));
+                            U(t, a, te, b);
                     }
                 }
             }
@@ -721,16 +713,16 @@ __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restri
         const u32* FN = FACES + tn * FACE_STRIDE;
         if (INTER) {
             if (!same_x)
-                for (int e = tid; e < ncz * CY; e += NTHREADS) {
+                for (int e = tid; e < ncz * CY; e += nthr) {
                     const int cy = e % CY;
                     if (cy >= ncy) continue;
                     const u32 a = F[F_XLO + e];
                     if (!a) continue;
                     const u32 b = FN[F_XHI + e];
-                    if ((a >> 16) & (b >> 16)) gunion(P, K, base + (a & 0xFFFFu), node_of(tn, b));
+                    if ((a >> 16) & (b >> 16)) U(t, a, tn, b);
                 }
         } else if (same_x) {
-            for (int e = tid; e < ncz * CY; e += NTHREADS) {
+            for (int e = tid; e < ncz * CY; e += nthr) {
                 const int cz = e / CY, cy = e % CY;
                 if (cy >= ncy) continue;
                 const u32 a = F[F_XLO + e];
@@ -744,7 +736,7 @@ __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restri
                         const u32 b = FN[F_XHI + nz * CY + ny];
                         if (!b) continue;
                         if (((a >> 16) & fsel(self_sel(dz), self_sel(dy))) && ((b >> 16) & fsel(nbr_sel(dz), nbr_sel(dy))))
-                            gunion(P, K, base + (a & 0xFFFFu), node_of(tn, b));
+                            U(t, a, tn, b);
                     }
                 }
             }
@@ -757,6 +749,149 @@ __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restri
 // ------------------------------------------------------------------------------------------
 // one wave per tile: tile t = blockIdx.x * WAVES + wave
 constexpr int WAVES = NTHREADS / 64;
+
+// Global-memory stitch (one workgroup per tile; keys: first voxel (intra) or rid (inter)).
+// INTRA only runs for tiles of blocks that k_stitch_block could not take (big[block] != 0).
+template <bool INTER>
+__global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restrict__ FACES, u32* P,
+                                                     const u64* __restrict__ K, const u8* __restrict__ big) {
+    __shared__ u64 hs[HSET];
+    const int64_t t = blockIdx.x;
+    const TileInfo ti = tile_info(g, t);
+    if (!INTER && !big[ti.block]) return;
+    for (int i = threadIdx.x; i < HSET; i += NTHREADS) hs[i] = ~0ull;
+    __syncthreads();
+    const u32 capu = (u32)g.cap;
+    stitch_tile<INTER>(g, FACES, t, ti, threadIdx.x, NTHREADS, [&](int64_t t1, u32 e1, int64_t t2, u32 e2) {
+        const u32 a = (u32)(t1 * capu) + (e1 & 0xFFFFu), b = (u32)(t2 * capu) + (e2 & 0xFFFFu);
+        if (hset_insert(hs, ((u64)a << 32) | b)) gunion(P, K, a, b);
+    });
+}
+
+// ------------------------------------------------------------------------------------------
+// k_stitch_block: the intra-block (26-connected) seams of one reference block, with the
+// union-find over the block's tile-local components held in LDS (no global atomics).  A block
+// with more than SB_MAXT tiles or SB_LCAP components is flagged in big[] and left to k_stitch.
+// ------------------------------------------------------------------------------------------
+constexpr int SB_THREADS = 1024;
+constexpr int SB_MAXT = 1024;
+constexpr int SB_LCAP = 8192;
+
+__device__ __forceinline__ u32 lfind_k(lds_u32* par, u32 x) {
+    volatile lds_u32* vp = par;
+    u32 p = vp[x];
+    while (p != x) {
+        const u32 gp = vp[p];
+        if (gp == p) return p;
+        vp[x] = gp;
+        x = gp;
+        p = vp[x];
+    }
+    return x;
+}
+
+// link the root with the larger key under the root with the smaller key (keys unique)
+__device__ __forceinline__ void lunion_key(lds_u32* par, const u64* key, u32 a, u32 b) {
+    while (true) {
+        a = lfind_k(par, a);
+        b = lfind_k(par, b);
+        if (a == b) return;
+        if (key[a] < key[b]) { const u32 t = a; a = b; b = t; }
+        if (__hip_atomic_compare_exchange_strong(&par[a], &a, b, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP))
+            return;
+    }
+}
+
+__global__ __launch_bounds__(SB_THREADS) void k_stitch_block(Geom g, const u32* __restrict__ FACES,
+                                                             const u32* __restrict__ COUNT, u32* P,
+                                                             const u64* __restrict__ KEY, u8* big) {
+    __shared__ u32 noff[SB_MAXT + 1];
+    __shared__ u32 lpar[SB_LCAP];
+    __shared__ u64 lkey[SB_LCAP];
+    __shared__ u32 red[SB_THREADS / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int NW = SB_THREADS / 64;
+    const int64_t b = blockIdx.x;
+    const int bx = (int)(b % g.nb[2]), by = (int)((b / g.nb[2]) % g.nb[1]), bz = (int)(b / ((int64_t)g.nb[2] * g.nb[1]));
+    const int iz0 = g.bt0[0][bz], iy0 = g.bt0[1][by], ix0 = g.bt0[2][bx];
+    const int nz = g.btn[0][bz], ny = g.btn[1][by], nx = g.btn[2][bx];
+    const int ntb = nz * ny * nx;
+    if (ntb > SB_MAXT) {
+        if (tid == 0) big[b] = 1;
+        return;
+    }
+    auto tile_of = [&](int lt) -> int64_t {
+        const int lx = lt % nx, ly = (lt / nx) % ny, lz = lt / (nx * ny);
+        return ((int64_t)(iz0 + lz) * g.nt[1] + (iy0 + ly)) * g.nt[2] + (ix0 + lx);
+    };
+    auto local_of = [&](int64_t t) -> int {
+        const int ix = (int)(t % g.nt[2]), iy = (int)((t / g.nt[2]) % g.nt[1]), iz = (int)(t / ((int64_t)g.nt[2] * g.nt[1]));
+        return ((iz - iz0) * ny + (iy - iy0)) * nx + (ix - ix0);
+    };
+    // node offsets: exclusive scan of the tiles' component counts (wave-serial chunks of 64)
+    if (wave == 0) {
+        u32 run = 0;
+        for (int c0 = 0; c0 < ntb; c0 += 64) {
+            const int lt = c0 + lane;
+            const u32 v = lt < ntb ? COUNT[tile_of(lt)] : 0;
+            u32 x = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const u32 y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            if (lt < ntb) noff[lt] = run + x - v;
+            run += __shfl(x, 63, 64);
+        }
+        if (lane == 0) noff[ntb] = run;
+    }
+    __syncthreads();
+    const u32 N = noff[ntb];
+    if (N > SB_LCAP) {
+        if (tid == 0) big[b] = 1;
+        return;
+    }
+    if (tid == 0) big[b] = 0;
+    // nodes: one wave per tile
+    for (int lt = wave; lt < ntb; lt += NW) {
+        const int64_t t = tile_of(lt);
+        const u32 o = noff[lt], n = noff[lt + 1] - o;
+        for (u32 k = lane; k < n; k += 64) {
+            lpar[o + k] = o + k;
+            lkey[o + k] = KEY[(u64)t * g.cap + k];
+        }
+    }
+    __syncthreads();
+    lds_u32* par = as_lds(lpar);
+    for (int lt = 0; lt < ntb; ++lt) {
+        const int64_t t = tile_of(lt);
+        const TileInfo ti = tile_info(g, t);
+        stitch_tile<false>(g, FACES, t, ti, tid, SB_THREADS, [&](int64_t t1, u32 e1, int64_t t2, u32 e2) {
+            const u32 a = noff[local_of(t1)] + (e1 & 0xFFFFu), c = noff[local_of(t2)] + (e2 & 0xFFFFu);
+            lunion_key(par, lkey, a, c);
+        });
+    }
+    __syncthreads();
+    // write the block-local roots back to the global union-find
+    for (int lt = wave; lt < ntb; lt += NW) {
+        const int64_t t = tile_of(lt);
+        const u32 o = noff[lt], n = noff[lt + 1] - o;
+        for (u32 k = lane; k < n; k += 64) {
+            const u32 r = lfind_k(par, o + k);
+            if (r != o + k) {
+                // global node of local r: find its tile by binary search over noff
+                int lo = 0, hi = ntb - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (noff[mid] <= r) lo = mid; else hi = mid - 1;
+                }
+                P[(u64)t * g.cap + k] = (u32)((u64)tile_of(lo) * g.cap + (r - noff[lo]));
+            }
+        }
+    }
+    (void)red;
+}
 
 // block-local roots per tile (no atomics: counts, then an exclusive scan, then a collect that
 // writes each tile's roots at its scanned offset in node order)
@@ -1011,8 +1146,8 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
 // instantiate the templates used by the host side
 template __global__ void k_pass1<false>(Geom, const float*, const u8*, const BlockParam*, float, int, u64*, u32*, u32*, u32*, u64*);
 template __global__ void k_pass1<true>(Geom, const float*, const u8*, const BlockParam*, float, int, u64*, u32*, u32*, u32*, u64*);
-template __global__ void k_stitch<false>(Geom, const u32*, u32*, const u64*);
-template __global__ void k_stitch<true>(Geom, const u32*, u32*, const u64*);
+template __global__ void k_stitch<false>(Geom, const u32*, u32*, const u64*, const u8*);
+template __global__ void k_stitch<true>(Geom, const u32*, u32*, const u64*, const u8*);
 template __global__ void k_finalize<false>(Geom, const u32*, u32*, const u64*, const u64*, const u64*, const u64*, int64_t, u64*);
 template __global__ void k_finalize<true>(Geom, const u32*, u32*, const u64*, const u64*, const u64*, const u64*, int64_t, u64*);
 template __global__ void k_plane_labels<false>(Geom, const u32*, u32*, const u64*, u64*);

@@ -67,7 +67,7 @@ struct cc_ctx {
     // workspace
     DevBuf tiles, bstat, bparam, bits, faces, count, rc, roff, P, KR, FIN, keys, keys2, vals, vals2, seg,
         values, offsets, lut, cub_tmp, scalars, scalars2, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2,
-        flags, map_ids, map_ids2, map_vals, map_par;
+        flags, map_ids, map_ids2, map_vals, map_par, big;
     // last run
     int64_t n_blocks = 0;
     uint64_t n_labels = 0;
@@ -187,6 +187,12 @@ static HostGeom make_geom(const int64_t shape[3], const int64_t block_shape[3], 
         hg.tab.insert(hg.tab.end(), ln[a].begin(), ln[a].end());
         hg.tab.insert(hg.tab.end(), bk[a].begin(), bk[a].end());
     }
+    for (int a = 0; a < 3; ++a) {          // block -> first tile, tile count
+        std::vector<int32_t> b0(g.nb[a], 0), bn(g.nb[a], 0);
+        for (int i = (int)bk[a].size() - 1; i >= 0; --i) { b0[bk[a][i]] = i; bn[bk[a][i]] += 1; }
+        hg.tab.insert(hg.tab.end(), b0.begin(), b0.end());
+        hg.tab.insert(hg.tab.end(), bn.begin(), bn.end());
+    }
     return hg;
 }
 
@@ -203,6 +209,12 @@ static void upload_geom(cc_ctx* c, HostGeom& hg) {
         hg.g.tlen[a] = base + off + n;
         hg.g.tblk[a] = base + off + 2 * n;
         off += 3 * n;
+    }
+    for (int a = 0; a < 3; ++a) {
+        const int n = hg.g.nb[a];
+        hg.g.bt0[a] = base + off;
+        hg.g.btn[a] = base + off + n;
+        off += 2 * n;
     }
 }
 
@@ -281,7 +293,10 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         launch(c, "k_pass1", [&] { k_pass1<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, mask, bp, thr, mode, BITS, FACES, COUNT, P, KR); });
     else
         launch(c, "k_pass1", [&] { k_pass1<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, nullptr, bp, thr, mode, BITS, FACES, COUNT, P, KR); });
-    launch(c, "k_stitch_intra", [&] { k_stitch<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, FACES, P, KR); });
+    c->big.ensure(nb);
+    u8* big = c->big.as<u8>();
+    launch(c, "k_stitch_block", [&] { k_stitch_block<<<(unsigned)nb, SB_THREADS, 0, s>>>(g, FACES, COUNT, P, KR, big); });
+    launch(c, "k_stitch_intra", [&] { k_stitch<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, FACES, P, KR, big); });
 
     // block-local roots: per-tile counts -> exclusive scan -> one host read of the total (the one
     // mid-run host sync; it sizes the radix sort)
@@ -367,7 +382,7 @@ static void phase_rid(cc_ctx* c, uint64_t base) {
                                                     offsets, c->KR.as<u64>());
         });
     if (!st.local_only)
-        launch(c, "k_stitch_inter", [&] { k_stitch<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->faces.as<u32>(), c->P.as<u32>(), c->KR.as<u64>()); });
+        launch(c, "k_stitch_inter", [&] { k_stitch<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->faces.as<u32>(), c->P.as<u32>(), c->KR.as<u64>(), c->big.as<u8>()); });
     st.n_map = 0;
     st.stage = 2;
 }
@@ -560,7 +575,7 @@ void cc_destroy(cc_ctx* c) {
                       &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
                       &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
-                      &c->map_ids2, &c->map_vals, &c->map_par};
+                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big};
     for (DevBuf* b : bufs) b->release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
