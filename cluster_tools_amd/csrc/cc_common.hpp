@@ -67,11 +67,14 @@ struct TileInfo {
     int64_t block;
 };
 
+// tile ids fit u32 (node ids t * cap are u32, checked on the host): 32-bit division only
 __device__ __forceinline__ TileInfo tile_info(const Geom& g, int64_t t) {
     TileInfo ti;
-    ti.ix = (int)(t % g.nt[2]);
-    ti.iy = (int)((t / g.nt[2]) % g.nt[1]);
-    ti.iz = (int)(t / ((int64_t)g.nt[2] * g.nt[1]));
+    const u32 tt = (u32)t, n2 = (u32)g.nt[2], n1 = (u32)g.nt[1];
+    const u32 q = tt / n2, qz = q / n1;
+    ti.ix = (int)(tt - q * n2);
+    ti.iy = (int)(q - qz * n1);
+    ti.iz = (int)qz;
     ti.z0 = g.tstart[0][ti.iz]; ti.lz = g.tlen[0][ti.iz];
     ti.y0 = g.tstart[1][ti.iy]; ti.ly = g.tlen[1][ti.iy];
     ti.x0 = g.tstart[2][ti.ix]; ti.lx = g.tlen[2][ti.ix];

@@ -524,6 +524,20 @@ __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restr
 constexpr int HSET = 2048;
 
 __device__ __forceinline__ bool hset_insert(u64* hs, u64 key) {
+    // Face cubes of one component mostly produce the same pair: drop lanes whose key equals the
+    // wave's first active lane's (up to 3 rounds) before touching the LDS table, so identical
+    // keys do not serialise on one LDS address.
+    const u32 lane = __lane_id();
+#pragma unroll 1
+    for (int r = 0; r < 2; ++r) {
+        const u64 lk = ((u64)__builtin_amdgcn_readfirstlane((u32)(key >> 32)) << 32) |
+                       (u64)__builtin_amdgcn_readfirstlane((u32)key);
+        const u32 leader = __builtin_amdgcn_readfirstlane(lane);
+        if (key == lk) {
+            if (lane != leader) return false;
+            break;
+        }
+    }
     u32 h = (u32)((key * 0x9E3779B97F4A7C15ull) >> 53) & (HSET - 1);
 #pragma unroll 1
     for (int probe = 0; probe < 16; ++probe) {
@@ -535,14 +549,114 @@ __device__ __forceinline__ bool hset_insert(u64* hs, u64 key) {
     return true;   // table crowded: do the (idempotent) union anyway
 }
 
-// Unions across the lower seams of tile t: calls U(t, entry, t_nbr, entry_nbr) for every pair of
-// face cubes that are connected (face entry = k | bits << 16).
+// Stage the face planes tile t needs from its three face neighbours into LDS, in the FACE_STRIDE
+// layout: own ZLO/YLO/XLO and the z-/y-/x-lower neighbours' ZHI/YHI/XHI (0 where absent).  One
+// parallel load round instead of dependent global loads per face cube.
+__device__ __forceinline__ void stage_faces(const Geom& g, const u32* __restrict__ FACES, int64_t t,
+                                            const TileInfo& ti, u32* S, int tid, int nthr) {
+    const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
+    for (int i = tid; i < FACE_STRIDE; i += nthr) {
+        u32 v = 0;
+        if (i < F_ZHI || (i >= F_YLO && i < F_YHI) || (i >= F_XLO && i < F_XHI)) {
+            v = FACES[t * FACE_STRIDE + i];
+        } else if (i < F_YLO) {
+            if (ti.iz > 0) v = FACES[(t - sz) * FACE_STRIDE + i];
+        } else if (i < F_XLO) {
+            if (ti.iy > 0) v = FACES[(t - sy) * FACE_STRIDE + i];
+        } else {
+            if (ti.ix > 0) v = FACES[(t - 1) * FACE_STRIDE + i];
+        }
+        S[i] = v;
+    }
+}
+
+// Up to two distinct neighbour components of one face cube, gathered without branches; a third
+// distinct one sets ovf and the caller falls back to visiting every neighbour.
+struct Cand {
+    u32 b1 = 0, b2 = 0;
+    bool ovf = false;
+    __device__ __forceinline__ void add(u32 b) {
+        const bool new1 = b && b1 && ((b ^ b1) & 0xFFFFu);
+        const bool new2 = new1 && b2 && ((b ^ b2) & 0xFFFFu);
+        ovf |= new2;
+        b2 = (new1 && !b2) ? b : b2;
+        b1 = b1 ? b1 : b;
+    }
+};
+
+// Connected neighbour entry or 0: face cube a (bits ab) and neighbour entry b with the 4-bit face
+// selections sa (own side) and sb (neighbour side).
+__device__ __forceinline__ u32 face_link(u32 ab, u32 sa, u32 b, u32 sb) {
+    return ((ab & sa) && ((b >> 16) & sb)) ? b : 0u;
+}
+
+// 3x3 neighbourhood across a face plane: own entry a at (p, q), neighbour plane FN with row
+// stride QS and valid extent np x nq.  Calls U(t, a, tn, b) once per distinct neighbour component.
+template <int QS, class UF>
+__device__ __forceinline__ void face3x3(const u32* FN, u32 a, int p, int q, int np, int nq, int64_t t, int64_t tn,
+                                        UF& U) {
+    const u32 ab = a >> 16;
+    auto nb = [&](int dp, int dq) -> u32 {
+        const int pp = p + dp, qq = q + dq;
+        const bool ok = pp >= 0 && pp < np && qq >= 0 && qq < nq;
+        const u32 b = FN[ok ? pp * QS + qq : 0];
+        return ok ? face_link(ab, fsel(self_sel(dp), self_sel(dq)), b, fsel(nbr_sel(dp), nbr_sel(dq))) : 0u;
+    };
+    Cand c;
+#pragma unroll
+    for (int dp = -1; dp <= 1; ++dp)
+#pragma unroll
+        for (int dq = -1; dq <= 1; ++dq) c.add(nb(dp, dq));
+    if (c.b1) U(t, a, tn, c.b1);
+    if (c.b2) U(t, a, tn, c.b2);
+    if (c.ovf) {
+#pragma unroll 1
+        for (int i = 0; i < 9; ++i) {
+            const u32 b = nb(i / 3 - 1, i % 3 - 1);
+            if (b) U(t, a, tn, b);
+        }
+    }
+}
+
+// Three neighbours along one axis of an edge: own entry a at q, neighbour row FR (stride 1 in q)
+// of extent nq; sa/sb fixed selection of the other axis (own / neighbour side).
+template <bool Q_IS_P, class UF>
+__device__ __forceinline__ void edge3(const u32* FR, int RS, u32 a, int q, int nq, int so, int sn, int64_t t,
+                                      int64_t te, UF& U) {
+    const u32 ab = a >> 16;
+    Cand c;
+#pragma unroll
+    for (int d = -1; d <= 1; ++d) {
+        const int qq = q + d;
+        const bool ok = qq >= 0 && qq < nq;
+        const u32 b = FR[(ok ? qq : 0) * RS];
+        const u32 sa = Q_IS_P ? fsel(self_sel(d), so) : fsel(so, self_sel(d));
+        const u32 sb = Q_IS_P ? fsel(nbr_sel(d), sn) : fsel(sn, nbr_sel(d));
+        c.add(ok ? face_link(ab, sa, b, sb) : 0u);
+    }
+    if (c.b1) U(t, a, te, c.b1);
+    if (c.b2) U(t, a, te, c.b2);
+    if (c.ovf) {
+#pragma unroll 1
+        for (int d = -1; d <= 1; ++d) {
+            const int qq = q + d;
+            if (qq < 0 || qq >= nq) continue;
+            const u32 sa = Q_IS_P ? fsel(self_sel(d), so) : fsel(so, self_sel(d));
+            const u32 sb = Q_IS_P ? fsel(nbr_sel(d), sn) : fsel(sn, nbr_sel(d));
+            const u32 b = face_link(ab, sa, FR[qq * RS], sb);
+            if (b) U(t, a, te, b);
+        }
+    }
+}
+
+// Unions across the lower seams of tile t: calls U(t, entry, t_nbr, entry_nbr) for connected face
+// cubes (face entry = k | bits << 16), at least once per connected pair of tile components.
+// S = stage_faces() copy; edge and corner neighbours are read from FACES.
 //   INTER = false: seams inside one block, 26-connectivity (13 tile directions).
 //   INTER = true : seams on block faces, 6-connectivity (3 face directions).
 template <bool INTER, class UF>
-__device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict__ FACES, int64_t t,
-                                            const TileInfo& ti, int tid, int nthr, UF&& U) {
-    const u32* F = FACES + t * FACE_STRIDE;
+__device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict__ FACES, const u32* S,
+                                            int64_t t, const TileInfo& ti, int tid, int nthr, UF&& U) {
     const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2, ncz = (ti.lz + 1) / 2;
     const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
 
@@ -550,85 +664,50 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
     if (ti.iz > 0) {
         const bool same_z = g.tblk[0][ti.iz] == g.tblk[0][ti.iz - 1];
         const int64_t tn = t - sz;
-        const u32* FN = FACES + tn * FACE_STRIDE;
         if (INTER) {
             if (!same_z)
                 for (int e = tid; e < ncy * CX; e += nthr) {
-                    const int cy = e / CX, cx = e % CX;
+                    const int cx = e % CX;
                     if (cx >= ncx) continue;
-                    const u32 a = F[F_ZLO + e];
+                    const u32 a = S[F_ZLO + e];
                     if (!a) continue;
-                    const u32 b = FN[F_ZHI + e];
+                    const u32 b = S[F_ZHI + e];
                     if ((a >> 16) & (b >> 16)) U(t, a, tn, b);
-                    (void)cy;
                 }
         } else if (same_z) {
-            // face (-1, 0, 0): 9 cube offsets in (dy, dx)
-            for (int e = tid; e < ncy * CX; e += nthr) {
+            for (int e = tid; e < ncy * CX; e += nthr) {          // face (-1, 0, 0): offsets (dy, dx)
                 const int cy = e / CX, cx = e % CX;
                 if (cx >= ncx) continue;
-                const u32 a = F[F_ZLO + e];
-                if (!a) continue;
-                const u32 ab = a >> 16;
-                for (int dy = -1; dy <= 1; ++dy) {
-                    const int ny = cy + dy;
-                    if (ny < 0 || ny >= ncy) continue;
-                    for (int dx = -1; dx <= 1; ++dx) {
-                        const int nx = cx + dx;
-                        if (nx < 0 || nx >= ncx) continue;
-                        const u32 b = FN[F_ZHI + ny * CX + nx];
-                        if (!b) continue;
-                        if ((ab & fsel(self_sel(dy), self_sel(dx))) && ((b >> 16) & fsel(nbr_sel(dy), nbr_sel(dx))))
-                            U(t, a, tn, b);
-                    }
-                }
+                const u32 a = S[F_ZLO + e];
+                if (a) face3x3<CX>(S + F_ZHI, a, cy, cx, ncy, ncx, t, tn, U);
             }
-            // edges (-1, sy, 0)
-            for (int s = -1; s <= 1; s += 2) {
+            for (int s = -1; s <= 1; s += 2) {                    // edges (-1, s, 0)
                 const int jy = ti.iy + s;
                 if (jy < 0 || jy >= g.nt[1] || g.tblk[1][jy] != g.tblk[1][ti.iy]) continue;
                 const int64_t te = tn + s * sy;
                 const int lyn = g.tlen[1][jy];
                 const int cyo = s < 0 ? 0 : ncy - 1, cyn = s < 0 ? (lyn - 1) / 2 : 0;
                 const int jo = s < 0 ? 0 : (ti.ly - 1) & 1, jn = s < 0 ? (lyn - 1) & 1 : 0;
-                const u32* FE = FACES + te * FACE_STRIDE;
+                const u32* FR = FACES + te * FACE_STRIDE + F_ZHI + cyn * CX;
                 for (int cx = tid; cx < ncx; cx += nthr) {
-                    const u32 a = F[F_ZLO + cyo * CX + cx];
-                    if (!a) continue;
-                    for (int dx = -1; dx <= 1; ++dx) {
-                        const int nx = cx + dx;
-                        if (nx < 0 || nx >= ncx) continue;
-                        const u32 b = FE[F_ZHI + cyn * CX + nx];
-                        if (!b) continue;
-                        if (((a >> 16) & fsel(jo, self_sel(dx))) && ((b >> 16) & fsel(jn, nbr_sel(dx))))
-                            U(t, a, te, b);
-                    }
+                    const u32 a = S[F_ZLO + cyo * CX + cx];
+                    if (a) edge3<false>(FR, 1, a, cx, ncx, jo, jn, t, te, U);
                 }
             }
-            // edges (-1, 0, sx)
-            for (int s = -1; s <= 1; s += 2) {
+            for (int s = -1; s <= 1; s += 2) {                    // edges (-1, 0, s)
                 const int jx = ti.ix + s;
                 if (jx < 0 || jx >= g.nt[2] || g.tblk[2][jx] != g.tblk[2][ti.ix]) continue;
                 const int64_t te = tn + s;
                 const int lxn = g.tlen[2][jx];
                 const int cxo = s < 0 ? 0 : ncx - 1, cxn = s < 0 ? (lxn - 1) / 2 : 0;
                 const int io = s < 0 ? 0 : (ti.lx - 1) & 1, in_ = s < 0 ? (lxn - 1) & 1 : 0;
-                const u32* FE = FACES + te * FACE_STRIDE;
+                const u32* FR = FACES + te * FACE_STRIDE + F_ZHI + cxn;
                 for (int cy = tid; cy < ncy; cy += nthr) {
-                    const u32 a = F[F_ZLO + cy * CX + cxo];
-                    if (!a) continue;
-                    for (int dy = -1; dy <= 1; ++dy) {
-                        const int ny = cy + dy;
-                        if (ny < 0 || ny >= ncy) continue;
-                        const u32 b = FE[F_ZHI + ny * CX + cxn];
-                        if (!b) continue;
-                        if (((a >> 16) & fsel(self_sel(dy), io)) && ((b >> 16) & fsel(nbr_sel(dy), in_)))
-                            U(t, a, te, b);
-                    }
+                    const u32 a = S[F_ZLO + cy * CX + cxo];
+                    if (a) edge3<true>(FR, CX, a, cy, ncy, io, in_, t, te, U);
                 }
             }
-            // corners (-1, sy, sx)
-            if (tid < 4) {
+            if (tid < 4) {                                         // corners (-1, s1, s2)
                 const int s1 = (tid & 2) ? 1 : -1, s2 = (tid & 1) ? 1 : -1;
                 const int jy = ti.iy + s1, jx = ti.ix + s2;
                 if (jy >= 0 && jy < g.nt[1] && jx >= 0 && jx < g.nt[2] &&
@@ -639,7 +718,7 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
                     const int cxo = s2 < 0 ? 0 : ncx - 1, cxn = s2 < 0 ? (lxn - 1) / 2 : 0;
                     const int jo = s1 < 0 ? 0 : (ti.ly - 1) & 1, jn = s1 < 0 ? (lyn - 1) & 1 : 0;
                     const int io = s2 < 0 ? 0 : (ti.lx - 1) & 1, in_ = s2 < 0 ? (lxn - 1) & 1 : 0;
-                    const u32 a = F[F_ZLO + cyo * CX + cxo];
+                    const u32 a = S[F_ZLO + cyo * CX + cxo];
                     const u32 b = FACES[tc * FACE_STRIDE + F_ZHI + cyn * CX + cxn];
                     if (a && b && ((a >> 16) & fsel(jo, io)) && ((b >> 16) & fsel(jn, in_)))
                         U(t, a, tc, b);
@@ -651,57 +730,34 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
     if (ti.iy > 0) {
         const bool same_y = g.tblk[1][ti.iy] == g.tblk[1][ti.iy - 1];
         const int64_t tn = t - sy;
-        const u32* FN = FACES + tn * FACE_STRIDE;
         if (INTER) {
             if (!same_y)
                 for (int e = tid; e < ncz * CX; e += nthr) {
                     const int cx = e % CX;
                     if (cx >= ncx) continue;
-                    const u32 a = F[F_YLO + e];
+                    const u32 a = S[F_YLO + e];
                     if (!a) continue;
-                    const u32 b = FN[F_YHI + e];
+                    const u32 b = S[F_YHI + e];
                     if ((a >> 16) & (b >> 16)) U(t, a, tn, b);
                 }
         } else if (same_y) {
-            // face (0, -1, 0): offsets (dz, dx)
-            for (int e = tid; e < ncz * CX; e += nthr) {
+            for (int e = tid; e < ncz * CX; e += nthr) {          // face (0, -1, 0): offsets (dz, dx)
                 const int cz = e / CX, cx = e % CX;
                 if (cx >= ncx) continue;
-                const u32 a = F[F_YLO + e];
-                if (!a) continue;
-                for (int dz = -1; dz <= 1; ++dz) {
-                    const int nz = cz + dz;
-                    if (nz < 0 || nz >= ncz) continue;
-                    for (int dx = -1; dx <= 1; ++dx) {
-                        const int nx = cx + dx;
-                        if (nx < 0 || nx >= ncx) continue;
-                        const u32 b = FN[F_YHI + nz * CX + nx];
-                        if (!b) continue;
-                        if (((a >> 16) & fsel(self_sel(dz), self_sel(dx))) && ((b >> 16) & fsel(nbr_sel(dz), nbr_sel(dx))))
-                            U(t, a, tn, b);
-                    }
-                }
+                const u32 a = S[F_YLO + e];
+                if (a) face3x3<CX>(S + F_YHI, a, cz, cx, ncz, ncx, t, tn, U);
             }
-            // edges (0, -1, sx)
-            for (int s = -1; s <= 1; s += 2) {
+            for (int s = -1; s <= 1; s += 2) {                    // edges (0, -1, s)
                 const int jx = ti.ix + s;
                 if (jx < 0 || jx >= g.nt[2] || g.tblk[2][jx] != g.tblk[2][ti.ix]) continue;
                 const int64_t te = tn + s;
                 const int lxn = g.tlen[2][jx];
                 const int cxo = s < 0 ? 0 : ncx - 1, cxn = s < 0 ? (lxn - 1) / 2 : 0;
                 const int io = s < 0 ? 0 : (ti.lx - 1) & 1, in_ = s < 0 ? (lxn - 1) & 1 : 0;
-                const u32* FE = FACES + te * FACE_STRIDE;
+                const u32* FR = FACES + te * FACE_STRIDE + F_YHI + cxn;
                 for (int cz = tid; cz < ncz; cz += nthr) {
-                    const u32 a = F[F_YLO + cz * CX + cxo];
-                    if (!a) continue;
-                    for (int dz = -1; dz <= 1; ++dz) {
-                        const int nz = cz + dz;
-                        if (nz < 0 || nz >= ncz) continue;
-                        const u32 b = FE[F_YHI + nz * CX + cxn];
-                        if (!b) continue;
-                        if (((a >> 16) & fsel(self_sel(dz), io)) && ((b >> 16) & fsel(nbr_sel(dz), in_)))
-                            U(t, a, te, b);
-                    }
+                    const u32 a = S[F_YLO + cz * CX + cxo];
+                    if (a) edge3<true>(FR, CX, a, cz, ncz, io, in_, t, te, U);
                 }
             }
         }
@@ -710,72 +766,125 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
     if (ti.ix > 0) {
         const bool same_x = g.tblk[2][ti.ix] == g.tblk[2][ti.ix - 1];
         const int64_t tn = t - 1;
-        const u32* FN = FACES + tn * FACE_STRIDE;
         if (INTER) {
             if (!same_x)
                 for (int e = tid; e < ncz * CY; e += nthr) {
                     const int cy = e % CY;
                     if (cy >= ncy) continue;
-                    const u32 a = F[F_XLO + e];
+                    const u32 a = S[F_XLO + e];
                     if (!a) continue;
-                    const u32 b = FN[F_XHI + e];
+                    const u32 b = S[F_XHI + e];
                     if ((a >> 16) & (b >> 16)) U(t, a, tn, b);
                 }
         } else if (same_x) {
-            for (int e = tid; e < ncz * CY; e += nthr) {
+            for (int e = tid; e < ncz * CY; e += nthr) {          // face (0, 0, -1): offsets (dz, dy)
                 const int cz = e / CY, cy = e % CY;
                 if (cy >= ncy) continue;
-                const u32 a = F[F_XLO + e];
-                if (!a) continue;
-                for (int dz = -1; dz <= 1; ++dz) {
-                    const int nz = cz + dz;
-                    if (nz < 0 || nz >= ncz) continue;
-                    for (int dy = -1; dy <= 1; ++dy) {
-                        const int ny = cy + dy;
-                        if (ny < 0 || ny >= ncy) continue;
-                        const u32 b = FN[F_XHI + nz * CY + ny];
-                        if (!b) continue;
-                        if (((a >> 16) & fsel(self_sel(dz), self_sel(dy))) && ((b >> 16) & fsel(nbr_sel(dz), nbr_sel(dy))))
-                            U(t, a, tn, b);
-                    }
-                }
+                const u32 a = S[F_XLO + e];
+                if (a) face3x3<CY>(S + F_XHI, a, cz, cy, ncz, ncy, t, tn, U);
             }
         }
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// block-local roots -> sort keys
-// ------------------------------------------------------------------------------------------
-// one wave per tile: tile t = blockIdx.x * WAVES + wave
-constexpr int WAVES = NTHREADS / 64;
-
 // Global-memory stitch (one workgroup per tile; keys: first voxel (intra) or rid (inter)).
-// INTRA only runs for tiles of blocks that k_stitch_block could not take (big[block] != 0).
+// INTRA only runs for tiles of blocks that the LDS path could not take (big[block] != 0).
 template <bool INTER>
 __global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restrict__ FACES, u32* P,
                                                      const u64* __restrict__ K, const u8* __restrict__ big) {
     __shared__ u64 hs[HSET];
+    __shared__ u32 S[FACE_STRIDE];
     const int64_t t = blockIdx.x;
     const TileInfo ti = tile_info(g, t);
     if (!INTER && !big[ti.block]) return;
     for (int i = threadIdx.x; i < HSET; i += NTHREADS) hs[i] = ~0ull;
+    stage_faces(g, FACES, t, ti, S, threadIdx.x, NTHREADS);
     __syncthreads();
     const u32 capu = (u32)g.cap;
-    stitch_tile<INTER>(g, FACES, t, ti, threadIdx.x, NTHREADS, [&](int64_t t1, u32 e1, int64_t t2, u32 e2) {
+    stitch_tile<INTER>(g, FACES, S, t, ti, threadIdx.x, NTHREADS, [&](int64_t t1, u32 e1, int64_t t2, u32 e2) {
         const u32 a = (u32)(t1 * capu) + (e1 & 0xFFFFu), b = (u32)(t2 * capu) + (e2 & 0xFFFFu);
         if (hset_insert(hs, ((u64)a << 32) | b)) gunion(P, K, a, b);
     });
 }
 
 // ------------------------------------------------------------------------------------------
-// k_stitch_block: the intra-block (26-connected) seams of one reference block, with the
-// union-find over the block's tile-local components held in LDS (no global atomics).  A block
-// with more than SB_MAXT tiles or SB_LCAP components is flagged in big[] and left to k_stitch.
+// Intra-block seams without global atomics, in two launches:
+//   k_stitch_pairs  one workgroup per tile: connected (own component, neighbour component) pairs
+//                   across its lower intra-block seams, deduplicated in LDS, appended to the
+//                   tile's slot list as block-local ids (local tile << 12 | k);
+//   k_block_uf      one workgroup per block: union-find over the block's components in LDS fed
+//                   by those lists, roots = smallest first voxel; the result goes to P.
+// A block whose lists overflow, or with more than SB_MAXT tiles or SB_LCAP components, is
+// flagged in big[] and stitched by k_stitch<false> instead.
 // ------------------------------------------------------------------------------------------
+constexpr int TPC = 512;           // pair slots per tile
 constexpr int SB_THREADS = 1024;
 constexpr int SB_MAXT = 1024;
 constexpr int SB_LCAP = 8192;
+
+// index of tile t inside its block (z-major over the block's tiles); tile ids fit u32
+__device__ __forceinline__ u32 block_local(const Geom& g, u32 t) {
+    const u32 n2 = (u32)g.nt[2], n1 = (u32)g.nt[1];
+    const u32 q = t / n2, ix = t - q * n2, iz = q / n1, iy = q - iz * n1;
+    const int bz = g.tblk[0][iz], by = g.tblk[1][iy], bx = g.tblk[2][ix];
+    return (u32)(((iz - g.bt0[0][bz]) * g.btn[1][by] + (iy - g.bt0[1][by])) * g.btn[2][bx] + (ix - g.bt0[2][bx]));
+}
+
+// Wave-level duplicate filter: lanes whose key equals the first active lane's key drop out (two
+// rounds); returns whether this lane still has to emit its key.
+__device__ __forceinline__ bool wave_first(u64 key) {
+    const u32 lane = __lane_id();
+#pragma unroll 1
+    for (int r = 0; r < 2; ++r) {
+        const u64 lk = ((u64)__builtin_amdgcn_readfirstlane((u32)(key >> 32)) << 32) |
+                       (u64)__builtin_amdgcn_readfirstlane((u32)key);
+        const u32 leader = __builtin_amdgcn_readfirstlane(lane);
+        if (key == lk) return lane == leader;
+    }
+    return true;
+}
+
+// One wave per tile: stage the seam faces in LDS, emit (own, neighbour) component pairs as
+// block-local ids with wave-aggregated slot allocation.  Duplicates that survive the per-cube
+// (Cand) and per-wave filters are harmless to k_block_uf.
+constexpr int SP_WAVES = 4;
+__global__ __launch_bounds__(SP_WAVES * 64) void k_stitch_pairs(Geom g, const u32* __restrict__ FACES, u64* PAIRS,
+                                                                u32* PC, u8* big) {
+    __shared__ u32 Sall[SP_WAVES][FACE_STRIDE];
+    __shared__ u32 cnt[SP_WAVES];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t t = (int64_t)blockIdx.x * SP_WAVES + w;
+    const bool valid = t < g.n_tiles;
+    u32* S = Sall[w];
+    TileInfo ti;
+    if (valid) {
+        ti = tile_info(g, t);
+        stage_faces(g, FACES, t, ti, S, lane, 64);
+    }
+    if (lane == 0) cnt[w] = 0;
+    __syncthreads();
+    if (!valid) return;
+    const u32 lt_own = block_local(g, (u32)t);
+    u64* out = PAIRS + t * TPC;
+    stitch_tile<false>(g, FACES, S, t, ti, lane, 64, [&](int64_t t1, u32 e1, int64_t t2, u32 e2) {
+        (void)t1;
+        const u32 k1 = e1 & 0xFFFu, k2 = e2 & 0xFFFu;
+        if (!wave_first(((u64)k1 << 52) | ((u64)(t - t2) << 12) | k2)) return;
+        const u64 m = __ballot(1);
+        u32 base = 0;
+        if (lane == (int)(__ffsll((unsigned long long)m) - 1)) base = atomicAdd(&cnt[w], (u32)__popcll(m));
+        base = __builtin_amdgcn_readfirstlane(base);
+        const u32 pos = base + (u32)__popcll(m & ((1ull << lane) - 1));
+        if (pos < TPC) out[pos] = ((u64)((lt_own << 12) | k1) << 32) | ((block_local(g, (u32)t2) << 12) | k2);
+    });
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) {
+        const u32 n = cnt[w];
+        PC[t] = n < TPC ? n : TPC;
+        if (n > TPC) big[ti.block] = 1;
+    }
+}
 
 __device__ __forceinline__ u32 lfind_k(lds_u32* par, u32 x) {
     volatile lds_u32* vp = par;
@@ -803,16 +912,16 @@ __device__ __forceinline__ void lunion_key(lds_u32* par, const u64* key, u32 a, 
     }
 }
 
-__global__ __launch_bounds__(SB_THREADS) void k_stitch_block(Geom g, const u32* __restrict__ FACES,
-                                                             const u32* __restrict__ COUNT, u32* P,
-                                                             const u64* __restrict__ KEY, u8* big) {
+__global__ __launch_bounds__(SB_THREADS) void k_block_uf(Geom g, const u32* __restrict__ COUNT,
+                                                         const u64* __restrict__ PAIRS, const u32* __restrict__ PC,
+                                                         u32* P, const u64* __restrict__ KEY, u8* big) {
     __shared__ u32 noff[SB_MAXT + 1];
     __shared__ u32 lpar[SB_LCAP];
     __shared__ u64 lkey[SB_LCAP];
-    __shared__ u32 red[SB_THREADS / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int NW = SB_THREADS / 64;
     const int64_t b = blockIdx.x;
+    if (big[b]) return;
     const int bx = (int)(b % g.nb[2]), by = (int)((b / g.nb[2]) % g.nb[1]), bz = (int)(b / ((int64_t)g.nb[2] * g.nb[1]));
     const int iz0 = g.bt0[0][bz], iy0 = g.bt0[1][by], ix0 = g.bt0[2][bx];
     const int nz = g.btn[0][bz], ny = g.btn[1][by], nx = g.btn[2][bx];
@@ -825,12 +934,7 @@ __global__ __launch_bounds__(SB_THREADS) void k_stitch_block(Geom g, const u32* 
         const int lx = lt % nx, ly = (lt / nx) % ny, lz = lt / (nx * ny);
         return ((int64_t)(iz0 + lz) * g.nt[1] + (iy0 + ly)) * g.nt[2] + (ix0 + lx);
     };
-    auto local_of = [&](int64_t t) -> int {
-        const int ix = (int)(t % g.nt[2]), iy = (int)((t / g.nt[2]) % g.nt[1]), iz = (int)(t / ((int64_t)g.nt[2] * g.nt[1]));
-        return ((iz - iz0) * ny + (iy - iy0)) * nx + (ix - ix0);
-    };
-    // node offsets: exclusive scan of the tiles' component counts (wave-serial chunks of 64)
-    if (wave == 0) {
+    if (wave == 0) {                       // exclusive scan of the tiles' component counts
         u32 run = 0;
         for (int c0 = 0; c0 < ntb; c0 += 64) {
             const int lt = c0 + lane;
@@ -852,8 +956,6 @@ __global__ __launch_bounds__(SB_THREADS) void k_stitch_block(Geom g, const u32* 
         if (tid == 0) big[b] = 1;
         return;
     }
-    if (tid == 0) big[b] = 0;
-    // nodes: one wave per tile
     for (int lt = wave; lt < ntb; lt += NW) {
         const int64_t t = tile_of(lt);
         const u32 o = noff[lt], n = noff[lt + 1] - o;
@@ -864,24 +966,24 @@ __global__ __launch_bounds__(SB_THREADS) void k_stitch_block(Geom g, const u32* 
     }
     __syncthreads();
     lds_u32* par = as_lds(lpar);
-    for (int lt = 0; lt < ntb; ++lt) {
+    for (int lt = wave; lt < ntb; lt += NW) {
         const int64_t t = tile_of(lt);
-        const TileInfo ti = tile_info(g, t);
-        stitch_tile<false>(g, FACES, t, ti, tid, SB_THREADS, [&](int64_t t1, u32 e1, int64_t t2, u32 e2) {
-            const u32 a = noff[local_of(t1)] + (e1 & 0xFFFFu), c = noff[local_of(t2)] + (e2 & 0xFFFFu);
-            lunion_key(par, lkey, a, c);
-        });
+        const u32 n = PC[t];
+        const u64* pl = PAIRS + t * TPC;
+        for (u32 i = lane; i < n; i += 64) {
+            const u64 pr = pl[i];
+            const u32 a = (u32)(pr >> 32), c = (u32)pr;
+            lunion_key(par, lkey, noff[a >> 12] + (a & 0xFFFu), noff[c >> 12] + (c & 0xFFFu));
+        }
     }
     __syncthreads();
-    // write the block-local roots back to the global union-find
     for (int lt = wave; lt < ntb; lt += NW) {
         const int64_t t = tile_of(lt);
         const u32 o = noff[lt], n = noff[lt + 1] - o;
         for (u32 k = lane; k < n; k += 64) {
             const u32 r = lfind_k(par, o + k);
             if (r != o + k) {
-                // global node of local r: find its tile by binary search over noff
-                int lo = 0, hi = ntb - 1;
+                int lo = 0, hi = ntb - 1;            // tile of local node r
                 while (lo < hi) {
                     const int mid = (lo + hi + 1) >> 1;
                     if (noff[mid] <= r) lo = mid; else hi = mid - 1;
@@ -890,8 +992,9 @@ __global__ __launch_bounds__(SB_THREADS) void k_stitch_block(Geom g, const u32* 
             }
         }
     }
-    (void)red;
 }
+
+constexpr int WAVES = NTHREADS / 64;
 
 // block-local roots per tile (no atomics: counts, then an exclusive scan, then a collect that
 // writes each tile's roots at its scanned offset in node order)

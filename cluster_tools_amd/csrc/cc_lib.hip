@@ -67,7 +67,7 @@ struct cc_ctx {
     // workspace
     DevBuf tiles, bstat, bparam, bits, faces, count, rc, roff, P, KR, FIN, keys, keys2, vals, vals2, seg,
         values, offsets, lut, cub_tmp, scalars, scalars2, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2,
-        flags, map_ids, map_ids2, map_vals, map_par, big;
+        flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc;
     // last run
     int64_t n_blocks = 0;
     uint64_t n_labels = 0;
@@ -294,8 +294,12 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     else
         launch(c, "k_pass1", [&] { k_pass1<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, nullptr, bp, thr, mode, BITS, FACES, COUNT, P, KR); });
     c->big.ensure(nb);
+    c->pairsl.ensure((size_t)nt * TPC * sizeof(u64));
+    c->pc.ensure(nt * sizeof(u32));
     u8* big = c->big.as<u8>();
-    launch(c, "k_stitch_block", [&] { k_stitch_block<<<(unsigned)nb, SB_THREADS, 0, s>>>(g, FACES, COUNT, P, KR, big); });
+    HIP_OK(hipMemsetAsync(big, 0, nb, s));
+    launch(c, "k_stitch_pairs", [&] { k_stitch_pairs<<<(unsigned)((nt + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), big); });
+    launch(c, "k_block_uf", [&] { k_block_uf<<<(unsigned)nb, SB_THREADS, 0, s>>>(g, COUNT, c->pairsl.as<u64>(), c->pc.as<u32>(), P, KR, big); });
     launch(c, "k_stitch_intra", [&] { k_stitch<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, FACES, P, KR, big); });
 
     // block-local roots: per-tile counts -> exclusive scan -> one host read of the total (the one
@@ -575,7 +579,7 @@ void cc_destroy(cc_ctx* c) {
                       &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
                       &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
-                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big};
+                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc};
     for (DevBuf* b : bufs) b->release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
