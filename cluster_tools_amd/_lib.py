@@ -22,7 +22,7 @@ EXPORTS = (
     'cc_get_lut', 'cc_block_components', 'cc_merge_offsets', 'cc_block_faces',
     'cc_merge_assignments', 'cc_write', 'cc_generate_boundary_map', 'cc_set_profiling',
     'cc_get_profile', 'cc_reset_profile', 'cc_shard_begin', 'cc_shard_assign', 'cc_shard_planes',
-    'cc_seam_pairs', 'cc_shard_finish',
+    'cc_seam_pairs', 'cc_shard_finish', 'cc_set_debug',
 )
 
 
@@ -67,6 +67,7 @@ def load():
         'cc_set_profiling': (I, [P, I]),
         'cc_get_profile': (I, [P, ctypes.c_char_p, I, P, P, I]),
         'cc_reset_profile': (I, [P]),
+        'cc_set_debug': (I, [P, I]),
         'cc_shard_begin': (I, [P, P, P, P, P, ctypes.c_double, I, i64, P]),
         'cc_shard_assign': (I, [P, u64]),
         'cc_shard_planes': (I, [P, P, P]),
@@ -273,6 +274,10 @@ class Context:
     # ---- profiling ----
     def set_profiling(self, on=True):
         _check(load().cc_set_profiling(self._h, 1 if on else 0))
+
+    def set_debug(self, flags):
+        """Test hook (include/cc_mi355x.h): 1 = global union-find for intra-block seams."""
+        _check(load().cc_set_debug(self._h, int(flags)))
 
     def reset_profile(self):
         _check(load().cc_reset_profile(self._h))

@@ -519,36 +519,6 @@ __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restr
 //   INTER = true : seams on block faces, 6-connectivity (3 face directions).
 // Keys: first-voxel index (intra) or rid (inter); the union keeps the smaller key as root.
 // ------------------------------------------------------------------------------------------
-// LDS set of (node, node) pairs already sent to the global union-find by this workgroup: most
-// face-cube pairs of a seam connect the same two tile-local components.
-constexpr int HSET = 2048;
-
-__device__ __forceinline__ bool hset_insert(u64* hs, u64 key) {
-    // Face cubes of one component mostly produce the same pair: drop lanes whose key equals the
-    // wave's first active lane's (up to 3 rounds) before touching the LDS table, so identical
-    // keys do not serialise on one LDS address.
-    const u32 lane = __lane_id();
-#pragma unroll 1
-    for (int r = 0; r < 2; ++r) {
-        const u64 lk = ((u64)__builtin_amdgcn_readfirstlane((u32)(key >> 32)) << 32) |
-                       (u64)__builtin_amdgcn_readfirstlane((u32)key);
-        const u32 leader = __builtin_amdgcn_readfirstlane(lane);
-        if (key == lk) {
-            if (lane != leader) return false;
-            break;
-        }
-    }
-    u32 h = (u32)((key * 0x9E3779B97F4A7C15ull) >> 53) & (HSET - 1);
-#pragma unroll 1
-    for (int probe = 0; probe < 16; ++probe) {
-        const u64 old = atomicCAS((unsigned long long*)&hs[h], ~0ull, (unsigned long long)key);
-        if (old == ~0ull) return true;
-        if (old == key) return false;
-        h = (h + 1) & (HSET - 1);
-    }
-    return true;   // table crowded: do the (idempotent) union anyway
-}
-
 // Stage the face planes tile t needs from its three face neighbours into LDS, in the FACE_STRIDE
 // layout: own ZLO/YLO/XLO and the z-/y-/x-lower neighbours' ZHI/YHI/XHI (0 where absent).  One
 // parallel load round instead of dependent global loads per face cube.
@@ -787,26 +757,6 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
     }
 }
 
-// Global-memory stitch (one workgroup per tile; keys: first voxel (intra) or rid (inter)).
-// INTRA only runs for tiles of blocks that the LDS path could not take (big[block] != 0).
-template <bool INTER>
-__global__ __launch_bounds__(NTHREADS) void k_stitch(Geom g, const u32* __restrict__ FACES, u32* P,
-                                                     const u64* __restrict__ K, const u8* __restrict__ big) {
-    __shared__ u64 hs[HSET];
-    __shared__ u32 S[FACE_STRIDE];
-    const int64_t t = blockIdx.x;
-    const TileInfo ti = tile_info(g, t);
-    if (!INTER && !big[ti.block]) return;
-    for (int i = threadIdx.x; i < HSET; i += NTHREADS) hs[i] = ~0ull;
-    stage_faces(g, FACES, t, ti, S, threadIdx.x, NTHREADS);
-    __syncthreads();
-    const u32 capu = (u32)g.cap;
-    stitch_tile<INTER>(g, FACES, S, t, ti, threadIdx.x, NTHREADS, [&](int64_t t1, u32 e1, int64_t t2, u32 e2) {
-        const u32 a = (u32)(t1 * capu) + (e1 & 0xFFFFu), b = (u32)(t2 * capu) + (e2 & 0xFFFFu);
-        if (hset_insert(hs, ((u64)a << 32) | b)) gunion(P, K, a, b);
-    });
-}
-
 // ------------------------------------------------------------------------------------------
 // Intra-block seams without global atomics, in two launches:
 //   k_stitch_pairs  one workgroup per tile: connected (own component, neighbour component) pairs
@@ -884,6 +834,37 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_stitch_pairs(Geom g, const u3
         PC[t] = n < TPC ? n : TPC;
         if (n > TPC) big[ti.block] = 1;
     }
+}
+
+// Global-memory stitch, one wave per tile (keys: first voxel (intra) or rid (inter)).  INTER:
+// tiles with a lower block-face seam; INTRA: only tiles of blocks the LDS path could not take
+// (big[block] != 0).
+template <bool INTER>
+__global__ __launch_bounds__(SP_WAVES * 64) void k_stitch(Geom g, const u32* __restrict__ FACES, u32* P,
+                                                          const u64* __restrict__ K, const u8* __restrict__ big) {
+    __shared__ u32 Sall[SP_WAVES][FACE_STRIDE];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t t = (int64_t)blockIdx.x * SP_WAVES + w;
+    bool active = t < g.n_tiles;
+    u32* S = Sall[w];
+    TileInfo ti;
+    if (active) {
+        ti = tile_info(g, t);
+        if (INTER)
+            active = (ti.iz > 0 && g.tblk[0][ti.iz] != g.tblk[0][ti.iz - 1]) ||
+                     (ti.iy > 0 && g.tblk[1][ti.iy] != g.tblk[1][ti.iy - 1]) ||
+                     (ti.ix > 0 && g.tblk[2][ti.ix] != g.tblk[2][ti.ix - 1]);
+        else
+            active = big[ti.block] != 0;
+        if (active) stage_faces(g, FACES, t, ti, S, lane, 64);
+    }
+    __syncthreads();
+    if (!active) return;
+    const u32 capu = (u32)g.cap;
+    stitch_tile<INTER>(g, FACES, S, t, ti, lane, 64, [&](int64_t t1, u32 e1, int64_t t2, u32 e2) {
+        const u32 a = (u32)(t1 * capu) + (e1 & 0xFFFFu), b = (u32)(t2 * capu) + (e2 & 0xFFFFu);
+        if (wave_first(((u64)a << 32) | b)) gunion(P, K, a, b);
+    });
 }
 
 __device__ __forceinline__ u32 lfind_k(lds_u32* par, u32 x) {

@@ -76,6 +76,7 @@ struct cc_ctx {
     bool lut_valid = false;
     // profiling
     bool prof = false;
+    int debug = 0;         // CC_DEBUG_* test hooks
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, ProfEntry> prof_acc;
@@ -297,10 +298,17 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     c->pairsl.ensure((size_t)nt * TPC * sizeof(u64));
     c->pc.ensure(nt * sizeof(u32));
     u8* big = c->big.as<u8>();
-    HIP_OK(hipMemsetAsync(big, 0, nb, s));
-    launch(c, "k_stitch_pairs", [&] { k_stitch_pairs<<<(unsigned)((nt + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), big); });
-    launch(c, "k_block_uf", [&] { k_block_uf<<<(unsigned)nb, SB_THREADS, 0, s>>>(g, COUNT, c->pairsl.as<u64>(), c->pc.as<u32>(), P, KR, big); });
-    launch(c, "k_stitch_intra", [&] { k_stitch<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, FACES, P, KR, big); });
+    HIP_OK(hipMemsetAsync(big, (c->debug & CC_DEBUG_GLOBAL_STITCH) ? 1 : 0, nb, s));
+    if (!(c->debug & CC_DEBUG_GLOBAL_STITCH)) {
+        launch(c, "k_stitch_pairs", [&] {
+            k_stitch_pairs<<<(unsigned)((nt + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(
+                g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), big);
+        });
+        launch(c, "k_block_uf", [&] {
+            k_block_uf<<<(unsigned)nb, SB_THREADS, 0, s>>>(g, COUNT, c->pairsl.as<u64>(), c->pc.as<u32>(), P, KR, big);
+        });
+    }
+    launch(c, "k_stitch_intra", [&] { k_stitch<false><<<(unsigned)((nt + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(g, FACES, P, KR, big); });
 
     // block-local roots: per-tile counts -> exclusive scan -> one host read of the total (the one
     // mid-run host sync; it sizes the radix sort)
@@ -386,7 +394,7 @@ static void phase_rid(cc_ctx* c, uint64_t base) {
                                                     offsets, c->KR.as<u64>());
         });
     if (!st.local_only)
-        launch(c, "k_stitch_inter", [&] { k_stitch<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->faces.as<u32>(), c->P.as<u32>(), c->KR.as<u64>(), c->big.as<u8>()); });
+        launch(c, "k_stitch_inter", [&] { k_stitch<true><<<(unsigned)((nt + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(g, c->faces.as<u32>(), c->P.as<u32>(), c->KR.as<u64>(), c->big.as<u8>()); });
     st.n_map = 0;
     st.stage = 2;
 }
@@ -689,6 +697,13 @@ int cc_set_profiling(cc_ctx* c, int enable) {
     CC_TRY({
         CC_REQUIRE(c, "ctx is NULL");
         c->prof = enable != 0;
+    })
+}
+
+int cc_set_debug(cc_ctx* c, int flags) {
+    CC_TRY({
+        CC_REQUIRE(c, "ctx is NULL");
+        c->debug = flags;
     })
 }
 

@@ -156,6 +156,10 @@ int cc_set_profiling(cc_ctx* ctx, int enable);
 int cc_get_profile(cc_ctx* ctx, char* names, int names_cap, int64_t* counts, double* total_ms,
                    int cap);
 int cc_reset_profile(cc_ctx* ctx);
+/* Test hook: CC_DEBUG_GLOBAL_STITCH routes every block's intra-block seams through the global
+ * union-find fallback instead of the per-block LDS path (both must give identical results). */
+#define CC_DEBUG_GLOBAL_STITCH 1
+int cc_set_debug(cc_ctx* ctx, int flags);
 
 #ifdef __cplusplus
 }

@@ -142,3 +142,24 @@ def test_c2_vs_oracle(ctx):
     inp = x.cpu().numpy()
     _check_against_oracle(ctx, inp, (128, 128, 128), 0.5, 'greater', res=res,
                           lab=lab.cpu().numpy().view(np.uint64))
+
+
+@pytest.mark.parametrize('shape,bs,mode', SYNTH[:5])
+def test_global_stitch_fallback(ctx, shape, bs, mode):
+    """Intra-block seams through the global union-find (the path for blocks whose pair lists or
+    component counts exceed the per-block LDS union-find) give the same results."""
+    inp = O.boundary_map(shape, origin=(7, 3, 1))
+    ctx.set_debug(1)
+    try:
+        _check_against_oracle(ctx, inp, bs, 0.5, mode)
+    finally:
+        ctx.set_debug(0)
+
+
+def test_white_noise_large_block(ctx):
+    """Many components per tile and per block (block pair lists / LDS capacity overflow -> mixed
+    LDS and global stitching within one volume)."""
+    rng = np.random.default_rng(11)
+    inp = rng.random((64, 192, 256), dtype=np.float32)
+    _check_against_oracle(ctx, inp, (64, 192, 256), 0.3, 'less')
+    _check_against_oracle(ctx, inp, (32, 96, 128), 0.3, 'less')
