@@ -40,8 +40,10 @@ def parse():
     p.add_argument('--shape', default=None, help='override Z,Y,X (per-rank slab for N > 1)')
     p.add_argument('--block-shape', default='64,512,512')
     p.add_argument('--no-cpu-baseline', action='store_true')
-    p.add_argument('--cpu-sample-z', type=int, default=128)
-    p.add_argument('--traffic-json', default=None, help='rocprofv3 PMC summary to fill roofline.traffic')
+    p.add_argument('--cpu-sample-z', type=int, default=1024)
+    p.add_argument('--traffic-json', default=None,
+                   help='tools/prof_summary.py output (rocprofv3 FETCH_SIZE / WRITE_SIZE passes) to fill '
+                        'roofline.traffic; default profiles/traffic_<workload tag>.json when present')
     return p.parse_args()
 
 
@@ -87,7 +89,9 @@ def main():
     else:
         slab = (1024, 2048, 2048) if world == 1 else (256, 4096, 4096)
     gshape = (slab[0] * world,) + slab[1:]
-    workload = ('C3 (1024,2048,2048) f32, 1 GPU' if world == 1 and not args.shape else
+    tag = ('c3' if world == 1 and not args.shape else 'c5slab' if not args.shape else 'custom') + \
+        ('_mask' if args.mask else '') + ('' if args.mode == 'greater' else '_' + args.mode)
+    workload = ('C3%s (1024,2048,2048) f32, 1 GPU' % (' + uint8 mask (C4 at N=1)' if args.mask else '') if world == 1 and not args.shape else
                 'C5-style z-slabs (256N,4096,4096) f32' if not args.shape else 'custom %s' % (gshape,))
 
     ctx = _lib.Context(local_rank)
@@ -145,8 +149,13 @@ def main():
     if dom == 'k_pass1' and args.mask:
         kb += 1.0
     traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        traffic = json.load(open(args.traffic_json)).get(dom)
+    tj = args.traffic_json or os.path.join(ROOT, 'profiles', 'traffic_%s.json' % tag)
+    if os.path.exists(tj):
+        # per-launch HBM bytes of the same kernel on the same workload (PMC passes, corrected as
+        # MI355X_MICROARCH.md §HBM says; tools/prof_summary.py)
+        for k, v in json.load(open(tj)).items():
+            if k.split('<')[0] == dom and 'traffic' in v:
+                traffic = int(v['traffic'])
     roofline = None
     if kb is not None:
         achieved = kb * nvox_rank / (avg_ms * 1e-3) / 1e9

@@ -61,3 +61,13 @@ def test_product_never_imports_oracle():
                     s = line.strip()
                     if s.startswith('import') or s.startswith('from'):
                         assert 'oracle' not in s, (f, s)
+
+
+@pytest.mark.parametrize('gshape,z0,nz', [((37, 20, 23), 0, 37), ((40, 16, 18), 10, 20)])
+def test_device_mask_generator_matches_oracle(gshape, z0, nz):
+    import torch
+    from cluster_tools_amd.synthetic import ellipsoid_mask_device
+    from oracle.synth import ellipsoid_mask
+    got = ellipsoid_mask_device(gshape, z0, nz, torch.device('cpu'), chunk=7).numpy()
+    ref = ellipsoid_mask(gshape)[z0:z0 + nz]
+    assert np.array_equal(got, ref)
