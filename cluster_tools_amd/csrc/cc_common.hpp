@@ -67,6 +67,8 @@ struct TileInfo {
     int64_t block;
 };
 
+__device__ __forceinline__ int cc_tid() { return threadIdx.x; }
+
 // tile ids fit u32 (node ids t * cap are u32, checked on the host): 32-bit division only
 __device__ __forceinline__ TileInfo tile_info(const Geom& g, int64_t t) {
     TileInfo ti;
@@ -177,7 +179,7 @@ __device__ __forceinline__ void gunion(u32* P, const u64* K, u32 a, u32 b) {
 
 // ---- block-wide exclusive scan (NTHREADS threads) ----
 __device__ __forceinline__ u32 block_excl_scan(u32 v, u32* scratch, u32* total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int tid = cc_tid(), lane = tid & 63, wave = tid >> 6;
     u32 x = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {

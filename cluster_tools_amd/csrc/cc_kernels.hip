@@ -105,9 +105,9 @@ __device__ __forceinline__ u64 xlinks(const u64 a[4]) {
 struct TileCCL {
     u64 rstart[NCROW];     // run starts of each cube row (even representation)
     u32 par[NC];           // union-find, entries at run starts only
-    u32 rcnt[NCROW];       // roots per cube row
     u32 scratch[8];
 };
+static_assert(NTHREADS == 4 * NCROW, "tile_ccl maps one thread to each quarter cube row");
 
 __device__ __forceinline__ void load_row4(const u64* rows, int row, u64 a[4]) {
     const int cz = row / CY, cy = row % CY;
@@ -126,19 +126,27 @@ __device__ __forceinline__ u32 run_of(const TileCCL& T, int row, int cx) {
     return (u32)(row * CX + (hibit_le(T.rstart[row], 2 * cx) >> 1));
 }
 
+// quarter q of a cube row: cubes [8q, 8q + 8) = even-representation bits [16q, 16q + 16)
+__device__ __forceinline__ u64 quarter(u64 m, int q) { return m & (0xFFFFull << (16 * q)); }
+
+// Thread (row = tid / 4, q = tid % 4) owns the run starts in quarter q of cube row `row`, so the
+// per-run phases keep all 8 waves busy; tid order is cube order.
 __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T) {
-    const int tid = threadIdx.x;
+    const int tid = cc_tid();
+    const int qrow = tid >> 2, q = tid & 3;
     u32* par = T.par;
     // 1. runs per cube row; every run start is its own parent
-    for (int row = tid; row < NCROW; row += NTHREADS) {
+    u64 Bq;
+    {
         u64 a[4];
-        load_row4(rows, row, a);
+        load_row4(rows, qrow, a);
         const u64 E = xlinks(a);
         const u64 u = a[0] | a[1] | a[2] | a[3];
         const u64 B = (u | (u >> 1)) & EVEN64 & ~(E << 2);
-        T.rstart[row] = B;
-        for (u64 m = B; m; m &= m - 1) {
-            const u32 s0 = (u32)(row * CX + (__builtin_ctzll(m) >> 1));
+        if (q == 0) T.rstart[qrow] = B;
+        Bq = quarter(B, q);
+        for (u64 m = Bq; m; m &= m - 1) {
+            const u32 s0 = (u32)(qrow * CX + (__builtin_ctzll(m) >> 1));
             par[s0] = s0;
         }
     }
@@ -173,39 +181,31 @@ __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T) {
         }
     }
     __syncthreads();
-    // 3. compress run starts; count the roots of each cube row
-    for (int row = tid; row < NCROW; row += NTHREADS) {
-        u32 n = 0;
-        for (u64 m = T.rstart[row]; m; m &= m - 1) {
-            const u32 s0 = (u32)(row * CX + (__builtin_ctzll(m) >> 1));
-            const u32 r = lfind(as_lds(par), s0);
-            par[s0] = r;
-            n += (r == s0);
-        }
-        T.rcnt[row] = n;
+    // 3. compress run starts; count the roots of each quarter row
+    u32 n = 0;
+    for (u64 m = Bq; m; m &= m - 1) {
+        const u32 s0 = (u32)(qrow * CX + (__builtin_ctzll(m) >> 1));
+        const u32 r = lfind(as_lds(par), s0);
+        par[s0] = r;
+        n += (r == s0);
     }
     __syncthreads();
     // 4. compact index k of every root, in cube order
     u32 total = 0;
     {
-        const u32 v = tid < NCROW ? T.rcnt[tid] : 0;
-        const u32 base = block_excl_scan(v, T.scratch, &total);
-        if (tid < NCROW) {
-            u32 k = base;
-            for (u64 m = T.rstart[tid]; m; m &= m - 1) {
-                const u32 s0 = (u32)(tid * CX + (__builtin_ctzll(m) >> 1));
-                if (par[s0] == s0) par[s0] = s0 | (k++ << 16);
-            }
+        const u32 base = block_excl_scan(n, T.scratch, &total);
+        u32 k = base;
+        for (u64 m = Bq; m; m &= m - 1) {
+            const u32 s0 = (u32)(qrow * CX + (__builtin_ctzll(m) >> 1));
+            if (par[s0] == s0) par[s0] = s0 | (k++ << 16);
         }
     }
     __syncthreads();
     // 5. every run start carries its component's k
-    for (int row = tid; row < NCROW; row += NTHREADS) {
-        for (u64 m = T.rstart[row]; m; m &= m - 1) {
-            const u32 s0 = (u32)(row * CX + (__builtin_ctzll(m) >> 1));
-            const u32 r = par[s0] & 0xFFFFu;
-            if (r != s0) par[s0] = r | (par[r] & 0xFFFF0000u);
-        }
+    for (u64 m = Bq; m; m &= m - 1) {
+        const u32 s0 = (u32)(qrow * CX + (__builtin_ctzll(m) >> 1));
+        const u32 r = par[s0] & 0xFFFFu;
+        if (r != s0) par[s0] = r | (par[r] & 0xFFFF0000u);
     }
     __syncthreads();
     return total;
@@ -233,7 +233,7 @@ __device__ __forceinline__ bool vec4_ok(const Geom& g, const TileInfo& ti) {
 template <bool HAS_MASK, class F4, class F1>
 __device__ __forceinline__ void for_tile_rows(const Geom& g, const TileInfo& ti, const float* __restrict__ in,
                                               const u8* __restrict__ mask, F4&& f4, F1&& f1) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int tid_ = cc_tid(), lane = tid_ & 63, wave = tid_ >> 6;
     constexpr int NW = NTHREADS / 64;
     if (vec4_ok(g, ti)) {
         const int q = lane >> 4, i = lane & 15;
@@ -286,12 +286,10 @@ __device__ __forceinline__ void for_tile_rows(const Geom& g, const TileInfo& ti,
 // ------------------------------------------------------------------------------------------
 // k_block_stats: per-block ordered min / max and NaN flag.  One workgroup per tile.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(NTHREADS) void k_block_stats(Geom g, const float* __restrict__ in,
-                                                          u32* smin, u32* smax, u32* sflag) {
-    __shared__ u32 red[3][NTHREADS / 64];
-    const int64_t t = blockIdx.x;
-    const TileInfo ti = tile_info(g, t);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// Stats of one tile folded into its block's (smin, smax, sflag); red = LDS scratch [3][WAVES].
+__device__ __forceinline__ void stats_tile(const Geom& g, const TileInfo& ti, const float* __restrict__ in,
+                                           u32* smin, u32* smax, u32* sflag, u32 (*red)[NTHREADS / 64]) {
+    const int tid_ = cc_tid(), lane = tid_ & 63, wave = tid_ >> 6;
     u32 mn = 0xFFFFFFFFu, mx = 0u;
     bool nan = false;
     auto acc = [&](float x) {
@@ -314,17 +312,25 @@ __global__ __launch_bounds__(NTHREADS) void k_block_stats(Geom g, const float* _
     const bool anynan = __any(nan);
     if (lane == 0) { red[0][wave] = mn; red[1][wave] = mx; red[2][wave] = anynan; }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (tid_ == 0) {
         u32 a = red[0][0], b = red[1][0], f = red[2][0];
         for (int w = 1; w < NTHREADS / 64; ++w) {
             a = red[0][w] < a ? red[0][w] : a;
             b = red[1][w] > b ? red[1][w] : b;
             f |= red[2][w];
         }
-        atomicMin(smin + ti.block, a);
-        atomicMax(smax + ti.block, b);
-        if (f) atomicOr(sflag + ti.block, 1u);
+        // returning atomics: the caller waits for them before it hands the block on
+        const u32 o1 = atomicMin(smin + ti.block, a);
+        const u32 o2 = atomicMax(smax + ti.block, b);
+        const u32 o3 = f ? atomicOr(sflag + ti.block, 1u) : 0u;
+        (void)o1; (void)o2; (void)o3;
     }
+}
+
+__global__ __launch_bounds__(NTHREADS) void k_block_stats(Geom g, const float* __restrict__ in,
+                                                          u32* smin, u32* smax, u32* sflag) {
+    __shared__ u32 red[3][NTHREADS / 64];
+    stats_tile(g, tile_info(g, blockIdx.x), in, smin, smax, sflag, red);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -339,22 +345,18 @@ __device__ __forceinline__ float norm_at(u32 o, float mn, float m) {
     return y;
 }
 
-__global__ void k_block_params(int64_t nb, const u32* smin, const u32* smax, const u32* sflag,
-                               float thr, int mode, BlockParam* bp) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) return;
+__device__ BlockParam block_param(u32 vmin, u32 vmax, u32 vflag, float thr, int mode) {
     BlockParam p;
     p.kind = BP_EMPTY; p.lo = 1; p.hi = 0; p.pad = 0;
-    const u32 omn = smin[b], omx = smax[b];
+    const u32 omn = vmin, omx = vmax;
     const float mn = __uint_as_float(ord2f(omn)), mx = __uint_as_float(ord2f(omx));
     p.mn = mn;
     p.m = 0.0f;
-    if (sflag[b] & 1u) { bp[b] = p; return; }                 // NaN anywhere: numpy min is NaN
+    if (vflag & 1u) return p;                                  // NaN anywhere: numpy min is NaN
     if (isinf(mn) || isinf(mx)) {
         p.kind = BP_EXACT;
         p.m = isinf(mn) ? __uint_as_float(0x7FC00000u) : mx - mn;
-        bp[b] = p;
-        return;
+        return p;
     }
     const float m = mx - mn;
     p.m = m;
@@ -381,7 +383,14 @@ __global__ void k_block_params(int64_t nb, const u32* smin, const u32* smax, con
             if (a <= bb) { p.kind = BP_INTERVAL; p.lo = a; p.hi = bb; }
         }
     }
-    bp[b] = p;
+    return p;
+}
+
+
+__global__ void k_block_params(int64_t nb, const u32* smin, const u32* smax, const u32* sflag,
+                               float thr, int mode, BlockParam* bp) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nb) bp[b] = block_param(smin[b], smax[b], sflag[b], thr, mode);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -391,7 +400,7 @@ template <bool HAS_MASK>
 __device__ __forceinline__ void load_rows(const Geom& g, const TileInfo& ti, const float* __restrict__ in,
                                           const u8* __restrict__ mask, const BlockParam& p, float thr,
                                           int mode, u64* rows) {
-    const int lane = threadIdx.x & 63;
+    const int lane = cc_tid() & 63;
     for_tile_rows<HAS_MASK>(g, ti, in, mask,
         [&](int r, int i, bool act, float4 v, u32 mk) {
             u32 nib = 0;
@@ -457,34 +466,43 @@ __device__ __forceinline__ u32 face_entry(int i, const u64* rows, const TileCCL&
 // ------------------------------------------------------------------------------------------
 // k_pass1: bit rows, tile-local components, their first voxels, face planes
 // ------------------------------------------------------------------------------------------
-template <bool HAS_MASK>
-__global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restrict__ in,
-                                                    const u8* __restrict__ mask, const BlockParam* bp,
-                                                    float thr, int mode, u64* BITS, u32* FACES,
-                                                    u32* COUNT, u32* P, u64* KEY) {
-    __shared__ u64 rows[NROWS];
-    __shared__ TileCCL T;
-    __shared__ u32 key[NC];              // first voxel (tile raster index) of each component
-    const int64_t t = blockIdx.x;
-    const TileInfo ti = tile_info(g, t);
-    const BlockParam p = bp[ti.block];
-    const int tid = threadIdx.x;
+// LDS of one pass-1 tile
+struct Pass1LDS {
+    u64 rows[NROWS];
+    TileCCL T;
+    u32 key[NC];              // first voxel (tile raster index) of each component
+};
+
+// Pass 1 of tile t (block parameters p): bit rows -> BITS, tile CCL -> COUNT, nodes (P, KEY),
+// face planes.  ABL (kernel ablation harness tools/ablate.hip only; 0 in the library): stop
+// after phase ABL (1 bits, 2 CCL, 3 first voxels).
+template <bool HAS_MASK, int ABL = 0>
+__device__ __forceinline__ void pass1_tile(const Geom& g, int64_t t, const TileInfo& ti, const BlockParam& p,
+                                           const float* __restrict__ in, const u8* __restrict__ mask, float thr,
+                                           int mode, u64* BITS, u32* FACES, u32* COUNT, u32* P, u64* KEY,
+                                           Pass1LDS& L) {
+    u64* rows = L.rows;
+    TileCCL& T = L.T;
+    u32* key = L.key;
+    const int tid = cc_tid();
     for (int i = tid; i < NROWS; i += NTHREADS) rows[i] = 0;
     __syncthreads();
     if (p.kind != BP_EMPTY) load_rows<HAS_MASK>(g, ti, in, mask, p, thr, mode, rows);
     __syncthreads();
     for (int i = tid; i < NROWS; i += NTHREADS) BITS[t * NROWS + i] = rows[i];
+    if (ABL == 1) return;
     const u32 R = tile_ccl(rows, T);
+    if (ABL == 2) { if (tid == 0) COUNT[t] = R; return; }
     for (u32 k = tid; k < R; k += NTHREADS) key[k] = NONE;
     __syncthreads();
     // first voxel of each run: voxel order inside a run is (dz, dy) first, then x
-    for (int row = tid; row < NCROW; row += NTHREADS) {
+    {
+        const int row = tid >> 2, q = tid & 3;
         const int cz = row / CY, cy = row % CY;
         u64 a[4];
         load_row4(rows, row, a);
-        const u64 B = T.rstart[row];
         const u64 E = xlinks(a);
-        for (u64 m = B; m; m &= m - 1) {
+        for (u64 m = quarter(T.rstart[row], q); m; m &= m - 1) {
             const int b0 = __builtin_ctzll(m);                              // 2 * start cube
             const u64 tail = ~(E >> b0) & EVEN64;                           // first unlinked cube
             const int b1 = b0 + __builtin_ctzll(tail | (1ull << 62));       // 2 * end cube
@@ -501,6 +519,7 @@ __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restr
     }
     __syncthreads();
     if (tid == 0) COUNT[t] = R;
+    if (ABL == 3) return;
     const u32 base = (u32)(t * g.cap);
     for (u32 k = tid; k < R; k += NTHREADS) {
         const u32 node = base + k;
@@ -511,6 +530,180 @@ __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restr
     }
     u32* F = FACES + t * FACE_STRIDE;
     for (int i = tid; i < FACE_STRIDE; i += NTHREADS) F[i] = face_entry(i, rows, T, ti);
+}
+
+// k_pass1: one workgroup per tile, block parameters precomputed (ablation harness; the library
+// runs pass 1 inside k_front)
+template <bool HAS_MASK, int ABL = 0>
+__global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restrict__ in,
+                                                    const u8* __restrict__ mask, const BlockParam* bp,
+                                                    float thr, int mode, u64* BITS, u32* FACES,
+                                                    u32* COUNT, u32* P, u64* KEY) {
+    __shared__ Pass1LDS L;
+    const int64_t t = blockIdx.x;
+    const TileInfo ti = tile_info(g, t);
+    pass1_tile<HAS_MASK, ABL>(g, t, ti, bp[ti.block], in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L);
+}
+
+// ------------------------------------------------------------------------------------------
+// k_front: block statistics, block parameters and pass 1 in ONE persistent launch, ordered so
+// that pass 1 re-reads a block's input from the 256 MiB Infinity Cache instead of HBM.
+//
+// Work items (one tile each) are taken in order from an atomic ticket: segments
+//   S(0) .. S(lag-1), then S(k), P(k - lag) for k = lag .. nb-1, then P(nb-lag) .. P(nb-1)
+// where S(b) = the stats items of block b's tiles and P(b) = its pass-1 items (ITEMS[i] =
+// tile | is-pass-1 << 31, built by k_front_items from the host's segment table).  The last stats
+// item of a block computes the block's parameters and publishes them; a pass-1 item waits for
+// its block.  The hand-off uses relaxed device-scope atomics only (performed at the coherence
+// point; the writer waits for each step to return before the next).  Every item a pass-1 item can wait on was taken before it, by a
+// workgroup that is running and waits on nothing, so the waits always end (they are also bounded
+// by a clock limit that raises an error flag instead of hanging).  One item per workgroup: the
+// grid has one workgroup per item (a persistent loop raised register pressure past 4 WG / CU).
+// ------------------------------------------------------------------------------------------
+struct FrontArgs {
+    const u32* items;         // 2 * n_tiles entries: tile | is-pass-1 << 31
+    int64_t n_items;
+    u32* smin; u32* smax; u32* sflag;
+    u32* sdone;               // stats items done per block
+    u32* ready;               // block parameters published
+    BlockParam* bp;
+    u32* queue;               // [0] ticket counter, [1] error flag (wait timeout)
+};
+
+// global tile id of local tile lt (z-major inside the block) of block b
+__device__ __forceinline__ int64_t block_tile(const Geom& g, int64_t b, int lt) {
+    const int bx = (int)(b % g.nb[2]), by = (int)((b / g.nb[2]) % g.nb[1]), bz = (int)(b / ((int64_t)g.nb[2] * g.nb[1]));
+    const int nx = g.btn[2][bx], ny = g.btn[1][by];
+    const int lx = lt % nx, ly = (lt / nx) % ny, lz = lt / (nx * ny);
+    return ((int64_t)(g.bt0[0][bz] + lz) * g.nt[1] + (g.bt0[1][by] + ly)) * g.nt[2] + (g.bt0[2][bx] + lx);
+}
+
+__device__ __forceinline__ int block_ntiles(const Geom& g, int64_t b) {
+    const int bx = (int)(b % g.nb[2]), by = (int)((b / g.nb[2]) % g.nb[1]), bz = (int)(b / ((int64_t)g.nb[2] * g.nb[1]));
+    return g.btn[0][bz] * g.btn[1][by] * g.btn[2][bx];
+}
+
+// ITEMS from the segment table SEG (nseg + 1 starts, then nseg u32 block | is-pass-1 << 31)
+__global__ void k_front_items(Geom g, const int64_t* seg, int32_t nseg, u32* items) {
+    const u32* segb = (const u32*)(seg + nseg + 1);
+    CC_FOR(i, seg[nseg]) {
+        int lo = 0, hi = nseg - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (seg[mid] <= i) lo = mid; else hi = mid - 1;
+        }
+        const u32 sb = segb[lo];
+        items[i] = (u32)block_tile(g, sb & 0x7FFFFFFFu, (int)(i - seg[lo])) | (sb & 0x80000000u);
+    }
+}
+
+// tile tables read inside the persistent loop come back in VGPRs (vector loads after stores);
+// the values are workgroup-uniform, so move them to SGPRs
+__device__ __forceinline__ TileInfo uniform_ti(TileInfo ti) {
+    ti.iz = __builtin_amdgcn_readfirstlane(ti.iz); ti.iy = __builtin_amdgcn_readfirstlane(ti.iy);
+    ti.ix = __builtin_amdgcn_readfirstlane(ti.ix); ti.z0 = __builtin_amdgcn_readfirstlane(ti.z0);
+    ti.y0 = __builtin_amdgcn_readfirstlane(ti.y0); ti.x0 = __builtin_amdgcn_readfirstlane(ti.x0);
+    ti.lz = __builtin_amdgcn_readfirstlane(ti.lz); ti.ly = __builtin_amdgcn_readfirstlane(ti.ly);
+    ti.lx = __builtin_amdgcn_readfirstlane(ti.lx);
+    const u64 b = (u64)ti.block;
+    ti.block = (int64_t)(((u64)__builtin_amdgcn_readfirstlane((u32)(b >> 32)) << 32) | __builtin_amdgcn_readfirstlane((u32)b));
+    return ti;
+}
+
+// TV (ablation harness only; 0 in the library): 2 = no wait, 3 = 2 + skip pass-1 items,
+// 4 = 2 + skip stats items, 5 = 3 without the ticket (item = blockIdx.x), 6 = ticket only
+template <bool HAS_MASK, int TV>
+__device__ __forceinline__ void front_item(const Geom& g, const FrontArgs& fa, const float* __restrict__ in,
+                                           const u8* __restrict__ mask, float thr, int mode, u64* BITS,
+                                           u32* FACES, u32* COUNT, u32* P, u64* KEY) {
+    __shared__ Pass1LDS L;
+    __shared__ u32 red[3][NTHREADS / 64];
+    __shared__ u32 s_entry;
+    __shared__ BlockParam s_bp;
+    const int tid = cc_tid();
+    // one item per workgroup, in ticket order (dispatch order is undefined, the ticket is not)
+    if (tid == 0) {
+        const u32 k = TV == 5 ? blockIdx.x : atomicAdd(&fa.queue[0], 1u);
+        s_entry = k < fa.n_items ? fa.items[k] : 0u;
+    }
+    __syncthreads();
+    if (TV == 6) return;
+    {
+        const u32 entry = __builtin_amdgcn_readfirstlane(s_entry);
+        const int64_t t = entry & 0x7FFFFFFFu;
+        const bool is_p1 = entry >> 31;
+        const TileInfo ti = uniform_ti(tile_info(g, t));
+        const int64_t b = ti.block;
+        if ((TV == 3 || TV == 5) && is_p1) return;
+        if (TV == 4 && !is_p1) return;
+        if (!is_p1) {
+            stats_tile(g, ti, in, fa.smin, fa.smax, fa.sflag, red);
+            if (tid == 0) {
+                // the block's min / max / flag atomics (stats_tile) have returned, i.e. are performed
+                // at the coherence point, before this item counts itself done.  Only relaxed
+                // atomics are used for the hand-off: an agent-scope release / acquire would write
+                // back / invalidate this XCD's L2 on every item.
+                __builtin_amdgcn_s_waitcnt(0);
+                const u32 n = (u32)block_ntiles(g, b);
+                const u32 done = atomicAdd(&fa.sdone[b], 1u);
+                if (done + 1 == n) {                      // last stats item of the block
+                    const u32 vmin = atomicMin(&fa.smin[b], 0xFFFFFFFFu);      // atomic reads
+                    const u32 vmax = atomicMax(&fa.smax[b], 0u);
+                    const u32 vfl = atomicOr(&fa.sflag[b], 0u);
+                    const BlockParam bp = block_param(vmin, vmax, vfl, thr, mode);
+                    u32* w = (u32*)&fa.bp[b];
+                    atomicExch(w + 0, __float_as_uint(bp.mn));
+                    atomicExch(w + 1, __float_as_uint(bp.m));
+                    atomicExch(w + 2, bp.lo);
+                    atomicExch(w + 3, bp.hi);
+                    atomicExch(w + 4, bp.kind);
+                    __builtin_amdgcn_s_waitcnt(0);
+                    atomicExch(&fa.ready[b], 1u);
+                }
+            }
+        } else {
+            if (tid == 0) {
+                if (TV < 2 || TV > 6) {
+                    const int64_t t0 = wall_clock64();
+                    while (atomicOr(&fa.ready[b], 0u) == 0u) {
+                        __builtin_amdgcn_s_sleep(4);
+                        if (wall_clock64() - t0 > (int64_t)100000000) {      // ~1 s at 100 MHz: never expected
+                            atomicOr(&fa.queue[1], 1u);
+                            break;
+                        }
+                    }
+                }
+                u32* w = (u32*)&fa.bp[b];
+                const u32 w0 = atomicOr(w + 0, 0u), w1 = atomicOr(w + 1, 0u), w2 = atomicOr(w + 2, 0u),
+                          w3 = atomicOr(w + 3, 0u), w4 = atomicOr(w + 4, 0u);
+                s_bp.mn = __uint_as_float(w0); s_bp.m = __uint_as_float(w1);
+                s_bp.lo = w2; s_bp.hi = w3; s_bp.kind = w4;
+            }
+            __syncthreads();
+            BlockParam p;
+            p.mn = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(s_bp.mn)));
+            p.m = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(s_bp.m)));
+            p.lo = __builtin_amdgcn_readfirstlane(s_bp.lo);
+            p.hi = __builtin_amdgcn_readfirstlane(s_bp.hi);
+            p.kind = __builtin_amdgcn_readfirstlane(s_bp.kind);
+            p.pad = 0;
+            pass1_tile<HAS_MASK>(g, t, ti, p, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L);
+        }
+    }
+}
+
+// without a mask the item fits 64 VGPRs (4 workgroups / CU, the LDS limit); with one it would spill
+template <int TV = 0>
+__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_front(
+    Geom g, FrontArgs fa, const float* __restrict__ in, float thr, int mode, u64* BITS, u32* FACES, u32* COUNT,
+    u32* P, u64* KEY) {
+    front_item<false, TV>(g, fa, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KEY);
+}
+
+__global__ __launch_bounds__(NTHREADS) void k_front_mask(Geom g, FrontArgs fa, const float* __restrict__ in,
+                                                         const u8* __restrict__ mask, float thr, int mode, u64* BITS,
+                                                         u32* FACES, u32* COUNT, u32* P, u64* KEY) {
+    front_item<true, 0>(g, fa, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1228,8 +1421,9 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
 }
 
 // instantiate the templates used by the host side
-template __global__ void k_pass1<false>(Geom, const float*, const u8*, const BlockParam*, float, int, u64*, u32*, u32*, u32*, u64*);
-template __global__ void k_pass1<true>(Geom, const float*, const u8*, const BlockParam*, float, int, u64*, u32*, u32*, u32*, u64*);
+template __global__ void k_front<5>(Geom, FrontArgs, const float*, float, int, u64*, u32*, u32*, u32*, u64*);
+template __global__ void k_front<6>(Geom, FrontArgs, const float*, float, int, u64*, u32*, u32*, u32*, u64*);
+template __global__ void k_front<0>(Geom, FrontArgs, const float*, float, int, u64*, u32*, u32*, u32*, u64*);
 template __global__ void k_stitch<false>(Geom, const u32*, u32*, const u64*, const u8*);
 template __global__ void k_stitch<true>(Geom, const u32*, u32*, const u64*, const u8*);
 template __global__ void k_finalize<false>(Geom, const u32*, u32*, const u64*, const u64*, const u64*, const u64*, int64_t, u64*);

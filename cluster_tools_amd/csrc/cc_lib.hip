@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -19,21 +20,7 @@ using namespace cc;
 
 static thread_local std::string g_err;
 
-struct CCError {
-    std::string msg;
-};
-
-#define HIP_OK(expr)                                                                           \
-    do {                                                                                       \
-        hipError_t e_ = (expr);                                                                \
-        if (e_ != hipSuccess)                                                                  \
-            throw CCError{std::string(#expr) + ": " + hipGetErrorString(e_)};                  \
-    } while (0)
-
-#define CC_REQUIRE(cond, msg)                                                                  \
-    do {                                                                                       \
-        if (!(cond)) throw CCError{msg};                                                       \
-    } while (0)
+#include "cc_host.hpp"
 
 struct DevBuf {
     void* p = nullptr;
@@ -65,7 +52,7 @@ struct cc_ctx {
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     // workspace
-    DevBuf tiles, bstat, bparam, bits, faces, count, rc, roff, P, KR, FIN, keys, keys2, vals, vals2, seg,
+    DevBuf front, tiles, bstat, bparam, bits, faces, count, rc, roff, P, KR, FIN, keys, keys2, vals, vals2, seg,
         values, offsets, lut, cub_tmp, scalars, scalars2, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2,
         flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc;
     // last run
@@ -73,6 +60,7 @@ struct cc_ctx {
     uint64_t n_labels = 0;
     std::vector<uint64_t> h_values, h_offsets;
     std::vector<int32_t> h_tab;
+    std::vector<int64_t> h_front;    // k_front segment table (kept alive until the stream consumed it)
     bool lut_valid = false;
     // profiling
     bool prof = false;
@@ -139,84 +127,12 @@ static inline unsigned grid1d(int64_t n, int bs = 256) {
 }
 static inline unsigned grid_stride(int64_t n, int bs = 256) { return (unsigned)std::min<int64_t>(1 << 20, std::max<int64_t>(1, (n + bs - 1) / bs)); }
 
-// Block grid + tile tables (tiles tiled from each block's origin).
-struct HostGeom {
-    Geom g;
-    std::vector<int32_t> tab;  // [3][3][nt] packed
-    int64_t nvox;
-};
-
-static HostGeom make_geom(const int64_t shape[3], const int64_t block_shape[3], int64_t zoff) {
-    HostGeom hg;
-    Geom& g = hg.g;
-    std::memset(&g, 0, sizeof(g));
-    const int T[3] = {TZ, TY, TX};
-    std::vector<int32_t> st[3], ln[3], bk[3];
-    int maxlen[3] = {0, 0, 0};
-    for (int a = 0; a < 3; ++a) {
-        CC_REQUIRE(shape[a] >= 1 && shape[a] < (1LL << 31), "shape must be in [1, 2^31)");
-        CC_REQUIRE(block_shape[a] >= 1, "block_shape must be >= 1");
-        const int64_t nb = (shape[a] + block_shape[a] - 1) / block_shape[a];
-        g.nb[a] = (int32_t)nb;
-        for (int64_t b = 0; b < nb; ++b) {
-            const int64_t b0 = b * block_shape[a], b1 = std::min(b0 + block_shape[a], shape[a]);
-            for (int64_t s = b0; s < b1; s += T[a]) {
-                const int l = (int)std::min<int64_t>(T[a], b1 - s);
-                st[a].push_back((int32_t)s);
-                ln[a].push_back(l);
-                bk[a].push_back((int32_t)b);
-                maxlen[a] = std::max(maxlen[a], l);
-            }
-        }
-        g.nt[a] = (int32_t)st[a].size();
-    }
-    g.Z = shape[0]; g.Y = shape[1]; g.X = shape[2];
-    g.gY = shape[1]; g.gX = shape[2];
-    g.zoff = zoff;
-    g.n_tiles = (int64_t)g.nt[0] * g.nt[1] * g.nt[2];
-    g.n_blocks = (int64_t)g.nb[0] * g.nb[1] * g.nb[2];
-    g.cap = ((maxlen[0] + 1) / 2) * ((maxlen[1] + 1) / 2) * ((maxlen[2] + 1) / 2);
-    hg.nvox = shape[0] * shape[1] * shape[2];
-    CC_REQUIRE((uint64_t)g.n_tiles * (uint64_t)g.cap < 0xFFFFFFF0ull,
-               "too many tiles x cubes for 32-bit node ids (block shape too small for this volume)");
-    CC_REQUIRE(g.n_blocks < (1LL << (64 - KEY_BITS)), "too many blocks");
-    CC_REQUIRE((uint64_t)(zoff + shape[0]) * (uint64_t)shape[1] * (uint64_t)shape[2] < (1ull << KEY_BITS),
-               "volume too large (>= 2^36 voxels)");
-    CC_REQUIRE(g.n_tiles < (1LL << 31), "too many tiles");
-    for (int a = 0; a < 3; ++a) {
-        hg.tab.insert(hg.tab.end(), st[a].begin(), st[a].end());
-        hg.tab.insert(hg.tab.end(), ln[a].begin(), ln[a].end());
-        hg.tab.insert(hg.tab.end(), bk[a].begin(), bk[a].end());
-    }
-    for (int a = 0; a < 3; ++a) {          // block -> first tile, tile count
-        std::vector<int32_t> b0(g.nb[a], 0), bn(g.nb[a], 0);
-        for (int i = (int)bk[a].size() - 1; i >= 0; --i) { b0[bk[a][i]] = i; bn[bk[a][i]] += 1; }
-        hg.tab.insert(hg.tab.end(), b0.begin(), b0.end());
-        hg.tab.insert(hg.tab.end(), bn.begin(), bn.end());
-    }
-    return hg;
-}
-
 static void upload_geom(cc_ctx* c, HostGeom& hg) {
     c->h_tab = hg.tab;     // kept alive in the ctx until the stream has consumed it
     c->tiles.ensure(c->h_tab.size() * sizeof(int32_t));
     HIP_OK(hipMemcpyAsync(c->tiles.p, c->h_tab.data(), c->h_tab.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                           c->stream));
-    int32_t* base = c->tiles.as<int32_t>();
-    int64_t off = 0;
-    for (int a = 0; a < 3; ++a) {
-        const int n = hg.g.nt[a];
-        hg.g.tstart[a] = base + off;
-        hg.g.tlen[a] = base + off + n;
-        hg.g.tblk[a] = base + off + 2 * n;
-        off += 3 * n;
-    }
-    for (int a = 0; a < 3; ++a) {
-        const int n = hg.g.nb[a];
-        hg.g.bt0[a] = base + off;
-        hg.g.btn[a] = base + off + n;
-        off += 2 * n;
-    }
+    bind_geom_tables(hg, c->tiles.as<int32_t>());
 }
 
 static int to_mode(int mode) {
@@ -261,7 +177,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     const uint64_t nodes = (uint64_t)nt * g.cap;
     hipStream_t s = c->stream;
 
-    c->bstat.ensure(nb * 3 * sizeof(u32));
+    c->bstat.ensure(nb * 5 * sizeof(u32) + 2 * sizeof(u32));
     c->bparam.ensure(nb * sizeof(BlockParam));
     c->bits.ensure(nt * NROWS * sizeof(u64));
     c->faces.ensure(nt * FACE_STRIDE * sizeof(u32));
@@ -273,11 +189,14 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     c->offsets.ensure(nb * sizeof(u64));
     c->scalars.ensure(4 * sizeof(u64));
 
+    // block statistics, parameters and pass 1 in one launch (k_front): smin, smax, sflag, sdone,
+    // ready per block + the item ticket and an error flag
     u32* smin = c->bstat.as<u32>();
     u32* smax = smin + nb;
     u32* sflag = smax + nb;
+    u32* queue = smin + 5 * nb;
     HIP_OK(hipMemsetAsync(smin, 0xFF, nb * sizeof(u32), s));
-    HIP_OK(hipMemsetAsync(smax, 0x00, 2 * nb * sizeof(u32), s));
+    HIP_OK(hipMemsetAsync(smax, 0x00, (4 * nb + 2) * sizeof(u32), s));
     HIP_OK(hipMemsetAsync(c->scalars.p, 0, 4 * sizeof(u64), s));
 
     BlockParam* bp = c->bparam.as<BlockParam>();
@@ -288,12 +207,31 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     u64* KR = c->KR.as<u64>();
     const float thr = st.thr;
 
-    launch(c, "k_block_stats", [&] { k_block_stats<<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, smin, smax, sflag); });
-    launch(c, "k_block_params", [&] { k_block_params<<<grid1d(nb), 256, 0, s>>>(nb, smin, smax, sflag, thr, mode, bp); });
-    if (mask)
-        launch(c, "k_pass1", [&] { k_pass1<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, mask, bp, thr, mode, BITS, FACES, COUNT, P, KR); });
-    else
-        launch(c, "k_pass1", [&] { k_pass1<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, nullptr, bp, thr, mode, BITS, FACES, COUNT, P, KR); });
+    {
+        int64_t lag = 1;
+        if (const char* e = std::getenv("CC_FRONT_LAG")) lag = std::max<int64_t>(1, std::atoll(e));
+        std::vector<int64_t>& h = c->h_front;
+        const int64_t nseg = build_front_segments(st.hg, lag, h);
+        const int64_t n_items = 2 * nt;
+        CC_REQUIRE(n_items < (1LL << 31), "too many tiles for one k_front launch");
+        c->front.ensure(h.size() * sizeof(int64_t) + n_items * sizeof(u32));
+        HIP_OK(hipMemcpyAsync(c->front.p, h.data(), h.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        u32* items = (u32*)(c->front.as<int64_t>() + h.size());
+        launch(c, "k_front_items", [&] {
+            k_front_items<<<grid_stride(n_items), 256, 0, s>>>(g, c->front.as<int64_t>(), (int32_t)nseg, items);
+        });
+        FrontArgs fa;
+        fa.items = items;
+        fa.n_items = n_items;
+        fa.smin = smin; fa.smax = smax; fa.sflag = sflag;
+        fa.sdone = smin + 3 * nb; fa.ready = smin + 4 * nb;
+        fa.bp = bp;
+        fa.queue = queue;
+        if (mask)
+            launch(c, "k_front", [&] { k_front_mask<<<(unsigned)n_items, NTHREADS, 0, s>>>(g, fa, in, mask, thr, mode, BITS, FACES, COUNT, P, KR); });
+        else
+            launch(c, "k_front", [&] { k_front<0><<<(unsigned)n_items, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KR); });
+    }
     c->big.ensure(nb);
     c->pairsl.ensure((size_t)nt * TPC * sizeof(u64));
     c->pc.ensure(nt * sizeof(u32));
@@ -326,9 +264,11 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             HIP_OK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, RC, ROFF, (int)nt + 1, s));
         });
     }
-    u32 n_roots_h = 0;
+    u32 n_roots_h = 0, front_err = 0;
     HIP_OK(hipMemcpyAsync(&n_roots_h, ROFF + nt, sizeof(u32), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(&front_err, queue + 1, sizeof(u32), hipMemcpyDeviceToHost, s));
     sync(c);
+    CC_REQUIRE(front_err == 0, "k_front: a pass-1 item timed out waiting for its block statistics");
     const int64_t nr = n_roots_h;
     st.nr = nr;
     c->keys.ensure(std::max<int64_t>(1, nr) * sizeof(u64));
@@ -583,7 +523,7 @@ void cc_destroy(cc_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->tiles, &c->bstat, &c->bparam, &c->bits, &c->faces, &c->count, &c->rc, &c->roff, &c->P, &c->KR,
+    DevBuf* bufs[] = {&c->front, &c->tiles, &c->bstat, &c->bparam, &c->bits, &c->faces, &c->count, &c->rc, &c->roff, &c->P, &c->KR,
                       &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
                       &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
