@@ -131,6 +131,7 @@ __device__ __forceinline__ u64 quarter(u64 m, int q) { return m & (0xFFFFull << 
 
 // Thread (row = tid / 4, q = tid % 4) owns the run starts in quarter q of cube row `row`, so the
 // per-run phases keep all 8 waves busy; tid order is cube order.
+template <int STOP = 0>   // ablation harness only: return after phase STOP (1..3)
 __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T) {
     const int tid = cc_tid();
     const int qrow = tid >> 2, q = tid & 3;
@@ -151,6 +152,7 @@ __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T) {
         }
     }
     __syncthreads();
+    if (STOP == 1) return 0;
     // 2. unions between runs of neighbouring cube rows: thread = (row, direction group)
     for (int w = tid; w < NCROW * 4; w += NTHREADS) {
         const int row = w % NCROW, grp = w / NCROW;          // grp is uniform per 2 waves
@@ -181,6 +183,7 @@ __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T) {
         }
     }
     __syncthreads();
+    if (STOP == 2) return 0;
     // 3. compress run starts; count the roots of each quarter row
     u32 n = 0;
     for (u64 m = Bq; m; m &= m - 1) {
@@ -190,6 +193,7 @@ __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T) {
         n += (r == s0);
     }
     __syncthreads();
+    if (STOP == 3) return 0;
     // 4. compact index k of every root, in cube order
     u32 total = 0;
     {
@@ -220,68 +224,78 @@ __device__ __forceinline__ u32 cube_k(const TileCCL& T, int c) { return cube_k(T
 // ------------------------------------------------------------------------------------------
 // k_block_stats: per-block ordered min / max and NaN flag.  One workgroup per tile, lane = x.
 // ------------------------------------------------------------------------------------------
-constexpr int UNR = 16;   // rows in flight per wave (scalar path)
-constexpr int G4 = 4;     // float4 row groups (4 rows each) in flight per wave
+// Visit every voxel row of the tile, lane = x: f(j, value, mask byte) for the wave's rows
+// (lz, ly = wave + NW * b), j = lz * RY + b in [0, TZ * RY) the row's slot in the wave (a
+// compile-time constant: the loops are fully unrolled).  One 4-B
+// load per lane and row (256 B per wave instruction) from SGPR row pointers; RZ planes x RY rows
+// = 16 loads in flight per wave.  Full tiles take a branch-free path; on edge tiles lanes past the
+// x extent re-load the last column (duplicates: harmless to min / max; the bit rows are masked
+// by the caller) and rows past the extent are skipped (f is not called for them).
+constexpr int RZ = 4;                       // planes per round
+constexpr int NWAVE = NTHREADS / 64;
+constexpr int RY = TY / NWAVE;              // rows per plane and wave
+static_assert(TZ * RY == 64, "one wave slot per row: a wave owns 64 rows of a tile");
 
-// Can the tile's rows be read as float4 (16-B aligned, 16 lanes per row)?
-__device__ __forceinline__ bool vec4_ok(const Geom& g, const TileInfo& ti) {
-    return ((ti.x0 | ti.lx | (int)(g.X & 3)) & 3) == 0;
-}
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(cc_tid() >> 6); }
 
-// Visit every voxel row of the tile with its values: f(row index r = lz*TY + ly, lane-held
-// values).  Vector path: lane = (row q = lane/16, float4 i = lane%16); scalar path: lane = x.
-template <bool HAS_MASK, class F4, class F1>
+template <bool HAS_MASK, class F>
 __device__ __forceinline__ void for_tile_rows(const Geom& g, const TileInfo& ti, const float* __restrict__ in,
-                                              const u8* __restrict__ mask, F4&& f4, F1&& f1) {
-    const int tid_ = cc_tid(), lane = tid_ & 63, wave = tid_ >> 6;
-    constexpr int NW = NTHREADS / 64;
-    if (vec4_ok(g, ti)) {
-        const int q = lane >> 4, i = lane & 15;
-        const bool xact = 4 * i < ti.lx;
-        for (int r0 = wave * 4 * G4; r0 < NROWS; r0 += NW * 4 * G4) {
-            float4 v[G4];
-            u32 mk[G4];
-            bool act[G4];
+                                              const u8* __restrict__ mask, F&& f) {
+    const int lane = cc_tid() & 63, wave = wave_id();
+    const int64_t sz = g.Y * g.X, sy = NWAVE * g.X;
+    const int64_t o0 = ((int64_t)ti.z0 * g.Y + ti.y0 + wave) * g.X + ti.x0;
+    if (ti.lz == TZ && ti.ly == TY && ti.lx == TX) {
+        const float* pz = in + o0;
+        const u8* mz = HAS_MASK ? mask + o0 : nullptr;
 #pragma unroll
-            for (int j = 0; j < G4; ++j) {
-                const int r = r0 + 4 * j + q, lz = r / TY, ly = r % TY;
-                act[j] = xact && lz < ti.lz && ly < ti.ly;
-                v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-                mk[j] = 0;
-                if (act[j]) {
-                    const int64_t idx = ((int64_t)(ti.z0 + lz) * g.Y + ti.y0 + ly) * g.X + ti.x0 + 4 * i;
-                    v[j] = *reinterpret_cast<const float4*>(in + idx);
-                    if (HAS_MASK) mk[j] = *reinterpret_cast<const u32*>(mask + idx);
+        for (int z0 = 0; z0 < TZ; z0 += RZ, pz += RZ * sz) {
+            float v[RZ][RY];
+            u8 mk[RZ][RY];
+#pragma unroll
+            for (int a = 0; a < RZ; ++a)
+#pragma unroll
+                for (int b = 0; b < RY; ++b) {
+                    v[a][b] = pz[a * sz + b * sy + lane];
+                    if (HAS_MASK) mk[a][b] = mz[(z0 + a) * sz + b * sy + lane];
+                }
+#pragma unroll
+            for (int a = 0; a < RZ; ++a)
+#pragma unroll
+                for (int b = 0; b < RY; ++b) f((z0 + a) * RY + b, v[a][b], HAS_MASK ? (u32)mk[a][b] : 1u);
+        }
+        return;
+    }
+    const int lx = lane < ti.lx ? lane : ti.lx - 1;
+#pragma unroll
+    for (int z0 = 0; z0 < TZ; z0 += RZ) {
+        if (z0 >= ti.lz) break;
+        float v[RZ][RY];
+        u8 mk[RZ][RY];
+#pragma unroll
+        for (int a = 0; a < RZ; ++a)
+#pragma unroll
+            for (int b = 0; b < RY; ++b) {
+                const int lz = z0 + a, ly = wave + NWAVE * b;
+                v[a][b] = 0.0f;
+                mk[a][b] = 0;
+                if (lz < ti.lz && ly < ti.ly) {
+                    const int64_t row = o0 + lz * sz + b * sy;
+                    v[a][b] = in[row + lx];
+                    if (HAS_MASK) mk[a][b] = mask[row + lx];
                 }
             }
 #pragma unroll
-            for (int j = 0; j < G4; ++j) f4(r0 + 4 * j + q, i, act[j], v[j], mk[j]);
-        }
-    } else {
-        const bool act = lane < ti.lx;
-        const int nrows = ti.lz * ti.ly;
-        for (int r0 = wave * UNR; r0 < nrows; r0 += NW * UNR) {
-            float v[UNR];
-            u8 mk[UNR];
+        for (int a = 0; a < RZ; ++a)
 #pragma unroll
-            for (int j = 0; j < UNR; ++j) {
-                const int r = r0 + j;
-                v[j] = 0.0f;
-                mk[j] = 0;
-                if (act && r < nrows) {
-                    const int64_t idx = ((int64_t)(ti.z0 + r / ti.ly) * g.Y + ti.y0 + r % ti.ly) * g.X + ti.x0 + lane;
-                    v[j] = in[idx];
-                    if (HAS_MASK) mk[j] = mask[idx];
-                }
+            for (int b = 0; b < RY; ++b) {
+                const int lz = z0 + a, ly = wave + NWAVE * b;
+                if (lz < ti.lz && ly < ti.ly) f(lz * RY + b, v[a][b], (u32)mk[a][b]);
             }
-#pragma unroll
-            for (int j = 0; j < UNR; ++j) {
-                const int r = r0 + j;
-                f1((r / ti.ly) * TY + r % ti.ly, act && r < nrows, v[j], (u32)mk[j]);
-            }
-        }
     }
 }
+
+// tile row index of wave slot j (see for_tile_rows)
+__device__ __forceinline__ int slot_row(int j, int wave) { return (j / RY) * TY + wave + NWAVE * (j % RY); }
 
 // ------------------------------------------------------------------------------------------
 // k_block_stats: per-block ordered min / max and NaN flag.  One workgroup per tile.
@@ -291,25 +305,20 @@ __device__ __forceinline__ void stats_tile(const Geom& g, const TileInfo& ti, co
                                            u32* smin, u32* smax, u32* sflag, u32 (*red)[NTHREADS / 64]) {
     const int tid_ = cc_tid(), lane = tid_ & 63, wave = tid_ >> 6;
     u32 mn = 0xFFFFFFFFu, mx = 0u;
-    bool nan = false;
-    auto acc = [&](float x) {
-        if (x != x) nan = true;
-        else {
-            const u32 o = f2ord(__float_as_uint(x));
-            mn = o < mn ? o : mn;
-            mx = o > mx ? o : mx;
-        }
-    };
-    for_tile_rows<false>(g, ti, in, nullptr,
-                  [&](int, int, bool act, float4 v, u32) { if (act) { acc(v.x); acc(v.y); acc(v.z); acc(v.w); } },
-                  [&](int, bool act, float v, u32) { if (act) acc(v); });
+    // ordered min / max over all values; a NaN orders above +inf or below -inf, so the NaN flag
+    // is read off the extremes instead of being tested per voxel
+    for_tile_rows<false>(g, ti, in, nullptr, [&](int, float x, u32) {
+        const u32 o = f2ord(__float_as_uint(x));
+        mn = o < mn ? o : mn;
+        mx = o > mx ? o : mx;
+    });
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const u32 a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
         mn = a < mn ? a : mn;
         mx = b > mx ? b : mx;
     }
-    const bool anynan = __any(nan);
+    const bool anynan = mx > 0xFF800000u || mn < 0x007FFFFFu;      // > ord(+inf) or < ord(-inf)
     if (lane == 0) { red[0][wave] = mn; red[1][wave] = mx; red[2][wave] = anynan; }
     __syncthreads();
     if (tid_ == 0) {
@@ -396,34 +405,39 @@ __global__ void k_block_params(int64_t nb, const u32* smin, const u32* smax, con
 // ------------------------------------------------------------------------------------------
 // shared: load the tile's foreground bit rows (threshold + mask) into LDS
 // ------------------------------------------------------------------------------------------
+// Bit rows of the tile into LDS: the wave's 64 row masks are collected one per lane
+// (writelane) and stored with one 8-B LDS write per lane.  Rows outside the tile stay 0.
 template <bool HAS_MASK>
 __device__ __forceinline__ void load_rows(const Geom& g, const TileInfo& ti, const float* __restrict__ in,
                                           const u8* __restrict__ mask, const BlockParam& p, float thr,
                                           int mode, u64* rows) {
-    const int lane = cc_tid() & 63;
-    for_tile_rows<HAS_MASK>(g, ti, in, mask,
-        [&](int r, int i, bool act, float4 v, u32 mk) {
-            u32 nib = 0;
-            if (act) {
-                nib = (u32)voxel_pred(p, v.x, thr, mode) | ((u32)voxel_pred(p, v.y, thr, mode) << 1) |
-                      ((u32)voxel_pred(p, v.z, thr, mode) << 2) | ((u32)voxel_pred(p, v.w, thr, mode) << 3);
-                if (HAS_MASK)
-                    nib &= (u32)((mk & 0xFFu) != 0) | ((u32)((mk & 0xFF00u) != 0) << 1) |
-                           ((u32)((mk & 0xFF0000u) != 0) << 2) | ((u32)((mk & 0xFF000000u) != 0) << 3);
-            }
-            u64 w = (u64)nib << (4 * i);
-            w |= __shfl_xor(w, 1, 64);
-            w |= __shfl_xor(w, 2, 64);
-            w |= __shfl_xor(w, 4, 64);
-            w |= __shfl_xor(w, 8, 64);
-            if (i == 0 && r / TY < ti.lz && r % TY < ti.ly) rows[r] = w;
-        },
-        [&](int r, bool act, float v, u32 mk) {
-            bool fg = act && voxel_pred(p, v, thr, mode);
-            if (HAS_MASK) fg = fg && mk != 0;
-            const u64 bal = __ballot(fg);
-            if (lane == 0 && act) rows[r] = bal;
+    const int lane = cc_tid() & 63, wave = wave_id();
+    const u64 lanes = ti.lx >= 64 ? ~0ull : ((1ull << ti.lx) - 1);
+    u32 mlo = 0, mhi = 0;                   // lane j: row mask of slot j
+    auto put = [&](int j, u64 bal) {
+        bal &= lanes;
+        const u32 blo = (u32)bal, bhi = (u32)(bal >> 32);
+        asm("v_writelane_b32 %0, %1, %2" : "+v"(mlo) : "s"(blo), "i"(j));
+        asm("v_writelane_b32 %0, %1, %2" : "+v"(mhi) : "s"(bhi), "i"(j));
+    };
+    if (p.kind == BP_INTERVAL) {
+        // lo <= ord(x) <= hi as two float compares: the interval never splits -0 from +0 (the
+        // predicate is the same for both) and interval blocks hold no NaN
+        const float flo = __uint_as_float(ord2f(p.lo)), fhi = __uint_as_float(ord2f(p.hi));
+        for_tile_rows<HAS_MASK>(g, ti, in, mask, [&](int j, float x, u32 mk) {
+            u64 bal = __ballot(x >= flo) & __ballot(x <= fhi);
+            if (HAS_MASK) bal &= __ballot(mk != 0);
+            put(j, bal);
         });
+    } else if (p.kind == BP_EXACT) {
+        for_tile_rows<HAS_MASK>(g, ti, in, mask, [&](int j, float x, u32 mk) {
+            bool fg = exact_pred(x, p.mn, p.m, thr, mode);
+            if (HAS_MASK) fg = fg && mk != 0;
+            put(j, __ballot(fg));
+        });
+    }
+    const int r = slot_row(lane, wave);
+    if (r / TY < ti.lz && r % TY < ti.ly) rows[r] = ((u64)mhi << 32) | mlo;
 }
 
 // face plane entry i of a tile (see cc_common.hpp for the layout)
@@ -475,7 +489,7 @@ struct Pass1LDS {
 
 // Pass 1 of tile t (block parameters p): bit rows -> BITS, tile CCL -> COUNT, nodes (P, KEY),
 // face planes.  ABL (kernel ablation harness tools/ablate.hip only; 0 in the library): stop
-// after phase ABL (1 bits, 2 CCL, 3 first voxels).
+// after phase ABL (1 bits, 2 CCL, 3 first voxels; 11..13 inside the CCL after its phase 1..3).
 template <bool HAS_MASK, int ABL = 0>
 __device__ __forceinline__ void pass1_tile(const Geom& g, int64_t t, const TileInfo& ti, const BlockParam& p,
                                            const float* __restrict__ in, const u8* __restrict__ mask, float thr,
@@ -485,12 +499,16 @@ __device__ __forceinline__ void pass1_tile(const Geom& g, int64_t t, const TileI
     TileCCL& T = L.T;
     u32* key = L.key;
     const int tid = cc_tid();
-    for (int i = tid; i < NROWS; i += NTHREADS) rows[i] = 0;
-    __syncthreads();
+    const bool full = ti.lz == TZ && ti.ly == TY && ti.lx == TX;
+    if (!full || p.kind == BP_EMPTY) {
+        for (int i = tid; i < NROWS; i += NTHREADS) rows[i] = 0;
+        __syncthreads();
+    }
     if (p.kind != BP_EMPTY) load_rows<HAS_MASK>(g, ti, in, mask, p, thr, mode, rows);
     __syncthreads();
     for (int i = tid; i < NROWS; i += NTHREADS) BITS[t * NROWS + i] = rows[i];
     if (ABL == 1) return;
+    if (ABL >= 10) { tile_ccl<ABL - 10>(rows, T); return; }
     const u32 R = tile_ccl(rows, T);
     if (ABL == 2) { if (tid == 0) COUNT[t] = R; return; }
     for (u32 k = tid; k < R; k += NTHREADS) key[k] = NONE;

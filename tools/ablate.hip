@@ -142,6 +142,9 @@ int main(int argc, char** argv) {
         }
 #define P1(A) k_pass1<false, A><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, nullptr, bp, thr, mode, BITS, FACES, COUNT, P, KEY)
         r.push_back({"k_pass1_abl1_load_bits", time_ms(s, iters, [&] { P1(1); })});
+        r.push_back({"k_pass1_ccl_ph1_runs", time_ms(s, iters, [&] { P1(11); })});
+        r.push_back({"k_pass1_ccl_ph2_unions", time_ms(s, iters, [&] { P1(12); })});
+        r.push_back({"k_pass1_ccl_ph3_compress", time_ms(s, iters, [&] { P1(13); })});
         r.push_back({"k_pass1_abl2_ccl", time_ms(s, iters, [&] { P1(2); })});
         r.push_back({"k_pass1_abl3_keys", time_ms(s, iters, [&] { P1(3); })});
         r.push_back({"k_pass1_full", time_ms(s, iters, [&] { P1(0); })});
