@@ -835,7 +835,7 @@ __device__ __forceinline__ void edge3(const u32* FR, int RS, u32 a, int q, int n
 // S = stage_faces() copy; edge and corner neighbours are read from FACES.
 //   INTER = false: seams inside one block, 26-connectivity (13 tile directions).
 //   INTER = true : seams on block faces, 6-connectivity (3 face directions).
-template <bool INTER, class UF>
+template <bool INTER, class UF, bool EDGES_ONLY = false>
 __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict__ FACES, const u32* S,
                                             int64_t t, const TileInfo& ti, int tid, int nthr, UF&& U) {
     const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2, ncz = (ti.lz + 1) / 2;
@@ -856,6 +856,7 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
                     if ((a >> 16) & (b >> 16)) U(t, a, tn, b);
                 }
         } else if (same_z) {
+            if (!EDGES_ONLY)
             for (int e = tid; e < ncy * CX; e += nthr) {          // face (-1, 0, 0): offsets (dy, dx)
                 const int cy = e / CX, cx = e % CX;
                 if (cx >= ncx) continue;
@@ -922,6 +923,7 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
                     if ((a >> 16) & (b >> 16)) U(t, a, tn, b);
                 }
         } else if (same_y) {
+            if (!EDGES_ONLY)
             for (int e = tid; e < ncz * CX; e += nthr) {          // face (0, -1, 0): offsets (dz, dx)
                 const int cz = e / CX, cx = e % CX;
                 if (cx >= ncx) continue;
@@ -957,7 +959,7 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
                     const u32 b = S[F_XHI + e];
                     if ((a >> 16) & (b >> 16)) U(t, a, tn, b);
                 }
-        } else if (same_x) {
+        } else if (same_x && !EDGES_ONLY) {
             for (int e = tid; e < ncz * CY; e += nthr) {          // face (0, 0, -1): offsets (dz, dy)
                 const int cz = e / CY, cy = e % CY;
                 if (cy >= ncy) continue;
@@ -1047,12 +1049,205 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_stitch_pairs(Geom g, const u3
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// k_seams: the tile's three lower seams with voxel-row bit masks, one wave per tile.
+//
+// A seam plane is rebuilt from the staged face entries as rows of bits (z seam: rows y, bits x;
+// y seam: rows z, bits x; x seam: rows z, bits y); lane r holds row r of both sides.  Voxel x of
+// own row r touches voxel x + dx of neighbour row r + dr; C = A & shift(B, dx) marks those, and
+// one pair is emitted per run of C (consecutive set voxels of one row are one component on each
+// side).  Intra-block seams use all 9 (dr, dx) (26-connectivity), block faces only (0, 0)
+// (6-connectivity, block_faces.py:99-111).  Intra pairs go to the tile's slot list for k_block_uf
+// (block-local ids), block-face pairs to the tile's inter list (node ids) for k_inter_union;
+// edges and corners (intra only) go through stitch_tile.  Overflowing tiles are flagged: their
+// block (big[]) or the tile itself (iovf[]) is handled by the global fallback k_stitch.
+// ------------------------------------------------------------------------------------------
+constexpr int TPI = 256;           // block-face pair slots per tile
+constexpr int SEAM_HASH_BITS = 9, SEAM_HASH = 1 << SEAM_HASH_BITS;   // per-wave pair set
+
+// row r of a staged face plane F (entries of (r / 2, bit position / 2), bits (r & 1) * 2 + (pos & 1))
+template <int STRIDE>
+__device__ __forceinline__ u64 face_row(const u32* F, int r, int lane) {
+    const bool ok = STRIDE == CX || lane < 2 * STRIDE;
+    const u32 e = ok ? F[(r >> 1) * STRIDE + (lane >> 1)] : 0u;
+    return __ballot((e >> (16 + ((r & 1) << 1) + (lane & 1))) & 1u);
+}
+
+// One seam: own plane FA, neighbour plane FB (STRIDE entries per entry row, NR voxel rows).
+// EMIT(kA, kB) per connected run.
+template <int STRIDE, int NR, class E>
+__device__ __forceinline__ void seam_rows(const u32* FA, const u32* FB, bool full26, int lane, E&& emit) {
+    u32 alo = 0, ahi = 0, blo = 0, bhi = 0;            // lane r: rows r of both sides
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const u64 a = face_row<STRIDE>(FA, r, lane), b = face_row<STRIDE>(FB, r, lane);
+        const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
+        asm("v_writelane_b32 %0, %1, %2" : "+v"(alo) : "s"(a0), "i"(r));
+        asm("v_writelane_b32 %0, %1, %2" : "+v"(ahi) : "s"(a1), "i"(r));
+        asm("v_writelane_b32 %0, %1, %2" : "+v"(blo) : "s"(b0), "i"(r));
+        asm("v_writelane_b32 %0, %1, %2" : "+v"(bhi) : "s"(b1), "i"(r));
+    }
+    const u64 A = ((u64)ahi << 32) | alo, B0 = ((u64)bhi << 32) | blo;
+    // rows r - 1 / r + 1 of the neighbour (all lanes take part in the shuffles: an inactive
+    // source lane would read as 0)
+    const u64 Bm_ = __shfl(B0, lane > 0 ? lane - 1 : 0, 64), Bp = __shfl(B0, lane + 1 < 64 ? lane + 1 : 63, 64);
+    const u64 Bm = lane > 0 ? Bm_ : 0ull;
+    if (lane >= NR || !A) return;
+    u32 la = NONE, lb = NONE;                                         // last pair emitted by this lane
+#pragma unroll
+    for (int dr = -1; dr <= 1; ++dr) {
+        if (dr && !full26) continue;
+        const u64 B = dr < 0 ? Bm : dr > 0 ? (lane + 1 < NR ? Bp : 0ull) : B0;
+        if (!B) continue;
+        const int rb = lane + dr;
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+            if (dx && !full26) continue;
+            const u64 C = A & (dx > 0 ? B >> 1 : dx < 0 ? B << 1 : B);
+            for (u64 m = C & ~(C << 1); m; m &= m - 1) {
+                const int x = __builtin_ctzll(m);
+                const u32 ka = FA[(lane >> 1) * STRIDE + (x >> 1)] & 0xFFFFu;
+                const u32 kb = FB[(rb >> 1) * STRIDE + ((x + dx) >> 1)] & 0xFFFFu;
+                if (ka == la && kb == lb) continue;             // cheap first filter
+                la = ka; lb = kb;
+                emit(ka, kb);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const u32* __restrict__ FACES, u64* PAIRS, u32* PC,
+                                                         u8* big, u64* IPAIRS, u32* IPC, u8* iovf) {
+    __shared__ u32 Sall[SP_WAVES][FACE_STRIDE];
+    __shared__ u32 Hall[SP_WAVES][SEAM_HASH];
+    __shared__ u32 cnt[SP_WAVES][2];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t t = (int64_t)blockIdx.x * SP_WAVES + w;
+    const bool valid = t < g.n_tiles;
+    u32* S = Sall[w];
+    u32* H = Hall[w];
+    TileInfo ti;
+    if (valid) {
+        ti = tile_info(g, t);
+        stage_faces(g, FACES, t, ti, S, lane, 64);
+    }
+    for (int i = lane; i < SEAM_HASH; i += 64) H[i] = NONE;
+    if (lane < 2) cnt[w][lane] = 0;
+    __syncthreads();
+    if (!valid) return;
+    const u32 lt_own = block_local(g, (u32)t);
+    const u32 capu = (u32)g.cap;
+    u64* out = PAIRS + t * TPC;
+    u64* iout = IPAIRS + t * TPI;
+    // wave-aggregated append of one pair per active lane to list `which` (0 intra, 1 inter)
+    auto append = [&](int which, u64 v) {
+        const u64 m = __ballot(1);
+        u32 base = 0;
+        if (lane == (int)(__ffsll((unsigned long long)m) - 1)) base = atomicAdd(&cnt[w][which], (u32)__popcll(m));
+        base = __builtin_amdgcn_readfirstlane(base);
+        const u32 pos = base + (u32)__popcll(m & ((1ull << lane) - 1));
+        if (which == 0) { if (pos < TPC) out[pos] = v; }
+        else if (pos < TPI) iout[pos] = v;
+    };
+    const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
+    // exact code of a lower neighbour tile (the 13 lex-negative offsets)
+    auto dir_code = [&](int64_t tn) -> u32 {
+        const int64_t d = t - tn;
+        u32 c = 0;
+#pragma unroll
+        for (int dz = 0; dz <= 1; ++dz)
+#pragma unroll
+            for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                for (int dx = -1; dx <= 1; ++dx) {
+                    const int code = dz * 9 + (dy + 1) * 3 + (dx + 1);   // d = dz sz - dy sy - dx
+                    if (d == dz * sz - dy * sy - dx) c = (u32)code;
+                }
+        return c;
+    };
+    // first sighting of (neighbour, ka, kb) in this tile? (LDS hash set; a full set lets
+    // duplicates through, which the consumers tolerate)
+    auto fresh = [&](u32 code, u32 ka, u32 kb) -> bool {
+        const u32 key = (code << 24) | ((ka & 0xFFFu) << 12) | (kb & 0xFFFu);
+        u32 h = (key * 0x9E3779B1u) >> (32 - SEAM_HASH_BITS);
+        for (int probe = 0; probe < 32; ++probe) {
+            const u32 old = atomicCAS(&H[h], NONE, key);
+            if (old == NONE) return true;
+            if (old == key) return false;
+            h = (h + 1) & (SEAM_HASH - 1);
+        }
+        return true;
+    };
+    auto intra = [&](int64_t tn) {
+        const u32 lt_n = block_local(g, (u32)tn), code = dir_code(tn);
+        return [&, lt_n, code](u32 ka, u32 kb) {
+            if (!fresh(code, ka, kb)) return;
+            append(0, ((u64)((lt_own << 12) | ka) << 32) | ((lt_n << 12) | kb));
+        };
+    };
+    auto inter = [&](int64_t tn) {
+        const u32 code = dir_code(tn);
+        return [&, tn, code](u32 ka, u32 kb) {
+            if (!fresh(code, ka, kb)) return;
+            append(1, ((u64)((u32)t * capu + ka) << 32) | ((u32)tn * capu + kb));
+        };
+    };
+    if (ti.iz > 0) {                                   // z seam: rows y, bits x
+        const bool same = g.tblk[0][ti.iz] == g.tblk[0][ti.iz - 1];
+        if (same) seam_rows<CX, TY>(S + F_ZLO, S + F_ZHI, true, lane, intra(t - sz));
+        else seam_rows<CX, TY>(S + F_ZLO, S + F_ZHI, false, lane, inter(t - sz));
+    }
+    if (ti.iy > 0) {                                   // y seam: rows z, bits x
+        const bool same = g.tblk[1][ti.iy] == g.tblk[1][ti.iy - 1];
+        if (same) seam_rows<CX, TZ>(S + F_YLO, S + F_YHI, true, lane, intra(t - sy));
+        else seam_rows<CX, TZ>(S + F_YLO, S + F_YHI, false, lane, inter(t - sy));
+    }
+    if (ti.ix > 0) {                                   // x seam: rows z, bits y
+        const bool same = g.tblk[2][ti.ix] == g.tblk[2][ti.ix - 1];
+        if (same) seam_rows<CY, TZ>(S + F_XLO, S + F_XHI, true, lane, intra(t - 1));
+        else seam_rows<CY, TZ>(S + F_XLO, S + F_XHI, false, lane, inter(t - 1));
+    }
+    // edges and corners inside the block
+    auto edge_u = [&](int64_t, u32 e1, int64_t t2, u32 e2) {
+        const u32 k1 = e1 & 0xFFFu, k2 = e2 & 0xFFFu;
+        if (!fresh(dir_code(t2), k1, k2)) return;
+        append(0, ((u64)((lt_own << 12) | k1) << 32) | ((block_local(g, (u32)t2) << 12) | k2));
+    };
+    stitch_tile<false, decltype(edge_u)&, true>(g, FACES, S, t, ti, lane, 64, edge_u);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) {
+        const u32 n = cnt[w][0], ni = cnt[w][1];
+        PC[t] = n < TPC ? n : TPC;
+        if (n > TPC) big[ti.block] = 1;
+        IPC[t] = ni < TPI ? ni : TPI;
+        if (ni > TPI) iovf[t] = 1;
+    }
+}
+
+// Block-face unions from the k_seams lists, one wave per tile: node pairs -> current roots,
+// duplicate root pairs dropped per wave, union keyed by rid (the smaller rid becomes the root).
+__global__ __launch_bounds__(SP_WAVES * 64) void k_inter_union(Geom g, const u64* __restrict__ IPAIRS,
+                                                               const u32* __restrict__ IPC, u32* P,
+                                                               const u64* __restrict__ K) {
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * SP_WAVES + (threadIdx.x >> 6);
+    if (t >= g.n_tiles) return;
+    const u32 n = IPC[t];
+    for (u32 i = lane; i < n; i += 64) {
+        const u64 pr = IPAIRS[t * TPI + i];
+        const u32 ra = gfind(P, (u32)(pr >> 32)), rb = gfind(P, (u32)pr);
+        if (ra != rb && wave_first(((u64)ra << 32) | rb)) gunion(P, K, ra, rb);
+    }
+}
+
 // Global-memory stitch, one wave per tile (keys: first voxel (intra) or rid (inter)).  INTER:
 // tiles with a lower block-face seam; INTRA: only tiles of blocks the LDS path could not take
 // (big[block] != 0).
 template <bool INTER>
 __global__ __launch_bounds__(SP_WAVES * 64) void k_stitch(Geom g, const u32* __restrict__ FACES, u32* P,
-                                                          const u64* __restrict__ K, const u8* __restrict__ big) {
+                                                          const u64* __restrict__ K, const u8* __restrict__ big,
+                                                          const u8* __restrict__ only) {
     __shared__ u32 Sall[SP_WAVES][FACE_STRIDE];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t t = (int64_t)blockIdx.x * SP_WAVES + w;
@@ -1062,9 +1257,9 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_stitch(Geom g, const u32* __r
     if (active) {
         ti = tile_info(g, t);
         if (INTER)
-            active = (ti.iz > 0 && g.tblk[0][ti.iz] != g.tblk[0][ti.iz - 1]) ||
+            active = (!only || only[t]) && ((ti.iz > 0 && g.tblk[0][ti.iz] != g.tblk[0][ti.iz - 1]) ||
                      (ti.iy > 0 && g.tblk[1][ti.iy] != g.tblk[1][ti.iy - 1]) ||
-                     (ti.ix > 0 && g.tblk[2][ti.ix] != g.tblk[2][ti.ix - 1]);
+                     (ti.ix > 0 && g.tblk[2][ti.ix] != g.tblk[2][ti.ix - 1]));
         else
             active = big[ti.block] != 0;
         if (active) stage_faces(g, FACES, t, ti, S, lane, 64);
@@ -1442,8 +1637,8 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
 template __global__ void k_front<5>(Geom, FrontArgs, const float*, float, int, u64*, u32*, u32*, u32*, u64*);
 template __global__ void k_front<6>(Geom, FrontArgs, const float*, float, int, u64*, u32*, u32*, u32*, u64*);
 template __global__ void k_front<0>(Geom, FrontArgs, const float*, float, int, u64*, u32*, u32*, u32*, u64*);
-template __global__ void k_stitch<false>(Geom, const u32*, u32*, const u64*, const u8*);
-template __global__ void k_stitch<true>(Geom, const u32*, u32*, const u64*, const u8*);
+template __global__ void k_stitch<false>(Geom, const u32*, u32*, const u64*, const u8*, const u8*);
+template __global__ void k_stitch<true>(Geom, const u32*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_finalize<false>(Geom, const u32*, u32*, const u64*, const u64*, const u64*, const u64*, int64_t, u64*);
 template __global__ void k_finalize<true>(Geom, const u32*, u32*, const u64*, const u64*, const u64*, const u64*, int64_t, u64*);
 template __global__ void k_plane_labels<false>(Geom, const u32*, u32*, const u64*, u64*);

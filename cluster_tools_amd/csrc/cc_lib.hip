@@ -54,7 +54,7 @@ struct cc_ctx {
     // workspace
     DevBuf front, tiles, bstat, bparam, bits, faces, count, rc, roff, P, KR, FIN, keys, keys2, vals, vals2, seg,
         values, offsets, lut, cub_tmp, scalars, scalars2, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2,
-        flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc;
+        flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf;
     // last run
     int64_t n_blocks = 0;
     uint64_t n_labels = 0;
@@ -235,18 +235,24 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     c->big.ensure(nb);
     c->pairsl.ensure((size_t)nt * TPC * sizeof(u64));
     c->pc.ensure(nt * sizeof(u32));
+    c->ipairs.ensure((size_t)nt * TPI * sizeof(u64));
+    c->ipc.ensure(nt * sizeof(u32));
+    c->iovf.ensure(nt);
     u8* big = c->big.as<u8>();
     HIP_OK(hipMemsetAsync(big, (c->debug & CC_DEBUG_GLOBAL_STITCH) ? 1 : 0, nb, s));
+    HIP_OK(hipMemsetAsync(c->iovf.p, (c->debug & CC_DEBUG_GLOBAL_STITCH) ? 1 : 0, nt, s));
+    HIP_OK(hipMemsetAsync(c->ipc.p, 0, nt * sizeof(u32), s));
     if (!(c->debug & CC_DEBUG_GLOBAL_STITCH)) {
-        launch(c, "k_stitch_pairs", [&] {
-            k_stitch_pairs<<<(unsigned)((nt + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(
-                g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), big);
+        launch(c, "k_seams", [&] {
+            k_seams<<<(unsigned)((nt + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(
+                g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), big, c->ipairs.as<u64>(), c->ipc.as<u32>(),
+                c->iovf.as<u8>());
         });
         launch(c, "k_block_uf", [&] {
             k_block_uf<<<(unsigned)nb, SB_THREADS, 0, s>>>(g, COUNT, c->pairsl.as<u64>(), c->pc.as<u32>(), P, KR, big);
         });
     }
-    launch(c, "k_stitch_intra", [&] { k_stitch<false><<<(unsigned)((nt + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(g, FACES, P, KR, big); });
+    launch(c, "k_stitch_intra", [&] { k_stitch<false><<<(unsigned)((nt + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(g, FACES, P, KR, big, nullptr); });
 
     // block-local roots: per-tile counts -> exclusive scan -> one host read of the total (the one
     // mid-run host sync; it sizes the radix sort)
@@ -333,8 +339,14 @@ static void phase_rid(cc_ctx* c, uint64_t base) {
             k_assign_rid<<<grid1d(nr), 256, 0, s>>>(nr, c->keys2.as<u64>(), c->vals2.as<u32>(), c->seg.as<u32>(),
                                                     offsets, c->KR.as<u64>());
         });
-    if (!st.local_only)
-        launch(c, "k_stitch_inter", [&] { k_stitch<true><<<(unsigned)((nt + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(g, c->faces.as<u32>(), c->P.as<u32>(), c->KR.as<u64>(), c->big.as<u8>()); });
+    if (!st.local_only) {
+        const unsigned grid = (unsigned)((nt + SP_WAVES - 1) / SP_WAVES);
+        launch(c, "k_inter_union", [&] {
+            k_inter_union<<<grid, SP_WAVES * 64, 0, s>>>(g, c->ipairs.as<u64>(), c->ipc.as<u32>(), c->P.as<u32>(), c->KR.as<u64>());
+        });
+        // tiles whose block-face pairs overflowed their list (and every tile under CC_DEBUG_GLOBAL_STITCH)
+        launch(c, "k_stitch_inter", [&] { k_stitch<true><<<grid, SP_WAVES * 64, 0, s>>>(g, c->faces.as<u32>(), c->P.as<u32>(), c->KR.as<u64>(), c->big.as<u8>(), c->iovf.as<u8>()); });
+    }
     st.n_map = 0;
     st.stage = 2;
 }
@@ -527,7 +539,7 @@ void cc_destroy(cc_ctx* c) {
                       &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
                       &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
-                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc};
+                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf};
     for (DevBuf* b : bufs) b->release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);

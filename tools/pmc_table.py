@@ -10,7 +10,7 @@ for r in csv.DictReader(open(f)):
     key = (int(r['Dispatch_Id']), n)
     per.setdefault(key, {})[r['Counter_Name']] = float(r['Counter_Value'])
 seen = set()
-cols = ['SQ_INSTS_VALU', 'SQ_INSTS_SALU', 'SQ_INSTS_LDS', 'SQ_LDS_BANK_CONFLICT', 'SQ_WAIT_ANY', 'SQ_ACTIVE_INST_ANY', 'SQ_WAVE_CYCLES']
+cols = ['SQ_INSTS_VALU', 'SQ_INSTS_SALU', 'SQ_INSTS_LDS', 'SQ_LDS_BANK_CONFLICT', 'SQ_WAIT_ANY', 'SQ_ACTIVE_INST_ANY', 'SQ_WAVE_CYCLES', 'SQ_INSTS_VMEM_RD']
 print('%-34s' % 'kernel (per tile)' + ''.join('%12s' % c.replace('SQ_', '')[:11] for c in cols))
 for (did, n), v in sorted(per.items()):
     if n in seen or n.startswith('__amd') or 'generate' in n:
