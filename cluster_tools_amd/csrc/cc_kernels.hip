@@ -407,6 +407,8 @@ __global__ void k_block_params(int64_t nb, const u32* smin, const u32* smax, con
 // ------------------------------------------------------------------------------------------
 // Bit rows of the tile into LDS: the wave's 64 row masks are collected one per lane
 // (writelane) and stored with one 8-B LDS write per lane.  Rows outside the tile stay 0.
+// The v_writelane asm relies on wave-uniform control flow here (the wave index and the tile are
+// SGPR values); under a branch the compiler treats as divergent it produced wrong rows (k_seams).
 template <bool HAS_MASK>
 __device__ __forceinline__ void load_rows(const Geom& g, const TileInfo& ti, const float* __restrict__ in,
                                           const u8* __restrict__ mask, const BlockParam& p, float thr,
@@ -736,18 +738,33 @@ __global__ __launch_bounds__(NTHREADS) void k_front_mask(Geom g, FrontArgs fa, c
 __device__ __forceinline__ void stage_faces(const Geom& g, const u32* __restrict__ FACES, int64_t t,
                                             const TileInfo& ti, u32* S, int tid, int nthr) {
     const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
-    for (int i = tid; i < FACE_STRIDE; i += nthr) {
-        u32 v = 0;
-        if (i < F_ZHI || (i >= F_YLO && i < F_YHI) || (i >= F_XLO && i < F_XHI)) {
-            v = FACES[t * FACE_STRIDE + i];
-        } else if (i < F_YLO) {
-            if (ti.iz > 0) v = FACES[(t - sz) * FACE_STRIDE + i];
-        } else if (i < F_XLO) {
-            if (ti.iy > 0) v = FACES[(t - sy) * FACE_STRIDE + i];
-        } else {
-            if (ti.ix > 0) v = FACES[(t - 1) * FACE_STRIDE + i];
+    // source tile of entry i: own lower faces, the lower neighbours' upper faces (-1: absent)
+    auto src = [&](int i) -> int64_t {
+        if (i < F_ZHI || (i >= F_YLO && i < F_YHI) || (i >= F_XLO && i < F_XHI)) return t;
+        if (i < F_YLO) return ti.iz > 0 ? t - sz : -1;
+        if (i < F_XLO) return ti.iy > 0 ? t - sy : -1;
+        return ti.ix > 0 ? t - 1 : -1;
+    };
+    if (nthr == 64) {
+        // one wave: every load issued before the first LDS write (one memory round trip); the
+        // face regions are multiples of 64 entries, so each unrolled step reads one tile
+        constexpr int NJ = (FACE_STRIDE + 63) / 64;
+        static_assert(F_Z % 64 == 0 && F_Y % 64 == 0 && F_X % 64 == 0, "face regions are whole waves");
+        u32 v[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int i = tid + 64 * j;
+            const int64_t ts = src(64 * j);
+            v[j] = (i < FACE_STRIDE && ts >= 0) ? FACES[ts * FACE_STRIDE + i] : 0u;
         }
-        S[i] = v;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+            if (tid + 64 * j < FACE_STRIDE) S[tid + 64 * j] = v[j];
+        return;
+    }
+    for (int i = tid; i < FACE_STRIDE; i += nthr) {
+        const int64_t ts = src(i);
+        S[i] = ts >= 0 ? FACES[ts * FACE_STRIDE + i] : 0u;
     }
 }
 
@@ -1065,6 +1082,15 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_stitch_pairs(Geom g, const u3
 constexpr int TPI = 256;           // block-face pair slots per tile
 constexpr int SEAM_HASH_BITS = 9, SEAM_HASH = 1 << SEAM_HASH_BITS;   // per-wave pair set
 
+// compile-time loop: f(std::integral_constant<int, i>) for i in [0, N)
+template <int N, class F, int I = 0>
+__device__ __forceinline__ void unroll_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        unroll_for<N, F, I + 1>(static_cast<F&&>(f));
+    }
+}
+
 // row r of a staged face plane F (entries of (r / 2, bit position / 2), bits (r & 1) * 2 + (pos & 1))
 template <int STRIDE>
 __device__ __forceinline__ u64 face_row(const u32* F, int r, int lane) {
@@ -1073,63 +1099,288 @@ __device__ __forceinline__ u64 face_row(const u32* F, int r, int lane) {
     return __ballot((e >> (16 + ((r & 1) << 1) + (lane & 1))) & 1u);
 }
 
-// One seam: own plane FA, neighbour plane FB (STRIDE entries per entry row, NR voxel rows).
-// EMIT(kA, kB) per connected run.
-template <int STRIDE, int NR, class E>
-__device__ __forceinline__ void seam_rows(const u32* FA, const u32* FB, bool full26, int lane, E&& emit) {
-    u32 alo = 0, ahi = 0, blo = 0, bhi = 0;            // lane r: rows r of both sides
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        const u64 a = face_row<STRIDE>(FA, r, lane), b = face_row<STRIDE>(FB, r, lane);
-        const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
-        asm("v_writelane_b32 %0, %1, %2" : "+v"(alo) : "s"(a0), "i"(r));
-        asm("v_writelane_b32 %0, %1, %2" : "+v"(ahi) : "s"(a1), "i"(r));
-        asm("v_writelane_b32 %0, %1, %2" : "+v"(blo) : "s"(b0), "i"(r));
-        asm("v_writelane_b32 %0, %1, %2" : "+v"(bhi) : "s"(b1), "i"(r));
-    }
+// lane L of w[0..3] = the (uniform) rows a, b split in 32-bit halves
+// (a select, not v_writelane inline asm: the asm form gave wrong rows in this kernel)
+template <int L>
+__device__ __forceinline__ void put_rows(u32 (&w)[4], u64 a, u64 b) {
+#ifdef CC_PUT_ASM
+    const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(w[0]) : "s"(a0), "i"(L));
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(w[1]) : "s"(a1), "i"(L));
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(w[2]) : "s"(b0), "i"(L));
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(w[3]) : "s"(b1), "i"(L));
+    return;
+#endif
+    if ((int)__lane_id() == L) { w[0] = (u32)a; w[1] = (u32)(a >> 32); w[2] = (u32)b; w[3] = (u32)(b >> 32); }
+}
+
+// The three lower seams at once, one voxel row per lane: lanes 0-31 the z seam (rows y, bits x),
+// 32-47 the y seam (rows z, bits x), 48-63 the x seam (rows z, bits y).  mode[s]: 0 no seam,
+// 1 inside the block (all 9 (dr, dx): 26-connectivity), 2 block face ((0, 0): 6-connectivity).
+// EMIT(seam, kA, kB) once per run of contacts.
+template <class EM>
+__device__ __forceinline__ void seam_rows3(const u32* S, const int mode[3], int lane, EM&& emit) {
+    u32 w4[4] = {0, 0, 0, 0};                          // this lane's row of both sides (lo, hi)
+    if (mode[0])
+        unroll_for<TY>([&](auto R) {
+            put_rows<decltype(R)::value>(w4, face_row<CX>(S + F_ZLO, R.value, lane), face_row<CX>(S + F_ZHI, R.value, lane));
+        });
+    if (mode[1])
+        unroll_for<TZ>([&](auto R) {
+            put_rows<32 + decltype(R)::value>(w4, face_row<CX>(S + F_YLO, R.value, lane), face_row<CX>(S + F_YHI, R.value, lane));
+        });
+    if (mode[2])
+        unroll_for<TZ>([&](auto R) {
+            put_rows<48 + decltype(R)::value>(w4, face_row<CY>(S + F_XLO, R.value, lane), face_row<CY>(S + F_XHI, R.value, lane));
+        });
+    const u32 alo = w4[0], ahi = w4[1], blo = w4[2], bhi = w4[3];
+    const int seam = lane < 32 ? 0 : lane < 48 ? 1 : 2;
+    const int r = lane - (seam == 0 ? 0 : seam == 1 ? 32 : 48), nr = seam == 0 ? TY : TZ;
+    const int stride = seam == 2 ? CY : CX;
+    const u32* FA = S + (seam == 0 ? F_ZLO : seam == 1 ? F_YLO : F_XLO);
+    const u32* FB = S + (seam == 0 ? F_ZHI : seam == 1 ? F_YHI : F_XHI);
+    const int md = mode[seam];
     const u64 A = ((u64)ahi << 32) | alo, B0 = ((u64)bhi << 32) | blo;
     // rows r - 1 / r + 1 of the neighbour (all lanes take part in the shuffles: an inactive
     // source lane would read as 0)
-    const u64 Bm_ = __shfl(B0, lane > 0 ? lane - 1 : 0, 64), Bp = __shfl(B0, lane + 1 < 64 ? lane + 1 : 63, 64);
-    const u64 Bm = lane > 0 ? Bm_ : 0ull;
-    if (lane >= NR || !A) return;
+    const u64 Bm_ = __shfl(B0, lane > 0 ? lane - 1 : 0, 64), Bp_ = __shfl(B0, lane + 1 < 64 ? lane + 1 : 63, 64);
+    const u64 Bm = r > 0 ? Bm_ : 0ull, Bp = r + 1 < nr ? Bp_ : 0ull;
+    if (!md || !A) return;
+    const bool full26 = md == 1;
     u32 la = NONE, lb = NONE;                                         // last pair emitted by this lane
 #pragma unroll
     for (int dr = -1; dr <= 1; ++dr) {
         if (dr && !full26) continue;
-        const u64 B = dr < 0 ? Bm : dr > 0 ? (lane + 1 < NR ? Bp : 0ull) : B0;
+        const u64 B = dr < 0 ? Bm : dr > 0 ? Bp : B0;
         if (!B) continue;
-        const int rb = lane + dr;
+        const int rb = r + dr;
 #pragma unroll
         for (int dx = -1; dx <= 1; ++dx) {
             if (dx && !full26) continue;
             const u64 C = A & (dx > 0 ? B >> 1 : dx < 0 ? B << 1 : B);
             for (u64 m = C & ~(C << 1); m; m &= m - 1) {
                 const int x = __builtin_ctzll(m);
-                const u32 ka = FA[(lane >> 1) * STRIDE + (x >> 1)] & 0xFFFFu;
-                const u32 kb = FB[(rb >> 1) * STRIDE + ((x + dx) >> 1)] & 0xFFFFu;
+                const u32 ka = FA[(r >> 1) * stride + (x >> 1)] & 0xFFFFu;
+                const u32 kb = FB[(rb >> 1) * stride + ((x + dx) >> 1)] & 0xFFFFu;
                 if (ka == la && kb == lb) continue;             // cheap first filter
                 la = ka; lb = kb;
-                emit(ka, kb);
+                emit(seam, ka, kb);
             }
         }
     }
 }
 
+// Face entries of the edge and corner neighbours inside the block (26-connectivity), staged in
+// LDS with the face planes so that no dependent global load remains (0 where absent):
+//   [0,32)   ZHI cube row (lyn-1)/2 of (-1,-1, 0)     [32,64)  ZHI cube row 0 of (-1,+1, 0)
+//   [64,80)  ZHI cube column (lxn-1)/2 of (-1,0,-1)   [80,96)  ZHI cube column 0 of (-1,0,+1)
+//   [96,104) YHI cube column (lxn-1)/2 of (0,-1,-1)   [104,112) YHI cube column 0 of (0,-1,+1)
+//   [112,116) ZHI corner entries of (-1, s1, s2), index (s1 > 0) * 2 + (s2 > 0)
+constexpr int EDGE_N = 128;
+
+__device__ __forceinline__ void stage_edges(const Geom& g, const u32* __restrict__ FACES, int64_t t,
+                                            const TileInfo& ti, u32* E, int lane) {
+    const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
+    const bool zok = ti.iz > 0 && g.tblk[0][ti.iz] == g.tblk[0][ti.iz - 1];
+    auto yok = [&](int s) { const int j = ti.iy + s; return j >= 0 && j < g.nt[1] && g.tblk[1][j] == g.tblk[1][ti.iy]; };
+    auto xok = [&](int s) { const int j = ti.ix + s; return j >= 0 && j < g.nt[2] && g.tblk[2][j] == g.tblk[2][ti.ix]; };
+    auto ylast = [&](int s) { return (g.tlen[1][ti.iy + s] - 1) / 2; };
+    auto xlast = [&](int s) { return (g.tlen[2][ti.ix + s] - 1) / 2; };
+#pragma unroll
+    for (int i = lane; i < EDGE_N; i += 64) {
+        u32 v = 0;
+        if (i < 32) {
+            if (zok && yok(-1)) v = FACES[(t - sz - sy) * FACE_STRIDE + F_ZHI + ylast(-1) * CX + i];
+        } else if (i < 64) {
+            if (zok && yok(1)) v = FACES[(t - sz + sy) * FACE_STRIDE + F_ZHI + (i - 32)];
+        } else if (i < 80) {
+            if (zok && xok(-1)) v = FACES[(t - sz - 1) * FACE_STRIDE + F_ZHI + (i - 64) * CX + xlast(-1)];
+        } else if (i < 96) {
+            if (zok && xok(1)) v = FACES[(t - sz + 1) * FACE_STRIDE + F_ZHI + (i - 80) * CX];
+        } else if (i < 104) {
+            if (ti.iy > 0 && yok(-1) && xok(-1)) v = FACES[(t - sy - 1) * FACE_STRIDE + F_YHI + (i - 96) * CX + xlast(-1)];
+        } else if (i < 112) {
+            if (ti.iy > 0 && yok(-1) && xok(1)) v = FACES[(t - sy + 1) * FACE_STRIDE + F_YHI + (i - 104) * CX];
+        } else if (i < 116) {
+            const int s1 = (i - 112) & 2 ? 1 : -1, s2 = (i - 112) & 1 ? 1 : -1;
+            if (zok && yok(s1) && xok(s2))
+                v = FACES[(t - sz + s1 * sy + s2) * FACE_STRIDE + F_ZHI + (s1 < 0 ? ylast(s1) : 0) * CX +
+                          (s2 < 0 ? xlast(s2) : 0)];
+        }
+        E[i] = v;
+    }
+}
+
+// Edge and corner seams as bit rows, one edge per lane (lanes 0-5), corners on lanes 6-9:
+//   lane 0/1 (-1,-1,0)/(-1,+1,0): own ZLO row y = 0 / ly-1 against the neighbour's ZHI row, bits x
+//   lane 2/3 (-1,0,-1)/(-1,0,+1): own ZLO column x = 0 / lx-1, bits y
+//   lane 4/5 (0,-1,-1)/(0,-1,+1): own YLO column x = 0 / lx-1, bits z
+// EMIT(lane code, tn, ka, kb) once per run of contacts (26-connectivity along the edge).
+template <class EM>
+__device__ __forceinline__ void seam_edges_rows(const Geom& g, const u32* S, const u32* E, int64_t t,
+                                                const TileInfo& ti, int lane, EM&& emit) {
+    const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2;
+    const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
+    const bool zok = ti.iz > 0 && g.tblk[0][ti.iz] == g.tblk[0][ti.iz - 1];
+    auto yok = [&](int s) { const int j = ti.iy + s; return j >= 0 && j < g.nt[1] && g.tblk[1][j] == g.tblk[1][ti.iy]; };
+    auto xok = [&](int s) { const int j = ti.ix + s; return j >= 0 && j < g.nt[2] && g.tblk[2][j] == g.tblk[2][ti.ix]; };
+    auto ypar = [&](int s) { return s < 0 ? (g.tlen[1][ti.iy + s] - 1) & 1 : 0; };   // neighbour's facing y parity
+    auto xpar = [&](int s) { return s < 0 ? (g.tlen[2][ti.ix + s] - 1) & 1 : 0; };
+    const bool ok[6] = {zok && yok(-1), zok && yok(1), zok && xok(-1), zok && xok(1),
+                        ti.iy > 0 && yok(-1) && xok(-1), ti.iy > 0 && yok(-1) && xok(1)};
+    // own / neighbour rows of the six edges (ballots over the position p = lane)
+    u64 A[6], B[6];
+    {
+        const int p = lane;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {                      // bits x
+            const int s = e ? 1 : -1, cyo = s < 0 ? 0 : ncy - 1, jo = s < 0 ? 0 : (ti.ly - 1) & 1;
+            const u32 ea = ok[e] ? S[F_ZLO + cyo * CX + (p >> 1)] : 0u, eb = ok[e] ? E[(e ? 32 : 0) + (p >> 1)] : 0u;
+            A[e] = __ballot((ea >> (16 + jo * 2 + (p & 1))) & 1u);
+            B[e] = __ballot((eb >> (16 + ypar(s) * 2 + (p & 1))) & 1u);
+        }
+#pragma unroll
+        for (int e = 2; e < 4; ++e) {                      // bits y
+            const int s = e == 3 ? 1 : -1, cxo = s < 0 ? 0 : ncx - 1, io = s < 0 ? 0 : (ti.lx - 1) & 1;
+            const bool in = ok[e] && p < TY;
+            const u32 ea = in ? S[F_ZLO + (p >> 1) * CX + cxo] : 0u, eb = in ? E[(e == 3 ? 80 : 64) + (p >> 1)] : 0u;
+            A[e] = __ballot((ea >> (16 + (p & 1) * 2 + io)) & 1u);
+            B[e] = __ballot((eb >> (16 + (p & 1) * 2 + xpar(s))) & 1u);
+        }
+#pragma unroll
+        for (int e = 4; e < 6; ++e) {                      // bits z
+            const int s = e == 5 ? 1 : -1, cxo = s < 0 ? 0 : ncx - 1, io = s < 0 ? 0 : (ti.lx - 1) & 1;
+            const bool in = ok[e] && p < TZ;
+            const u32 ea = in ? S[F_YLO + (p >> 1) * CX + cxo] : 0u, eb = in ? E[(e == 5 ? 104 : 96) + (p >> 1)] : 0u;
+            A[e] = __ballot((ea >> (16 + (p & 1) * 2 + io)) & 1u);
+            B[e] = __ballot((eb >> (16 + (p & 1) * 2 + xpar(s))) & 1u);
+        }
+    }
+    if (lane < 6) {
+        const int e = lane;
+        u64 a = 0, b = 0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) if (i == e) { a = A[i]; b = B[i]; }
+        const int s = (e & 1) ? 1 : -1;
+        const int64_t tn = e < 2 ? t - sz + s * sy : e < 4 ? t - sz + s : t - sy + s;
+        u32 la = NONE, lb = NONE;
+        if (a && b) {
+#pragma unroll
+            for (int d = -1; d <= 1; ++d) {
+                const u64 C = a & (d > 0 ? b >> 1 : d < 0 ? b << 1 : b);
+                for (u64 m = C & ~(C << 1); m; m &= m - 1) {
+                    const int p = __builtin_ctzll(m), q = p + d;
+                    u32 ka, kb;
+                    if (e < 2) {
+                        ka = S[F_ZLO + (s < 0 ? 0 : ncy - 1) * CX + (p >> 1)];
+                        kb = E[(e ? 32 : 0) + (q >> 1)];
+                    } else if (e < 4) {
+                        ka = S[F_ZLO + (p >> 1) * CX + (s < 0 ? 0 : ncx - 1)];
+                        kb = E[(e == 3 ? 80 : 64) + (q >> 1)];
+                    } else {
+                        ka = S[F_YLO + (p >> 1) * CX + (s < 0 ? 0 : ncx - 1)];
+                        kb = E[(e == 5 ? 104 : 96) + (q >> 1)];
+                    }
+                    ka &= 0xFFFFu; kb &= 0xFFFFu;
+                    if (ka == la && kb == lb) continue;
+                    la = ka; lb = kb;
+                    emit(tn, ka, kb);
+                }
+            }
+        }
+    } else if (lane < 10 && zok) {                          // corners (-1, s1, s2)
+        const int c = lane - 6, s1 = (c & 2) ? 1 : -1, s2 = (c & 1) ? 1 : -1;
+        if (yok(s1) && xok(s2)) {
+            const int cyo = s1 < 0 ? 0 : ncy - 1, cxo = s2 < 0 ? 0 : ncx - 1;
+            const int jo = s1 < 0 ? 0 : (ti.ly - 1) & 1, io = s2 < 0 ? 0 : (ti.lx - 1) & 1;
+            const u32 a = S[F_ZLO + cyo * CX + cxo], b = E[112 + c];
+            if (((a >> 16) & fsel(jo, io)) && ((b >> 16) & fsel(ypar(s1), xpar(s2))))
+                emit(t - sz + s1 * sy + s2, a & 0xFFFFu, b & 0xFFFFu);
+        }
+    }
+}
+
+// Edge and corner seams inside the block (the lex-negative directions with two or three nonzero
+// components), from the staged planes S and edge entries E.  U(t, entry, tn, entry_n).
+template <class UF>
+__device__ __forceinline__ void seam_edges(const Geom& g, const u32* S, const u32* E, int64_t t, const TileInfo& ti,
+                                           int lane, UF& U) {
+    const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2, ncz = (ti.lz + 1) / 2;
+    const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
+    const bool zok = ti.iz > 0 && g.tblk[0][ti.iz] == g.tblk[0][ti.iz - 1];
+    auto yok = [&](int s) { const int j = ti.iy + s; return j >= 0 && j < g.nt[1] && g.tblk[1][j] == g.tblk[1][ti.iy]; };
+    auto xok = [&](int s) { const int j = ti.ix + s; return j >= 0 && j < g.nt[2] && g.tblk[2][j] == g.tblk[2][ti.ix]; };
+    if (zok) {
+        for (int s = -1; s <= 1; s += 2) {                        // edges (-1, s, 0)
+            if (!yok(s)) continue;
+            const int lyn = g.tlen[1][ti.iy + s];
+            const int cyo = s < 0 ? 0 : ncy - 1;
+            const int jo = s < 0 ? 0 : (ti.ly - 1) & 1, jn = s < 0 ? (lyn - 1) & 1 : 0;
+            const u32* FR = E + (s < 0 ? 0 : 32);
+            for (int cx = lane; cx < ncx; cx += 64) {
+                const u32 a = S[F_ZLO + cyo * CX + cx];
+                if (a) edge3<false>(FR, 1, a, cx, ncx, jo, jn, t, t - sz + s * sy, U);
+            }
+        }
+        for (int s = -1; s <= 1; s += 2) {                        // edges (-1, 0, s)
+            if (!xok(s)) continue;
+            const int lxn = g.tlen[2][ti.ix + s];
+            const int cxo = s < 0 ? 0 : ncx - 1;
+            const int io = s < 0 ? 0 : (ti.lx - 1) & 1, in_ = s < 0 ? (lxn - 1) & 1 : 0;
+            const u32* FR = E + (s < 0 ? 64 : 80);
+            for (int cy = lane; cy < ncy; cy += 64) {
+                const u32 a = S[F_ZLO + cy * CX + cxo];
+                if (a) edge3<true>(FR, 1, a, cy, ncy, io, in_, t, t - sz + s, U);
+            }
+        }
+        if (lane < 4) {                                            // corners (-1, s1, s2)
+            const int s1 = (lane & 2) ? 1 : -1, s2 = (lane & 1) ? 1 : -1;
+            if (yok(s1) && xok(s2)) {
+                const int lyn = g.tlen[1][ti.iy + s1], lxn = g.tlen[2][ti.ix + s2];
+                const int cyo = s1 < 0 ? 0 : ncy - 1, cxo = s2 < 0 ? 0 : ncx - 1;
+                const int jo = s1 < 0 ? 0 : (ti.ly - 1) & 1, jn = s1 < 0 ? (lyn - 1) & 1 : 0;
+                const int io = s2 < 0 ? 0 : (ti.lx - 1) & 1, in_ = s2 < 0 ? (lxn - 1) & 1 : 0;
+                const u32 a = S[F_ZLO + cyo * CX + cxo];
+                const u32 b = E[112 + lane];
+                if (a && b && ((a >> 16) & fsel(jo, io)) && ((b >> 16) & fsel(jn, in_)))
+                    U(t, a, t - sz + s1 * sy + s2, b);
+            }
+        }
+    }
+    if (ti.iy > 0 && yok(-1)) {
+        for (int s = -1; s <= 1; s += 2) {                        // edges (0, -1, s)
+            if (!xok(s)) continue;
+            const int lxn = g.tlen[2][ti.ix + s];
+            const int cxo = s < 0 ? 0 : ncx - 1;
+            const int io = s < 0 ? 0 : (ti.lx - 1) & 1, in_ = s < 0 ? (lxn - 1) & 1 : 0;
+            const u32* FR = E + (s < 0 ? 96 : 104);
+            for (int cz = lane; cz < ncz; cz += 64) {
+                const u32 a = S[F_YLO + cz * CX + cxo];
+                if (a) edge3<true>(FR, 1, a, cz, ncz, io, in_, t, t - sy + s, U);
+            }
+        }
+    }
+}
+
+// STOP (ablation harness only; 0 in the library): 1 staged, 2 + z seam, 3 + y seam, 4 + x seam
+template <int STOP = 0>
 __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const u32* __restrict__ FACES, u64* PAIRS, u32* PC,
                                                          u8* big, u64* IPAIRS, u32* IPC, u8* iovf) {
     __shared__ u32 Sall[SP_WAVES][FACE_STRIDE];
     __shared__ u32 Hall[SP_WAVES][SEAM_HASH];
+    __shared__ u32 Eall[SP_WAVES][EDGE_N];
     __shared__ u32 cnt[SP_WAVES][2];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t t = (int64_t)blockIdx.x * SP_WAVES + w;
     const bool valid = t < g.n_tiles;
     u32* S = Sall[w];
     u32* H = Hall[w];
     TileInfo ti;
+    u32* E = Eall[w];
     if (valid) {
         ti = tile_info(g, t);
         stage_faces(g, FACES, t, ti, S, lane, 64);
+        stage_edges(g, FACES, t, ti, E, lane);
     }
     for (int i = lane; i < SEAM_HASH; i += 64) H[i] = NONE;
     if (lane < 2) cnt[w][lane] = 0;
@@ -1139,16 +1390,26 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const u32* __re
     const u32 capu = (u32)g.cap;
     u64* out = PAIRS + t * TPC;
     u64* iout = IPAIRS + t * TPI;
-    // wave-aggregated append of one pair per active lane to list `which` (0 intra, 1 inter)
-    auto append = [&](int which, u64 v) {
-        const u64 m = __ballot(1);
-        u32 base = 0;
-        if (lane == (int)(__ffsll((unsigned long long)m) - 1)) base = atomicAdd(&cnt[w][which], (u32)__popcll(m));
-        base = __builtin_amdgcn_readfirstlane(base);
-        const u32 pos = base + (u32)__popcll(m & ((1ull << lane) - 1));
-        if (which == 0) { if (pos < TPC) out[pos] = v; }
-        else if (pos < TPI) iout[pos] = v;
+    // wave-aggregated append of one pair per active lane to the intra (0) or inter (1) list
+    auto append = [&](bool to_inter, u64 v) {
+        const u64 act = __ballot(1), mi = __ballot(to_inter), ma = act & ~mi;
+        u32 base_a = 0, base_i = 0;
+        if (lane == (int)(__ffsll((unsigned long long)act) - 1)) {
+            if (ma) base_a = atomicAdd(&cnt[w][0], (u32)__popcll(ma));
+            if (mi) base_i = atomicAdd(&cnt[w][1], (u32)__popcll(mi));
+        }
+        base_a = __builtin_amdgcn_readfirstlane(base_a);
+        base_i = __builtin_amdgcn_readfirstlane(base_i);
+        const u64 below = (1ull << lane) - 1;
+        if (to_inter) {
+            const u32 pos = base_i + (u32)__popcll(mi & below);
+            if (pos < TPI) iout[pos] = v;
+        } else {
+            const u32 pos = base_a + (u32)__popcll(ma & below);
+            if (pos < TPC) out[pos] = v;
+        }
     };
+    if (STOP == 1) return;
     const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
     // exact code of a lower neighbour tile (the 13 lex-negative offsets)
     auto dir_code = [&](int64_t tn) -> u32 {
@@ -1178,42 +1439,26 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const u32* __re
         }
         return true;
     };
-    auto intra = [&](int64_t tn) {
-        const u32 lt_n = block_local(g, (u32)tn), code = dir_code(tn);
-        return [&, lt_n, code](u32 ka, u32 kb) {
-            if (!fresh(code, ka, kb)) return;
-            append(0, ((u64)((lt_own << 12) | ka) << 32) | ((lt_n << 12) | kb));
-        };
-    };
-    auto inter = [&](int64_t tn) {
-        const u32 code = dir_code(tn);
-        return [&, tn, code](u32 ka, u32 kb) {
-            if (!fresh(code, ka, kb)) return;
-            append(1, ((u64)((u32)t * capu + ka) << 32) | ((u32)tn * capu + kb));
-        };
-    };
-    if (ti.iz > 0) {                                   // z seam: rows y, bits x
-        const bool same = g.tblk[0][ti.iz] == g.tblk[0][ti.iz - 1];
-        if (same) seam_rows<CX, TY>(S + F_ZLO, S + F_ZHI, true, lane, intra(t - sz));
-        else seam_rows<CX, TY>(S + F_ZLO, S + F_ZHI, false, lane, inter(t - sz));
-    }
-    if (ti.iy > 0) {                                   // y seam: rows z, bits x
-        const bool same = g.tblk[1][ti.iy] == g.tblk[1][ti.iy - 1];
-        if (same) seam_rows<CX, TZ>(S + F_YLO, S + F_YHI, true, lane, intra(t - sy));
-        else seam_rows<CX, TZ>(S + F_YLO, S + F_YHI, false, lane, inter(t - sy));
-    }
-    if (ti.ix > 0) {                                   // x seam: rows z, bits y
-        const bool same = g.tblk[2][ti.ix] == g.tblk[2][ti.ix - 1];
-        if (same) seam_rows<CY, TZ>(S + F_XLO, S + F_XHI, true, lane, intra(t - 1));
-        else seam_rows<CY, TZ>(S + F_XLO, S + F_XHI, false, lane, inter(t - 1));
-    }
+    // the three lower seams: neighbour tile, mode (0 none, 1 intra 26-conn, 2 block face 6-conn)
+    int mode[3] = {0, 0, 0};
+    if (ti.iz > 0) mode[0] = g.tblk[0][ti.iz] == g.tblk[0][ti.iz - 1] ? 1 : 2;
+    if (ti.iy > 0) mode[1] = g.tblk[1][ti.iy] == g.tblk[1][ti.iy - 1] ? 1 : 2;
+    if (ti.ix > 0) mode[2] = g.tblk[2][ti.ix] == g.tblk[2][ti.ix - 1] ? 1 : 2;
+    const int myseam = lane < 32 ? 0 : lane < 48 ? 1 : 2;
+    const int64_t tn_l = t - (myseam == 0 ? sz : myseam == 1 ? sy : 1);
+    const u32 code_l = myseam == 0 ? dir_code(t - sz) : myseam == 1 ? dir_code(t - sy) : dir_code(t - 1);
+    const u32 ltn_l = mode[myseam] == 1 ? block_local(g, (u32)tn_l) : 0u;
+    seam_rows3(S, mode, lane, [&](int seam, u32 ka, u32 kb) {
+        if (!fresh(code_l, ka, kb)) return;
+        if (mode[seam] == 1) append(false, ((u64)((lt_own << 12) | ka) << 32) | ((ltn_l << 12) | kb));
+        else append(true, ((u64)((u32)t * capu + ka) << 32) | ((u32)tn_l * capu + kb));
+    });
+    if (STOP == 4) return;
     // edges and corners inside the block
-    auto edge_u = [&](int64_t, u32 e1, int64_t t2, u32 e2) {
-        const u32 k1 = e1 & 0xFFFu, k2 = e2 & 0xFFFu;
+    seam_edges_rows(g, S, E, t, ti, lane, [&](int64_t t2, u32 k1, u32 k2) {
         if (!fresh(dir_code(t2), k1, k2)) return;
-        append(0, ((u64)((lt_own << 12) | k1) << 32) | ((block_local(g, (u32)t2) << 12) | k2));
-    };
-    stitch_tile<false, decltype(edge_u)&, true>(g, FACES, S, t, ti, lane, 64, edge_u);
+        append(false, ((u64)((lt_own << 12) | k1) << 32) | ((block_local(g, (u32)t2) << 12) | k2));
+    });
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (lane == 0) {
@@ -1637,6 +1882,7 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
 template __global__ void k_front<5>(Geom, FrontArgs, const float*, float, int, u64*, u32*, u32*, u32*, u64*);
 template __global__ void k_front<6>(Geom, FrontArgs, const float*, float, int, u64*, u32*, u32*, u32*, u64*);
 template __global__ void k_front<0>(Geom, FrontArgs, const float*, float, int, u64*, u32*, u32*, u32*, u64*);
+template __global__ void k_seams<0>(Geom, const u32*, u64*, u32*, u8*, u64*, u32*, u8*);
 template __global__ void k_stitch<false>(Geom, const u32*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_stitch<true>(Geom, const u32*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_finalize<false>(Geom, const u32*, u32*, const u64*, const u64*, const u64*, const u64*, int64_t, u64*);

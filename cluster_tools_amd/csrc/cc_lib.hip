@@ -244,7 +244,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     HIP_OK(hipMemsetAsync(c->ipc.p, 0, nt * sizeof(u32), s));
     if (!(c->debug & CC_DEBUG_GLOBAL_STITCH)) {
         launch(c, "k_seams", [&] {
-            k_seams<<<(unsigned)((nt + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(
+            k_seams<0><<<(unsigned)((nt + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(
                 g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), big, c->ipairs.as<u64>(), c->ipc.as<u32>(),
                 c->iovf.as<u8>());
         });

@@ -183,6 +183,28 @@ int main(int argc, char** argv) {
             HIP_OK(hipMemcpy(&err, fst + 5 * nb + 1, 4, hipMemcpyDeviceToHost));
             if (err) std::fprintf(stderr, "k_front variant %d: wait timeout flagged\n", v);
         }
+        // seam kernel variants (FACES from the last full pass-1 run above)
+        {
+            P1(0);
+            u64 *pairs, *ipairs;
+            u32 *pc, *ipc;
+            u8 *big, *iovf;
+            HIP_OK(hipMalloc(&pairs, (size_t)nt * TPC * 8));
+            HIP_OK(hipMalloc(&ipairs, (size_t)nt * TPI * 8));
+            HIP_OK(hipMalloc(&pc, nt * 4));
+            HIP_OK(hipMalloc(&ipc, nt * 4));
+            HIP_OK(hipMalloc(&big, nb));
+            HIP_OK(hipMalloc(&iovf, nt));
+            HIP_OK(hipMemset(big, 0, nb));
+            HIP_OK(hipMemset(iovf, 0, nt));
+            const unsigned sg = (unsigned)((nt + SP_WAVES - 1) / SP_WAVES);
+#define SEAMS(V) k_seams<V><<<sg, SP_WAVES * 64, 0, s>>>(g, FACES, pairs, pc, big, ipairs, ipc, iovf)
+            r.push_back({"k_seams_stage", time_ms(s, iters, [&] { SEAMS(1); })});
+            r.push_back({"k_seams_z", time_ms(s, iters, [&] { SEAMS(2); })});
+            r.push_back({"k_seams_zy", time_ms(s, iters, [&] { SEAMS(3); })});
+            r.push_back({"k_seams_zyx", time_ms(s, iters, [&] { SEAMS(4); })});
+            r.push_back({"k_seams_full", time_ms(s, iters, [&] { SEAMS(0); })});
+        }
         r.push_back({"k_pass2", time_ms(s, iters, [&] { k_pass2<<<(unsigned)nt, NTHREADS, 0, s>>>(g, BITS, COUNT, FIN, out); })});
         std::printf("{\"shape\": [%lld, %lld, %lld], \"block\": [%lld, %lld, %lld], \"mode\": %d, \"tiles\": %lld",
                     (long long)shape[0], (long long)shape[1], (long long)shape[2], (long long)bs[0], (long long)bs[1],
