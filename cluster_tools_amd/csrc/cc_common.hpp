@@ -69,7 +69,8 @@ struct TileInfo {
     int64_t block;
 };
 
-__device__ __forceinline__ int cc_tid() { return threadIdx.x; }
+// thread index inside a 512-thread tile team (k_front runs two teams per workgroup)
+__device__ __forceinline__ int cc_tid() { return threadIdx.x & (NTHREADS - 1); }
 
 // tile ids fit u32 (node ids t * cap are u32, checked on the host): 32-bit division only
 __device__ __forceinline__ TileInfo tile_info(const Geom& g, int64_t t) {

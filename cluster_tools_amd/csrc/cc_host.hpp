@@ -115,9 +115,11 @@ static int64_t block_ntiles_host(const HostGeom& hg, int64_t b) {
 }
 
 // k_front segment table (cc_kernels.hip): S(0..lag-1), then S(k), P(k-lag) for k = lag..nb-1,
-// then P(nb-lag..nb-1).  h = [2 nb + 1 int64 segment starts][2 nb u32 block | pass1 << 31].
-// Returns the number of segments.
-static int64_t build_front_segments(const HostGeom& hg, int64_t lag, std::vector<int64_t>& h) {
+// then P(nb-lag..nb-1).  h = [2 nb + 1 int64 segment starts (in items)][2 nb u32 block |
+// pass1 << 31]; a stats item covers per_s tiles of its block, a pass-1 item per_p.  Returns the
+// number of segments; h[2 nb] is the number of items.
+static int64_t build_front_segments(const HostGeom& hg, int64_t lag, std::vector<int64_t>& h, int per_s = 1,
+                                    int per_p = 1) {
     const int64_t nb = hg.g.n_blocks;
     lag = std::max<int64_t>(1, std::min<int64_t>(lag, nb));
     const int64_t nseg = 2 * nb;
@@ -127,7 +129,8 @@ static int64_t build_front_segments(const HostGeom& hg, int64_t lag, std::vector
     auto add = [&](int64_t b, bool pass1) {
         h[j] = pos;
         hb[j] = (uint32_t)b | (pass1 ? 0x80000000u : 0u);
-        pos += block_ntiles_host(hg, b);
+        const int64_t per = pass1 ? per_p : per_s;
+        pos += (block_ntiles_host(hg, b) + per - 1) / per;
         ++j;
     };
     for (int64_t k = 0; k < nb; ++k) {
@@ -136,8 +139,21 @@ static int64_t build_front_segments(const HostGeom& hg, int64_t lag, std::vector
     }
     for (int64_t b = nb - lag; b < nb; ++b) add(b, true);
     h[nseg] = pos;
-    CC_REQUIRE(j == nseg && pos == 2 * hg.g.n_tiles && nb < (1LL << 31), "k_front segment table");
+    CC_REQUIRE(j == nseg && nb < (1LL << 31), "k_front segment table");
     return nseg;
+}
+
+// k_front2 item table (cc_kernels.hip): prologue stats tiles of blocks 0 .. lag-1, then one
+// pair item per tile of every block, in block order.  item = block | pair << 31 | lt << 32.
+static void build_front2_items(const HostGeom& hg, int64_t lag, std::vector<uint64_t>& items) {
+    const int64_t nb = hg.g.n_blocks;
+    items.clear();
+    for (int64_t b = 0; b < std::min<int64_t>(lag, nb); ++b)
+        for (int64_t l = 0; l < block_ntiles_host(hg, b); ++l) items.push_back((uint64_t)b | ((uint64_t)l << 32));
+    for (int64_t b = 0; b < nb; ++b)
+        for (int64_t l = 0; l < block_ntiles_host(hg, b); ++l)
+            items.push_back((uint64_t)b | 0x80000000ull | ((uint64_t)l << 32));
+    CC_REQUIRE(nb < (1LL << 31), "k_front2 item table");
 }
 
 }  // namespace cc

@@ -496,19 +496,18 @@ template <bool HAS_MASK, int ABL = 0>
 __device__ __forceinline__ void pass1_tile(const Geom& g, int64_t t, const TileInfo& ti, const BlockParam& p,
                                            const float* __restrict__ in, const u8* __restrict__ mask, float thr,
                                            int mode, u64* BITS, u32* FACES, u32* COUNT, u32* P, u64* KEY,
-                                           Pass1LDS& L) {
+                                           Pass1LDS& L, bool write = true) {
     u64* rows = L.rows;
     TileCCL& T = L.T;
     u32* key = L.key;
     const int tid = cc_tid();
-    const bool full = ti.lz == TZ && ti.ly == TY && ti.lx == TX;
-    if (!full || p.kind == BP_EMPTY) {
-        for (int i = tid; i < NROWS; i += NTHREADS) rows[i] = 0;
-        __syncthreads();
-    }
+    // (unconditional zeroing: every caller passes the same barriers, also the halves of k_front)
+    for (int i = tid; i < NROWS; i += NTHREADS) rows[i] = 0;
+    __syncthreads();
     if (p.kind != BP_EMPTY) load_rows<HAS_MASK>(g, ti, in, mask, p, thr, mode, rows);
     __syncthreads();
-    for (int i = tid; i < NROWS; i += NTHREADS) BITS[t * NROWS + i] = rows[i];
+    if (write)
+        for (int i = tid; i < NROWS; i += NTHREADS) BITS[t * NROWS + i] = rows[i];
     if (ABL == 1) return;
     if (ABL >= 10) { tile_ccl<ABL - 10>(rows, T); return; }
     const u32 R = tile_ccl(rows, T);
@@ -538,8 +537,8 @@ __device__ __forceinline__ void pass1_tile(const Geom& g, int64_t t, const TileI
         }
     }
     __syncthreads();
-    if (tid == 0) COUNT[t] = R;
-    if (ABL == 3) return;
+    if (tid == 0 && write) COUNT[t] = R;
+    if (ABL == 3 || !write) return;
     const u32 base = (u32)(t * g.cap);
     for (u32 k = tid; k < R; k += NTHREADS) {
         const u32 node = base + k;
@@ -566,23 +565,29 @@ __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restr
 }
 
 // ------------------------------------------------------------------------------------------
-// k_front: block statistics, block parameters and pass 1 in ONE persistent launch, ordered so
-// that pass 1 re-reads a block's input from the 256 MiB Infinity Cache instead of HBM.
+// k_front: block statistics, block parameters and pass 1 in ONE launch, ordered so that pass 1
+// re-reads a block's input from the 256 MiB Infinity Cache instead of HBM.
 //
-// Work items (one tile each) are taken in order from an atomic ticket: segments
+// Work items are taken in order from an atomic ticket: segments
 //   S(0) .. S(lag-1), then S(k), P(k - lag) for k = lag .. nb-1, then P(nb-lag) .. P(nb-1)
-// where S(b) = the stats items of block b's tiles and P(b) = its pass-1 items (ITEMS[i] =
-// tile | is-pass-1 << 31, built by k_front_items from the host's segment table).  The last stats
-// item of a block computes the block's parameters and publishes them; a pass-1 item waits for
-// its block.  The hand-off uses relaxed device-scope atomics only (performed at the coherence
-// point; the writer waits for each step to return before the next).  Every item a pass-1 item can wait on was taken before it, by a
-// workgroup that is running and waits on nothing, so the waits always end (they are also bounded
-// by a clock limit that raises an error flag instead of hanging).  One item per workgroup: the
-// grid has one workgroup per item (a persistent loop raised register pressure past 4 WG / CU).
+// where S(b) = the stats items of block b and P(b) = its pass-1 items.  A workgroup of H tile
+// teams (512 threads each) takes one item: a stats item covers per_s consecutive tiles of the
+// block (per_s / H per team), a pass-1 item H tiles (one per team).  The ticket is one device
+// atomic on one word (~88 per us chip-wide).  The library runs H = 1, one tile per item.
+// ITEMS[i] = block | is-pass-1 << 31 | (first local tile | tile count << 16) << 32, built by
+// k_front_items from the host's segment table.  The last stats item of a block computes the
+// block's parameters and publishes them; a pass-1 item waits for its block.  The hand-off uses
+// relaxed device-scope atomics only (performed at the coherence point; the writer waits for
+// each step to return before the next): an agent-scope release / acquire would write back /
+// invalidate the XCD's L2 on every item.  Every item a pass-1 item can wait on was taken before
+// it, by a workgroup that is running and waits on nothing, so the waits always end (they are
+// also bounded by a clock limit that raises an error flag instead of hanging).  One item per
+// workgroup (a persistent loop raised register pressure past the LDS-bound occupancy).
 // ------------------------------------------------------------------------------------------
 struct FrontArgs {
-    const u32* items;         // 2 * n_tiles entries: tile | is-pass-1 << 31
+    const u64* items;         // work items (see above)
     int64_t n_items;
+    int32_t per_s, per_p;     // tiles per stats / pass-1 item
     u32* smin; u32* smax; u32* sflag;
     u32* sdone;               // stats items done per block
     u32* ready;               // block parameters published
@@ -603,8 +608,8 @@ __device__ __forceinline__ int block_ntiles(const Geom& g, int64_t b) {
     return g.btn[0][bz] * g.btn[1][by] * g.btn[2][bx];
 }
 
-// ITEMS from the segment table SEG (nseg + 1 starts, then nseg u32 block | is-pass-1 << 31)
-__global__ void k_front_items(Geom g, const int64_t* seg, int32_t nseg, u32* items) {
+// ITEMS from the segment table SEG (nseg + 1 item starts, then nseg u32 block | is-pass-1 << 31)
+__global__ void k_front_items(Geom g, const int64_t* seg, int32_t nseg, int per_s, int per_p, u64* items) {
     const u32* segb = (const u32*)(seg + nseg + 1);
     CC_FOR(i, seg[nseg]) {
         int lo = 0, hi = nseg - 1;
@@ -613,12 +618,15 @@ __global__ void k_front_items(Geom g, const int64_t* seg, int32_t nseg, u32* ite
             if (seg[mid] <= i) lo = mid; else hi = mid - 1;
         }
         const u32 sb = segb[lo];
-        items[i] = (u32)block_tile(g, sb & 0x7FFFFFFFu, (int)(i - seg[lo])) | (sb & 0x80000000u);
+        const int per = (sb >> 31) ? per_p : per_s;
+        const int lt0 = (int)(i - seg[lo]) * per;
+        const int n = min(per, block_ntiles(g, sb & 0x7FFFFFFFu) - lt0);
+        items[i] = (u64)sb | ((u64)((u32)lt0 | ((u32)n << 16)) << 32);
     }
 }
 
-// tile tables read inside the persistent loop come back in VGPRs (vector loads after stores);
-// the values are workgroup-uniform, so move them to SGPRs
+// tile tables read after stores come back in VGPRs (vector loads); the values are
+// workgroup-uniform, so move them to SGPRs
 __device__ __forceinline__ TileInfo uniform_ti(TileInfo ti) {
     ti.iz = __builtin_amdgcn_readfirstlane(ti.iz); ti.iy = __builtin_amdgcn_readfirstlane(ti.iy);
     ti.ix = __builtin_amdgcn_readfirstlane(ti.ix); ti.z0 = __builtin_amdgcn_readfirstlane(ti.z0);
@@ -631,99 +639,135 @@ __device__ __forceinline__ TileInfo uniform_ti(TileInfo ti) {
 }
 
 // TV (ablation harness only; 0 in the library): 2 = no wait, 3 = 2 + skip pass-1 items,
-// 4 = 2 + skip stats items, 5 = 3 without the ticket (item = blockIdx.x), 6 = ticket only
-template <bool HAS_MASK, int TV>
+// 4 = 2 + skip stats items, 6 = ticket only
+template <bool HAS_MASK, int H, int TV>
 __device__ __forceinline__ void front_item(const Geom& g, const FrontArgs& fa, const float* __restrict__ in,
                                            const u8* __restrict__ mask, float thr, int mode, u64* BITS,
                                            u32* FACES, u32* COUNT, u32* P, u64* KEY) {
-    __shared__ Pass1LDS L;
-    __shared__ u32 red[3][NTHREADS / 64];
-    __shared__ u32 s_entry;
+    __shared__ Pass1LDS L[H];
+    __shared__ u32 red[2][H * NTHREADS / 64];
+    __shared__ u64 s_entry;
     __shared__ BlockParam s_bp;
-    const int tid = cc_tid();
+    const int ftid = threadIdx.x;
+    const int half = H == 1 ? 0 : __builtin_amdgcn_readfirstlane(ftid / NTHREADS);
+    const int tid = cc_tid();                       // thread index inside the half
     // one item per workgroup, in ticket order (dispatch order is undefined, the ticket is not)
-    if (tid == 0) {
-        const u32 k = TV == 5 ? blockIdx.x : atomicAdd(&fa.queue[0], 1u);
-        s_entry = k < fa.n_items ? fa.items[k] : 0u;
+    if (ftid == 0) {
+        const u32 k = atomicAdd(&fa.queue[0], 1u);
+        s_entry = k < fa.n_items ? fa.items[k] : 0ull;
     }
     __syncthreads();
     if (TV == 6) return;
-    {
-        const u32 entry = __builtin_amdgcn_readfirstlane(s_entry);
-        const int64_t t = entry & 0x7FFFFFFFu;
-        const bool is_p1 = entry >> 31;
-        const TileInfo ti = uniform_ti(tile_info(g, t));
-        const int64_t b = ti.block;
-        if ((TV == 3 || TV == 5) && is_p1) return;
-        if (TV == 4 && !is_p1) return;
-        if (!is_p1) {
-            stats_tile(g, ti, in, fa.smin, fa.smax, fa.sflag, red);
-            if (tid == 0) {
-                // the block's min / max / flag atomics (stats_tile) have returned, i.e. are performed
-                // at the coherence point, before this item counts itself done.  Only relaxed
-                // atomics are used for the hand-off: an agent-scope release / acquire would write
-                // back / invalidate this XCD's L2 on every item.
-                __builtin_amdgcn_s_waitcnt(0);
-                const u32 n = (u32)block_ntiles(g, b);
-                const u32 done = atomicAdd(&fa.sdone[b], 1u);
-                if (done + 1 == n) {                      // last stats item of the block
-                    const u32 vmin = atomicMin(&fa.smin[b], 0xFFFFFFFFu);      // atomic reads
-                    const u32 vmax = atomicMax(&fa.smax[b], 0u);
-                    const u32 vfl = atomicOr(&fa.sflag[b], 0u);
-                    const BlockParam bp = block_param(vmin, vmax, vfl, thr, mode);
-                    u32* w = (u32*)&fa.bp[b];
-                    atomicExch(w + 0, __float_as_uint(bp.mn));
-                    atomicExch(w + 1, __float_as_uint(bp.m));
-                    atomicExch(w + 2, bp.lo);
-                    atomicExch(w + 3, bp.hi);
-                    atomicExch(w + 4, bp.kind);
-                    __builtin_amdgcn_s_waitcnt(0);
-                    atomicExch(&fa.ready[b], 1u);
-                }
+    const u32 e0 = __builtin_amdgcn_readfirstlane((u32)s_entry), e1 = __builtin_amdgcn_readfirstlane((u32)(s_entry >> 32));
+    const int64_t b = e0 & 0x7FFFFFFFu;
+    const bool is_p1 = e0 >> 31;
+    const int lt0 = e1 & 0xFFFFu, n = e1 >> 16;
+    if (TV == 3 && is_p1) return;
+    if (TV == 4 && !is_p1) return;
+    if (!is_p1) {
+        // ordered min / max over this half's tiles (no barrier inside the loop)
+        u32 mn = 0xFFFFFFFFu, mx = 0u;
+        const int per_half = fa.per_s / H;
+        for (int j = 0; j < per_half; ++j) {
+            const int lt = lt0 + half * per_half + j;
+            if (lt >= lt0 + n) break;
+            const TileInfo ti = uniform_ti(tile_info(g, block_tile(g, b, lt)));
+            for_tile_rows<false>(g, ti, in, nullptr, [&](int, float x, u32) {
+                const u32 o = f2ord(__float_as_uint(x));
+                mn = o < mn ? o : mn;
+                mx = o > mx ? o : mx;
+            });
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const u32 a = __shfl_xor(mn, o, 64), c = __shfl_xor(mx, o, 64);
+            mn = a < mn ? a : mn;
+            mx = c > mx ? c : mx;
+        }
+        if ((ftid & 63) == 0) { red[0][ftid >> 6] = mn; red[1][ftid >> 6] = mx; }
+        __syncthreads();
+        if (ftid == 0) {
+            u32 a = red[0][0], c = red[1][0];
+            for (int w = 1; w < H * NTHREADS / 64; ++w) {
+                a = red[0][w] < a ? red[0][w] : a;
+                c = red[1][w] > c ? red[1][w] : c;
             }
-        } else {
-            if (tid == 0) {
-                if (TV < 2 || TV > 6) {
-                    const int64_t t0 = wall_clock64();
-                    while (atomicOr(&fa.ready[b], 0u) == 0u) {
-                        __builtin_amdgcn_s_sleep(4);
-                        if (wall_clock64() - t0 > (int64_t)100000000) {      // ~1 s at 100 MHz: never expected
-                            atomicOr(&fa.queue[1], 1u);
-                            break;
-                        }
+            // NaN orders above +inf or below -inf (volume_utils.py:98-105: a NaN block has no foreground)
+            const bool nan = c > 0xFF800000u || a < 0x007FFFFFu;
+            atomicMin(&fa.smin[b], a);
+            atomicMax(&fa.smax[b], c);
+            if (nan) atomicOr(&fa.sflag[b], 1u);
+            // the block's min / max / flag atomics are performed at the coherence point (returned)
+            // before this item counts itself done
+            __builtin_amdgcn_s_waitcnt(0);
+            const u32 n_s = (u32)((block_ntiles(g, b) + fa.per_s - 1) / fa.per_s);
+            const u32 done = atomicAdd(&fa.sdone[b], 1u);
+            if (done + 1 == n_s) {                         // last stats item of the block
+                const u32 vmin = atomicMin(&fa.smin[b], 0xFFFFFFFFu);      // atomic reads
+                const u32 vmax = atomicMax(&fa.smax[b], 0u);
+                const u32 vfl = atomicOr(&fa.sflag[b], 0u);
+                const BlockParam bp = block_param(vmin, vmax, vfl, thr, mode);
+                u32* w = (u32*)&fa.bp[b];
+                atomicExch(w + 0, __float_as_uint(bp.mn));
+                atomicExch(w + 1, __float_as_uint(bp.m));
+                atomicExch(w + 2, bp.lo);
+                atomicExch(w + 3, bp.hi);
+                atomicExch(w + 4, bp.kind);
+                __builtin_amdgcn_s_waitcnt(0);
+                atomicExch(&fa.ready[b], 1u);
+            }
+        }
+    } else {
+        if (ftid == 0) {
+            if (TV < 2) {
+                const int64_t t0 = wall_clock64();
+                while (atomicOr(&fa.ready[b], 0u) == 0u) {
+                    __builtin_amdgcn_s_sleep(4);
+                    if (wall_clock64() - t0 > (int64_t)100000000) {      // ~1 s at 100 MHz: never expected
+                        atomicOr(&fa.queue[1], 1u);
+                        break;
                     }
                 }
-                u32* w = (u32*)&fa.bp[b];
-                const u32 w0 = atomicOr(w + 0, 0u), w1 = atomicOr(w + 1, 0u), w2 = atomicOr(w + 2, 0u),
-                          w3 = atomicOr(w + 3, 0u), w4 = atomicOr(w + 4, 0u);
-                s_bp.mn = __uint_as_float(w0); s_bp.m = __uint_as_float(w1);
-                s_bp.lo = w2; s_bp.hi = w3; s_bp.kind = w4;
             }
-            __syncthreads();
-            BlockParam p;
-            p.mn = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(s_bp.mn)));
-            p.m = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(s_bp.m)));
-            p.lo = __builtin_amdgcn_readfirstlane(s_bp.lo);
-            p.hi = __builtin_amdgcn_readfirstlane(s_bp.hi);
-            p.kind = __builtin_amdgcn_readfirstlane(s_bp.kind);
-            p.pad = 0;
-            pass1_tile<HAS_MASK>(g, t, ti, p, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L);
+            u32* w = (u32*)&fa.bp[b];
+            const u32 w0 = atomicOr(w + 0, 0u), w1 = atomicOr(w + 1, 0u), w2 = atomicOr(w + 2, 0u),
+                      w3 = atomicOr(w + 3, 0u), w4 = atomicOr(w + 4, 0u);
+            s_bp.mn = __uint_as_float(w0); s_bp.m = __uint_as_float(w1);
+            s_bp.lo = w2; s_bp.hi = w3; s_bp.kind = w4;
         }
+        __syncthreads();
+        BlockParam p;
+        p.mn = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(s_bp.mn)));
+        p.m = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(s_bp.m)));
+        p.lo = __builtin_amdgcn_readfirstlane(s_bp.lo);
+        p.hi = __builtin_amdgcn_readfirstlane(s_bp.hi);
+        p.kind = __builtin_amdgcn_readfirstlane(s_bp.kind);
+        p.pad = 0;
+        // half h labels tile lt0 + h; a half without a tile runs tile lt0 again without writing
+        // anything, so that both halves pass the same barriers
+        const bool own = half < n;
+        const int64_t t = block_tile(g, b, lt0 + (own ? half : 0));
+        const TileInfo ti = uniform_ti(tile_info(g, t));
+        pass1_tile<HAS_MASK>(g, t, ti, p, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L[half], own);
     }
 }
 
-// without a mask the item fits 64 VGPRs (4 workgroups / CU, the LDS limit); with one it would spill
+// 512-thread workgroups, one tile per item (measured: 1024-thread workgroups with two tiles per
+// pass-1 item, multi-tile stats items and a "paired" stats(b + lag) + pass-1(b) item order were
+// all slower -- pass-1 items waited on the longer stats items, or the two tiles of a workgroup
+// waited on each other at every barrier)
 template <int TV = 0>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_front(
     Geom g, FrontArgs fa, const float* __restrict__ in, float thr, int mode, u64* BITS, u32* FACES, u32* COUNT,
     u32* P, u64* KEY) {
-    front_item<false, TV>(g, fa, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KEY);
+    front_item<false, 1, TV>(g, fa, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KEY);
 }
 
+// with a mask: 512-thread workgroups (the mask loads would spill at 64 VGPRs)
 __global__ __launch_bounds__(NTHREADS) void k_front_mask(Geom g, FrontArgs fa, const float* __restrict__ in,
                                                          const u8* __restrict__ mask, float thr, int mode, u64* BITS,
                                                          u32* FACES, u32* COUNT, u32* P, u64* KEY) {
-    front_item<true, 0>(g, fa, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY);
+    front_item<true, 1, 0>(g, fa, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1879,8 +1923,6 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
 }
 
 // instantiate the templates used by the host side
-template __global__ void k_front<5>(Geom, FrontArgs, const float*, float, int, u64*, u32*, u32*, u32*, u64*);
-template __global__ void k_front<6>(Geom, FrontArgs, const float*, float, int, u64*, u32*, u32*, u32*, u64*);
 template __global__ void k_front<0>(Geom, FrontArgs, const float*, float, int, u64*, u32*, u32*, u32*, u64*);
 template __global__ void k_seams<0>(Geom, const u32*, u64*, u32*, u8*, u64*, u32*, u8*);
 template __global__ void k_stitch<false>(Geom, const u32*, u32*, const u64*, const u8*, const u8*);

@@ -210,19 +210,23 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     {
         int64_t lag = 1;
         if (const char* e = std::getenv("CC_FRONT_LAG")) lag = std::max<int64_t>(1, std::atoll(e));
+        const int per_s = 2, per_p = 1;                  // tiles per stats / pass-1 item (2: measured best)
         std::vector<int64_t>& h = c->h_front;
-        const int64_t nseg = build_front_segments(st.hg, lag, h);
-        const int64_t n_items = 2 * nt;
-        CC_REQUIRE(n_items < (1LL << 31), "too many tiles for one k_front launch");
-        c->front.ensure(h.size() * sizeof(int64_t) + n_items * sizeof(u32));
+        const int64_t nseg = build_front_segments(st.hg, lag, h, per_s, per_p);
+        const int64_t n_items = h[nseg];
+        CC_REQUIRE(n_items < (1LL << 31), "too many items for one k_front launch");
+        c->front.ensure(h.size() * sizeof(int64_t) + n_items * sizeof(u64));
         HIP_OK(hipMemcpyAsync(c->front.p, h.data(), h.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
-        u32* items = (u32*)(c->front.as<int64_t>() + h.size());
+        u64* items = (u64*)(c->front.as<int64_t>() + h.size());
         launch(c, "k_front_items", [&] {
-            k_front_items<<<grid_stride(n_items), 256, 0, s>>>(g, c->front.as<int64_t>(), (int32_t)nseg, items);
+            k_front_items<<<grid_stride(n_items), 256, 0, s>>>(g, c->front.as<int64_t>(), (int32_t)nseg, per_s, per_p,
+                                                                items);
         });
         FrontArgs fa;
         fa.items = items;
         fa.n_items = n_items;
+        fa.per_s = per_s;
+        fa.per_p = per_p;
         fa.smin = smin; fa.smax = smax; fa.sflag = sflag;
         fa.sdone = smin + 3 * nb; fa.ready = smin + 4 * nb;
         fa.bp = bp;

@@ -133,7 +133,7 @@ int main(int argc, char** argv) {
         {
             r.push_back({"k_stats_blockmajor", time_ms(s, iters, [&] {
                 k_stats_bm<<<(unsigned)nt, NTHREADS, 16, s>>>(g, in, smin, smax, sflag, (int)(nt / nb), 1); })});
-            r.push_back({"k_stats_bm_lds38k", time_ms(s, iters, [&] {
+            r.push_back({"k_stats_bm_lds38k_unused", time_ms(s, iters, [&] {
                 k_stats_bm<<<(unsigned)nt, NTHREADS, 38400, s>>>(g, in, smin, smax, sflag, (int)(nt / nb), 1); })});
             r.push_back({"k_stats_bm_interleave2", time_ms(s, iters, [&] {
                 k_stats_bm<<<(unsigned)(2 * nt), NTHREADS, 16, s>>>(g, in, smin, smax, sflag, (int)(nt / nb), 2); })});
@@ -149,39 +149,43 @@ int main(int argc, char** argv) {
         r.push_back({"k_pass1_abl3_keys", time_ms(s, iters, [&] { P1(3); })});
         r.push_back({"k_pass1_full", time_ms(s, iters, [&] { P1(0); })});
         // fused front (stats + params + pass 1 in one launch)
-        u32* fst;
-        int64_t* fseg;
-        u32* items;
-        HIP_OK(hipMalloc(&fst, (5 * nb + 2) * 4));
-        HIP_OK(hipMalloc(&fseg, (4 * nb + 4) * 8));
-        HIP_OK(hipMalloc(&items, 2 * nt * 4));
-        std::vector<int64_t> hseg;
-        static const char* fnames[8] = {"k_front_lag1", "k_front_lag2", "k_front_lag3",
-                                        "k_front_lag1_nowait", "k_front_stats_only", "k_front_pass1_only",
-                                        "k_front_stats_only_noticket", "k_front_ticket_only"};
-        for (int v = 0; v < 8; ++v) {
-            const int lag = v < 3 ? v + 1 : 1;
-            const int64_t nseg = build_front_segments(hg, lag, hseg);
-            HIP_OK(hipMemcpy(fseg, hseg.data(), hseg.size() * 8, hipMemcpyHostToDevice));
-            k_front_items<<<1024, 256, 0, s>>>(g, fseg, (int32_t)nseg, items);
-            FrontArgs fa;
-            fa.items = items; fa.n_items = 2 * nt;
-            fa.smin = fst; fa.smax = fst + nb; fa.sflag = fst + 2 * nb; fa.sdone = fst + 3 * nb; fa.ready = fst + 4 * nb;
-            fa.bp = bp; fa.queue = fst + 5 * nb;
-            r.push_back({fnames[v], time_ms(s, iters, [&] {
-                HIP_OK(hipMemsetAsync(fst, 0xFF, nb * 4, s));
-                HIP_OK(hipMemsetAsync(fst + nb, 0, (4 * nb + 2) * 4, s));
-                const unsigned grid = (unsigned)(2 * nt);
-                if (v < 3) k_front<0><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
-                else if (v == 3) k_front<2><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
-                else if (v == 4) k_front<3><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
-                else if (v == 6) k_front<5><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
-                else if (v == 7) k_front<6><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
-                else k_front<4><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
-            })});
-            u32 err = 0;
-            HIP_OK(hipMemcpy(&err, fst + 5 * nb + 1, 4, hipMemcpyDeviceToHost));
-            if (err) std::fprintf(stderr, "k_front variant %d: wait timeout flagged\n", v);
+        {
+            u32* fst;
+            int64_t* fseg;
+            u64* items;
+            HIP_OK(hipMalloc(&fst, (5 * nb + 2) * 4));
+            HIP_OK(hipMalloc(&fseg, (4 * nb + 4) * 8));
+            HIP_OK(hipMalloc(&items, 2 * nt * 8));
+            std::vector<int64_t> hseg;
+            static const char* fnames[10] = {"k_front_lag1", "k_front_lag2", "k_front_lag1_nowait", "k_front_stats_only",
+                                            "k_front_pass1_only", "k_front_ticket_only", "k_front_lag1_s2",
+                                            "k_front_lag1_s3", "k_front_lag1_s4", "k_front_lag2_s2"};
+            for (int v = 0; v < 10; ++v) {
+                const int lag = v == 1 || v == 9 ? 2 : 1;
+                const int per_s = v == 6 || v == 9 ? 2 : v == 7 ? 3 : v == 8 ? 4 : 1, per_p = 1;
+                const int64_t nseg = build_front_segments(hg, lag, hseg, per_s, per_p);
+                const int64_t n_items = hseg[nseg];
+                HIP_OK(hipMemcpy(fseg, hseg.data(), hseg.size() * 8, hipMemcpyHostToDevice));
+                k_front_items<<<1024, 256, 0, s>>>(g, fseg, (int32_t)nseg, per_s, per_p, items);
+                FrontArgs fa;
+                fa.items = items; fa.n_items = n_items; fa.per_s = per_s; fa.per_p = per_p;
+                fa.smin = fst; fa.smax = fst + nb; fa.sflag = fst + 2 * nb; fa.sdone = fst + 3 * nb; fa.ready = fst + 4 * nb;
+                fa.bp = bp; fa.queue = fst + 5 * nb;
+                r.push_back({fnames[v], time_ms(s, iters, [&] {
+                    HIP_OK(hipMemsetAsync(fst, 0xFF, nb * 4, s));
+                    HIP_OK(hipMemsetAsync(fst + nb, 0, (4 * nb + 2) * 4, s));
+                    const unsigned grid = (unsigned)n_items;
+                    const int tv = v < 2 || v >= 6 ? 0 : v == 2 ? 2 : v == 3 ? 3 : v == 4 ? 4 : 6;
+                    if (tv == 0) k_front<0><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
+                    else if (tv == 2) k_front<2><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
+                    else if (tv == 3) k_front<3><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
+                    else if (tv == 4) k_front<4><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
+                    else k_front<6><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
+                })});
+                u32 err = 0;
+                HIP_OK(hipMemcpy(&err, fst + 5 * nb + 1, 4, hipMemcpyDeviceToHost));
+                if (err) std::fprintf(stderr, "k_front variant %d: wait timeout flagged\n", v);
+            }
         }
         // seam kernel variants (FACES from the last full pass-1 run above)
         {
