@@ -51,22 +51,34 @@ __host__ __device__ constexpr u32 fsel(int sp, int sq) {
     X(-1, 1, 0) X(-1, 1, 1) X(0, -1, -1) X(0, -1, 0) X(0, -1, 1)
 
 // ------------------------------------------------------------------------------------------
-// tile CCL in LDS.  rows[NROWS] holds the tile's foreground bits (zero outside its extent).
-// After return (R = number of tile-local components): for every non-empty cube c,
-//   root = par[c] & 0xFFFF, k = par[root] >> 16 (k in [0, R), deterministic).
+// Tile CCL in LDS.
 //
-// Cube c = tid + NTHREADS*i, so lanes 0-31 / 32-63 of a wave hold cx = 0..31 of two cube rows:
-// the x-direction unions are done with two ballots (runs of x-linked cubes, root = run start)
-// and only the 12 other lex-negative directions go through the LDS union-find.
+// Bit rows use the SPLIT representation: one 64-bit word per voxel row (z, y) of the tile, low
+// half = the even voxels (bit cx <-> x = 2 cx), high half = the odd voxels (bit cx <-> x = 2cx+1),
+// so every cube-level mask is a 32-bit word with bit cx <-> cube cx (load_rows loads lane = x
+// and splits each row once, split_row).
+//
+// A cube row (fixed cz, cy) holds 32 cubes of 2x2x2 voxels; all foreground voxels of a cube are
+// mutually 26-adjacent.  Consecutive cubes are 26-linked along x iff the left one has a voxel at
+// local x = 1 and the right one at local x = 0: E = H & (L >> 1) with L / H the OR of the row's
+// even / odd halves.  Maximal x-linked sequences ("runs", up to 32 per cube row) are the
+// union-find nodes, numbered in cube order (run id = first run id of the row + rank of its start
+// among the row's run starts), so the root of a component -- its smallest run id -- is its first
+// run in cube order (deterministic).  For each of the 12 other lex-negative cube directions the
+// cube pairs are a 32-bit mask per pair of cube rows; a pair implied by the runs and the pair one
+// cube to the left is dropped, only the rest reach the LDS union-find.
+//
+// After tile_ccl: par[run] = root | k << 16 for every run, k in [0, R) the component's compact
+// index (roots in cube order).
 // ------------------------------------------------------------------------------------------
-constexpr u32 XLO_BITS = sel_bits(2, 2, 0), XHI_BITS = sel_bits(2, 2, 1);
-constexpr u64 EVEN64 = 0x5555555555555555ull;
 constexpr int NCROW = CZ * CY;          // cube rows per tile
-constexpr int NDIR = 12;                // lex-negative directions other than (0,0,-1)
-// direction d = grp*3 + (dx+1), grp: (dz,dy) = (-1,-1), (-1,0), (-1,1), (0,-1)
-__host__ __device__ constexpr int dir_dz(int d) { return d / 3 == 3 ? 0 : -1; }
-__host__ __device__ constexpr int dir_dy(int d) { return d / 3 == 3 ? -1 : d / 3 - 1; }
-__host__ __device__ constexpr int dir_dx(int d) { return d % 3 - 1; }
+constexpr int NRUN = NCROW * CX;        // a run per occupied cube at most (adjacent cubes need not link)
+static_assert(NTHREADS == 4 * NCROW, "tile_ccl maps one thread to each quarter cube row");
+
+__device__ __forceinline__ u32 lo32(u64 w) { return (u32)w; }
+__device__ __forceinline__ u32 hi32(u64 w) { return (u32)(w >> 32); }
+// mask of bits 0..b (b in [0, 31])
+__device__ __forceinline__ u32 mask_le(int b) { return (u32)((2ull << b) - 1); }
 
 // OR of the voxel rows of a cube row whose (lz, ly) match selections (sz, sy); a[lz*2+ly]
 __device__ __forceinline__ u64 pick_rows(const u64 a[4], int sz, int sy) {
@@ -77,37 +89,14 @@ __device__ __forceinline__ u64 pick_rows(const u64 a[4], int sz, int sy) {
     if (sz != 0 && sy != 0) u |= a[3];
     return u;
 }
-// cube-level mask in "even" representation (cube cx <-> bit 2cx) of voxels with lx in sx
-__device__ __forceinline__ u64 xsel(u64 u, int sx) {
-    return sx == 0 ? (u & EVEN64) : sx == 1 ? ((u >> 1) & EVEN64) : ((u | (u >> 1)) & EVEN64);
-}
-__device__ __forceinline__ u64 shift_dx(u64 m, int dx) { return dx > 0 ? m >> 2 : dx < 0 ? m << 2 : m; }
-// x-links of a cube row, even repr: bit 2cx set iff cube cx is 26-linked to cube cx+1
-__device__ __forceinline__ u64 xlinks(const u64 a[4]) {
-    const u64 u = a[0] | a[1] | a[2] | a[3];
-    return ((u >> 1) & EVEN64) & ((u & EVEN64) >> 2);
-}
 
-// ------------------------------------------------------------------------------------------
-// Run-based tile CCL.
-//
-// A cube row (fixed cz, cy) holds 32 cubes; consecutive cubes are 26-linked along x iff the left
-// one has a voxel at local x=1 and the right one a voxel at local x=0.  Maximal x-linked
-// sequences ("runs") are the union-find nodes; a run is named by its first cube index, so the
-// root of a component is its smallest cube index (deterministic).  Per cube row, 64-bit masks in
-// "even" representation (cube cx <-> bit 2cx) give the runs and, for each of the 12 other
-// lex-negative directions, the cube pairs whose union is not already implied by the runs and by
-// the pair one cube to the left.  Only those pairs reach the LDS union-find.
-//
-// After tile_ccl every run start s holds par[s] = root | (k << 16), k in [0, R) the component's
-// compact index (deterministic: roots in cube order).
-// ------------------------------------------------------------------------------------------
 struct TileCCL {
-    u64 rstart[NCROW];     // run starts of each cube row (even representation)
-    u32 par[NC];           // union-find, entries at run starts only
+    u32 B[NCROW];          // run starts of each cube row (bit cx)
+    u32 E[NCROW];          // x-links: bit cx iff cube cx is 26-linked to cube cx + 1
+    u32 roff[NCROW];       // run id of each cube row's first run
+    u32 par[NRUN];         // union-find over run ids, then root | k << 16
     u32 scratch[8];
 };
-static_assert(NTHREADS == 4 * NCROW, "tile_ccl maps one thread to each quarter cube row");
 
 __device__ __forceinline__ void load_row4(const u64* rows, int row, u64 a[4]) {
     const int cz = row / CY, cy = row % CY;
@@ -115,41 +104,35 @@ __device__ __forceinline__ void load_row4(const u64* rows, int row, u64 a[4]) {
     for (int j = 0; j < 4; ++j) a[j] = rows[(2 * cz + (j >> 1)) * TY + 2 * cy + (j & 1)];
 }
 
-// highest set bit of m at or below bit position b
-__device__ __forceinline__ int hibit_le(u64 m, int b) {
-    const u64 below = b >= 63 ? ~0ull : ((2ull << b) - 1);
-    return 63 - __builtin_clzll((m & below) | 1ull);
-}
-
-// run start (cube index) of occupied cube (row, cx)
+// run id of occupied cube cx of cube row `row`
 __device__ __forceinline__ u32 run_of(const TileCCL& T, int row, int cx) {
-    return (u32)(row * CX + (hibit_le(T.rstart[row], 2 * cx) >> 1));
+    return T.roff[row] + (u32)__popc(T.B[row] & mask_le(cx)) - 1;
+}
+// run id of the run starting at cube cx0 (a set bit of B)
+__device__ __forceinline__ u32 run_at(const TileCCL& T, int row, int cx0) {
+    return T.roff[row] + (u32)__popc(T.B[row] & ((1u << cx0) - 1));
 }
 
-// quarter q of a cube row: cubes [8q, 8q + 8) = even-representation bits [16q, 16q + 16)
-__device__ __forceinline__ u64 quarter(u64 m, int q) { return m & (0xFFFFull << (16 * q)); }
-
-// Thread (row = tid / 4, q = tid % 4) owns the run starts in quarter q of cube row `row`, so the
-// per-run phases keep all 8 waves busy; tid order is cube order.
+// Thread (row = tid / 4, q = tid % 4) owns the run starts in cubes [8q, 8q + 8) of cube row `row`,
+// so the per-run phases keep all 8 waves busy; tid order is run-id order.
 template <int STOP = 0>   // ablation harness only: return after phase STOP (1..3)
 __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T) {
     const int tid = cc_tid();
     const int qrow = tid >> 2, q = tid & 3;
     u32* par = T.par;
-    // 1. runs per cube row; every run start is its own parent
-    u64 Bq;
+    // 1. runs per cube row, run ids (scan of the run counts), every run its own parent
+    u32 Bq;
     {
         u64 a[4];
         load_row4(rows, qrow, a);
-        const u64 E = xlinks(a);
-        const u64 u = a[0] | a[1] | a[2] | a[3];
-        const u64 B = (u | (u >> 1)) & EVEN64 & ~(E << 2);
-        if (q == 0) T.rstart[qrow] = B;
-        Bq = quarter(B, q);
-        for (u64 m = Bq; m; m &= m - 1) {
-            const u32 s0 = (u32)(qrow * CX + (__builtin_ctzll(m) >> 1));
-            par[s0] = s0;
-        }
+        const u32 L = lo32(a[0] | a[1] | a[2] | a[3]), H = hi32(a[0] | a[1] | a[2] | a[3]);
+        const u32 E = H & (L >> 1);
+        const u32 B = (L | H) & ~(E << 1);
+        u32 nrun = 0;
+        const u32 off = block_excl_scan(q == 0 ? (u32)__popc(B) : 0u, T.scratch, &nrun);
+        if (q == 0) { T.B[qrow] = B; T.E[qrow] = E; T.roff[qrow] = off; }
+        for (u32 i = tid; i < nrun; i += NTHREADS) par[i] = i;
+        Bq = B & (0xFFu << (8 * q));
     }
     __syncthreads();
     if (STOP == 1) return 0;
@@ -167,58 +150,60 @@ __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T) {
         const int szs = dz < 0 ? 0 : 2, szn = dz < 0 ? 1 : 2;
         const int sys = dy < 0 ? 0 : dy > 0 ? 1 : 2, syn = dy < 0 ? 1 : dy > 0 ? 0 : 2;
         const u64 ua = pick_rows(a, szs, sys), ub = pick_rows(b, szn, syn);
-        const u64 ea_prev = xlinks(a) << 2, eb_prev = xlinks(b) << 2;
-        const u64 BA = T.rstart[row], BB = T.rstart[rowb];
+        const u32 ua0 = lo32(ua), ua1 = hi32(ua), ub0 = lo32(ub), ub1 = hi32(ub);
+        const u32 ea_prev = T.E[row] << 1, eb_prev = T.E[rowb] << 1;     // bit cx: cube cx-1 linked to cx
+        const u32 BA = T.B[row], BB = T.B[rowb], ra0 = T.roff[row], rb0 = T.roff[rowb];
 #pragma unroll
         for (int dx = -1; dx <= 1; ++dx) {
-            const int sxs = dx < 0 ? 0 : dx > 0 ? 1 : 2, sxn = dx < 0 ? 1 : dx > 0 ? 0 : 2;
-            const u64 C = xsel(ua, sxs) & shift_dx(xsel(ub, sxn), dx);
-            const u64 red = (C << 2) & ea_prev & shift_dx(eb_prev, dx);
-            for (u64 m = C & ~red; m; m &= m - 1) {
-                const int bit = __builtin_ctzll(m);           // 2 cx
-                const u32 ra = (u32)(row * CX + (hibit_le(BA, bit) >> 1));
-                const u32 rb = (u32)(rowb * CX + (hibit_le(BB, bit + 2 * dx) >> 1));
+            // own cube cx with neighbour cube cx + dx: own voxels facing -dx, neighbour voxels facing dx
+            const u32 C = dx < 0 ? ua0 & (ub1 << 1) : dx > 0 ? ua1 & (ub0 >> 1) : (ua0 | ua1) & (ub0 | ub1);
+            const u32 ebs = dx < 0 ? eb_prev << 1 : dx > 0 ? eb_prev >> 1 : eb_prev;
+            const u32 red = (C << 1) & ea_prev & ebs;
+            for (u32 m = C & ~red; m; m &= m - 1) {
+                const int cx = __builtin_ctz(m);
+                const u32 ra = ra0 + (u32)__popc(BA & mask_le(cx)) - 1;
+                const u32 rb = rb0 + (u32)__popc(BB & mask_le(cx + dx)) - 1;
                 lunion(par, ra, rb);
             }
         }
     }
     __syncthreads();
     if (STOP == 2) return 0;
-    // 3. compress run starts; count the roots of each quarter row
+    // 3. compress; count the roots of each quarter row
+    const u32 r0 = T.roff[qrow];
+    const u32 Brow = T.B[qrow];
     u32 n = 0;
-    for (u64 m = Bq; m; m &= m - 1) {
-        const u32 s0 = (u32)(qrow * CX + (__builtin_ctzll(m) >> 1));
-        const u32 r = lfind(as_lds(par), s0);
-        par[s0] = r;
-        n += (r == s0);
+    for (u32 m = Bq; m; m &= m - 1) {
+        const u32 r = r0 + (u32)__popc(Brow & ((1u << __builtin_ctz(m)) - 1));
+        const u32 root = lfind(as_lds(par), r);
+        par[r] = root;
+        n += (root == r);
     }
     __syncthreads();
     if (STOP == 3) return 0;
-    // 4. compact index k of every root, in cube order
+    // 4. compact index k of every root, in run-id order
     u32 total = 0;
     {
         const u32 base = block_excl_scan(n, T.scratch, &total);
         u32 k = base;
-        for (u64 m = Bq; m; m &= m - 1) {
-            const u32 s0 = (u32)(qrow * CX + (__builtin_ctzll(m) >> 1));
-            if (par[s0] == s0) par[s0] = s0 | (k++ << 16);
+        for (u32 m = Bq; m; m &= m - 1) {
+            const u32 r = r0 + (u32)__popc(Brow & ((1u << __builtin_ctz(m)) - 1));
+            if (par[r] == r) par[r] = r | (k++ << 16);
         }
     }
     __syncthreads();
-    // 5. every run start carries its component's k
-    for (u64 m = Bq; m; m &= m - 1) {
-        const u32 s0 = (u32)(qrow * CX + (__builtin_ctzll(m) >> 1));
-        const u32 r = par[s0] & 0xFFFFu;
-        if (r != s0) par[s0] = r | (par[r] & 0xFFFF0000u);
+    // 5. every run carries its component's k
+    for (u32 m = Bq; m; m &= m - 1) {
+        const u32 r = r0 + (u32)__popc(Brow & ((1u << __builtin_ctz(m)) - 1));
+        const u32 root = par[r] & 0xFFFFu;
+        if (root != r) par[r] = root | (par[root] & 0xFFFF0000u);
     }
     __syncthreads();
     return total;
 }
 
 // component index k of an occupied cube
-__device__ __forceinline__ u32 cube_k(const TileCCL& T, int row, int cx) {
-    return T.par[run_of(T, row, cx)] >> 16;
-}
+__device__ __forceinline__ u32 cube_k(const TileCCL& T, int row, int cx) { return T.par[run_of(T, row, cx)] >> 16; }
 __device__ __forceinline__ u32 cube_k(const TileCCL& T, int c) { return cube_k(T, c / CX, c % CX); }
 
 // ------------------------------------------------------------------------------------------
@@ -409,6 +394,18 @@ __global__ void k_block_params(int64_t nb, const u32* smin, const u32* smax, con
 // (writelane) and stored with one 8-B LDS write per lane.  Rows outside the tile stay 0.
 // The v_writelane asm relies on wave-uniform control flow here (the wave index and the tile are
 // SGPR values); under a branch the compiler treats as divergent it produced wrong rows (k_seams).
+// natural bit row (bit x <-> voxel x) -> split row (even voxels low, odd voxels high): the
+// inverse perfect shuffle, once per row after the (coalesced, lane = x) loads
+__device__ __forceinline__ u64 split_row(u64 x) {
+    u64 t;
+    t = (x ^ (x >> 1)) & 0x2222222222222222ull;  x ^= t ^ (t << 1);
+    t = (x ^ (x >> 2)) & 0x0C0C0C0C0C0C0C0Cull;  x ^= t ^ (t << 2);
+    t = (x ^ (x >> 4)) & 0x00F000F000F000F0ull;  x ^= t ^ (t << 4);
+    t = (x ^ (x >> 8)) & 0x0000FF000000FF00ull;  x ^= t ^ (t << 8);
+    t = (x ^ (x >> 16)) & 0x00000000FFFF0000ull; x ^= t ^ (t << 16);
+    return x;
+}
+
 template <bool HAS_MASK>
 __device__ __forceinline__ void load_rows(const Geom& g, const TileInfo& ti, const float* __restrict__ in,
                                           const u8* __restrict__ mask, const BlockParam& p, float thr,
@@ -439,8 +436,13 @@ __device__ __forceinline__ void load_rows(const Geom& g, const TileInfo& ti, con
         });
     }
     const int r = slot_row(lane, wave);
-    if (r / TY < ti.lz && r % TY < ti.ly) rows[r] = ((u64)mhi << 32) | mlo;
+    if (r / TY < ti.lz && r % TY < ti.ly) rows[r] = split_row(((u64)mhi << 32) | mlo);
 }
+
+// voxel x of a split bit row
+__device__ __forceinline__ u32 vbit(u64 w, int x) { return (u32)(w >> ((x & 1) * 32 + (x >> 1))) & 1u; }
+// the two voxels (2cx, 2cx + 1) of cube column cx of a split row, as bits 0 / 1
+__device__ __forceinline__ u32 vpair(u64 w, int cx) { return ((u32)(w >> cx) & 1u) | (((u32)(w >> (32 + cx)) & 1u) << 1); }
 
 // face plane entry i of a tile (see cc_common.hpp for the layout)
 __device__ __forceinline__ u32 face_entry(int i, const u64* rows, const TileCCL& T, const TileInfo& ti) {
@@ -452,8 +454,7 @@ __device__ __forceinline__ u32 face_entry(int i, const u64* rows, const TileCCL&
         const int cy = e / CX, cx = e % CX;
         if (2 * cy >= ti.ly || 2 * cx >= ti.lx) return 0;
         const int z = hi ? ti.lz - 1 : 0;
-        const u64 r0 = rows[z * TY + 2 * cy], r1 = rows[z * TY + 2 * cy + 1];
-        bits = (u32)((r0 >> (2 * cx)) & 3) | ((u32)((r1 >> (2 * cx)) & 3) << 2);
+        bits = vpair(rows[z * TY + 2 * cy], cx) | (vpair(rows[z * TY + 2 * cy + 1], cx) << 2);
         c = ((z >> 1) * CY + cy) * CX + cx;
     } else if (i < F_XLO) {                // y faces: (cz, cx), bits (z-local)*2 + (x-local)
         const bool hi = i >= F_YHI;
@@ -461,8 +462,7 @@ __device__ __forceinline__ u32 face_entry(int i, const u64* rows, const TileCCL&
         const int cz = e / CX, cx = e % CX;
         if (2 * cz >= ti.lz || 2 * cx >= ti.lx) return 0;
         const int y = hi ? ti.ly - 1 : 0;
-        const u64 r0 = rows[(2 * cz) * TY + y], r1 = rows[(2 * cz + 1) * TY + y];
-        bits = (u32)((r0 >> (2 * cx)) & 3) | ((u32)((r1 >> (2 * cx)) & 3) << 2);
+        bits = vpair(rows[(2 * cz) * TY + y], cx) | (vpair(rows[(2 * cz + 1) * TY + y], cx) << 2);
         c = (cz * CY + (y >> 1)) * CX + cx;
     } else {                               // x faces: (cz, cy), bits (z-local)*2 + (y-local)
         const bool hi = i >= F_XHI;
@@ -471,8 +471,8 @@ __device__ __forceinline__ u32 face_entry(int i, const u64* rows, const TileCCL&
         if (2 * cz >= ti.lz || 2 * cy >= ti.ly) return 0;
         const int x = hi ? ti.lx - 1 : 0;
         const int r = (2 * cz) * TY + 2 * cy;
-        bits = (u32)((rows[r] >> x) & 1) | ((u32)((rows[r + 1] >> x) & 1) << 1) |
-               ((u32)((rows[r + TY] >> x) & 1) << 2) | ((u32)((rows[r + TY + 1] >> x) & 1) << 3);
+        bits = vbit(rows[r], x) | (vbit(rows[r + 1], x) << 1) | (vbit(rows[r + TY], x) << 2) |
+               (vbit(rows[r + TY + 1], x) << 3);
         c = (cz * CY + cy) * CX + (x >> 1);
     }
     if (!bits) return 0;
@@ -486,7 +486,7 @@ __device__ __forceinline__ u32 face_entry(int i, const u64* rows, const TileCCL&
 struct Pass1LDS {
     u64 rows[NROWS];
     TileCCL T;
-    u32 key[NC];              // first voxel (tile raster index) of each component
+    u32 key[NRUN];            // first voxel (tile raster index) of each component (<= one per run)
 };
 
 // Pass 1 of tile t (block parameters p): bit rows -> BITS, tile CCL -> COUNT, nodes (P, KEY),
@@ -514,26 +514,28 @@ __device__ __forceinline__ void pass1_tile(const Geom& g, int64_t t, const TileI
     if (ABL == 2) { if (tid == 0) COUNT[t] = R; return; }
     for (u32 k = tid; k < R; k += NTHREADS) key[k] = NONE;
     __syncthreads();
-    // first voxel of each run: voxel order inside a run is (dz, dy) first, then x
+    // first voxel of each run in raster order: the first sub-row (lz, ly) with a voxel in the
+    // run's cubes, then its smallest x
     {
         const int row = tid >> 2, q = tid & 3;
         const int cz = row / CY, cy = row % CY;
         u64 a[4];
         load_row4(rows, row, a);
-        const u64 E = xlinks(a);
-        for (u64 m = quarter(T.rstart[row], q); m; m &= m - 1) {
-            const int b0 = __builtin_ctzll(m);                              // 2 * start cube
-            const u64 tail = ~(E >> b0) & EVEN64;                           // first unlinked cube
-            const int b1 = b0 + __builtin_ctzll(tail | (1ull << 62));       // 2 * end cube
-            const u64 hi = b1 + 1 >= 63 ? ~0ull : ((2ull << (b1 + 1)) - 1);
-            const u64 xr = hi & ~((1ull << b0) - 1);
+        const u32 Brow = T.B[row], E = T.E[row], r0 = T.roff[row];
+        for (u32 m = Brow & (0xFFu << (8 * q)); m; m &= m - 1) {
+            const int c0 = __builtin_ctz(m);                                  // start cube
+            const int c1 = c0 + __builtin_ctz(~(E >> c0));                    // end cube
+            const u32 M = mask_le(c1) & ~((1u << c0) - 1);
             u32 idx = NONE;
 #pragma unroll
             for (int j = 3; j >= 0; --j) {
-                const u64 r = a[j] & xr;
-                if (r) idx = (u32)(((2 * cz + (j >> 1)) * TY + 2 * cy + (j & 1)) * TX + __builtin_ctzll(r));
+                const u32 ev = lo32(a[j]) & M, od = hi32(a[j]) & M;
+                if (ev | od) {
+                    const int xe = ev ? 2 * __builtin_ctz(ev) : TX, xo = od ? 2 * __builtin_ctz(od) + 1 : TX;
+                    idx = (u32)(((2 * cz + (j >> 1)) * TY + 2 * cy + (j & 1)) * TX + (xe < xo ? xe : xo));
+                }
             }
-            atomicMin(&key[T.par[row * CX + (b0 >> 1)] >> 16], idx);
+            atomicMin(&key[T.par[r0 + (u32)__popc(Brow & ((1u << c0) - 1))] >> 16], idx);
         }
     }
     __syncthreads();
@@ -1868,7 +1870,7 @@ __device__ __forceinline__ void store2(u64* __restrict__ out, int64_t idx, u64 v
 
 __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restrict__ BITS, const u32* COUNT,
                                                     const u64* __restrict__ FIN, u64* __restrict__ out) {
-    __shared__ u64 rows[NROWS];
+    __shared__ u64 rows[NROWS];             // split bit rows (see tile_ccl)
     __shared__ TileCCL T;
     __shared__ u64 lab[LABCAP];
     const int64_t t = blockIdx.x;
@@ -1900,9 +1902,9 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
     for (int c = tid; c < NC; c += NTHREADS) {
         const int cz = c / (CY * CX), cy = (c / CX) % CY, cx = c % CX;
         if (cz >= ncz || cy >= ncy || cx >= ncx) continue;
-        const int r = (2 * cz) * TY + 2 * cy, sh = 2 * cx;
-        const u32 m = (u32)((rows[r] >> sh) & 3) | ((u32)((rows[r + 1] >> sh) & 3) << 2) |
-                      ((u32)((rows[r + TY] >> sh) & 3) << 4) | ((u32)((rows[r + TY + 1] >> sh) & 3) << 6);
+        const int r = (2 * cz) * TY + 2 * cy;
+        const u32 m = vpair(rows[r], cx) | (vpair(rows[r + 1], cx) << 2) | (vpair(rows[r + TY], cx) << 4) |
+                      (vpair(rows[r + TY + 1], cx) << 6);
         u64 v = 0;
         if (m) {
             const u32 k = cube_k(T, c);

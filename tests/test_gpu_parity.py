@@ -98,6 +98,19 @@ def test_white_noise_tile_seams(ctx, density):
     _check_against_oracle(ctx, inp, (20, 40, 75), 1 - density, 'greater')
 
 
+def test_max_runs_per_tile(ctx):
+    """Worst case for the tile union-find: every 2x2x2 cube occupied but no two x-neighbouring
+    cubes linked (foreground only at even x), i.e. one run per cube (4096 per tile), plus
+    white noise in the odd columns of a few slabs so some runs do link."""
+    rng = np.random.default_rng(11)
+    inp = np.zeros((48, 96, 192), dtype=np.float32)
+    inp[:, :, 0::2] = 1.0
+    inp[24:, :, 1::2] = (rng.random((24, 96, 96)) < 0.3).astype(np.float32)
+    _check_against_oracle(ctx, inp, (48, 96, 192), 0.5, 'greater')
+    _check_against_oracle(ctx, inp, (16, 32, 64), 0.5, 'greater')
+    _check_against_oracle(ctx, inp, (48, 96, 192), 0.5, 'less')
+
+
 def test_mask_vs_oracle(ctx):
     from oracle.synth import ellipsoid_mask
     shape = (64, 160, 192)
