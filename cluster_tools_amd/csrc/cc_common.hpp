@@ -45,6 +45,20 @@ struct BlockParam {      // per reference block, from its min/max (volume_utils.
     u32 pad;
 };
 
+// block parameters read from global memory come back in VGPRs (the compiler cannot prove the
+// buffer unwritten); branches on them must be seen as uniform or the writelane row collection in
+// load_rows runs under a divergent region and produces wrong rows: move them to SGPRs
+__device__ __forceinline__ BlockParam uniform_bp(const BlockParam& q) {
+    BlockParam p;
+    p.mn = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(q.mn)));
+    p.m = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(q.m)));
+    p.lo = __builtin_amdgcn_readfirstlane(q.lo);
+    p.hi = __builtin_amdgcn_readfirstlane(q.hi);
+    p.kind = __builtin_amdgcn_readfirstlane(q.kind);
+    p.pad = 0;
+    return p;
+}
+
 struct Geom {
     int64_t Z, Y, X;          // volume (or z-slab) shape
     int64_t zoff;             // global z of this volume's first plane (keys / multi-GPU)

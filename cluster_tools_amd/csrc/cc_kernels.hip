@@ -394,6 +394,15 @@ __global__ void k_block_params(int64_t nb, const u32* smin, const u32* smax, con
 // (writelane) and stored with one 8-B LDS write per lane.  Rows outside the tile stay 0.
 // The v_writelane asm relies on wave-uniform control flow here (the wave index and the tile are
 // SGPR values); under a branch the compiler treats as divergent it produced wrong rows (k_seams).
+// lane j of (lo, hi) := the SGPR pair (blo, bhi).  The s_nop: the ballot feeding blo is often
+// the VALU instruction right before, and v_writelane reading an SGPR a VALU has just written
+// took the stale value (lanes 0-31 of rows lost in k_spec); inline asm is opaque to the
+// compiler's hazard recognizer, so the wait states are spelled out.  j must be a constant.
+#define CC_WRITELANE2(lo, hi, blo, bhi, j)                                                        \
+    asm("s_nop 3\n\tv_writelane_b32 %0, %2, %4\n\tv_writelane_b32 %1, %3, %4"                      \
+        : "+v"(lo), "+v"(hi)                                                                      \
+        : "s"(blo), "s"(bhi), "i"(j))
+
 // natural bit row (bit x <-> voxel x) -> split row (even voxels low, odd voxels high): the
 // inverse perfect shuffle, once per row after the (coalesced, lane = x) loads
 __device__ __forceinline__ u64 split_row(u64 x) {
@@ -416,8 +425,7 @@ __device__ __forceinline__ void load_rows(const Geom& g, const TileInfo& ti, con
     auto put = [&](int j, u64 bal) {
         bal &= lanes;
         const u32 blo = (u32)bal, bhi = (u32)(bal >> 32);
-        asm("v_writelane_b32 %0, %1, %2" : "+v"(mlo) : "s"(blo), "i"(j));
-        asm("v_writelane_b32 %0, %1, %2" : "+v"(mhi) : "s"(bhi), "i"(j));
+        CC_WRITELANE2(mlo, mhi, blo, bhi, j);
     };
     if (p.kind == BP_INTERVAL) {
         // lo <= ord(x) <= hi as two float compares: the interval never splits -0 from +0 (the
@@ -489,6 +497,10 @@ struct Pass1LDS {
     u32 key[NRUN];            // first voxel (tile raster index) of each component (<= one per run)
 };
 
+template <int ABL>
+__device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const TileInfo& ti, u64* BITS, u32* FACES,
+                                             u32* COUNT, u32* P, u64* KEY, Pass1LDS& L, bool write);
+
 // Pass 1 of tile t (block parameters p): bit rows -> BITS, tile CCL -> COUNT, nodes (P, KEY),
 // face planes.  ABL (kernel ablation harness tools/ablate.hip only; 0 in the library): stop
 // after phase ABL (1 bits, 2 CCL, 3 first voxels; 11..13 inside the CCL after its phase 1..3).
@@ -497,15 +509,23 @@ __device__ __forceinline__ void pass1_tile(const Geom& g, int64_t t, const TileI
                                            const float* __restrict__ in, const u8* __restrict__ mask, float thr,
                                            int mode, u64* BITS, u32* FACES, u32* COUNT, u32* P, u64* KEY,
                                            Pass1LDS& L, bool write = true) {
+    const int tid = cc_tid();
+    // (unconditional zeroing: every caller passes the same barriers, also the halves of k_front)
+    for (int i = tid; i < NROWS; i += NTHREADS) L.rows[i] = 0;
+    __syncthreads();
+    if (p.kind != BP_EMPTY) load_rows<HAS_MASK>(g, ti, in, mask, p, thr, mode, L.rows);
+    __syncthreads();
+    pass1_finish<ABL>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, write);
+}
+
+// Pass 1 after the bit rows are in L.rows (and a barrier): BITS, tile CCL, COUNT, nodes, faces.
+template <int ABL>
+__device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const TileInfo& ti, u64* BITS, u32* FACES,
+                                             u32* COUNT, u32* P, u64* KEY, Pass1LDS& L, bool write) {
     u64* rows = L.rows;
     TileCCL& T = L.T;
     u32* key = L.key;
     const int tid = cc_tid();
-    // (unconditional zeroing: every caller passes the same barriers, also the halves of k_front)
-    for (int i = tid; i < NROWS; i += NTHREADS) rows[i] = 0;
-    __syncthreads();
-    if (p.kind != BP_EMPTY) load_rows<HAS_MASK>(g, ti, in, mask, p, thr, mode, rows);
-    __syncthreads();
     if (write)
         for (int i = tid; i < NROWS; i += NTHREADS) BITS[t * NROWS + i] = rows[i];
     if (ABL == 1) return;
@@ -563,7 +583,7 @@ __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restr
     __shared__ Pass1LDS L;
     const int64_t t = blockIdx.x;
     const TileInfo ti = tile_info(g, t);
-    pass1_tile<HAS_MASK, ABL>(g, t, ti, bp[ti.block], in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L);
+    pass1_tile<HAS_MASK, ABL>(g, t, ti, uniform_bp(bp[ti.block]), in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -638,6 +658,183 @@ __device__ __forceinline__ TileInfo uniform_ti(TileInfo ti) {
     const u64 b = (u64)ti.block;
     ti.block = (int64_t)(((u64)__builtin_amdgcn_readfirstlane((u32)(b >> 32)) << 32) | __builtin_amdgcn_readfirstlane((u32)b));
     return ti;
+}
+
+// ------------------------------------------------------------------------------------------
+// Speculative front (the library's path): block statistics and pass 1 from ONE read of the input.
+//
+// The foreground of a block is an interval of the float order fixed by the block's min / max
+// (k_block_params), which are only known once the whole block has been read.  k_sample guesses
+// each block's interval from a sparse sample (1/128 of the block); k_spec then reads every tile
+// once, accumulating the exact block statistics AND labelling the tile (pass 1) with the guessed
+// interval [lg, hg], and records per tile the nearest values on both sides of each guessed bound:
+//   TB = { max ord < lg, min ord >= lg, max ord <= hg, min ord > hg }  (masked-out voxels excluded).
+// With the exact interval [lt, ht] (k_block_params) a tile's bits are the exact bits iff no voxel
+// lies between lg and lt nor between hg and ht -- decided from TB alone (spec_valid).  k_verify
+// k_fix relabels the tiles that fail from the input with the exact interval.
+// A one-sided interval is kept open to the end of the order (widen): it then differs from the
+// exact one only in its finite bound.  The guess is made only where the sample looks quantized
+// (its extremes occur more than once): on continuous data a sampled bound is almost never exact,
+// so those blocks skip the speculation (k_spec reads them for statistics only, k_fix labels them).
+// Results never depend on the guess; only the amount of k_fix work does.
+// ------------------------------------------------------------------------------------------
+constexpr int SAMPLE_DZ = 8, SAMPLE_DY = 16;      // one voxel row per 8 planes x 16 rows of a block
+
+__device__ __forceinline__ void block_extent(const Geom& g, int64_t b, int e0[3], int el[3]) {
+    const int bi[3] = {(int)(b / ((int64_t)g.nb[2] * g.nb[1])), (int)((b / g.nb[2]) % g.nb[1]), (int)(b % g.nb[2])};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const int t0 = g.bt0[a][bi[a]], t1 = t0 + g.btn[a][bi[a]] - 1;
+        e0[a] = g.tstart[a][t0];
+        el[a] = g.tstart[a][t1] + g.tlen[a][t1] - e0[a];
+    }
+}
+
+__device__ __forceinline__ BlockParam widen(BlockParam p, int mode) {
+    if (p.kind == BP_INTERVAL) {
+        if (mode == MODE_GREATER) p.hi = 0xFFFFFFFFu;
+        else if (mode == MODE_LESS) p.lo = 0u;
+    }
+    return p;
+}
+
+// block-wide reduction of one value per thread (red: NTHREADS / 64 words); result in every thread
+template <class Op>
+__device__ __forceinline__ u32 block_reduce(u32 v, u32* red, Op op) {
+    const int tid = cc_tid();
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o, 64));
+    __syncthreads();
+    if ((tid & 63) == 0) red[tid >> 6] = v;
+    __syncthreads();
+    v = red[0];
+#pragma unroll
+    for (int w = 1; w < NTHREADS / 64; ++w) v = op(v, red[w]);
+    return v;
+}
+
+__global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __restrict__ in, float thr, int mode,
+                                                     BlockParam* guess) {
+    __shared__ u32 red[NTHREADS / 64];
+    const int64_t b = blockIdx.x;
+    const int tid = cc_tid();
+    int e0[3], el[3];
+    block_extent(g, b, e0, el);
+    const int nzs = max(1, el[0] / SAMPLE_DZ), nys = max(1, el[1] / SAMPLE_DY);
+    const int zo = min(SAMPLE_DZ / 2, (el[0] - 1) / 2), yo = min(SAMPLE_DY / 2, (el[1] - 1) / 2);
+    auto sweep = [&](auto&& f) {
+        for (int r = 0; r < nzs * nys; ++r) {
+            const int z = e0[0] + (r / nys) * SAMPLE_DZ + zo, y = e0[1] + (r % nys) * SAMPLE_DY + yo;
+            const float* row = in + ((int64_t)z * g.Y + y) * g.X + e0[2];
+#pragma unroll 4
+            for (int x = tid; x < el[2]; x += NTHREADS) f(f2ord(__float_as_uint(row[x])));
+        }
+    };
+    u32 mn = 0xFFFFFFFFu, mx = 0u;
+    sweep([&](u32 o) { mn = min(mn, o); mx = max(mx, o); });
+    mn = block_reduce(mn, red, [](u32 a, u32 c) { return min(a, c); });
+    mx = block_reduce(mx, red, [](u32 a, u32 c) { return max(a, c); });
+    u32 nmn = 0, nmx = 0;
+    sweep([&](u32 o) { nmn += (o == mn); nmx += (o == mx); });
+    nmn = block_reduce(nmn, red, [](u32 a, u32 c) { return a + c; });
+    nmx = block_reduce(nmx, red, [](u32 a, u32 c) { return a + c; });
+    if (tid == 0) {
+        const bool nan = mx > 0xFF800000u || mn < 0x007FFFFFu;
+        BlockParam p = block_param(mn, mx, nan ? 1u : 0u, thr, mode);
+        if (nmn < 2 || nmx < 2) p.kind = BP_EMPTY;     // continuous values: no guess
+        guess[b] = widen(p, mode);
+    }
+}
+
+struct SpecArgs {
+    const BlockParam* guess;
+    u32* smin; u32* smax; u32* sflag;
+    u32* TB;                  // 4 per tile (see above)
+};
+
+// SIDES: bounds of the guessed interval that can move (1 lower: 'greater', 2 upper: 'less', 3 both)
+template <bool HAS_MASK, int SIDES>
+__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_spec(
+    Geom g, SpecArgs sa, const float* __restrict__ in, const u8* __restrict__ mask, u64* BITS, u32* FACES,
+    u32* COUNT, u32* P, u64* KEY) {
+    __shared__ Pass1LDS L;
+    __shared__ u32 red[6][NTHREADS / 64];
+    const int64_t t = blockIdx.x;
+    const TileInfo ti = tile_info(g, t);
+    const BlockParam p = uniform_bp(sa.guess[ti.block]);
+    if (p.kind != BP_INTERVAL) {                   // no guess: statistics only, k_fix labels the tile
+        stats_tile(g, ti, in, sa.smin, sa.smax, sa.sflag, red);
+        return;
+    }
+    const int tid = cc_tid(), lane = tid & 63, wave = wave_id();
+    for (int i = tid; i < NROWS; i += NTHREADS) L.rows[i] = 0;
+    __syncthreads();
+    const u32 lo = p.lo, hi = p.hi;
+    const u64 lanes = ti.lx >= 64 ? ~0ull : ((1ull << ti.lx) - 1);
+    u32 mn = 0xFFFFFFFFu, mx = 0u, A = 0u, B = 0xFFFFFFFFu, C = 0u, D = 0xFFFFFFFFu;
+    u32 mlo = 0, mhi = 0;                         // lane j: row mask of slot j (see load_rows)
+    for_tile_rows<HAS_MASK>(g, ti, in, mask, [&](int j, float x, u32 mk) {
+        const u32 o = f2ord(__float_as_uint(x));
+        mn = min(mn, o);
+        mx = max(mx, o);
+        const bool ge = o >= lo, le = o <= hi;
+        const bool use = !HAS_MASK || mk != 0;
+        const bool fg = use && (SIDES == 1 ? ge : SIDES == 2 ? le : ge && le);
+        if (SIDES & 1) { A = max(A, use && !ge ? o : 0u); B = min(B, use && ge ? o : 0xFFFFFFFFu); }
+        if (SIDES & 2) { C = max(C, use && le ? o : 0u); D = min(D, use && !le ? o : 0xFFFFFFFFu); }
+        const u64 bal = __ballot(fg) & lanes;
+        const u32 blo = (u32)bal, bhi = (u32)(bal >> 32);
+        CC_WRITELANE2(mlo, mhi, blo, bhi, j);
+    });
+    const int r = slot_row(lane, wave);
+    if (r / TY < ti.lz && r % TY < ti.ly) L.rows[r] = split_row(((u64)mhi << 32) | mlo);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (u32)__shfl_xor(mn, o, 64));
+        mx = max(mx, (u32)__shfl_xor(mx, o, 64));
+        if (SIDES & 1) { A = max(A, (u32)__shfl_xor(A, o, 64)); B = min(B, (u32)__shfl_xor(B, o, 64)); }
+        if (SIDES & 2) { C = max(C, (u32)__shfl_xor(C, o, 64)); D = min(D, (u32)__shfl_xor(D, o, 64)); }
+    }
+    if (lane == 0) {
+        red[0][wave] = mn; red[1][wave] = mx; red[2][wave] = A; red[3][wave] = B; red[4][wave] = C; red[5][wave] = D;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < NTHREADS / 64; ++w) {
+            mn = min(mn, red[0][w]); mx = max(mx, red[1][w]);
+            A = max(A, red[2][w]); B = min(B, red[3][w]); C = max(C, red[4][w]); D = min(D, red[5][w]);
+        }
+        atomicMin(sa.smin + ti.block, mn);
+        atomicMax(sa.smax + ti.block, mx);
+        if (mx > 0xFF800000u || mn < 0x007FFFFFu) atomicOr(sa.sflag + ti.block, 1u);    // NaN
+        u32* tb = sa.TB + 4 * t;
+        tb[0] = A; tb[1] = B; tb[2] = C; tb[3] = D;
+    }
+    pass1_finish<0>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, true);
+}
+
+// are the bits computed with the guess G those of the exact parameters T? (see above)
+__device__ __forceinline__ bool spec_valid(const BlockParam& G, BlockParam T, const u32* tb, int mode) {
+    if (G.kind != BP_INTERVAL || T.kind != BP_INTERVAL) return false;
+    T = widen(T, mode);
+    if (T.lo != G.lo && (T.lo > G.lo ? tb[1] < T.lo : tb[0] >= T.lo)) return false;
+    if (T.hi != G.hi && (T.hi < G.hi ? tb[2] > T.hi : tb[3] <= T.hi)) return false;
+    return true;
+}
+
+// pass 1 with the exact parameters for every tile whose guessed bits were not exact; one
+// workgroup per tile (the others return at once: a persistent loop over a tile list hoisted the
+// tile set-up out of the loop and spilled)
+template <bool HAS_MASK>
+__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_fix(
+    Geom g, const BlockParam* guess, const BlockParam* bp, const u32* TB, const float* __restrict__ in,
+    const u8* __restrict__ mask, float thr, int mode, u64* BITS, u32* FACES, u32* COUNT, u32* P, u64* KEY) {
+    __shared__ Pass1LDS L;
+    const int64_t t = blockIdx.x;
+    const TileInfo ti = tile_info(g, t);
+    const BlockParam p = uniform_bp(bp[ti.block]);
+    if (__builtin_amdgcn_readfirstlane((int)spec_valid(guess[ti.block], p, TB + 4 * t, mode))) return;
+    pass1_tile<HAS_MASK>(g, t, ti, p, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L);
 }
 
 // TV (ablation harness only; 0 in the library): 2 = no wait, 3 = 2 + skip pass-1 items,
@@ -1151,7 +1348,7 @@ template <int L>
 __device__ __forceinline__ void put_rows(u32 (&w)[4], u64 a, u64 b) {
 #ifdef CC_PUT_ASM
     const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
-    asm("v_writelane_b32 %0, %1, %2" : "+v"(w[0]) : "s"(a0), "i"(L));
+    asm("s_nop 3\n\tv_writelane_b32 %0, %1, %2" : "+v"(w[0]) : "s"(a0), "i"(L));
     asm("v_writelane_b32 %0, %1, %2" : "+v"(w[1]) : "s"(a1), "i"(L));
     asm("v_writelane_b32 %0, %1, %2" : "+v"(w[2]) : "s"(b0), "i"(L));
     asm("v_writelane_b32 %0, %1, %2" : "+v"(w[3]) : "s"(b1), "i"(L));
@@ -1926,6 +2123,14 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
 
 // instantiate the templates used by the host side
 template __global__ void k_front<0>(Geom, FrontArgs, const float*, float, int, u64*, u32*, u32*, u32*, u64*);
+#define CC_SPEC(M, S) \
+    template __global__ void k_spec<M, S>(Geom, SpecArgs, const float*, const u8*, u64*, u32*, u32*, u32*, u64*);
+CC_SPEC(false, 1) CC_SPEC(false, 2) CC_SPEC(false, 3) CC_SPEC(true, 1) CC_SPEC(true, 2) CC_SPEC(true, 3)
+#undef CC_SPEC
+template __global__ void k_fix<false>(Geom, const BlockParam*, const BlockParam*, const u32*, const float*, const u8*,
+                                      float, int, u64*, u32*, u32*, u32*, u64*);
+template __global__ void k_fix<true>(Geom, const BlockParam*, const BlockParam*, const u32*, const float*, const u8*,
+                                     float, int, u64*, u32*, u32*, u32*, u64*);
 template __global__ void k_seams<0>(Geom, const u32*, u64*, u32*, u8*, u64*, u32*, u8*);
 template __global__ void k_stitch<false>(Geom, const u32*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_stitch<true>(Geom, const u32*, u32*, const u64*, const u8*, const u8*);

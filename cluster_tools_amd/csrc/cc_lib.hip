@@ -54,7 +54,7 @@ struct cc_ctx {
     // workspace
     DevBuf front, tiles, bstat, bparam, bits, faces, count, rc, roff, P, KR, FIN, keys, keys2, vals, vals2, seg,
         values, offsets, lut, cub_tmp, scalars, scalars2, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2,
-        flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf;
+        flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf, spec;
     // last run
     int64_t n_blocks = 0;
     uint64_t n_labels = 0;
@@ -178,7 +178,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     hipStream_t s = c->stream;
 
     c->bstat.ensure(nb * 5 * sizeof(u32) + 2 * sizeof(u32));
-    c->bparam.ensure(nb * sizeof(BlockParam));
+    c->bparam.ensure(2 * nb * sizeof(BlockParam));     // exact parameters, then the guesses (k_sample)
     c->bits.ensure(nt * NROWS * sizeof(u64));
     c->faces.ensure(nt * FACE_STRIDE * sizeof(u32));
     c->count.ensure(nt * sizeof(u32));
@@ -207,7 +207,41 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     u64* KR = c->KR.as<u64>();
     const float thr = st.thr;
 
-    {
+    const char* fe = std::getenv("CC_FRONT");
+    if (!(fe && std::string(fe) == "fused")) {
+        // speculative front: sample -> one read for statistics + pass 1 -> exact parameters ->
+        // relabel the tiles whose guessed interval was not exact (see k_spec)
+        BlockParam* guess = bp + nb;
+        c->spec.ensure(4 * nt * sizeof(u32));
+        u32* TB = c->spec.as<u32>();
+        launch(c, "k_sample", [&] { k_sample<<<(unsigned)nb, NTHREADS, 0, s>>>(g, in, thr, mode, guess); });
+        if (const char* e = std::getenv("CC_SPEC"); e && std::string(e) == "0")     // test hook: no guesses
+            HIP_OK(hipMemsetAsync(guess, 0, nb * sizeof(BlockParam), s));
+        SpecArgs sa;
+        sa.guess = guess;
+        sa.smin = smin; sa.smax = smax; sa.sflag = sflag;
+        sa.TB = TB;
+        launch(c, "k_spec", [&] {
+#define CC_SPEC_LAUNCH(M, S) k_spec<M, S><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, mask, BITS, FACES, COUNT, P, KR)
+            if (mask) {
+                if (mode == MODE_GREATER) CC_SPEC_LAUNCH(true, 1);
+                else if (mode == MODE_LESS) CC_SPEC_LAUNCH(true, 2);
+                else CC_SPEC_LAUNCH(true, 3);
+            } else {
+                if (mode == MODE_GREATER) CC_SPEC_LAUNCH(false, 1);
+                else if (mode == MODE_LESS) CC_SPEC_LAUNCH(false, 2);
+                else CC_SPEC_LAUNCH(false, 3);
+            }
+#undef CC_SPEC_LAUNCH
+        });
+        launch(c, "k_block_params", [&] {
+            k_block_params<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, smin, smax, sflag, thr, mode, bp);
+        });
+        launch(c, "k_fix", [&] {
+            if (mask) k_fix<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, guess, bp, TB, in, mask, thr, mode, BITS, FACES, COUNT, P, KR);
+            else k_fix<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, guess, bp, TB, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR);
+        });
+    } else {
         int64_t lag = 1;
         if (const char* e = std::getenv("CC_FRONT_LAG")) lag = std::max<int64_t>(1, std::atoll(e));
         const int per_s = 2, per_p = 1;                  // tiles per stats / pass-1 item (2: measured best)
@@ -543,7 +577,7 @@ void cc_destroy(cc_ctx* c) {
                       &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
                       &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
-                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf};
+                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec};
     for (DevBuf* b : bufs) b->release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);

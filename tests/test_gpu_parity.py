@@ -111,6 +111,22 @@ def test_max_runs_per_tile(ctx):
     _check_against_oracle(ctx, inp, (48, 96, 192), 0.5, 'less')
 
 
+@pytest.mark.parametrize('outlier', [-1.0, -1.0 / 32, 3.0, 1.0 + 1.0 / 64])
+@pytest.mark.parametrize('mode,thr', [('greater', 0.5), ('less', 0.5), ('equal', 0.5), ('greater', 0.3)])
+def test_speculated_interval_corrected(ctx, mode, thr, outlier):
+    """Quantized data whose block extremes the sample misses (one outlier voxel off the sampled
+    rows): the guessed interval is wrong; tiles with voxels between the guessed and the exact
+    bounds must be relabelled (large outliers), the others kept (small outliers)."""
+    rng = np.random.default_rng(3)
+    inp = (rng.integers(0, 17, (64, 128, 192)) / np.float32(16)).astype(np.float32)
+    inp[1, 1, 5] = outlier               # block (0, 0, 0); sample rows are z = 4 mod 8, y = 8 mod 16
+    inp[33, 70, 100] = outlier           # block (1, 1, 1)
+    for bs in [(32, 64, 96), (64, 128, 192)]:
+        _check_against_oracle(ctx, inp, bs, thr, mode)
+    mask = (rng.random(inp.shape) < 0.9).astype(np.uint8)
+    _check_against_oracle(ctx, inp, (32, 64, 96), thr, mode, mask)
+
+
 def test_mask_vs_oracle(ctx):
     from oracle.synth import ellipsoid_mask
     shape = (64, 160, 192)
