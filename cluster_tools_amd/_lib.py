@@ -29,7 +29,7 @@ EXPORTS = (
 class CCResult(ctypes.Structure):
     _fields_ = [('n_blocks', ctypes.c_int64), ('n_labels', ctypes.c_uint64),
                 ('max_id', ctypes.c_uint64), ('n_components', ctypes.c_uint64),
-                ('n_block_components', ctypes.c_uint64)]
+                ('n_block_components', ctypes.c_uint64), ('n_relabelled_tiles', ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}

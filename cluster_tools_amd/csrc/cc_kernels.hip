@@ -151,14 +151,19 @@ __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T) {
         const int sys = dy < 0 ? 0 : dy > 0 ? 1 : 2, syn = dy < 0 ? 1 : dy > 0 ? 0 : 2;
         const u64 ua = pick_rows(a, szs, sys), ub = pick_rows(b, szn, syn);
         const u32 ua0 = lo32(ua), ua1 = hi32(ua), ub0 = lo32(ub), ub1 = hi32(ub);
-        const u32 ea_prev = T.E[row] << 1, eb_prev = T.E[rowb] << 1;     // bit cx: cube cx-1 linked to cx
+        const u32 Ea = T.E[row], Eb = T.E[rowb];                  // bit cx: cube cx linked to cx + 1
         const u32 BA = T.B[row], BB = T.B[rowb], ra0 = T.roff[row], rb0 = T.roff[rowb];
+        const u32 C0 = (ua0 | ua1) & (ub0 | ub1);                 // contacts (cx, cx)
 #pragma unroll
         for (int dx = -1; dx <= 1; ++dx) {
             // own cube cx with neighbour cube cx + dx: own voxels facing -dx, neighbour voxels facing dx
-            const u32 C = dx < 0 ? ua0 & (ub1 << 1) : dx > 0 ? ua1 & (ub0 >> 1) : (ua0 | ua1) & (ub0 | ub1);
-            const u32 ebs = dx < 0 ? eb_prev << 1 : dx > 0 ? eb_prev >> 1 : eb_prev;
-            const u32 red = (C << 1) & ea_prev & ebs;
+            const u32 C = dx < 0 ? ua0 & (ub1 << 1) : dx > 0 ? ua1 & (ub0 >> 1) : C0;
+            // implied unions: the same contact one cube to the left with both pairs of cubes linked,
+            // and (dx != 0) a (cx, cx) contact next to it with the cubes in between linked
+            const u32 ebs = dx < 0 ? Eb << 2 : dx > 0 ? Eb : Eb << 1;
+            u32 red = (C << 1) & (Ea << 1) & ebs;
+            if (dx > 0) red |= ((C0 >> 1) & Ea) | (C0 & Eb);
+            if (dx < 0) red |= ((C0 & Ea) << 1) | (C0 & (Eb << 1));
             for (u32 m = C & ~red; m; m &= m - 1) {
                 const int cx = __builtin_ctz(m);
                 const u32 ra = ra0 + (u32)__popc(BA & mask_le(cx)) - 1;
@@ -665,20 +670,20 @@ __device__ __forceinline__ TileInfo uniform_ti(TileInfo ti) {
 //
 // The foreground of a block is an interval of the float order fixed by the block's min / max
 // (k_block_params), which are only known once the whole block has been read.  k_sample guesses
-// each block's interval from a sparse sample (1/128 of the block); k_spec then reads every tile
+// each block's interval from a sparse sample (1/512 of the block, k_sample + k_guess); k_spec then reads every tile
 // once, accumulating the exact block statistics AND labelling the tile (pass 1) with the guessed
 // interval [lg, hg], and records per tile the nearest values on both sides of each guessed bound:
 //   TB = { max ord < lg, min ord >= lg, max ord <= hg, min ord > hg }  (masked-out voxels excluded).
 // With the exact interval [lt, ht] (k_block_params) a tile's bits are the exact bits iff no voxel
 // lies between lg and lt nor between hg and ht -- decided from TB alone (spec_valid).  k_verify
-// k_fix relabels the tiles that fail from the input with the exact interval.
+// k_verify lists the tiles that fail and k_fix relabels them from the input with the exact interval.
 // A one-sided interval is kept open to the end of the order (widen): it then differs from the
 // exact one only in its finite bound.  The guess is made only where the sample looks quantized
 // (its extremes occur more than once): on continuous data a sampled bound is almost never exact,
 // so those blocks skip the speculation (k_spec reads them for statistics only, k_fix labels them).
 // Results never depend on the guess; only the amount of k_fix work does.
 // ------------------------------------------------------------------------------------------
-constexpr int SAMPLE_DZ = 8, SAMPLE_DY = 16;      // one voxel row per 8 planes x 16 rows of a block
+constexpr int SAMPLE_DZ = 16, SAMPLE_DY = 32;     // one voxel row per 16 planes x 32 rows of a block
 
 __device__ __forceinline__ void block_extent(const Geom& g, int64_t b, int e0[3], int el[3]) {
     const int bi[3] = {(int)(b / ((int64_t)g.nb[2] * g.nb[1])), (int)((b / g.nb[2]) % g.nb[1]), (int)(b % g.nb[2])};
@@ -713,37 +718,61 @@ __device__ __forceinline__ u32 block_reduce(u32 v, u32* red, Op op) {
     return v;
 }
 
-__global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __restrict__ in, float thr, int mode,
-                                                     BlockParam* guess) {
+// k_sample: workgroup (b, part) reads every SAMPLE_PARTS-th sample row of block b and writes its
+// (min, count of min, max, count of max); k_guess combines the parts of each block.
+constexpr int SAMPLE_PARTS = 8;
+
+__global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __restrict__ in, u32* part) {
     __shared__ u32 red[NTHREADS / 64];
-    const int64_t b = blockIdx.x;
+    const int64_t b = blockIdx.x / SAMPLE_PARTS;
+    const int pt = blockIdx.x % SAMPLE_PARTS;
     const int tid = cc_tid();
     int e0[3], el[3];
     block_extent(g, b, e0, el);
     const int nzs = max(1, el[0] / SAMPLE_DZ), nys = max(1, el[1] / SAMPLE_DY);
     const int zo = min(SAMPLE_DZ / 2, (el[0] - 1) / 2), yo = min(SAMPLE_DY / 2, (el[1] - 1) / 2);
     auto sweep = [&](auto&& f) {
-        for (int r = 0; r < nzs * nys; ++r) {
+        for (int r = pt; r < nzs * nys; r += SAMPLE_PARTS) {
             const int z = e0[0] + (r / nys) * SAMPLE_DZ + zo, y = e0[1] + (r % nys) * SAMPLE_DY + yo;
             const float* row = in + ((int64_t)z * g.Y + y) * g.X + e0[2];
 #pragma unroll 4
             for (int x = tid; x < el[2]; x += NTHREADS) f(f2ord(__float_as_uint(row[x])));
         }
     };
-    u32 mn = 0xFFFFFFFFu, mx = 0u;
-    sweep([&](u32 o) { mn = min(mn, o); mx = max(mx, o); });
-    mn = block_reduce(mn, red, [](u32 a, u32 c) { return min(a, c); });
-    mx = block_reduce(mx, red, [](u32 a, u32 c) { return max(a, c); });
-    u32 nmn = 0, nmx = 0;
-    sweep([&](u32 o) { nmn += (o == mn); nmx += (o == mx); });
-    nmn = block_reduce(nmn, red, [](u32 a, u32 c) { return a + c; });
-    nmx = block_reduce(nmx, red, [](u32 a, u32 c) { return a + c; });
+    // running (min, count of min) and (max, count of max) in one sweep
+    u32 mn = 0xFFFFFFFFu, mx = 0u, nmn = 0, nmx = 0;
+    sweep([&](u32 o) {
+        nmn = o < mn ? 1u : nmn + (o == mn);
+        nmx = o > mx ? 1u : nmx + (o == mx);
+        mn = min(mn, o);
+        mx = max(mx, o);
+    });
+    const u32 bmn = block_reduce(mn, red, [](u32 a, u32 c) { return min(a, c); });
+    const u32 bmx = block_reduce(mx, red, [](u32 a, u32 c) { return max(a, c); });
+    nmn = block_reduce(mn == bmn ? nmn : 0u, red, [](u32 a, u32 c) { return a + c; });
+    nmx = block_reduce(mx == bmx ? nmx : 0u, red, [](u32 a, u32 c) { return a + c; });
+    mn = bmn;
+    mx = bmx;
     if (tid == 0) {
-        const bool nan = mx > 0xFF800000u || mn < 0x007FFFFFu;
-        BlockParam p = block_param(mn, mx, nan ? 1u : 0u, thr, mode);
-        if (nmn < 2 || nmx < 2) p.kind = BP_EMPTY;     // continuous values: no guess
-        guess[b] = widen(p, mode);
+        u32* q = part + 4 * blockIdx.x;
+        q[0] = mn; q[1] = nmn; q[2] = mx; q[3] = nmx;
     }
+}
+
+__global__ void k_guess(int64_t nb, const u32* part, float thr, int mode, BlockParam* guess) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const u32* q = part + 4 * SAMPLE_PARTS * b;
+    u32 mn = 0xFFFFFFFFu, mx = 0u, nmn = 0, nmx = 0;
+    for (int p = 0; p < SAMPLE_PARTS; ++p) { mn = min(mn, q[4 * p]); mx = max(mx, q[4 * p + 2]); }
+    for (int p = 0; p < SAMPLE_PARTS; ++p) {
+        if (q[4 * p + 1] && q[4 * p] == mn) nmn += q[4 * p + 1];
+        if (q[4 * p + 3] && q[4 * p + 2] == mx) nmx += q[4 * p + 3];
+    }
+    const bool nan = mx > 0xFF800000u || mn < 0x007FFFFFu;
+    BlockParam p = block_param(mn, mx, nan ? 1u : 0u, thr, mode);
+    if (nmn < 2 || nmx < 2) p.kind = BP_EMPTY;     // continuous values: no guess
+    guess[b] = widen(p, mode);
 }
 
 struct SpecArgs {
@@ -822,18 +851,25 @@ __device__ __forceinline__ bool spec_valid(const BlockParam& G, BlockParam T, co
     return true;
 }
 
-// pass 1 with the exact parameters for every tile whose guessed bits were not exact; one
-// workgroup per tile (the others return at once: a persistent loop over a tile list hoisted the
-// tile set-up out of the loop and spilled)
+// FIX[0] = number of tiles to relabel, FIX[1..] = their ids
+__global__ void k_verify(Geom g, const BlockParam* guess, const BlockParam* bp, const u32* TB, int mode, u32* FIX) {
+    CC_FOR(t, g.n_tiles) {
+        const int64_t b = tile_info(g, t).block;
+        if (!spec_valid(guess[b], bp[b], TB + 4 * t, mode)) FIX[1 + atomicAdd(FIX, 1u)] = (u32)t;
+    }
+}
+
+// pass 1 with the exact parameters for the listed tiles, one workgroup per tile (the host reads
+// the count first: a fixed grid walking the list hoisted the tile set-up out of the loop and
+// spilled; a grid over all tiles paid ~2 us of dependent loads per returning workgroup)
 template <bool HAS_MASK>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_fix(
-    Geom g, const BlockParam* guess, const BlockParam* bp, const u32* TB, const float* __restrict__ in,
-    const u8* __restrict__ mask, float thr, int mode, u64* BITS, u32* FACES, u32* COUNT, u32* P, u64* KEY) {
+    Geom g, const u32* FIX, const BlockParam* bp, const float* __restrict__ in, const u8* __restrict__ mask,
+    float thr, int mode, u64* BITS, u32* FACES, u32* COUNT, u32* P, u64* KEY) {
     __shared__ Pass1LDS L;
-    const int64_t t = blockIdx.x;
-    const TileInfo ti = tile_info(g, t);
+    const int64_t t = __builtin_amdgcn_readfirstlane(FIX[1 + blockIdx.x]);
+    const TileInfo ti = uniform_ti(tile_info(g, t));
     const BlockParam p = uniform_bp(bp[ti.block]);
-    if (__builtin_amdgcn_readfirstlane((int)spec_valid(guess[ti.block], p, TB + 4 * t, mode))) return;
     pass1_tile<HAS_MASK>(g, t, ti, p, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L);
 }
 
@@ -2127,10 +2163,10 @@ template __global__ void k_front<0>(Geom, FrontArgs, const float*, float, int, u
     template __global__ void k_spec<M, S>(Geom, SpecArgs, const float*, const u8*, u64*, u32*, u32*, u32*, u64*);
 CC_SPEC(false, 1) CC_SPEC(false, 2) CC_SPEC(false, 3) CC_SPEC(true, 1) CC_SPEC(true, 2) CC_SPEC(true, 3)
 #undef CC_SPEC
-template __global__ void k_fix<false>(Geom, const BlockParam*, const BlockParam*, const u32*, const float*, const u8*,
-                                      float, int, u64*, u32*, u32*, u32*, u64*);
-template __global__ void k_fix<true>(Geom, const BlockParam*, const BlockParam*, const u32*, const float*, const u8*,
-                                     float, int, u64*, u32*, u32*, u32*, u64*);
+template __global__ void k_fix<false>(Geom, const u32*, const BlockParam*, const float*, const u8*, float, int, u64*,
+                                      u32*, u32*, u32*, u64*);
+template __global__ void k_fix<true>(Geom, const u32*, const BlockParam*, const float*, const u8*, float, int, u64*,
+                                     u32*, u32*, u32*, u64*);
 template __global__ void k_seams<0>(Geom, const u32*, u64*, u32*, u8*, u64*, u32*, u8*);
 template __global__ void k_stitch<false>(Geom, const u32*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_stitch<true>(Geom, const u32*, u32*, const u64*, const u8*, const u8*);

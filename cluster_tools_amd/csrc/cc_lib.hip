@@ -153,6 +153,7 @@ struct RunState {
     uint64_t base = 0;         // global id base of this slab
     int64_t n_map = 0;         // seam mapping size
     bool local_only = false;
+    uint64_t n_fix = 0;        // tiles relabelled by k_fix
     int stage = 0;             // 1 local done, 2 rid done, 3 final done
 };
 
@@ -212,9 +213,13 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         // speculative front: sample -> one read for statistics + pass 1 -> exact parameters ->
         // relabel the tiles whose guessed interval was not exact (see k_spec)
         BlockParam* guess = bp + nb;
-        c->spec.ensure(4 * nt * sizeof(u32));
+        c->spec.ensure((4 * nt + 4 * SAMPLE_PARTS * nb + nt + 1) * sizeof(u32));
         u32* TB = c->spec.as<u32>();
-        launch(c, "k_sample", [&] { k_sample<<<(unsigned)nb, NTHREADS, 0, s>>>(g, in, thr, mode, guess); });
+        u32* SPART = TB + 4 * nt;
+        u32* FIX = SPART + 4 * SAMPLE_PARTS * nb;
+        HIP_OK(hipMemsetAsync(FIX, 0, sizeof(u32), s));
+        launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART); });
+        launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, mode, guess); });
         if (const char* e = std::getenv("CC_SPEC"); e && std::string(e) == "0")     // test hook: no guesses
             HIP_OK(hipMemsetAsync(guess, 0, nb * sizeof(BlockParam), s));
         SpecArgs sa;
@@ -237,10 +242,16 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         launch(c, "k_block_params", [&] {
             k_block_params<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, smin, smax, sflag, thr, mode, bp);
         });
-        launch(c, "k_fix", [&] {
-            if (mask) k_fix<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, guess, bp, TB, in, mask, thr, mode, BITS, FACES, COUNT, P, KR);
-            else k_fix<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, guess, bp, TB, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR);
-        });
+        launch(c, "k_verify", [&] { k_verify<<<grid_stride(nt), 256, 0, s>>>(g, guess, bp, TB, mode, FIX); });
+        u32 nfix = 0;
+        HIP_OK(hipMemcpyAsync(&nfix, FIX, sizeof(u32), hipMemcpyDeviceToHost, s));
+        HIP_OK(hipStreamSynchronize(s));
+        st.n_fix = nfix;
+        if (nfix)
+            launch(c, "k_fix", [&] {
+                if (mask) k_fix<true><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, in, mask, thr, mode, BITS, FACES, COUNT, P, KR);
+                else k_fix<false><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR);
+            });
     } else {
         int64_t lag = 1;
         if (const char* e = std::getenv("CC_FRONT_LAG")) lag = std::max<int64_t>(1, std::atoll(e));
@@ -522,6 +533,7 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
         res->max_id = res->n_labels - 1;       // lut[n_labels-1] = n_labels-1 is never merged
         res->n_components = st.local_only ? 0 : sc[1];
         res->n_block_components = (uint64_t)nr;
+        res->n_relabelled_tiles = st.n_fix;
     }
 }
 

@@ -44,6 +44,8 @@ typedef struct {
     uint64_t max_id;        /* write.py:281-289 (attrs['maxId'])               */
     uint64_t n_components;  /* number of distinct non-zero output labels      */
     uint64_t n_block_components; /* sum over blocks of n_i (block-local comps) */
+    uint64_t n_relabelled_tiles; /* tiles whose speculated foreground interval was not exact and
+                                    were labelled again (instrumentation; results never depend on it) */
 } cc_result;
 
 /* --- context ----------------------------------------------------------- */

@@ -119,10 +119,14 @@ def test_speculated_interval_corrected(ctx, mode, thr, outlier):
     bounds must be relabelled (large outliers), the others kept (small outliers)."""
     rng = np.random.default_rng(3)
     inp = (rng.integers(0, 17, (64, 128, 192)) / np.float32(16)).astype(np.float32)
-    inp[1, 1, 5] = outlier               # block (0, 0, 0); sample rows are z = 4 mod 8, y = 8 mod 16
+    inp[1, 1, 5] = outlier               # block (0, 0, 0); sample rows are z = 8 mod 16, y = 16 mod 32
     inp[33, 70, 100] = outlier           # block (1, 1, 1)
     for bs in [(32, 64, 96), (64, 128, 192)]:
-        _check_against_oracle(ctx, inp, bs, thr, mode)
+        _, res, _ = _check_against_oracle(ctx, inp, bs, thr, mode)
+        if mode != 'equal' and outlier in (-1.0, 3.0):
+            assert res['n_relabelled_tiles'] > 0        # the guess moved past quantization levels
+        if (mode, thr, outlier) == ('greater', 0.3, -1.0 / 32):
+            assert res['n_relabelled_tiles'] == 0       # guess != exact, but no voxel in between
     mask = (rng.random(inp.shape) < 0.9).astype(np.uint8)
     _check_against_oracle(ctx, inp, (32, 64, 96), thr, mode, mask)
 

@@ -56,7 +56,10 @@ int main(int argc, char** argv) {
         k_block_stats<<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, smin, smax, sflag);
         k_block_params<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, smin, smax, sflag, thr, mode, bp);
         k_pass1<false, 0><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, nullptr, bp, thr, mode, BITS[0], FACES, COUNT[0], P, KEY);
-        k_sample<<<(unsigned)nb, NTHREADS, 0, s>>>(g, in, thr, mode, guess);
+        u32* part;
+        HIP_OK(hipMalloc(&part, nb * SAMPLE_PARTS * 16));
+        k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, part);
+        k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, part, thr, mode, guess);
         HIP_OK(hipDeviceSynchronize());
         std::vector<BlockParam> hb(nb), hgs(nb);
         HIP_OK(hipMemcpy(hb.data(), bp, nb * sizeof(BlockParam), hipMemcpyDeviceToHost));
