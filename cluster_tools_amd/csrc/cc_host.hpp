@@ -102,58 +102,5 @@ static void bind_geom_tables(HostGeom& hg, int32_t* base) {
     }
 }
 
-// tiles of block b (from the block tables of hg.tab)
-static int64_t block_ntiles_host(const HostGeom& hg, int64_t b) {
-    const Geom& g = hg.g;
-    const int64_t bi[3] = {b / ((int64_t)g.nb[2] * g.nb[1]), (b / g.nb[2]) % g.nb[1], b % g.nb[2]};
-    int64_t off = 3 * ((int64_t)g.nt[0] + g.nt[1] + g.nt[2]), n = 1;
-    for (int a = 0; a < 3; ++a) {
-        n *= hg.tab[off + g.nb[a] + bi[a]];        // btn[a][bi]
-        off += 2 * g.nb[a];
-    }
-    return n;
-}
-
-// k_front segment table (cc_kernels.hip): S(0..lag-1), then S(k), P(k-lag) for k = lag..nb-1,
-// then P(nb-lag..nb-1).  h = [2 nb + 1 int64 segment starts (in items)][2 nb u32 block |
-// pass1 << 31]; a stats item covers per_s tiles of its block, a pass-1 item per_p.  Returns the
-// number of segments; h[2 nb] is the number of items.
-static int64_t build_front_segments(const HostGeom& hg, int64_t lag, std::vector<int64_t>& h, int per_s = 1,
-                                    int per_p = 1) {
-    const int64_t nb = hg.g.n_blocks;
-    lag = std::max<int64_t>(1, std::min<int64_t>(lag, nb));
-    const int64_t nseg = 2 * nb;
-    h.assign(nseg + 1 + (nseg + 1) / 2, 0);
-    uint32_t* hb = (uint32_t*)(h.data() + nseg + 1);
-    int64_t pos = 0, j = 0;
-    auto add = [&](int64_t b, bool pass1) {
-        h[j] = pos;
-        hb[j] = (uint32_t)b | (pass1 ? 0x80000000u : 0u);
-        const int64_t per = pass1 ? per_p : per_s;
-        pos += (block_ntiles_host(hg, b) + per - 1) / per;
-        ++j;
-    };
-    for (int64_t k = 0; k < nb; ++k) {
-        add(k, false);
-        if (k >= lag) add(k - lag, true);
-    }
-    for (int64_t b = nb - lag; b < nb; ++b) add(b, true);
-    h[nseg] = pos;
-    CC_REQUIRE(j == nseg && nb < (1LL << 31), "k_front segment table");
-    return nseg;
-}
-
-// k_front2 item table (cc_kernels.hip): prologue stats tiles of blocks 0 .. lag-1, then one
-// pair item per tile of every block, in block order.  item = block | pair << 31 | lt << 32.
-static void build_front2_items(const HostGeom& hg, int64_t lag, std::vector<uint64_t>& items) {
-    const int64_t nb = hg.g.n_blocks;
-    items.clear();
-    for (int64_t b = 0; b < std::min<int64_t>(lag, nb); ++b)
-        for (int64_t l = 0; l < block_ntiles_host(hg, b); ++l) items.push_back((uint64_t)b | ((uint64_t)l << 32));
-    for (int64_t b = 0; b < nb; ++b)
-        for (int64_t l = 0; l < block_ntiles_host(hg, b); ++l)
-            items.push_back((uint64_t)b | 0x80000000ull | ((uint64_t)l << 32));
-    CC_REQUIRE(nb < (1LL << 31), "k_front2 item table");
-}
 
 }  // namespace cc

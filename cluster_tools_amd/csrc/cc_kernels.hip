@@ -515,7 +515,6 @@ __device__ __forceinline__ void pass1_tile(const Geom& g, int64_t t, const TileI
                                            int mode, u64* BITS, u32* FACES, u32* COUNT, u32* P, u64* KEY,
                                            Pass1LDS& L, bool write = true) {
     const int tid = cc_tid();
-    // (unconditional zeroing: every caller passes the same barriers, also the halves of k_front)
     for (int i = tid; i < NROWS; i += NTHREADS) L.rows[i] = 0;
     __syncthreads();
     if (p.kind != BP_EMPTY) load_rows<HAS_MASK>(g, ti, in, mask, p, thr, mode, L.rows);
@@ -579,7 +578,7 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
 }
 
 // k_pass1: one workgroup per tile, block parameters precomputed (ablation harness; the library
-// runs pass 1 inside k_front)
+// runs pass 1 inside k_spec / k_fix)
 template <bool HAS_MASK, int ABL = 0>
 __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restrict__ in,
                                                     const u8* __restrict__ mask, const BlockParam* bp,
@@ -591,65 +590,12 @@ __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restr
     pass1_tile<HAS_MASK, ABL>(g, t, ti, uniform_bp(bp[ti.block]), in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L);
 }
 
-// ------------------------------------------------------------------------------------------
-// k_front: block statistics, block parameters and pass 1 in ONE launch, ordered so that pass 1
-// re-reads a block's input from the 256 MiB Infinity Cache instead of HBM.
-//
-// Work items are taken in order from an atomic ticket: segments
-//   S(0) .. S(lag-1), then S(k), P(k - lag) for k = lag .. nb-1, then P(nb-lag) .. P(nb-1)
-// where S(b) = the stats items of block b and P(b) = its pass-1 items.  A workgroup of H tile
-// teams (512 threads each) takes one item: a stats item covers per_s consecutive tiles of the
-// block (per_s / H per team), a pass-1 item H tiles (one per team).  The ticket is one device
-// atomic on one word (~88 per us chip-wide).  The library runs H = 1, one tile per item.
-// ITEMS[i] = block | is-pass-1 << 31 | (first local tile | tile count << 16) << 32, built by
-// k_front_items from the host's segment table.  The last stats item of a block computes the
-// block's parameters and publishes them; a pass-1 item waits for its block.  The hand-off uses
-// relaxed device-scope atomics only (performed at the coherence point; the writer waits for
-// each step to return before the next): an agent-scope release / acquire would write back /
-// invalidate the XCD's L2 on every item.  Every item a pass-1 item can wait on was taken before
-// it, by a workgroup that is running and waits on nothing, so the waits always end (they are
-// also bounded by a clock limit that raises an error flag instead of hanging).  One item per
-// workgroup (a persistent loop raised register pressure past the LDS-bound occupancy).
-// ------------------------------------------------------------------------------------------
-struct FrontArgs {
-    const u64* items;         // work items (see above)
-    int64_t n_items;
-    int32_t per_s, per_p;     // tiles per stats / pass-1 item
-    u32* smin; u32* smax; u32* sflag;
-    u32* sdone;               // stats items done per block
-    u32* ready;               // block parameters published
-    BlockParam* bp;
-    u32* queue;               // [0] ticket counter, [1] error flag (wait timeout)
-};
-
 // global tile id of local tile lt (z-major inside the block) of block b
 __device__ __forceinline__ int64_t block_tile(const Geom& g, int64_t b, int lt) {
     const int bx = (int)(b % g.nb[2]), by = (int)((b / g.nb[2]) % g.nb[1]), bz = (int)(b / ((int64_t)g.nb[2] * g.nb[1]));
     const int nx = g.btn[2][bx], ny = g.btn[1][by];
     const int lx = lt % nx, ly = (lt / nx) % ny, lz = lt / (nx * ny);
     return ((int64_t)(g.bt0[0][bz] + lz) * g.nt[1] + (g.bt0[1][by] + ly)) * g.nt[2] + (g.bt0[2][bx] + lx);
-}
-
-__device__ __forceinline__ int block_ntiles(const Geom& g, int64_t b) {
-    const int bx = (int)(b % g.nb[2]), by = (int)((b / g.nb[2]) % g.nb[1]), bz = (int)(b / ((int64_t)g.nb[2] * g.nb[1]));
-    return g.btn[0][bz] * g.btn[1][by] * g.btn[2][bx];
-}
-
-// ITEMS from the segment table SEG (nseg + 1 item starts, then nseg u32 block | is-pass-1 << 31)
-__global__ void k_front_items(Geom g, const int64_t* seg, int32_t nseg, int per_s, int per_p, u64* items) {
-    const u32* segb = (const u32*)(seg + nseg + 1);
-    CC_FOR(i, seg[nseg]) {
-        int lo = 0, hi = nseg - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (seg[mid] <= i) lo = mid; else hi = mid - 1;
-        }
-        const u32 sb = segb[lo];
-        const int per = (sb >> 31) ? per_p : per_s;
-        const int lt0 = (int)(i - seg[lo]) * per;
-        const int n = min(per, block_ntiles(g, sb & 0x7FFFFFFFu) - lt0);
-        items[i] = (u64)sb | ((u64)((u32)lt0 | ((u32)n << 16)) << 32);
-    }
 }
 
 // tile tables read after stores come back in VGPRs (vector loads); the values are
@@ -871,138 +817,6 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     const TileInfo ti = uniform_ti(tile_info(g, t));
     const BlockParam p = uniform_bp(bp[ti.block]);
     pass1_tile<HAS_MASK>(g, t, ti, p, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L);
-}
-
-// TV (ablation harness only; 0 in the library): 2 = no wait, 3 = 2 + skip pass-1 items,
-// 4 = 2 + skip stats items, 6 = ticket only
-template <bool HAS_MASK, int H, int TV>
-__device__ __forceinline__ void front_item(const Geom& g, const FrontArgs& fa, const float* __restrict__ in,
-                                           const u8* __restrict__ mask, float thr, int mode, u64* BITS,
-                                           u32* FACES, u32* COUNT, u32* P, u64* KEY) {
-    __shared__ Pass1LDS L[H];
-    __shared__ u32 red[2][H * NTHREADS / 64];
-    __shared__ u64 s_entry;
-    __shared__ BlockParam s_bp;
-    const int ftid = threadIdx.x;
-    const int half = H == 1 ? 0 : __builtin_amdgcn_readfirstlane(ftid / NTHREADS);
-    const int tid = cc_tid();                       // thread index inside the half
-    // one item per workgroup, in ticket order (dispatch order is undefined, the ticket is not)
-    if (ftid == 0) {
-        const u32 k = atomicAdd(&fa.queue[0], 1u);
-        s_entry = k < fa.n_items ? fa.items[k] : 0ull;
-    }
-    __syncthreads();
-    if (TV == 6) return;
-    const u32 e0 = __builtin_amdgcn_readfirstlane((u32)s_entry), e1 = __builtin_amdgcn_readfirstlane((u32)(s_entry >> 32));
-    const int64_t b = e0 & 0x7FFFFFFFu;
-    const bool is_p1 = e0 >> 31;
-    const int lt0 = e1 & 0xFFFFu, n = e1 >> 16;
-    if (TV == 3 && is_p1) return;
-    if (TV == 4 && !is_p1) return;
-    if (!is_p1) {
-        // ordered min / max over this half's tiles (no barrier inside the loop)
-        u32 mn = 0xFFFFFFFFu, mx = 0u;
-        const int per_half = fa.per_s / H;
-        for (int j = 0; j < per_half; ++j) {
-            const int lt = lt0 + half * per_half + j;
-            if (lt >= lt0 + n) break;
-            const TileInfo ti = uniform_ti(tile_info(g, block_tile(g, b, lt)));
-            for_tile_rows<false>(g, ti, in, nullptr, [&](int, float x, u32) {
-                const u32 o = f2ord(__float_as_uint(x));
-                mn = o < mn ? o : mn;
-                mx = o > mx ? o : mx;
-            });
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const u32 a = __shfl_xor(mn, o, 64), c = __shfl_xor(mx, o, 64);
-            mn = a < mn ? a : mn;
-            mx = c > mx ? c : mx;
-        }
-        if ((ftid & 63) == 0) { red[0][ftid >> 6] = mn; red[1][ftid >> 6] = mx; }
-        __syncthreads();
-        if (ftid == 0) {
-            u32 a = red[0][0], c = red[1][0];
-            for (int w = 1; w < H * NTHREADS / 64; ++w) {
-                a = red[0][w] < a ? red[0][w] : a;
-                c = red[1][w] > c ? red[1][w] : c;
-            }
-            // NaN orders above +inf or below -inf (volume_utils.py:98-105: a NaN block has no foreground)
-            const bool nan = c > 0xFF800000u || a < 0x007FFFFFu;
-            atomicMin(&fa.smin[b], a);
-            atomicMax(&fa.smax[b], c);
-            if (nan) atomicOr(&fa.sflag[b], 1u);
-            // the block's min / max / flag atomics are performed at the coherence point (returned)
-            // before this item counts itself done
-            __builtin_amdgcn_s_waitcnt(0);
-            const u32 n_s = (u32)((block_ntiles(g, b) + fa.per_s - 1) / fa.per_s);
-            const u32 done = atomicAdd(&fa.sdone[b], 1u);
-            if (done + 1 == n_s) {                         // last stats item of the block
-                const u32 vmin = atomicMin(&fa.smin[b], 0xFFFFFFFFu);      // atomic reads
-                const u32 vmax = atomicMax(&fa.smax[b], 0u);
-                const u32 vfl = atomicOr(&fa.sflag[b], 0u);
-                const BlockParam bp = block_param(vmin, vmax, vfl, thr, mode);
-                u32* w = (u32*)&fa.bp[b];
-                atomicExch(w + 0, __float_as_uint(bp.mn));
-                atomicExch(w + 1, __float_as_uint(bp.m));
-                atomicExch(w + 2, bp.lo);
-                atomicExch(w + 3, bp.hi);
-                atomicExch(w + 4, bp.kind);
-                __builtin_amdgcn_s_waitcnt(0);
-                atomicExch(&fa.ready[b], 1u);
-            }
-        }
-    } else {
-        if (ftid == 0) {
-            if (TV < 2) {
-                const int64_t t0 = wall_clock64();
-                while (atomicOr(&fa.ready[b], 0u) == 0u) {
-                    __builtin_amdgcn_s_sleep(4);
-                    if (wall_clock64() - t0 > (int64_t)100000000) {      // ~1 s at 100 MHz: never expected
-                        atomicOr(&fa.queue[1], 1u);
-                        break;
-                    }
-                }
-            }
-            u32* w = (u32*)&fa.bp[b];
-            const u32 w0 = atomicOr(w + 0, 0u), w1 = atomicOr(w + 1, 0u), w2 = atomicOr(w + 2, 0u),
-                      w3 = atomicOr(w + 3, 0u), w4 = atomicOr(w + 4, 0u);
-            s_bp.mn = __uint_as_float(w0); s_bp.m = __uint_as_float(w1);
-            s_bp.lo = w2; s_bp.hi = w3; s_bp.kind = w4;
-        }
-        __syncthreads();
-        BlockParam p;
-        p.mn = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(s_bp.mn)));
-        p.m = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(s_bp.m)));
-        p.lo = __builtin_amdgcn_readfirstlane(s_bp.lo);
-        p.hi = __builtin_amdgcn_readfirstlane(s_bp.hi);
-        p.kind = __builtin_amdgcn_readfirstlane(s_bp.kind);
-        p.pad = 0;
-        // half h labels tile lt0 + h; a half without a tile runs tile lt0 again without writing
-        // anything, so that both halves pass the same barriers
-        const bool own = half < n;
-        const int64_t t = block_tile(g, b, lt0 + (own ? half : 0));
-        const TileInfo ti = uniform_ti(tile_info(g, t));
-        pass1_tile<HAS_MASK>(g, t, ti, p, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L[half], own);
-    }
-}
-
-// 512-thread workgroups, one tile per item (measured: 1024-thread workgroups with two tiles per
-// pass-1 item, multi-tile stats items and a "paired" stats(b + lag) + pass-1(b) item order were
-// all slower -- pass-1 items waited on the longer stats items, or the two tiles of a workgroup
-// waited on each other at every barrier)
-template <int TV = 0>
-__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_front(
-    Geom g, FrontArgs fa, const float* __restrict__ in, float thr, int mode, u64* BITS, u32* FACES, u32* COUNT,
-    u32* P, u64* KEY) {
-    front_item<false, 1, TV>(g, fa, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KEY);
-}
-
-// with a mask: 512-thread workgroups (the mask loads would spill at 64 VGPRs)
-__global__ __launch_bounds__(NTHREADS) void k_front_mask(Geom g, FrontArgs fa, const float* __restrict__ in,
-                                                         const u8* __restrict__ mask, float thr, int mode, u64* BITS,
-                                                         u32* FACES, u32* COUNT, u32* P, u64* KEY) {
-    front_item<true, 1, 0>(g, fa, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1268,7 +1082,7 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
 
 // ------------------------------------------------------------------------------------------
 // Intra-block seams without global atomics, in two launches:
-//   k_stitch_pairs  one workgroup per tile: connected (own component, neighbour component) pairs
+//   k_seams         one wave per tile: connected (own component, neighbour component) pairs
 //                   across its lower intra-block seams, deduplicated in LDS, appended to the
 //                   tile's slot list as block-local ids (local tile << 12 | k);
 //   k_block_uf      one workgroup per block: union-find over the block's components in LDS fed
@@ -1303,47 +1117,7 @@ __device__ __forceinline__ bool wave_first(u64 key) {
     return true;
 }
 
-// One wave per tile: stage the seam faces in LDS, emit (own, neighbour) component pairs as
-// block-local ids with wave-aggregated slot allocation.  Duplicates that survive the per-cube
-// (Cand) and per-wave filters are harmless to k_block_uf.
-constexpr int SP_WAVES = 4;
-__global__ __launch_bounds__(SP_WAVES * 64) void k_stitch_pairs(Geom g, const u32* __restrict__ FACES, u64* PAIRS,
-                                                                u32* PC, u8* big) {
-    __shared__ u32 Sall[SP_WAVES][FACE_STRIDE];
-    __shared__ u32 cnt[SP_WAVES];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t t = (int64_t)blockIdx.x * SP_WAVES + w;
-    const bool valid = t < g.n_tiles;
-    u32* S = Sall[w];
-    TileInfo ti;
-    if (valid) {
-        ti = tile_info(g, t);
-        stage_faces(g, FACES, t, ti, S, lane, 64);
-    }
-    if (lane == 0) cnt[w] = 0;
-    __syncthreads();
-    if (!valid) return;
-    const u32 lt_own = block_local(g, (u32)t);
-    u64* out = PAIRS + t * TPC;
-    stitch_tile<false>(g, FACES, S, t, ti, lane, 64, [&](int64_t t1, u32 e1, int64_t t2, u32 e2) {
-        (void)t1;
-        const u32 k1 = e1 & 0xFFFu, k2 = e2 & 0xFFFu;
-        if (!wave_first(((u64)k1 << 52) | ((u64)(t - t2) << 12) | k2)) return;
-        const u64 m = __ballot(1);
-        u32 base = 0;
-        if (lane == (int)(__ffsll((unsigned long long)m) - 1)) base = atomicAdd(&cnt[w], (u32)__popcll(m));
-        base = __builtin_amdgcn_readfirstlane(base);
-        const u32 pos = base + (u32)__popcll(m & ((1ull << lane) - 1));
-        if (pos < TPC) out[pos] = ((u64)((lt_own << 12) | k1) << 32) | ((block_local(g, (u32)t2) << 12) | k2);
-    });
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane == 0) {
-        const u32 n = cnt[w];
-        PC[t] = n < TPC ? n : TPC;
-        if (n > TPC) big[ti.block] = 1;
-    }
-}
+constexpr int SP_WAVES = 4;            // waves (tiles) per workgroup of the seam kernels
 
 // ------------------------------------------------------------------------------------------
 // k_seams: the tile's three lower seams with voxel-row bit masks, one wave per tile.
@@ -1575,68 +1349,6 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const u32* S, con
             const u32 a = S[F_ZLO + cyo * CX + cxo], b = E[112 + c];
             if (((a >> 16) & fsel(jo, io)) && ((b >> 16) & fsel(ypar(s1), xpar(s2))))
                 emit(t - sz + s1 * sy + s2, a & 0xFFFFu, b & 0xFFFFu);
-        }
-    }
-}
-
-// Edge and corner seams inside the block (the lex-negative directions with two or three nonzero
-// components), from the staged planes S and edge entries E.  U(t, entry, tn, entry_n).
-template <class UF>
-__device__ __forceinline__ void seam_edges(const Geom& g, const u32* S, const u32* E, int64_t t, const TileInfo& ti,
-                                           int lane, UF& U) {
-    const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2, ncz = (ti.lz + 1) / 2;
-    const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
-    const bool zok = ti.iz > 0 && g.tblk[0][ti.iz] == g.tblk[0][ti.iz - 1];
-    auto yok = [&](int s) { const int j = ti.iy + s; return j >= 0 && j < g.nt[1] && g.tblk[1][j] == g.tblk[1][ti.iy]; };
-    auto xok = [&](int s) { const int j = ti.ix + s; return j >= 0 && j < g.nt[2] && g.tblk[2][j] == g.tblk[2][ti.ix]; };
-    if (zok) {
-        for (int s = -1; s <= 1; s += 2) {                        // edges (-1, s, 0)
-            if (!yok(s)) continue;
-            const int lyn = g.tlen[1][ti.iy + s];
-            const int cyo = s < 0 ? 0 : ncy - 1;
-            const int jo = s < 0 ? 0 : (ti.ly - 1) & 1, jn = s < 0 ? (lyn - 1) & 1 : 0;
-            const u32* FR = E + (s < 0 ? 0 : 32);
-            for (int cx = lane; cx < ncx; cx += 64) {
-                const u32 a = S[F_ZLO + cyo * CX + cx];
-                if (a) edge3<false>(FR, 1, a, cx, ncx, jo, jn, t, t - sz + s * sy, U);
-            }
-        }
-        for (int s = -1; s <= 1; s += 2) {                        // edges (-1, 0, s)
-            if (!xok(s)) continue;
-            const int lxn = g.tlen[2][ti.ix + s];
-            const int cxo = s < 0 ? 0 : ncx - 1;
-            const int io = s < 0 ? 0 : (ti.lx - 1) & 1, in_ = s < 0 ? (lxn - 1) & 1 : 0;
-            const u32* FR = E + (s < 0 ? 64 : 80);
-            for (int cy = lane; cy < ncy; cy += 64) {
-                const u32 a = S[F_ZLO + cy * CX + cxo];
-                if (a) edge3<true>(FR, 1, a, cy, ncy, io, in_, t, t - sz + s, U);
-            }
-        }
-        if (lane < 4) {                                            // corners (-1, s1, s2)
-            const int s1 = (lane & 2) ? 1 : -1, s2 = (lane & 1) ? 1 : -1;
-            if (yok(s1) && xok(s2)) {
-                const int lyn = g.tlen[1][ti.iy + s1], lxn = g.tlen[2][ti.ix + s2];
-                const int cyo = s1 < 0 ? 0 : ncy - 1, cxo = s2 < 0 ? 0 : ncx - 1;
-                const int jo = s1 < 0 ? 0 : (ti.ly - 1) & 1, jn = s1 < 0 ? (lyn - 1) & 1 : 0;
-                const int io = s2 < 0 ? 0 : (ti.lx - 1) & 1, in_ = s2 < 0 ? (lxn - 1) & 1 : 0;
-                const u32 a = S[F_ZLO + cyo * CX + cxo];
-                const u32 b = E[112 + lane];
-                if (a && b && ((a >> 16) & fsel(jo, io)) && ((b >> 16) & fsel(jn, in_)))
-                    U(t, a, t - sz + s1 * sy + s2, b);
-            }
-        }
-    }
-    if (ti.iy > 0 && yok(-1)) {
-        for (int s = -1; s <= 1; s += 2) {                        // edges (0, -1, s)
-            if (!xok(s)) continue;
-            const int lxn = g.tlen[2][ti.ix + s];
-            const int cxo = s < 0 ? 0 : ncx - 1;
-            const int io = s < 0 ? 0 : (ti.lx - 1) & 1, in_ = s < 0 ? (lxn - 1) & 1 : 0;
-            const u32* FR = E + (s < 0 ? 96 : 104);
-            for (int cz = lane; cz < ncz; cz += 64) {
-                const u32 a = S[F_YLO + cz * CX + cxo];
-                if (a) edge3<true>(FR, 1, a, cz, ncz, io, in_, t, t - sy + s, U);
-            }
         }
     }
 }
@@ -2158,7 +1870,6 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
 }
 
 // instantiate the templates used by the host side
-template __global__ void k_front<0>(Geom, FrontArgs, const float*, float, int, u64*, u32*, u32*, u32*, u64*);
 #define CC_SPEC(M, S) \
     template __global__ void k_spec<M, S>(Geom, SpecArgs, const float*, const u8*, u64*, u32*, u32*, u32*, u64*);
 CC_SPEC(false, 1) CC_SPEC(false, 2) CC_SPEC(false, 3) CC_SPEC(true, 1) CC_SPEC(true, 2) CC_SPEC(true, 3)

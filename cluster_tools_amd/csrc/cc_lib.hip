@@ -52,7 +52,7 @@ struct cc_ctx {
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     // workspace
-    DevBuf front, tiles, bstat, bparam, bits, faces, count, rc, roff, P, KR, FIN, keys, keys2, vals, vals2, seg,
+    DevBuf tiles, bstat, bparam, bits, faces, count, rc, roff, P, KR, FIN, keys, keys2, vals, vals2, seg,
         values, offsets, lut, cub_tmp, scalars, scalars2, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2,
         flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf, spec;
     // last run
@@ -60,7 +60,6 @@ struct cc_ctx {
     uint64_t n_labels = 0;
     std::vector<uint64_t> h_values, h_offsets;
     std::vector<int32_t> h_tab;
-    std::vector<int64_t> h_front;    // k_front segment table (kept alive until the stream consumed it)
     bool lut_valid = false;
     // profiling
     bool prof = false;
@@ -178,7 +177,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     const uint64_t nodes = (uint64_t)nt * g.cap;
     hipStream_t s = c->stream;
 
-    c->bstat.ensure(nb * 5 * sizeof(u32) + 2 * sizeof(u32));
+    c->bstat.ensure(nb * 3 * sizeof(u32));
     c->bparam.ensure(2 * nb * sizeof(BlockParam));     // exact parameters, then the guesses (k_sample)
     c->bits.ensure(nt * NROWS * sizeof(u64));
     c->faces.ensure(nt * FACE_STRIDE * sizeof(u32));
@@ -190,14 +189,12 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     c->offsets.ensure(nb * sizeof(u64));
     c->scalars.ensure(4 * sizeof(u64));
 
-    // block statistics, parameters and pass 1 in one launch (k_front): smin, smax, sflag, sdone,
-    // ready per block + the item ticket and an error flag
+    // block statistics (ordered min, max, NaN flag), accumulated by k_spec
     u32* smin = c->bstat.as<u32>();
     u32* smax = smin + nb;
     u32* sflag = smax + nb;
-    u32* queue = smin + 5 * nb;
     HIP_OK(hipMemsetAsync(smin, 0xFF, nb * sizeof(u32), s));
-    HIP_OK(hipMemsetAsync(smax, 0x00, (4 * nb + 2) * sizeof(u32), s));
+    HIP_OK(hipMemsetAsync(smax, 0x00, 2 * nb * sizeof(u32), s));
     HIP_OK(hipMemsetAsync(c->scalars.p, 0, 4 * sizeof(u64), s));
 
     BlockParam* bp = c->bparam.as<BlockParam>();
@@ -208,8 +205,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     u64* KR = c->KR.as<u64>();
     const float thr = st.thr;
 
-    const char* fe = std::getenv("CC_FRONT");
-    if (!(fe && std::string(fe) == "fused")) {
+    {
         // speculative front: sample -> one read for statistics + pass 1 -> exact parameters ->
         // relabel the tiles whose guessed interval was not exact (see k_spec)
         BlockParam* guess = bp + nb;
@@ -252,34 +248,6 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
                 if (mask) k_fix<true><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, in, mask, thr, mode, BITS, FACES, COUNT, P, KR);
                 else k_fix<false><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR);
             });
-    } else {
-        int64_t lag = 1;
-        if (const char* e = std::getenv("CC_FRONT_LAG")) lag = std::max<int64_t>(1, std::atoll(e));
-        const int per_s = 2, per_p = 1;                  // tiles per stats / pass-1 item (2: measured best)
-        std::vector<int64_t>& h = c->h_front;
-        const int64_t nseg = build_front_segments(st.hg, lag, h, per_s, per_p);
-        const int64_t n_items = h[nseg];
-        CC_REQUIRE(n_items < (1LL << 31), "too many items for one k_front launch");
-        c->front.ensure(h.size() * sizeof(int64_t) + n_items * sizeof(u64));
-        HIP_OK(hipMemcpyAsync(c->front.p, h.data(), h.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
-        u64* items = (u64*)(c->front.as<int64_t>() + h.size());
-        launch(c, "k_front_items", [&] {
-            k_front_items<<<grid_stride(n_items), 256, 0, s>>>(g, c->front.as<int64_t>(), (int32_t)nseg, per_s, per_p,
-                                                                items);
-        });
-        FrontArgs fa;
-        fa.items = items;
-        fa.n_items = n_items;
-        fa.per_s = per_s;
-        fa.per_p = per_p;
-        fa.smin = smin; fa.smax = smax; fa.sflag = sflag;
-        fa.sdone = smin + 3 * nb; fa.ready = smin + 4 * nb;
-        fa.bp = bp;
-        fa.queue = queue;
-        if (mask)
-            launch(c, "k_front", [&] { k_front_mask<<<(unsigned)n_items, NTHREADS, 0, s>>>(g, fa, in, mask, thr, mode, BITS, FACES, COUNT, P, KR); });
-        else
-            launch(c, "k_front", [&] { k_front<0><<<(unsigned)n_items, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KR); });
     }
     c->big.ensure(nb);
     c->pairsl.ensure((size_t)nt * TPC * sizeof(u64));
@@ -319,11 +287,9 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             HIP_OK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, RC, ROFF, (int)nt + 1, s));
         });
     }
-    u32 n_roots_h = 0, front_err = 0;
+    u32 n_roots_h = 0;
     HIP_OK(hipMemcpyAsync(&n_roots_h, ROFF + nt, sizeof(u32), hipMemcpyDeviceToHost, s));
-    HIP_OK(hipMemcpyAsync(&front_err, queue + 1, sizeof(u32), hipMemcpyDeviceToHost, s));
     sync(c);
-    CC_REQUIRE(front_err == 0, "k_front: a pass-1 item timed out waiting for its block statistics");
     const int64_t nr = n_roots_h;
     st.nr = nr;
     c->keys.ensure(std::max<int64_t>(1, nr) * sizeof(u64));
@@ -585,7 +551,7 @@ void cc_destroy(cc_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->front, &c->tiles, &c->bstat, &c->bparam, &c->bits, &c->faces, &c->count, &c->rc, &c->roff, &c->P, &c->KR,
+    DevBuf* bufs[] = {&c->tiles, &c->bstat, &c->bparam, &c->bits, &c->faces, &c->count, &c->rc, &c->roff, &c->P, &c->KR,
                       &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
                       &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,

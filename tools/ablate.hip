@@ -5,13 +5,15 @@
 //   copy_read / copy_write   plain float4 streaming read / 16-B uint64 store (the box's HBM ceiling)
 //   k_block_stats            per-block min/max pass
 //   k_pass1 ABL=1,2,3,0      stop after: load+threshold+bits | + tile CCL | + first voxels | full
-//   k_front lag 1..3         stats + params + pass 1 fused, Infinity-Cache ordered
+//   k_sample_guess / k_spec  speculative front (guess = exact parameters: no relabelling)
+//   k_seams STOP variants    staged faces | + the three seams | full (edges, corners)
 //   k_pass2                  relabel + uint64 write (FIN = 0: timing only)
 // Build: make -C tools ablate   Run: tools/ablate Z Y X bz by bx [mode] [iters]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "../cluster_tools_amd/csrc/cc_kernels.hip"
@@ -27,24 +29,6 @@ __global__ void k_read(const float4* __restrict__ in, int64_t n4, float* out) {
         acc += v.x + v.y + v.z + v.w;
     }
     if (acc == 1234.5f) out[0] = acc;
-}
-
-// stats in block-major tile order (one workgroup per tile); interleave > 1: only every
-// interleave-th workgroup works, in runs of per_block (the others exit at once)
-__global__ __launch_bounds__(NTHREADS) void k_stats_bm(Geom g, const float* __restrict__ in, u32* smin, u32* smax,
-                                                       u32* sflag, int per_block, int interleave) {
-    __shared__ u32 red[3][NTHREADS / 64];
-    extern __shared__ u32 dyn[];
-    int64_t idx = blockIdx.x;
-    if (interleave > 1) {
-        const int64_t run = idx / per_block;
-        if (run % interleave) return;
-        idx = (run / interleave) * per_block + idx % per_block;
-    }
-    if (dyn[0] == 0x12345678u) return;
-    const int64_t b = idx / per_block;
-    const int64_t t = block_tile(g, b, (int)(idx % per_block));
-    stats_tile(g, tile_info(g, t), in, smin, smax, sflag, red);
 }
 
 __global__ void k_write(ulonglong2* __restrict__ out, int64_t n2) {
@@ -129,17 +113,6 @@ int main(int argc, char** argv) {
         r.push_back({"copy_read", time_ms(s, iters, [&] { k_read<<<big, 256, 0, s>>>((const float4*)in, nvox / 4, dummy); })});
         r.push_back({"copy_write", time_ms(s, iters, [&] { k_write<<<big, 256, 0, s>>>((ulonglong2*)out, nvox / 2); })});
         r.push_back({"k_block_stats", time_ms(s, iters, stats)});
-        if (nt % nb == 0)
-        {
-            r.push_back({"k_stats_blockmajor", time_ms(s, iters, [&] {
-                k_stats_bm<<<(unsigned)nt, NTHREADS, 16, s>>>(g, in, smin, smax, sflag, (int)(nt / nb), 1); })});
-            r.push_back({"k_stats_bm_lds38k_unused", time_ms(s, iters, [&] {
-                k_stats_bm<<<(unsigned)nt, NTHREADS, 38400, s>>>(g, in, smin, smax, sflag, (int)(nt / nb), 1); })});
-            r.push_back({"k_stats_bm_interleave2", time_ms(s, iters, [&] {
-                k_stats_bm<<<(unsigned)(2 * nt), NTHREADS, 16, s>>>(g, in, smin, smax, sflag, (int)(nt / nb), 2); })});
-            r.push_back({"k_stats_bm_interleave2_lds38k", time_ms(s, iters, [&] {
-                k_stats_bm<<<(unsigned)(2 * nt), NTHREADS, 38400, s>>>(g, in, smin, smax, sflag, (int)(nt / nb), 2); })});
-        }
 #define P1(A) k_pass1<false, A><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, nullptr, bp, thr, mode, BITS, FACES, COUNT, P, KEY)
         r.push_back({"k_pass1_abl1_load_bits", time_ms(s, iters, [&] { P1(1); })});
         r.push_back({"k_pass1_ccl_ph1_runs", time_ms(s, iters, [&] { P1(11); })});
@@ -148,44 +121,32 @@ int main(int argc, char** argv) {
         r.push_back({"k_pass1_abl2_ccl", time_ms(s, iters, [&] { P1(2); })});
         r.push_back({"k_pass1_abl3_keys", time_ms(s, iters, [&] { P1(3); })});
         r.push_back({"k_pass1_full", time_ms(s, iters, [&] { P1(0); })});
-        // fused front (stats + params + pass 1 in one launch)
+        // speculative front: sample + guess, k_spec with the exact parameters as the guess (no relabel)
         {
-            u32* fst;
-            int64_t* fseg;
-            u64* items;
-            HIP_OK(hipMalloc(&fst, (5 * nb + 2) * 4));
-            HIP_OK(hipMalloc(&fseg, (4 * nb + 4) * 8));
-            HIP_OK(hipMalloc(&items, 2 * nt * 8));
-            std::vector<int64_t> hseg;
-            static const char* fnames[10] = {"k_front_lag1", "k_front_lag2", "k_front_lag1_nowait", "k_front_stats_only",
-                                            "k_front_pass1_only", "k_front_ticket_only", "k_front_lag1_s2",
-                                            "k_front_lag1_s3", "k_front_lag1_s4", "k_front_lag2_s2"};
-            for (int v = 0; v < 10; ++v) {
-                const int lag = v == 1 || v == 9 ? 2 : 1;
-                const int per_s = v == 6 || v == 9 ? 2 : v == 7 ? 3 : v == 8 ? 4 : 1, per_p = 1;
-                const int64_t nseg = build_front_segments(hg, lag, hseg, per_s, per_p);
-                const int64_t n_items = hseg[nseg];
-                HIP_OK(hipMemcpy(fseg, hseg.data(), hseg.size() * 8, hipMemcpyHostToDevice));
-                k_front_items<<<1024, 256, 0, s>>>(g, fseg, (int32_t)nseg, per_s, per_p, items);
-                FrontArgs fa;
-                fa.items = items; fa.n_items = n_items; fa.per_s = per_s; fa.per_p = per_p;
-                fa.smin = fst; fa.smax = fst + nb; fa.sflag = fst + 2 * nb; fa.sdone = fst + 3 * nb; fa.ready = fst + 4 * nb;
-                fa.bp = bp; fa.queue = fst + 5 * nb;
-                r.push_back({fnames[v], time_ms(s, iters, [&] {
-                    HIP_OK(hipMemsetAsync(fst, 0xFF, nb * 4, s));
-                    HIP_OK(hipMemsetAsync(fst + nb, 0, (4 * nb + 2) * 4, s));
-                    const unsigned grid = (unsigned)n_items;
-                    const int tv = v < 2 || v >= 6 ? 0 : v == 2 ? 2 : v == 3 ? 3 : v == 4 ? 4 : 6;
-                    if (tv == 0) k_front<0><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
-                    else if (tv == 2) k_front<2><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
-                    else if (tv == 3) k_front<3><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
-                    else if (tv == 4) k_front<4><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
-                    else k_front<6><<<grid, NTHREADS, 0, s>>>(g, fa, in, thr, mode, BITS, FACES, COUNT, P, KEY);
-                })});
-                u32 err = 0;
-                HIP_OK(hipMemcpy(&err, fst + 5 * nb + 1, 4, hipMemcpyDeviceToHost));
-                if (err) std::fprintf(stderr, "k_front variant %d: wait timeout flagged\n", v);
-            }
+            u32 *fst, *part, *TB;
+            BlockParam* guess;
+            HIP_OK(hipMalloc(&fst, 3 * nb * 4));
+            HIP_OK(hipMalloc(&part, nb * SAMPLE_PARTS * 16));
+            HIP_OK(hipMalloc(&TB, nt * 16));
+            HIP_OK(hipMalloc(&guess, nb * sizeof(BlockParam)));
+            r.push_back({"k_sample_guess", time_ms(s, iters, [&] {
+                k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, part);
+                k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, part, thr, mode, guess);
+            })});
+            std::vector<BlockParam> hb(nb);
+            HIP_OK(hipMemcpy(hb.data(), bp, nb * sizeof(BlockParam), hipMemcpyDeviceToHost));
+            for (auto& q : hb)
+                if (q.kind == BP_INTERVAL) { if (mode == 0) q.hi = 0xFFFFFFFFu; else if (mode == 1) q.lo = 0; }
+            HIP_OK(hipMemcpy(guess, hb.data(), nb * sizeof(BlockParam), hipMemcpyHostToDevice));
+            SpecArgs sa;
+            sa.guess = guess; sa.smin = fst; sa.smax = fst + nb; sa.sflag = fst + 2 * nb; sa.TB = TB;
+            r.push_back({"k_spec", time_ms(s, iters, [&] {
+                HIP_OK(hipMemsetAsync(fst, 0xFF, nb * 4, s));
+                HIP_OK(hipMemsetAsync(fst + nb, 0, 2 * nb * 4, s));
+                if (mode == 0) k_spec<false, 1><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS, FACES, COUNT, P, KEY);
+                else if (mode == 1) k_spec<false, 2><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS, FACES, COUNT, P, KEY);
+                else k_spec<false, 3><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS, FACES, COUNT, P, KEY);
+            })});
         }
         // seam kernel variants (FACES from the last full pass-1 run above)
         {
@@ -215,9 +176,13 @@ int main(int argc, char** argv) {
                     (long long)bs[2], mode, (long long)nt);
         for (auto& kv : r) std::printf(", \"%s\": %.4f", kv.first, kv.second);
         std::printf("}\n");
-        std::printf("# GB/s: read %.0f  write %.0f  stats %.0f  pass1(4B/vox) %.0f  pass2(8B/vox) %.0f\n",
-                    nvox * 4 / r[0].second / 1e6, nvox * 8 / r[1].second / 1e6, nvox * 4 / r[2].second / 1e6,
-                    nvox * 4 / r[10].second / 1e6, nvox * 8 / r.back().second / 1e6);
+        auto ms = [&](const char* name) {
+            for (auto& kv : r) if (std::string(kv.first) == name) return kv.second;
+            return 0.0;
+        };
+        std::printf("# GB/s: read %.0f  write %.0f  stats %.0f  k_spec(4B/vox) %.0f  pass2(8B/vox) %.0f\n",
+                    nvox * 4 / ms("copy_read") / 1e6, nvox * 8 / ms("copy_write") / 1e6, nvox * 4 / ms("k_block_stats") / 1e6,
+                    nvox * 4 / ms("k_spec") / 1e6, nvox * 8 / ms("k_pass2") / 1e6);
     } catch (const CCError& e) {
         std::fprintf(stderr, "error: %s\n", e.msg.c_str());
         return 1;
