@@ -27,11 +27,15 @@ constexpr int CZ = TZ / 2, CY = TY / 2, CX = TX / 2;
 constexpr int NC = CZ * CY * CX;           // cubes per full tile (4096)
 constexpr int NROWS = TZ * TY;             // bit rows per tile (512)
 constexpr int NTHREADS = 512;              // 8 waves of 64
-// face planes of a tile, in cubes; entry = k | (4 face-voxel bits << 16), 0 = no face voxel
+// face planes of a tile, in cubes; 16-bit entry = k | (4 face-voxel bits << FK_BITS), 0 = no
+// face voxel (k < 4096: at most one component per cube)
 constexpr int F_Z = CY * CX, F_Y = CZ * CX, F_X = CZ * CY;
 constexpr int F_ZLO = 0, F_ZHI = F_Z, F_YLO = 2 * F_Z, F_YHI = 2 * F_Z + F_Y;
 constexpr int F_XLO = 2 * F_Z + 2 * F_Y, F_XHI = 2 * F_Z + 2 * F_Y + F_X;
 constexpr int FACE_STRIDE = 2 * (F_Z + F_Y + F_X);
+using face_t = uint16_t;
+constexpr int FK_BITS = 12;
+constexpr unsigned FK_MASK = (1u << FK_BITS) - 1;
 constexpr u32 NONE = 0xFFFFFFFFu;
 constexpr int KEY_BITS = 36;               // packed sort key: block << 36 | first-voxel index
 

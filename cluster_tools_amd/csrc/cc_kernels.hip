@@ -489,7 +489,7 @@ __device__ __forceinline__ u32 face_entry(int i, const u64* rows, const TileCCL&
         c = (cz * CY + cy) * CX + (x >> 1);
     }
     if (!bits) return 0;
-    return cube_k(T, c) | (bits << 16);
+    return cube_k(T, c) | (bits << FK_BITS);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -503,7 +503,7 @@ struct Pass1LDS {
 };
 
 template <int ABL>
-__device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const TileInfo& ti, u64* BITS, u32* FACES,
+__device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const TileInfo& ti, u64* BITS, face_t* FACES,
                                              u32* COUNT, u32* P, u64* KEY, Pass1LDS& L, bool write);
 
 // Pass 1 of tile t (block parameters p): bit rows -> BITS, tile CCL -> COUNT, nodes (P, KEY),
@@ -512,7 +512,7 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
 template <bool HAS_MASK, int ABL = 0>
 __device__ __forceinline__ void pass1_tile(const Geom& g, int64_t t, const TileInfo& ti, const BlockParam& p,
                                            const float* __restrict__ in, const u8* __restrict__ mask, float thr,
-                                           int mode, u64* BITS, u32* FACES, u32* COUNT, u32* P, u64* KEY,
+                                           int mode, u64* BITS, face_t* FACES, u32* COUNT, u32* P, u64* KEY,
                                            Pass1LDS& L, bool write = true) {
     const int tid = cc_tid();
     for (int i = tid; i < NROWS; i += NTHREADS) L.rows[i] = 0;
@@ -524,7 +524,7 @@ __device__ __forceinline__ void pass1_tile(const Geom& g, int64_t t, const TileI
 
 // Pass 1 after the bit rows are in L.rows (and a barrier): BITS, tile CCL, COUNT, nodes, faces.
 template <int ABL>
-__device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const TileInfo& ti, u64* BITS, u32* FACES,
+__device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const TileInfo& ti, u64* BITS, face_t* FACES,
                                              u32* COUNT, u32* P, u64* KEY, Pass1LDS& L, bool write) {
     u64* rows = L.rows;
     TileCCL& T = L.T;
@@ -573,8 +573,9 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
         P[node] = node;
         KEY[node] = ((u64)(g.zoff + ti.z0 + lz) * (u64)g.Y + (u64)(ti.y0 + ly)) * (u64)g.X + (u64)(ti.x0 + lx);
     }
-    u32* F = FACES + t * FACE_STRIDE;
-    for (int i = tid; i < FACE_STRIDE; i += NTHREADS) F[i] = face_entry(i, rows, T, ti);
+    u32* FW = (u32*)(FACES + t * FACE_STRIDE);          // two 16-bit entries per store
+    for (int w = tid; w < FACE_STRIDE / 2; w += NTHREADS)
+        FW[w] = face_entry(2 * w, rows, T, ti) | (face_entry(2 * w + 1, rows, T, ti) << 16);
 }
 
 // k_pass1: one workgroup per tile, block parameters precomputed (ablation harness; the library
@@ -582,7 +583,7 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
 template <bool HAS_MASK, int ABL = 0>
 __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restrict__ in,
                                                     const u8* __restrict__ mask, const BlockParam* bp,
-                                                    float thr, int mode, u64* BITS, u32* FACES,
+                                                    float thr, int mode, u64* BITS, face_t* FACES,
                                                     u32* COUNT, u32* P, u64* KEY) {
     __shared__ Pass1LDS L;
     const int64_t t = blockIdx.x;
@@ -730,7 +731,7 @@ struct SpecArgs {
 // SIDES: bounds of the guessed interval that can move (1 lower: 'greater', 2 upper: 'less', 3 both)
 template <bool HAS_MASK, int SIDES>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_spec(
-    Geom g, SpecArgs sa, const float* __restrict__ in, const u8* __restrict__ mask, u64* BITS, u32* FACES,
+    Geom g, SpecArgs sa, const float* __restrict__ in, const u8* __restrict__ mask, u64* BITS, face_t* FACES,
     u32* COUNT, u32* P, u64* KEY) {
     __shared__ Pass1LDS L;
     __shared__ u32 red[6][NTHREADS / 64];
@@ -811,7 +812,7 @@ __global__ void k_verify(Geom g, const BlockParam* guess, const BlockParam* bp, 
 template <bool HAS_MASK>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_fix(
     Geom g, const u32* FIX, const BlockParam* bp, const float* __restrict__ in, const u8* __restrict__ mask,
-    float thr, int mode, u64* BITS, u32* FACES, u32* COUNT, u32* P, u64* KEY) {
+    float thr, int mode, u64* BITS, face_t* FACES, u32* COUNT, u32* P, u64* KEY) {
     __shared__ Pass1LDS L;
     const int64_t t = __builtin_amdgcn_readfirstlane(FIX[1 + blockIdx.x]);
     const TileInfo ti = uniform_ti(tile_info(g, t));
@@ -828,7 +829,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
 // Stage the face planes tile t needs from its three face neighbours into LDS, in the FACE_STRIDE
 // layout: own ZLO/YLO/XLO and the z-/y-/x-lower neighbours' ZHI/YHI/XHI (0 where absent).  One
 // parallel load round instead of dependent global loads per face cube.
-__device__ __forceinline__ void stage_faces(const Geom& g, const u32* __restrict__ FACES, int64_t t,
+__device__ __forceinline__ void stage_faces(const Geom& g, const face_t* __restrict__ FACES, int64_t t,
                                             const TileInfo& ti, u32* S, int tid, int nthr) {
     const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
     // source tile of entry i: own lower faces, the lower neighbours' upper faces (-1: absent)
@@ -839,25 +840,29 @@ __device__ __forceinline__ void stage_faces(const Geom& g, const u32* __restrict
         return ti.ix > 0 ? t - 1 : -1;
     };
     if (nthr == 64) {
-        // one wave: every load issued before the first LDS write (one memory round trip); the
-        // face regions are multiples of 64 entries, so each unrolled step reads one tile
-        constexpr int NJ = (FACE_STRIDE + 63) / 64;
-        static_assert(F_Z % 64 == 0 && F_Y % 64 == 0 && F_X % 64 == 0, "face regions are whole waves");
+        // one wave: every load issued before the first LDS write (one memory round trip), two
+        // 16-bit entries per lane and load; the face regions are multiples of 128 entries, so
+        // each unrolled step reads one tile
+        constexpr int NJ = (FACE_STRIDE / 2 + 63) / 64;
+        static_assert(F_Z % 128 == 0 && F_Y % 128 == 0 && F_X % 128 == 0, "face regions are whole waves");
+        const u32* FW = (const u32*)FACES;
         u32 v[NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            const int i = tid + 64 * j;
-            const int64_t ts = src(64 * j);
-            v[j] = (i < FACE_STRIDE && ts >= 0) ? FACES[ts * FACE_STRIDE + i] : 0u;
+            const int w = tid + 64 * j;
+            const int64_t ts = src(128 * j);
+            v[j] = (w < FACE_STRIDE / 2 && ts >= 0) ? FW[ts * (FACE_STRIDE / 2) + w] : 0u;
         }
 #pragma unroll
-        for (int j = 0; j < NJ; ++j)
-            if (tid + 64 * j < FACE_STRIDE) S[tid + 64 * j] = v[j];
+        for (int j = 0; j < NJ; ++j) {
+            const int w = tid + 64 * j;
+            if (w < FACE_STRIDE / 2) { S[2 * w] = v[j] & 0xFFFFu; S[2 * w + 1] = v[j] >> 16; }
+        }
         return;
     }
     for (int i = tid; i < FACE_STRIDE; i += nthr) {
         const int64_t ts = src(i);
-        S[i] = ts >= 0 ? FACES[ts * FACE_STRIDE + i] : 0u;
+        S[i] = ts >= 0 ? (u32)FACES[ts * FACE_STRIDE + i] : 0u;
     }
 }
 
@@ -867,8 +872,8 @@ struct Cand {
     u32 b1 = 0, b2 = 0;
     bool ovf = false;
     __device__ __forceinline__ void add(u32 b) {
-        const bool new1 = b && b1 && ((b ^ b1) & 0xFFFFu);
-        const bool new2 = new1 && b2 && ((b ^ b2) & 0xFFFFu);
+        const bool new1 = b && b1 && ((b ^ b1) & FK_MASK);
+        const bool new2 = new1 && b2 && ((b ^ b2) & FK_MASK);
         ovf |= new2;
         b2 = (new1 && !b2) ? b : b2;
         b1 = b1 ? b1 : b;
@@ -878,7 +883,7 @@ struct Cand {
 // Connected neighbour entry or 0: face cube a (bits ab) and neighbour entry b with the 4-bit face
 // selections sa (own side) and sb (neighbour side).
 __device__ __forceinline__ u32 face_link(u32 ab, u32 sa, u32 b, u32 sb) {
-    return ((ab & sa) && ((b >> 16) & sb)) ? b : 0u;
+    return ((ab & sa) && ((b >> FK_BITS) & sb)) ? b : 0u;
 }
 
 // 3x3 neighbourhood across a face plane: own entry a at (p, q), neighbour plane FN with row
@@ -886,7 +891,7 @@ __device__ __forceinline__ u32 face_link(u32 ab, u32 sa, u32 b, u32 sb) {
 template <int QS, class UF>
 __device__ __forceinline__ void face3x3(const u32* FN, u32 a, int p, int q, int np, int nq, int64_t t, int64_t tn,
                                         UF& U) {
-    const u32 ab = a >> 16;
+    const u32 ab = a >> FK_BITS;
     auto nb = [&](int dp, int dq) -> u32 {
         const int pp = p + dp, qq = q + dq;
         const bool ok = pp >= 0 && pp < np && qq >= 0 && qq < nq;
@@ -912,9 +917,9 @@ __device__ __forceinline__ void face3x3(const u32* FN, u32 a, int p, int q, int 
 // Three neighbours along one axis of an edge: own entry a at q, neighbour row FR (stride 1 in q)
 // of extent nq; sa/sb fixed selection of the other axis (own / neighbour side).
 template <bool Q_IS_P, class UF>
-__device__ __forceinline__ void edge3(const u32* FR, int RS, u32 a, int q, int nq, int so, int sn, int64_t t,
+__device__ __forceinline__ void edge3(const face_t* FR, int RS, u32 a, int q, int nq, int so, int sn, int64_t t,
                                       int64_t te, UF& U) {
-    const u32 ab = a >> 16;
+    const u32 ab = a >> FK_BITS;
     Cand c;
 #pragma unroll
     for (int d = -1; d <= 1; ++d) {
@@ -941,12 +946,12 @@ __device__ __forceinline__ void edge3(const u32* FR, int RS, u32 a, int q, int n
 }
 
 // Unions across the lower seams of tile t: calls U(t, entry, t_nbr, entry_nbr) for connected face
-// cubes (face entry = k | bits << 16), at least once per connected pair of tile components.
+// cubes (face entry = k | bits << FK_BITS), at least once per connected pair of tile components.
 // S = stage_faces() copy; edge and corner neighbours are read from FACES.
 //   INTER = false: seams inside one block, 26-connectivity (13 tile directions).
 //   INTER = true : seams on block faces, 6-connectivity (3 face directions).
 template <bool INTER, class UF, bool EDGES_ONLY = false>
-__device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict__ FACES, const u32* S,
+__device__ __forceinline__ void stitch_tile(const Geom& g, const face_t* __restrict__ FACES, const u32* S,
                                             int64_t t, const TileInfo& ti, int tid, int nthr, UF&& U) {
     const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2, ncz = (ti.lz + 1) / 2;
     const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
@@ -963,7 +968,7 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
                     const u32 a = S[F_ZLO + e];
                     if (!a) continue;
                     const u32 b = S[F_ZHI + e];
-                    if ((a >> 16) & (b >> 16)) U(t, a, tn, b);
+                    if ((a >> FK_BITS) & (b >> FK_BITS)) U(t, a, tn, b);
                 }
         } else if (same_z) {
             if (!EDGES_ONLY)
@@ -980,7 +985,7 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
                 const int lyn = g.tlen[1][jy];
                 const int cyo = s < 0 ? 0 : ncy - 1, cyn = s < 0 ? (lyn - 1) / 2 : 0;
                 const int jo = s < 0 ? 0 : (ti.ly - 1) & 1, jn = s < 0 ? (lyn - 1) & 1 : 0;
-                const u32* FR = FACES + te * FACE_STRIDE + F_ZHI + cyn * CX;
+                const face_t* FR = FACES + te * FACE_STRIDE + F_ZHI + cyn * CX;
                 for (int cx = tid; cx < ncx; cx += nthr) {
                     const u32 a = S[F_ZLO + cyo * CX + cx];
                     if (a) edge3<false>(FR, 1, a, cx, ncx, jo, jn, t, te, U);
@@ -993,7 +998,7 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
                 const int lxn = g.tlen[2][jx];
                 const int cxo = s < 0 ? 0 : ncx - 1, cxn = s < 0 ? (lxn - 1) / 2 : 0;
                 const int io = s < 0 ? 0 : (ti.lx - 1) & 1, in_ = s < 0 ? (lxn - 1) & 1 : 0;
-                const u32* FR = FACES + te * FACE_STRIDE + F_ZHI + cxn;
+                const face_t* FR = FACES + te * FACE_STRIDE + F_ZHI + cxn;
                 for (int cy = tid; cy < ncy; cy += nthr) {
                     const u32 a = S[F_ZLO + cy * CX + cxo];
                     if (a) edge3<true>(FR, CX, a, cy, ncy, io, in_, t, te, U);
@@ -1012,7 +1017,7 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
                     const int io = s2 < 0 ? 0 : (ti.lx - 1) & 1, in_ = s2 < 0 ? (lxn - 1) & 1 : 0;
                     const u32 a = S[F_ZLO + cyo * CX + cxo];
                     const u32 b = FACES[tc * FACE_STRIDE + F_ZHI + cyn * CX + cxn];
-                    if (a && b && ((a >> 16) & fsel(jo, io)) && ((b >> 16) & fsel(jn, in_)))
+                    if (a && b && ((a >> FK_BITS) & fsel(jo, io)) && ((b >> FK_BITS) & fsel(jn, in_)))
                         U(t, a, tc, b);
                 }
             }
@@ -1030,7 +1035,7 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
                     const u32 a = S[F_YLO + e];
                     if (!a) continue;
                     const u32 b = S[F_YHI + e];
-                    if ((a >> 16) & (b >> 16)) U(t, a, tn, b);
+                    if ((a >> FK_BITS) & (b >> FK_BITS)) U(t, a, tn, b);
                 }
         } else if (same_y) {
             if (!EDGES_ONLY)
@@ -1047,7 +1052,7 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
                 const int lxn = g.tlen[2][jx];
                 const int cxo = s < 0 ? 0 : ncx - 1, cxn = s < 0 ? (lxn - 1) / 2 : 0;
                 const int io = s < 0 ? 0 : (ti.lx - 1) & 1, in_ = s < 0 ? (lxn - 1) & 1 : 0;
-                const u32* FR = FACES + te * FACE_STRIDE + F_YHI + cxn;
+                const face_t* FR = FACES + te * FACE_STRIDE + F_YHI + cxn;
                 for (int cz = tid; cz < ncz; cz += nthr) {
                     const u32 a = S[F_YLO + cz * CX + cxo];
                     if (a) edge3<true>(FR, CX, a, cz, ncz, io, in_, t, te, U);
@@ -1067,7 +1072,7 @@ __device__ __forceinline__ void stitch_tile(const Geom& g, const u32* __restrict
                     const u32 a = S[F_XLO + e];
                     if (!a) continue;
                     const u32 b = S[F_XHI + e];
-                    if ((a >> 16) & (b >> 16)) U(t, a, tn, b);
+                    if ((a >> FK_BITS) & (b >> FK_BITS)) U(t, a, tn, b);
                 }
         } else if (same_x && !EDGES_ONLY) {
             for (int e = tid; e < ncz * CY; e += nthr) {          // face (0, 0, -1): offsets (dz, dy)
@@ -1149,7 +1154,7 @@ template <int STRIDE>
 __device__ __forceinline__ u64 face_row(const u32* F, int r, int lane) {
     const bool ok = STRIDE == CX || lane < 2 * STRIDE;
     const u32 e = ok ? F[(r >> 1) * STRIDE + (lane >> 1)] : 0u;
-    return __ballot((e >> (16 + ((r & 1) << 1) + (lane & 1))) & 1u);
+    return __ballot((e >> (FK_BITS + ((r & 1) << 1) + (lane & 1))) & 1u);
 }
 
 // lane L of w[0..3] = the (uniform) rows a, b split in 32-bit halves
@@ -1213,8 +1218,8 @@ __device__ __forceinline__ void seam_rows3(const u32* S, const int mode[3], int 
             const u64 C = A & (dx > 0 ? B >> 1 : dx < 0 ? B << 1 : B);
             for (u64 m = C & ~(C << 1); m; m &= m - 1) {
                 const int x = __builtin_ctzll(m);
-                const u32 ka = FA[(r >> 1) * stride + (x >> 1)] & 0xFFFFu;
-                const u32 kb = FB[(rb >> 1) * stride + ((x + dx) >> 1)] & 0xFFFFu;
+                const u32 ka = FA[(r >> 1) * stride + (x >> 1)] & FK_MASK;
+                const u32 kb = FB[(rb >> 1) * stride + ((x + dx) >> 1)] & FK_MASK;
                 if (ka == la && kb == lb) continue;             // cheap first filter
                 la = ka; lb = kb;
                 emit(seam, ka, kb);
@@ -1231,7 +1236,7 @@ __device__ __forceinline__ void seam_rows3(const u32* S, const int mode[3], int 
 //   [112,116) ZHI corner entries of (-1, s1, s2), index (s1 > 0) * 2 + (s2 > 0)
 constexpr int EDGE_N = 128;
 
-__device__ __forceinline__ void stage_edges(const Geom& g, const u32* __restrict__ FACES, int64_t t,
+__device__ __forceinline__ void stage_edges(const Geom& g, const face_t* __restrict__ FACES, int64_t t,
                                             const TileInfo& ti, u32* E, int lane) {
     const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
     const bool zok = ti.iz > 0 && g.tblk[0][ti.iz] == g.tblk[0][ti.iz - 1];
@@ -1289,24 +1294,24 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const u32* S, con
         for (int e = 0; e < 2; ++e) {                      // bits x
             const int s = e ? 1 : -1, cyo = s < 0 ? 0 : ncy - 1, jo = s < 0 ? 0 : (ti.ly - 1) & 1;
             const u32 ea = ok[e] ? S[F_ZLO + cyo * CX + (p >> 1)] : 0u, eb = ok[e] ? E[(e ? 32 : 0) + (p >> 1)] : 0u;
-            A[e] = __ballot((ea >> (16 + jo * 2 + (p & 1))) & 1u);
-            B[e] = __ballot((eb >> (16 + ypar(s) * 2 + (p & 1))) & 1u);
+            A[e] = __ballot((ea >> (FK_BITS + jo * 2 + (p & 1))) & 1u);
+            B[e] = __ballot((eb >> (FK_BITS + ypar(s) * 2 + (p & 1))) & 1u);
         }
 #pragma unroll
         for (int e = 2; e < 4; ++e) {                      // bits y
             const int s = e == 3 ? 1 : -1, cxo = s < 0 ? 0 : ncx - 1, io = s < 0 ? 0 : (ti.lx - 1) & 1;
             const bool in = ok[e] && p < TY;
             const u32 ea = in ? S[F_ZLO + (p >> 1) * CX + cxo] : 0u, eb = in ? E[(e == 3 ? 80 : 64) + (p >> 1)] : 0u;
-            A[e] = __ballot((ea >> (16 + (p & 1) * 2 + io)) & 1u);
-            B[e] = __ballot((eb >> (16 + (p & 1) * 2 + xpar(s))) & 1u);
+            A[e] = __ballot((ea >> (FK_BITS + (p & 1) * 2 + io)) & 1u);
+            B[e] = __ballot((eb >> (FK_BITS + (p & 1) * 2 + xpar(s))) & 1u);
         }
 #pragma unroll
         for (int e = 4; e < 6; ++e) {                      // bits z
             const int s = e == 5 ? 1 : -1, cxo = s < 0 ? 0 : ncx - 1, io = s < 0 ? 0 : (ti.lx - 1) & 1;
             const bool in = ok[e] && p < TZ;
             const u32 ea = in ? S[F_YLO + (p >> 1) * CX + cxo] : 0u, eb = in ? E[(e == 5 ? 104 : 96) + (p >> 1)] : 0u;
-            A[e] = __ballot((ea >> (16 + (p & 1) * 2 + io)) & 1u);
-            B[e] = __ballot((eb >> (16 + (p & 1) * 2 + xpar(s))) & 1u);
+            A[e] = __ballot((ea >> (FK_BITS + (p & 1) * 2 + io)) & 1u);
+            B[e] = __ballot((eb >> (FK_BITS + (p & 1) * 2 + xpar(s))) & 1u);
         }
     }
     if (lane < 6) {
@@ -1334,7 +1339,7 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const u32* S, con
                         ka = S[F_YLO + (p >> 1) * CX + (s < 0 ? 0 : ncx - 1)];
                         kb = E[(e == 5 ? 104 : 96) + (q >> 1)];
                     }
-                    ka &= 0xFFFFu; kb &= 0xFFFFu;
+                    ka &= FK_MASK; kb &= FK_MASK;
                     if (ka == la && kb == lb) continue;
                     la = ka; lb = kb;
                     emit(tn, ka, kb);
@@ -1347,15 +1352,15 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const u32* S, con
             const int cyo = s1 < 0 ? 0 : ncy - 1, cxo = s2 < 0 ? 0 : ncx - 1;
             const int jo = s1 < 0 ? 0 : (ti.ly - 1) & 1, io = s2 < 0 ? 0 : (ti.lx - 1) & 1;
             const u32 a = S[F_ZLO + cyo * CX + cxo], b = E[112 + c];
-            if (((a >> 16) & fsel(jo, io)) && ((b >> 16) & fsel(ypar(s1), xpar(s2))))
-                emit(t - sz + s1 * sy + s2, a & 0xFFFFu, b & 0xFFFFu);
+            if (((a >> FK_BITS) & fsel(jo, io)) && ((b >> FK_BITS) & fsel(ypar(s1), xpar(s2))))
+                emit(t - sz + s1 * sy + s2, a & FK_MASK, b & FK_MASK);
         }
     }
 }
 
 // STOP (ablation harness only; 0 in the library): 1 staged, 2 + z seam, 3 + y seam, 4 + x seam
 template <int STOP = 0>
-__global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const u32* __restrict__ FACES, u64* PAIRS, u32* PC,
+__global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* __restrict__ FACES, u64* PAIRS, u32* PC,
                                                          u8* big, u64* IPAIRS, u32* IPC, u8* iovf) {
     __shared__ u32 Sall[SP_WAVES][FACE_STRIDE];
     __shared__ u32 Hall[SP_WAVES][SEAM_HASH];
@@ -1481,7 +1486,7 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_inter_union(Geom g, const u64
 // tiles with a lower block-face seam; INTRA: only tiles of blocks the LDS path could not take
 // (big[block] != 0).
 template <bool INTER>
-__global__ __launch_bounds__(SP_WAVES * 64) void k_stitch(Geom g, const u32* __restrict__ FACES, u32* P,
+__global__ __launch_bounds__(SP_WAVES * 64) void k_stitch(Geom g, const face_t* __restrict__ FACES, u32* P,
                                                           const u64* __restrict__ K, const u8* __restrict__ big,
                                                           const u8* __restrict__ only) {
     __shared__ u32 Sall[SP_WAVES][FACE_STRIDE];
@@ -1504,7 +1509,7 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_stitch(Geom g, const u32* __r
     if (!active) return;
     const u32 capu = (u32)g.cap;
     stitch_tile<INTER>(g, FACES, S, t, ti, lane, 64, [&](int64_t t1, u32 e1, int64_t t2, u32 e2) {
-        const u32 a = (u32)(t1 * capu) + (e1 & 0xFFFFu), b = (u32)(t2 * capu) + (e2 & 0xFFFFu);
+        const u32 a = (u32)(t1 * capu) + (e1 & FK_MASK), b = (u32)(t2 * capu) + (e2 & FK_MASK);
         if (wave_first(((u64)a << 32) | b)) gunion(P, K, a, b);
     });
 }
@@ -1746,25 +1751,25 @@ __global__ __launch_bounds__(NTHREADS) void k_finalize(Geom g, const u32* COUNT,
 // layer.  One workgroup per tile of that layer.
 // ------------------------------------------------------------------------------------------
 template <bool TOP>
-__global__ __launch_bounds__(NTHREADS) void k_plane_labels(Geom g, const u32* __restrict__ FACES, u32* P,
+__global__ __launch_bounds__(NTHREADS) void k_plane_labels(Geom g, const face_t* __restrict__ FACES, u32* P,
                                                            const u64* __restrict__ KR, u64* plane) {
     const int64_t t = (TOP ? (int64_t)(g.nt[0] - 1) * g.nt[1] * g.nt[2] : 0) + blockIdx.x;
     const TileInfo ti = tile_info(g, t);
-    const u32* F = FACES + t * FACE_STRIDE + (TOP ? F_ZHI : F_ZLO);
+    const face_t* F = FACES + t * FACE_STRIDE + (TOP ? F_ZHI : F_ZLO);
     const u32 base = (u32)(t * g.cap);
     const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2;
     for (int e = threadIdx.x; e < ncy * CX; e += NTHREADS) {
         const int cy = e / CX, cx = e % CX;
         if (cx >= ncx) continue;
         const u32 a = F[e];
-        const u64 v = a ? KR[gfind(P, base + (a & 0xFFFFu))] : 0;
+        const u64 v = a ? KR[gfind(P, base + (a & FK_MASK))] : 0;
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const int y = 2 * cy + j, x = 2 * cx + i;
                 if (y < ti.ly && x < ti.lx)
-                    plane[(int64_t)(ti.y0 + y) * g.X + ti.x0 + x] = ((a >> (16 + j * 2 + i)) & 1) ? v : 0;
+                    plane[(int64_t)(ti.y0 + y) * g.X + ti.x0 + x] = ((a >> (FK_BITS + j * 2 + i)) & 1) ? v : 0;
             }
     }
 }
@@ -1871,19 +1876,19 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
 
 // instantiate the templates used by the host side
 #define CC_SPEC(M, S) \
-    template __global__ void k_spec<M, S>(Geom, SpecArgs, const float*, const u8*, u64*, u32*, u32*, u32*, u64*);
+    template __global__ void k_spec<M, S>(Geom, SpecArgs, const float*, const u8*, u64*, face_t*, u32*, u32*, u64*);
 CC_SPEC(false, 1) CC_SPEC(false, 2) CC_SPEC(false, 3) CC_SPEC(true, 1) CC_SPEC(true, 2) CC_SPEC(true, 3)
 #undef CC_SPEC
 template __global__ void k_fix<false>(Geom, const u32*, const BlockParam*, const float*, const u8*, float, int, u64*,
-                                      u32*, u32*, u32*, u64*);
+                                      face_t*, u32*, u32*, u64*);
 template __global__ void k_fix<true>(Geom, const u32*, const BlockParam*, const float*, const u8*, float, int, u64*,
-                                     u32*, u32*, u32*, u64*);
-template __global__ void k_seams<0>(Geom, const u32*, u64*, u32*, u8*, u64*, u32*, u8*);
-template __global__ void k_stitch<false>(Geom, const u32*, u32*, const u64*, const u8*, const u8*);
-template __global__ void k_stitch<true>(Geom, const u32*, u32*, const u64*, const u8*, const u8*);
+                                     face_t*, u32*, u32*, u64*);
+template __global__ void k_seams<0>(Geom, const face_t*, u64*, u32*, u8*, u64*, u32*, u8*);
+template __global__ void k_stitch<false>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);
+template __global__ void k_stitch<true>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_finalize<false>(Geom, const u32*, u32*, const u64*, const u64*, const u64*, const u64*, int64_t, u64*);
 template __global__ void k_finalize<true>(Geom, const u32*, u32*, const u64*, const u64*, const u64*, const u64*, int64_t, u64*);
-template __global__ void k_plane_labels<false>(Geom, const u32*, u32*, const u64*, u64*);
-template __global__ void k_plane_labels<true>(Geom, const u32*, u32*, const u64*, u64*);
+template __global__ void k_plane_labels<false>(Geom, const face_t*, u32*, const u64*, u64*);
+template __global__ void k_plane_labels<true>(Geom, const face_t*, u32*, const u64*, u64*);
 
 }  // namespace cc

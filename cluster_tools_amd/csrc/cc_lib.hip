@@ -180,7 +180,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     c->bstat.ensure(nb * 3 * sizeof(u32));
     c->bparam.ensure(2 * nb * sizeof(BlockParam));     // exact parameters, then the guesses (k_sample)
     c->bits.ensure(nt * NROWS * sizeof(u64));
-    c->faces.ensure(nt * FACE_STRIDE * sizeof(u32));
+    c->faces.ensure(nt * FACE_STRIDE * sizeof(face_t));
     c->count.ensure(nt * sizeof(u32));
     c->P.ensure(nodes * sizeof(u32));
     c->KR.ensure(nodes * sizeof(u64));
@@ -199,7 +199,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
 
     BlockParam* bp = c->bparam.as<BlockParam>();
     u64* BITS = c->bits.as<u64>();
-    u32* FACES = c->faces.as<u32>();
+    face_t* FACES = c->faces.as<face_t>();
     u32* COUNT = c->count.as<u32>();
     u32* P = c->P.as<u32>();
     u64* KR = c->KR.as<u64>();
@@ -360,7 +360,7 @@ static void phase_rid(cc_ctx* c, uint64_t base) {
             k_inter_union<<<grid, SP_WAVES * 64, 0, s>>>(g, c->ipairs.as<u64>(), c->ipc.as<u32>(), c->P.as<u32>(), c->KR.as<u64>());
         });
         // tiles whose block-face pairs overflowed their list (and every tile under CC_DEBUG_GLOBAL_STITCH)
-        launch(c, "k_stitch_inter", [&] { k_stitch<true><<<grid, SP_WAVES * 64, 0, s>>>(g, c->faces.as<u32>(), c->P.as<u32>(), c->KR.as<u64>(), c->big.as<u8>(), c->iovf.as<u8>()); });
+        launch(c, "k_stitch_inter", [&] { k_stitch<true><<<grid, SP_WAVES * 64, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), c->big.as<u8>(), c->iovf.as<u8>()); });
     }
     st.n_map = 0;
     st.stage = 2;
@@ -374,9 +374,9 @@ static void phase_planes(cc_ctx* c, uint64_t* bottom, uint64_t* top) {
     hipStream_t s = c->stream;
     const unsigned nlayer = (unsigned)((int64_t)g.nt[1] * g.nt[2]);
     if (bottom)
-        launch(c, "k_plane_labels", [&] { k_plane_labels<false><<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<u32>(), c->P.as<u32>(), c->KR.as<u64>(), bottom); });
+        launch(c, "k_plane_labels", [&] { k_plane_labels<false><<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), bottom); });
     if (top)
-        launch(c, "k_plane_labels", [&] { k_plane_labels<true><<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<u32>(), c->P.as<u32>(), c->KR.as<u64>(), top); });
+        launch(c, "k_plane_labels", [&] { k_plane_labels<true><<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), top); });
 }
 
 // sort (a, b) pairs lexicographically and drop duplicates; pa/pb are inputs (clobbered),

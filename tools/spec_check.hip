@@ -35,7 +35,8 @@ int main(int argc, char** argv) {
             const int64_t nxb = (shape[2] + 255) / 256;
             k_generate<<<dim3((unsigned)(shape[1] * nxb), (unsigned)shape[0]), 256, 0, s>>>(in, shape[0], shape[1], shape[2], 0, 0, 0, 0x5EED);
         }
-        u32 *st, *COUNT[2], *P, *FACES, *TB;
+        u32 *st, *COUNT[2], *P, *TB;
+        face_t* FACES;
         u64 *BITS[2], *KEY;
         BlockParam *bp, *guess;
         HIP_OK(hipMalloc(&st, nb * 12));
