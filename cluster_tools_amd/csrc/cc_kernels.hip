@@ -457,39 +457,52 @@ __device__ __forceinline__ u32 vbit(u64 w, int x) { return (u32)(w >> ((x & 1) *
 // the two voxels (2cx, 2cx + 1) of cube column cx of a split row, as bits 0 / 1
 __device__ __forceinline__ u32 vpair(u64 w, int cx) { return ((u32)(w >> cx) & 1u) | (((u32)(w >> (32 + cx)) & 1u) << 1); }
 
-// face plane entry i of a tile (see cc_common.hpp for the layout)
-__device__ __forceinline__ u32 face_entry(int i, const u64* rows, const TileCCL& T, const TileInfo& ti) {
-    u32 bits = 0;
-    int c = 0;
-    if (i < F_YLO) {                       // z faces: (cy, cx), bits (y-local j)*2 + (x-local i)
+
+// Face entries 2w and 2w + 1 (one 32-bit word of the face planes): two neighbouring cubes of one
+// face, so their voxel rows and cube rows are read once.  Rows and bits outside the tile are 0,
+// so no extent test is needed (an entry without face voxels is 0).
+__device__ __forceinline__ u32 face_k(const TileCCL& T, int row, int cx) {
+    return T.par[T.roff[row] + (u32)__popc(T.B[row] & mask_le(cx)) - 1] >> 16;
+}
+__device__ __forceinline__ u32 face_word(int w, const u64* rows, const TileCCL& T, const TileInfo& ti) {
+    const int i = 2 * w;
+    u32 b0, b1;
+    int row0, row1, c0, c1;
+    if (i < F_YLO) {                       // z faces: (cy, cx), (cy, cx + 1); bits (y-local)*2 + (x-local)
         const bool hi = i >= F_ZHI;
         const int e = hi ? i - F_ZHI : i;
         const int cy = e / CX, cx = e % CX;
-        if (2 * cy >= ti.ly || 2 * cx >= ti.lx) return 0;
         const int z = hi ? ti.lz - 1 : 0;
-        bits = vpair(rows[z * TY + 2 * cy], cx) | (vpair(rows[z * TY + 2 * cy + 1], cx) << 2);
-        c = ((z >> 1) * CY + cy) * CX + cx;
-    } else if (i < F_XLO) {                // y faces: (cz, cx), bits (z-local)*2 + (x-local)
+        const u64 r0 = rows[z * TY + 2 * cy], r1 = rows[z * TY + 2 * cy + 1];
+        b0 = vpair(r0, cx) | (vpair(r1, cx) << 2);
+        b1 = vpair(r0, cx + 1) | (vpair(r1, cx + 1) << 2);
+        row0 = row1 = (z >> 1) * CY + cy;
+        c0 = cx; c1 = cx + 1;
+    } else if (i < F_XLO) {                // y faces: (cz, cx), (cz, cx + 1); bits (z-local)*2 + (x-local)
         const bool hi = i >= F_YHI;
         const int e = hi ? i - F_YHI : i - F_YLO;
         const int cz = e / CX, cx = e % CX;
-        if (2 * cz >= ti.lz || 2 * cx >= ti.lx) return 0;
         const int y = hi ? ti.ly - 1 : 0;
-        bits = vpair(rows[(2 * cz) * TY + y], cx) | (vpair(rows[(2 * cz + 1) * TY + y], cx) << 2);
-        c = (cz * CY + (y >> 1)) * CX + cx;
-    } else {                               // x faces: (cz, cy), bits (z-local)*2 + (y-local)
+        const u64 r0 = rows[(2 * cz) * TY + y], r1 = rows[(2 * cz + 1) * TY + y];
+        b0 = vpair(r0, cx) | (vpair(r1, cx) << 2);
+        b1 = vpair(r0, cx + 1) | (vpair(r1, cx + 1) << 2);
+        row0 = row1 = cz * CY + (y >> 1);
+        c0 = cx; c1 = cx + 1;
+    } else {                               // x faces: (cz, cy), (cz, cy + 1); bits (z-local)*2 + (y-local)
         const bool hi = i >= F_XHI;
         const int e = hi ? i - F_XHI : i - F_XLO;
         const int cz = e / CY, cy = e % CY;
-        if (2 * cz >= ti.lz || 2 * cy >= ti.ly) return 0;
         const int x = hi ? ti.lx - 1 : 0;
-        const int r = (2 * cz) * TY + 2 * cy;
-        bits = vbit(rows[r], x) | (vbit(rows[r + 1], x) << 1) | (vbit(rows[r + TY], x) << 2) |
-               (vbit(rows[r + TY + 1], x) << 3);
-        c = (cz * CY + cy) * CX + (x >> 1);
+        const u64* r = rows + (2 * cz) * TY + 2 * cy;
+        b0 = vbit(r[0], x) | (vbit(r[1], x) << 1) | (vbit(r[TY], x) << 2) | (vbit(r[TY + 1], x) << 3);
+        b1 = vbit(r[2], x) | (vbit(r[3], x) << 1) | (vbit(r[TY + 2], x) << 2) | (vbit(r[TY + 3], x) << 3);
+        row0 = cz * CY + cy;
+        row1 = row0 + 1;
+        c0 = c1 = x >> 1;
     }
-    if (!bits) return 0;
-    return cube_k(T, c) | (bits << FK_BITS);
+    const u32 e0 = b0 ? face_k(T, row0, c0) | (b0 << FK_BITS) : 0u;
+    const u32 e1 = b1 ? face_k(T, row1, c1) | (b1 << FK_BITS) : 0u;
+    return e0 | (e1 << 16);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -574,8 +587,9 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
         KEY[node] = ((u64)(g.zoff + ti.z0 + lz) * (u64)g.Y + (u64)(ti.y0 + ly)) * (u64)g.X + (u64)(ti.x0 + lx);
     }
     u32* FW = (u32*)(FACES + t * FACE_STRIDE);          // two 16-bit entries per store
-    for (int w = tid; w < FACE_STRIDE / 2; w += NTHREADS)
-        FW[w] = face_entry(2 * w, rows, T, ti) | (face_entry(2 * w + 1, rows, T, ti) << 16);
+    static_assert(F_YLO == 2 * NTHREADS && FACE_STRIDE / 2 <= 2 * NTHREADS, "face words: z faces, then y / x");
+    FW[tid] = face_word(tid, rows, T, ti);
+    if (NTHREADS + tid < FACE_STRIDE / 2) FW[NTHREADS + tid] = face_word(NTHREADS + tid, rows, T, ti);
 }
 
 // k_pass1: one workgroup per tile, block parameters precomputed (ablation harness; the library
