@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'lib', 'libcc_mi355x.so')
+LIB_PATH = os.environ.get('CC_LIB_PATH') or os.path.join(_HERE, 'lib', 'libcc_mi355x.so')   # override: A/B timing only
 MODES = {'greater': 0, 'less': 1, 'equal': 2}
 
 # every symbol include/cc_mi355x.h declares (checked by tests/test_boundary.py)
@@ -273,7 +273,8 @@ class Context:
 
     # ---- profiling ----
     def set_profiling(self, on=True):
-        _check(load().cc_set_profiling(self._h, 1 if on else 0))
+        """on: False/0 off, True/1 every launch, 2 only the volume-sized kernels (k_spec, k_pass2)."""
+        _check(load().cc_set_profiling(self._h, int(on)))
 
     def set_debug(self, flags):
         """Test hook (include/cc_mi355x.h): 1 = global union-find for intra-block seams."""

@@ -740,6 +740,7 @@ struct SpecArgs {
     const BlockParam* guess;
     u32* smin; u32* smax; u32* sflag;
     u32* TB;                  // 4 per tile (see above)
+    int64_t t0;               // first tile of this launch (the front runs in z-layer chunks)
 };
 
 // SIDES: bounds of the guessed interval that can move (1 lower: 'greater', 2 upper: 'less', 3 both)
@@ -749,7 +750,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     u32* COUNT, u32* P, u64* KEY) {
     __shared__ Pass1LDS L;
     __shared__ u32 red[6][NTHREADS / 64];
-    const int64_t t = blockIdx.x;
+    const int64_t t = sa.t0 + blockIdx.x;
     const TileInfo ti = tile_info(g, t);
     const BlockParam p = uniform_bp(sa.guess[ti.block]);
     if (p.kind != BP_INTERVAL) {                   // no guess: statistics only, k_fix labels the tile
@@ -843,8 +844,10 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
 // Stage the face planes tile t needs from its three face neighbours into LDS, in the FACE_STRIDE
 // layout: own ZLO/YLO/XLO and the z-/y-/x-lower neighbours' ZHI/YHI/XHI (0 where absent).  One
 // parallel load round instead of dependent global loads per face cube.
+// ST: u32 (k_stitch) or face_t (k_seams: half the LDS, twice the waves per CU)
+template <class ST>
 __device__ __forceinline__ void stage_faces(const Geom& g, const face_t* __restrict__ FACES, int64_t t,
-                                            const TileInfo& ti, u32* S, int tid, int nthr) {
+                                            const TileInfo& ti, ST* S, int tid, int nthr) {
     const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
     // source tile of entry i: own lower faces, the lower neighbours' upper faces (-1: absent)
     auto src = [&](int i) -> int64_t {
@@ -870,13 +873,16 @@ __device__ __forceinline__ void stage_faces(const Geom& g, const face_t* __restr
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int w = tid + 64 * j;
-            if (w < FACE_STRIDE / 2) { S[2 * w] = v[j] & 0xFFFFu; S[2 * w + 1] = v[j] >> 16; }
+            if (w < FACE_STRIDE / 2) {
+                if constexpr (sizeof(ST) == 2) ((u32*)S)[w] = v[j];      // the two entries as stored
+                else { S[2 * w] = v[j] & 0xFFFFu; S[2 * w + 1] = v[j] >> 16; }
+            }
         }
         return;
     }
     for (int i = tid; i < FACE_STRIDE; i += nthr) {
         const int64_t ts = src(i);
-        S[i] = ts >= 0 ? (u32)FACES[ts * FACE_STRIDE + i] : 0u;
+        S[i] = ts >= 0 ? (ST)FACES[ts * FACE_STRIDE + i] : (ST)0;
     }
 }
 
@@ -1152,7 +1158,7 @@ constexpr int SP_WAVES = 4;            // waves (tiles) per workgroup of the sea
 // block (big[]) or the tile itself (iovf[]) is handled by the global fallback k_stitch.
 // ------------------------------------------------------------------------------------------
 constexpr int TPI = 256;           // block-face pair slots per tile
-constexpr int SEAM_HASH_BITS = 9, SEAM_HASH = 1 << SEAM_HASH_BITS;   // per-wave pair set
+constexpr int SEAM_HASH_BITS = 8, SEAM_HASH = 1 << SEAM_HASH_BITS;   // per-wave pair set
 
 // compile-time loop: f(std::integral_constant<int, i>) for i in [0, N)
 template <int N, class F, int I = 0>
@@ -1165,7 +1171,7 @@ __device__ __forceinline__ void unroll_for(F&& f) {
 
 // row r of a staged face plane F (entries of (r / 2, bit position / 2), bits (r & 1) * 2 + (pos & 1))
 template <int STRIDE>
-__device__ __forceinline__ u64 face_row(const u32* F, int r, int lane) {
+__device__ __forceinline__ u64 face_row(const face_t* F, int r, int lane) {
     const bool ok = STRIDE == CX || lane < 2 * STRIDE;
     const u32 e = ok ? F[(r >> 1) * STRIDE + (lane >> 1)] : 0u;
     return __ballot((e >> (FK_BITS + ((r & 1) << 1) + (lane & 1))) & 1u);
@@ -1191,7 +1197,7 @@ __device__ __forceinline__ void put_rows(u32 (&w)[4], u64 a, u64 b) {
 // 1 inside the block (all 9 (dr, dx): 26-connectivity), 2 block face ((0, 0): 6-connectivity).
 // EMIT(seam, kA, kB) once per run of contacts.
 template <class EM>
-__device__ __forceinline__ void seam_rows3(const u32* S, const int mode[3], int lane, EM&& emit) {
+__device__ __forceinline__ void seam_rows3(const face_t* S, const int mode[3], int lane, EM&& emit) {
     u32 w4[4] = {0, 0, 0, 0};                          // this lane's row of both sides (lo, hi)
     if (mode[0])
         unroll_for<TY>([&](auto R) {
@@ -1209,8 +1215,8 @@ __device__ __forceinline__ void seam_rows3(const u32* S, const int mode[3], int 
     const int seam = lane < 32 ? 0 : lane < 48 ? 1 : 2;
     const int r = lane - (seam == 0 ? 0 : seam == 1 ? 32 : 48), nr = seam == 0 ? TY : TZ;
     const int stride = seam == 2 ? CY : CX;
-    const u32* FA = S + (seam == 0 ? F_ZLO : seam == 1 ? F_YLO : F_XLO);
-    const u32* FB = S + (seam == 0 ? F_ZHI : seam == 1 ? F_YHI : F_XHI);
+    const face_t* FA = S + (seam == 0 ? F_ZLO : seam == 1 ? F_YLO : F_XLO);
+    const face_t* FB = S + (seam == 0 ? F_ZHI : seam == 1 ? F_YHI : F_XHI);
     const int md = mode[seam];
     const u64 A = ((u64)ahi << 32) | alo, B0 = ((u64)bhi << 32) | blo;
     // rows r - 1 / r + 1 of the neighbour (all lanes take part in the shuffles: an inactive
@@ -1251,7 +1257,7 @@ __device__ __forceinline__ void seam_rows3(const u32* S, const int mode[3], int 
 constexpr int EDGE_N = 128;
 
 __device__ __forceinline__ void stage_edges(const Geom& g, const face_t* __restrict__ FACES, int64_t t,
-                                            const TileInfo& ti, u32* E, int lane) {
+                                            const TileInfo& ti, face_t* E, int lane) {
     const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
     const bool zok = ti.iz > 0 && g.tblk[0][ti.iz] == g.tblk[0][ti.iz - 1];
     auto yok = [&](int s) { const int j = ti.iy + s; return j >= 0 && j < g.nt[1] && g.tblk[1][j] == g.tblk[1][ti.iy]; };
@@ -1279,7 +1285,7 @@ __device__ __forceinline__ void stage_edges(const Geom& g, const face_t* __restr
                 v = FACES[(t - sz + s1 * sy + s2) * FACE_STRIDE + F_ZHI + (s1 < 0 ? ylast(s1) : 0) * CX +
                           (s2 < 0 ? xlast(s2) : 0)];
         }
-        E[i] = v;
+        E[i] = (face_t)v;
     }
 }
 
@@ -1289,7 +1295,7 @@ __device__ __forceinline__ void stage_edges(const Geom& g, const face_t* __restr
 //   lane 4/5 (0,-1,-1)/(0,-1,+1): own YLO column x = 0 / lx-1, bits z
 // EMIT(lane code, tn, ka, kb) once per run of contacts (26-connectivity along the edge).
 template <class EM>
-__device__ __forceinline__ void seam_edges_rows(const Geom& g, const u32* S, const u32* E, int64_t t,
+__device__ __forceinline__ void seam_edges_rows(const Geom& g, const face_t* S, const face_t* E, int64_t t,
                                                 const TileInfo& ti, int lane, EM&& emit) {
     const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2;
     const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
@@ -1373,20 +1379,23 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const u32* S, con
 }
 
 // STOP (ablation harness only; 0 in the library): 1 staged, 2 + z seam, 3 + y seam, 4 + x seam
+// Tiles [t_begin, t_end): the seams of a z-layer chunk only read faces of that chunk and the
+// layers below it, so the library runs them on a side stream behind the k_spec chunks.
 template <int STOP = 0>
 __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* __restrict__ FACES, u64* PAIRS, u32* PC,
-                                                         u8* big, u64* IPAIRS, u32* IPC, u8* iovf) {
-    __shared__ u32 Sall[SP_WAVES][FACE_STRIDE];
+                                                         u8* big, u64* IPAIRS, u32* IPC, u8* iovf,
+                                                         int64_t t_begin, int64_t t_end) {
+    __shared__ face_t Sall[SP_WAVES][FACE_STRIDE];
     __shared__ u32 Hall[SP_WAVES][SEAM_HASH];
-    __shared__ u32 Eall[SP_WAVES][EDGE_N];
+    __shared__ face_t Eall[SP_WAVES][EDGE_N];
     __shared__ u32 cnt[SP_WAVES][2];
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t t = (int64_t)blockIdx.x * SP_WAVES + w;
-    const bool valid = t < g.n_tiles;
-    u32* S = Sall[w];
+    const int64_t t = t_begin + (int64_t)blockIdx.x * SP_WAVES + w;
+    const bool valid = t < t_end;
+    face_t* S = Sall[w];
     u32* H = Hall[w];
     TileInfo ti;
-    u32* E = Eall[w];
+    face_t* E = Eall[w];
     if (valid) {
         ti = tile_info(g, t);
         stage_faces(g, FACES, t, ti, S, lane, 64);
@@ -1897,7 +1906,7 @@ template __global__ void k_fix<false>(Geom, const u32*, const BlockParam*, const
                                       face_t*, u32*, u32*, u64*);
 template __global__ void k_fix<true>(Geom, const u32*, const BlockParam*, const float*, const u8*, float, int, u64*,
                                      face_t*, u32*, u32*, u64*);
-template __global__ void k_seams<0>(Geom, const face_t*, u64*, u32*, u8*, u64*, u32*, u8*);
+template __global__ void k_seams<0>(Geom, const face_t*, u64*, u32*, u8*, u64*, u32*, u8*, int64_t, int64_t);
 template __global__ void k_stitch<false>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_stitch<true>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_finalize<false>(Geom, const u32*, u32*, const u64*, const u64*, const u64*, const u64*, int64_t, u64*);

@@ -51,6 +51,7 @@ struct cc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
+    hipStream_t side = nullptr;      // k_seams of finished front chunks, concurrent with the next chunk
     // workspace
     DevBuf tiles, bstat, bparam, bits, faces, count, rc, roff, P, KR, FIN, keys, keys2, vals, vals2, seg,
         values, offsets, lut, cub_tmp, scalars, scalars2, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2,
@@ -62,8 +63,9 @@ struct cc_ctx {
     std::vector<int32_t> h_tab;
     bool lut_valid = false;
     // profiling
-    bool prof = false;
+    int prof = 0;          // 0 off, 1 every launch, 2 the volume-sized kernels only (cc_set_profiling)
     int debug = 0;         // CC_DEBUG_* test hooks
+    int front_chunks = 1;  // z-layer chunks of the speculative front (CC_FRONT_CHUNKS)
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, ProfEntry> prof_acc;
@@ -85,19 +87,32 @@ static hipEvent_t pool_event(cc_ctx* c) {
 }
 
 template <class F>
-static void launch(cc_ctx* c, const char* name, F&& f) {
+static void launch_on(cc_ctx* c, hipStream_t s, const char* name, F&& f) {
     hipEvent_t a = nullptr, b = nullptr;
-    if (c->prof) {
+    const bool timed = c->prof == 1 || (c->prof == 2 && (!std::strcmp(name, "k_spec") || !std::strcmp(name, "k_pass2")));
+    if (timed) {
         a = pool_event(c);
         b = pool_event(c);
-        HIP_OK(hipEventRecord(a, c->stream));
+        HIP_OK(hipEventRecord(a, s));
     }
     f();
     HIP_OK(hipGetLastError());
-    if (c->prof) {
-        HIP_OK(hipEventRecord(b, c->stream));
+    if (timed) {
+        HIP_OK(hipEventRecord(b, s));
         c->pending.push_back({name, {a, b}});
     }
+}
+
+template <class F>
+static void launch(cc_ctx* c, const char* name, F&& f) { launch_on(c, c->stream, name, static_cast<F&&>(f)); }
+
+// stream `waiter` waits for the work enqueued so far on `from`
+static void stream_wait(cc_ctx* c, hipStream_t from, hipStream_t waiter) {
+    hipEvent_t e;
+    HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(e, from));
+    HIP_OK(hipStreamWaitEvent(waiter, e, 0));
+    HIP_OK(hipEventDestroy(e));
 }
 
 static void resolve_profile(cc_ctx* c) {
@@ -222,19 +237,56 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         sa.guess = guess;
         sa.smin = smin; sa.smax = smax; sa.sflag = sflag;
         sa.TB = TB;
-        launch(c, "k_spec", [&] {
-#define CC_SPEC_LAUNCH(M, S) k_spec<M, S><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, mask, BITS, FACES, COUNT, P, KR)
-            if (mask) {
-                if (mode == MODE_GREATER) CC_SPEC_LAUNCH(true, 1);
-                else if (mode == MODE_LESS) CC_SPEC_LAUNCH(true, 2);
-                else CC_SPEC_LAUNCH(true, 3);
-            } else {
-                if (mode == MODE_GREATER) CC_SPEC_LAUNCH(false, 1);
-                else if (mode == MODE_LESS) CC_SPEC_LAUNCH(false, 2);
-                else CC_SPEC_LAUNCH(false, 3);
-            }
+        // seam outputs (k_seams sets flags, so they are cleared first)
+        c->big.ensure(nb);
+        c->pairsl.ensure((size_t)nt * TPC * sizeof(u64));
+        c->pc.ensure(nt * sizeof(u32));
+        c->ipairs.ensure((size_t)nt * TPI * sizeof(u64));
+        c->ipc.ensure(nt * sizeof(u32));
+        c->iovf.ensure(nt);
+        const bool lds_seams = !(c->debug & CC_DEBUG_GLOBAL_STITCH);
+        auto clear_seams = [&] {
+            HIP_OK(hipMemsetAsync(c->big.p, lds_seams ? 0 : 1, nb, s));
+            HIP_OK(hipMemsetAsync(c->iovf.p, lds_seams ? 0 : 1, nt, s));
+            HIP_OK(hipMemsetAsync(c->ipc.p, 0, nt * sizeof(u32), s));
+        };
+        auto seams = [&](hipStream_t q, int64_t t0, int64_t t1) {
+            launch_on(c, q, "k_seams", [&] {
+                k_seams<0><<<(unsigned)((t1 - t0 + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, q>>>(
+                    g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), c->big.as<u8>(), c->ipairs.as<u64>(),
+                    c->ipc.as<u32>(), c->iovf.as<u8>(), t0, t1);
+            });
+        };
+        clear_seams();
+        // The front runs in chunks of whole tile z-layers.  The seams of a chunk read only its
+        // faces and those of the layers below, so k_seams of chunk i runs on the side stream
+        // while k_spec of chunk i + 1 streams the input (k_seams is latency-bound, k_spec
+        // bandwidth-bound).  Tiles k_fix relabels later get their seams recomputed below.
+        const int64_t layer = (int64_t)g.nt[1] * g.nt[2];
+        const int64_t n_chunks = lds_seams ? std::min<int64_t>(g.nt[0], c->front_chunks) : 1;
+        if (lds_seams) stream_wait(c, s, c->side);
+        for (int64_t ci = 0; ci < n_chunks; ++ci) {
+            const int64_t t0 = g.nt[0] * ci / n_chunks * layer, t1 = g.nt[0] * (ci + 1) / n_chunks * layer;
+            sa.t0 = t0;
+            const unsigned ng = (unsigned)(t1 - t0);
+            launch(c, "k_spec", [&] {
+#define CC_SPEC_LAUNCH(M, S) k_spec<M, S><<<ng, NTHREADS, 0, s>>>(g, sa, in, mask, BITS, FACES, COUNT, P, KR)
+                if (mask) {
+                    if (mode == MODE_GREATER) CC_SPEC_LAUNCH(true, 1);
+                    else if (mode == MODE_LESS) CC_SPEC_LAUNCH(true, 2);
+                    else CC_SPEC_LAUNCH(true, 3);
+                } else {
+                    if (mode == MODE_GREATER) CC_SPEC_LAUNCH(false, 1);
+                    else if (mode == MODE_LESS) CC_SPEC_LAUNCH(false, 2);
+                    else CC_SPEC_LAUNCH(false, 3);
+                }
 #undef CC_SPEC_LAUNCH
-        });
+            });
+            if (lds_seams) {
+                stream_wait(c, s, c->side);
+                seams(c->side, t0, t1);
+            }
+        }
         launch(c, "k_block_params", [&] {
             k_block_params<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, smin, smax, sflag, thr, mode, bp);
         });
@@ -243,28 +295,20 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         HIP_OK(hipMemcpyAsync(&nfix, FIX, sizeof(u32), hipMemcpyDeviceToHost, s));
         HIP_OK(hipStreamSynchronize(s));
         st.n_fix = nfix;
-        if (nfix)
+        if (lds_seams) stream_wait(c, c->side, s);
+        if (nfix) {
             launch(c, "k_fix", [&] {
                 if (mask) k_fix<true><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, in, mask, thr, mode, BITS, FACES, COUNT, P, KR);
                 else k_fix<false><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR);
             });
+            if (lds_seams) {            // relabelled faces: all seams again
+                clear_seams();
+                seams(s, 0, nt);
+            }
+        }
     }
-    c->big.ensure(nb);
-    c->pairsl.ensure((size_t)nt * TPC * sizeof(u64));
-    c->pc.ensure(nt * sizeof(u32));
-    c->ipairs.ensure((size_t)nt * TPI * sizeof(u64));
-    c->ipc.ensure(nt * sizeof(u32));
-    c->iovf.ensure(nt);
     u8* big = c->big.as<u8>();
-    HIP_OK(hipMemsetAsync(big, (c->debug & CC_DEBUG_GLOBAL_STITCH) ? 1 : 0, nb, s));
-    HIP_OK(hipMemsetAsync(c->iovf.p, (c->debug & CC_DEBUG_GLOBAL_STITCH) ? 1 : 0, nt, s));
-    HIP_OK(hipMemsetAsync(c->ipc.p, 0, nt * sizeof(u32), s));
     if (!(c->debug & CC_DEBUG_GLOBAL_STITCH)) {
-        launch(c, "k_seams", [&] {
-            k_seams<0><<<(unsigned)((nt + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(
-                g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), big, c->ipairs.as<u64>(), c->ipc.as<u32>(),
-                c->iovf.as<u8>());
-        });
         launch(c, "k_block_uf", [&] {
             k_block_uf<<<(unsigned)nb, SB_THREADS, 0, s>>>(g, COUNT, c->pairsl.as<u64>(), c->pc.as<u32>(), P, KR, big);
         });
@@ -542,7 +586,9 @@ int cc_create(int device, cc_ctx** out) {
         cc_ctx* c = new cc_ctx();
         c->device = device;
         HIP_OK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+        HIP_OK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         c->stream = c->own_stream;
+        if (const char* e = std::getenv("CC_FRONT_CHUNKS")) c->front_chunks = std::max(1, atoi(e));
         *out = c;
     })
 }
@@ -551,6 +597,7 @@ void cc_destroy(cc_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->side) (void)hipStreamSynchronize(c->side);
     DevBuf* bufs[] = {&c->tiles, &c->bstat, &c->bparam, &c->bits, &c->faces, &c->count, &c->rc, &c->roff, &c->P, &c->KR,
                       &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
                       &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
@@ -560,6 +607,7 @@ void cc_destroy(cc_ctx* c) {
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    if (c->side) (void)hipStreamDestroy(c->side);
     delete (RunState*)c->run;
     delete c;
 }
@@ -664,7 +712,8 @@ int cc_merge_offsets(const uint64_t* values, int64_t n_blocks, uint64_t* offsets
 int cc_set_profiling(cc_ctx* c, int enable) {
     CC_TRY({
         CC_REQUIRE(c, "ctx is NULL");
-        c->prof = enable != 0;
+        CC_REQUIRE(enable >= 0 && enable <= 2, "profiling level must be 0, 1 or 2");
+        c->prof = enable;
     })
 }
 

@@ -151,7 +151,9 @@ int cc_generate_boundary_map(cc_ctx* ctx, float* out_dev, const int64_t shape[3]
                              const int64_t origin[3], uint64_t seed);
 
 /* --- instrumentation ---------------------------------------------------------- */
-/* Enable per-kernel HIP-event timing on the ctx stream (adds one event pair per launch). */
+/* Per-kernel HIP-event timing on the stream each kernel runs on: enable = 0 off, 1 every launch
+ * (one event pair per launch), 2 only the volume-sized kernels k_spec and k_pass2 (what bench.py
+ * keeps on inside its timed region). */
 int cc_set_profiling(cc_ctx* ctx, int enable);
 /* Accumulated per-kernel totals since the last reset: name list as "k1,k2,...",
  * and for each: launch count and total milliseconds.  Returns number of kernels. */

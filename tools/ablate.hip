@@ -140,7 +140,7 @@ int main(int argc, char** argv) {
                 if (q.kind == BP_INTERVAL) { if (mode == 0) q.hi = 0xFFFFFFFFu; else if (mode == 1) q.lo = 0; }
             HIP_OK(hipMemcpy(guess, hb.data(), nb * sizeof(BlockParam), hipMemcpyHostToDevice));
             SpecArgs sa;
-            sa.guess = guess; sa.smin = fst; sa.smax = fst + nb; sa.sflag = fst + 2 * nb; sa.TB = TB;
+            sa.guess = guess; sa.smin = fst; sa.smax = fst + nb; sa.sflag = fst + 2 * nb; sa.TB = TB; sa.t0 = 0;
             r.push_back({"k_spec", time_ms(s, iters, [&] {
                 HIP_OK(hipMemsetAsync(fst, 0xFF, nb * 4, s));
                 HIP_OK(hipMemsetAsync(fst + nb, 0, 2 * nb * 4, s));
@@ -164,7 +164,7 @@ int main(int argc, char** argv) {
             HIP_OK(hipMemset(big, 0, nb));
             HIP_OK(hipMemset(iovf, 0, nt));
             const unsigned sg = (unsigned)((nt + SP_WAVES - 1) / SP_WAVES);
-#define SEAMS(V) k_seams<V><<<sg, SP_WAVES * 64, 0, s>>>(g, FACES, pairs, pc, big, ipairs, ipc, iovf)
+#define SEAMS(V) k_seams<V><<<sg, SP_WAVES * 64, 0, s>>>(g, FACES, pairs, pc, big, ipairs, ipc, iovf, 0, nt)
             r.push_back({"k_seams_stage", time_ms(s, iters, [&] { SEAMS(1); })});
             r.push_back({"k_seams_z", time_ms(s, iters, [&] { SEAMS(2); })});
             r.push_back({"k_seams_zy", time_ms(s, iters, [&] { SEAMS(3); })});

@@ -74,7 +74,7 @@ int main(int argc, char** argv) {
         }
         HIP_OK(hipMemcpy(guess, hb.data(), nb * sizeof(BlockParam), hipMemcpyHostToDevice));
         SpecArgs sa;
-        sa.guess = guess; sa.smin = smin; sa.smax = smax; sa.sflag = sflag; sa.TB = TB;
+        sa.guess = guess; sa.smin = smin; sa.smax = smax; sa.sflag = sflag; sa.TB = TB; sa.t0 = 0;
         if (mode == 0) k_spec<false, 1><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS[1], FACES, COUNT[1], P, KEY);
         else if (mode == 1) k_spec<false, 2><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS[1], FACES, COUNT[1], P, KEY);
         else k_spec<false, 3><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS[1], FACES, COUNT[1], P, KEY);
