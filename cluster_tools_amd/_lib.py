@@ -22,7 +22,7 @@ EXPORTS = (
     'cc_get_lut', 'cc_block_components', 'cc_merge_offsets', 'cc_block_faces',
     'cc_merge_assignments', 'cc_write', 'cc_generate_boundary_map', 'cc_set_profiling',
     'cc_get_profile', 'cc_reset_profile', 'cc_shard_begin', 'cc_shard_assign', 'cc_shard_planes',
-    'cc_seam_pairs', 'cc_shard_finish', 'cc_set_debug',
+    'cc_seam_pairs', 'cc_shard_finish', 'cc_set_debug', 'cc_threshold',
 )
 
 
@@ -68,6 +68,7 @@ def load():
         'cc_get_profile': (I, [P, ctypes.c_char_p, I, P, P, I]),
         'cc_reset_profile': (I, [P]),
         'cc_set_debug': (I, [P, I]),
+        'cc_threshold': (I, [P, P, P, P, ctypes.c_double, I, P]),
         'cc_shard_begin': (I, [P, P, P, P, P, ctypes.c_double, I, i64, P]),
         'cc_shard_assign': (I, [P, u64]),
         'cc_shard_planes': (I, [P, P, P]),
@@ -169,6 +170,21 @@ class Context:
             _check(L.cc_label_volume_host(self._h, _ptr(inp), _ptr(mask), _ptr(shape), _ptr(bs),
                                           float(threshold), mode_id(mode), _ptr(out), ctypes.byref(res)))
         return out, res.as_dict()
+
+    def threshold(self, inp, block_shape, threshold, mode='greater', out=None):
+        """Threshold task (threshold.py:131-171): per-block normalize + compare -> uint8.
+        `inp` is a float32 torch CUDA tensor; returns a uint8 tensor of the same shape."""
+        import torch
+        assert hasattr(inp, 'data_ptr') and inp.is_cuda and inp.dtype == torch.float32 and inp.is_contiguous()
+        shape = _i64(inp.shape)
+        bs = _i64(block_shape)
+        assert len(shape) == 3 and len(bs) == 3
+        if out is None:
+            out = torch.empty(tuple(inp.shape), dtype=torch.uint8, device=inp.device)
+        assert out.dtype == torch.uint8 and out.shape == inp.shape and out.is_contiguous()
+        _check(load().cc_threshold(self._h, _ptr(inp), _ptr(shape), _ptr(bs), float(threshold),
+                                   mode_id(mode), _ptr(out)))
+        return out
 
     def block_values(self, n_blocks):
         a = np.empty(n_blocks, dtype=np.uint64)

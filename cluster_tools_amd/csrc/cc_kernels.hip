@@ -1832,6 +1832,7 @@ __global__ void k_map_values(int64_t m, const u64* U, const u64* root, u64* V) {
 constexpr int LABCAP = 2048;          // component labels cached in LDS
 
 // store the two voxels (x, x+1) of one cube row segment; 16-B store when aligned
+// (plain stores: non-temporal ones measured 0.3 ms slower over the 34 GB of C3)
 __device__ __forceinline__ void store2(u64* __restrict__ out, int64_t idx, u64 v0, u64 v1, bool two, bool vec) {
     if (two && vec) {
         *reinterpret_cast<ulonglong2*>(out + idx) = make_ulonglong2(v0, v1);
@@ -1893,6 +1894,38 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
                 store2(out, ((int64_t)(ti.z0 + z) * g.Y + ti.y0 + y) * g.X + ti.x0 + 2 * cx,
                        (b & 1) ? v : 0, (b & 2) ? v : 0, two, vec);
             }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_threshold: the reference Threshold task (thresholded_components/threshold.py:131-171):
+// per-block normalize (volume_utils.py:98-105) and compare, written as uint8.  One workgroup
+// per tile; the block parameters come from k_block_stats + k_block_params (the same exact
+// foreground interval the labelling path uses).  float4 loads / uchar4 stores on full tiles.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NTHREADS) void k_threshold(Geom g, const BlockParam* __restrict__ bp,
+                                                        const float* __restrict__ in, float thr, int mode,
+                                                        u8* __restrict__ out) {
+    const int64_t t = blockIdx.x;
+    const TileInfo ti = tile_info(g, t);
+    const BlockParam p = uniform_bp(bp[ti.block]);
+    const int tid = threadIdx.x;
+    const int n = ti.lz * ti.ly;
+    auto at = [&](int row, int x) { return ((int64_t)(ti.z0 + row / ti.ly) * g.Y + ti.y0 + row % ti.ly) * g.X + ti.x0 + x; };
+    if (ti.lx == TX && ((g.X | ti.x0) & 3) == 0) {
+        for (int i = tid; i < n * (TX / 4); i += NTHREADS) {
+            const int64_t o = at(i / (TX / 4), 4 * (i % (TX / 4)));
+            const float4 v = *reinterpret_cast<const float4*>(in + o);
+            uchar4 r;
+            r.x = voxel_pred(p, v.x, thr, mode); r.y = voxel_pred(p, v.y, thr, mode);
+            r.z = voxel_pred(p, v.z, thr, mode); r.w = voxel_pred(p, v.w, thr, mode);
+            *reinterpret_cast<uchar4*>(out + o) = r;
+        }
+    } else {
+        for (int i = tid; i < n * ti.lx; i += NTHREADS) {
+            const int64_t o = at(i / ti.lx, i % ti.lx);
+            out[o] = voxel_pred(p, in[o], thr, mode);
         }
     }
 }

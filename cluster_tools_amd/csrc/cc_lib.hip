@@ -695,6 +695,38 @@ int cc_block_components(cc_ctx* c, const float* in, const uint8_t* mask, const i
     })
 }
 
+int cc_threshold(cc_ctx* c, const float* in, const int64_t shape[3], const int64_t block_shape[3],
+                 double threshold, int mode, uint8_t* out) {
+    CC_TRY({
+        CC_REQUIRE(c && in && out && shape && block_shape, "NULL argument");
+        HIP_OK(hipSetDevice(c->device));
+        const int md = to_mode(mode);
+        RunState& st = state(c);
+        st = RunState();
+        st.hg = make_geom(shape, block_shape, 0);
+        upload_geom(c, st.hg);
+        Geom& g = st.hg.g;
+        const int64_t nt = g.n_tiles, nb = g.n_blocks;
+        hipStream_t s = c->stream;
+        c->bstat.ensure(nb * 3 * sizeof(u32));
+        c->bparam.ensure(2 * nb * sizeof(BlockParam));
+        u32* smin = c->bstat.as<u32>();
+        u32* smax = smin + nb;
+        u32* sflag = smax + nb;
+        BlockParam* bp = c->bparam.as<BlockParam>();
+        const float thr = (float)threshold;          // numpy: python float -> float32
+        HIP_OK(hipMemsetAsync(smin, 0xFF, nb * sizeof(u32), s));
+        HIP_OK(hipMemsetAsync(smax, 0x00, 2 * nb * sizeof(u32), s));
+        launch(c, "k_block_stats", [&] { k_block_stats<<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, smin, smax, sflag); });
+        launch(c, "k_block_params", [&] {
+            k_block_params<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, smin, smax, sflag, thr, md, bp);
+        });
+        launch(c, "k_threshold", [&] { k_threshold<<<(unsigned)nt, NTHREADS, 0, s>>>(g, bp, in, thr, md, out); });
+        sync(c);
+        st.stage = 0;
+    })
+}
+
 int cc_merge_offsets(const uint64_t* values, int64_t n_blocks, uint64_t* offsets, uint8_t* empty,
                      uint64_t* n_labels) {
     CC_TRY({

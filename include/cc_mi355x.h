@@ -98,6 +98,13 @@ int cc_block_components(cc_ctx* ctx, const float* in_dev, const uint8_t* mask_de
                         double threshold, int mode, uint64_t* labels_dev,
                         uint64_t* values_host, int64_t n_blocks);
 
+/* Threshold task (thresholded_components/threshold.py:131-171, _threshold_block): per
+ * reference block normalize (volume_utils.py:98-105) then `> / < / ==` threshold (float32), the
+ * result as uint8 0/1 of the same shape.  in_dev / out_dev are device pointers (C-order).
+ * channel / sigma_prefilter are not supported (rejected by the Python task). */
+int cc_threshold(cc_ctx* ctx, const float* in_dev, const int64_t shape[3], const int64_t block_shape[3],
+                 double threshold, int mode, uint8_t* out_dev);
+
 /* merge_offsets (merge_offsets.py:104-120): exclusive scan of values; writes offsets
  * and empty flags; returns n_labels through *n_labels. Host arrays. */
 int cc_merge_offsets(const uint64_t* values_host, int64_t n_blocks, uint64_t* offsets_host,

@@ -185,3 +185,38 @@ def graph_components(inp_fg, block_shape):
     lab = (lab + 1).reshape(shape).astype(np.uint64)
     lab[~fg] = 0
     return canon(lab)
+
+
+def threshold_volume(inp, block_shape, threshold, mode='greater'):
+    """Threshold task restated in numpy (TEST INFRASTRUCTURE ONLY).
+
+    Per block of the C-order block grid (nifty blocking from the origin, edge blocks truncated):
+    normalize as cluster_tools/utils/volume_utils.py:98-105 (float32: subtract the min, divide
+    by the max when it is > 0) and compare with the threshold as threshold.py:160-167 (python
+    float against a float32 array: a float32 compare), stored as uint8 (threshold.py:170).
+    """
+    x = np.asarray(inp)
+    out = np.zeros(x.shape, dtype=np.uint8)
+    thr = np.float32(threshold)
+    grids = [range(0, s, b) for s, b in zip(x.shape, block_shape)]
+    with np.errstate(invalid='ignore', divide='ignore'):
+        for z0 in grids[0]:
+            for y0 in grids[1]:
+                for x0 in grids[2]:
+                    bb = (slice(z0, z0 + block_shape[0]), slice(y0, y0 + block_shape[1]),
+                          slice(x0, x0 + block_shape[2]))
+                    y = x[bb].astype(np.float32)
+                    y -= y.min()
+                    m = y.max()
+                    if m > 0:
+                        y /= m
+                    if mode == 'greater':
+                        r = y > thr
+                    elif mode == 'less':
+                        r = y < thr
+                    elif mode == 'equal':
+                        r = y == thr
+                    else:
+                        raise RuntimeError('Thresholding Mode %s not supported' % mode)
+                    out[bb] = r.astype(np.uint8)
+    return out

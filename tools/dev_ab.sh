@@ -1,9 +1,11 @@
 #!/bin/bash
-# dev A/B timing: current library vs scratch/old (built from an earlier commit), same box
+# dev A/B timing: current library vs variant libraries (CC_LIB_PATH), interleaved on one box
 mkdir -p gpurun_out
-B="timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline"
-$B > gpurun_out/ab_new2.json || exit 1
-$B --timed-prof 1 > gpurun_out/ab_new1.json || exit 1
-CC_LIB_PATH=scratch/old/libcc_mi355x.so $B > gpurun_out/ab_old.json || exit 1
-$B > gpurun_out/ab_new2b.json || exit 1
-CC_LIB_PATH=scratch/old/libcc_mi355x.so $B > gpurun_out/ab_oldb.json || exit 1
+B="timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline $BENCH_ARGS"
+for r in 1 2; do
+  $B > gpurun_out/ab_cur_$r.json || exit 1
+  for v in scratch/var/*.so; do
+    n=$(basename $v .so)
+    CC_LIB_PATH=$v $B > gpurun_out/ab_${n}_$r.json || exit 1
+  done
+done
