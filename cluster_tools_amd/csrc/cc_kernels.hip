@@ -1160,67 +1160,45 @@ constexpr int SP_WAVES = 4;            // waves (tiles) per workgroup of the sea
 constexpr int TPI = 256;           // block-face pair slots per tile
 constexpr int SEAM_HASH_BITS = 8, SEAM_HASH = 1 << SEAM_HASH_BITS;   // per-wave pair set
 
-// compile-time loop: f(std::integral_constant<int, i>) for i in [0, N)
-template <int N, class F, int I = 0>
-__device__ __forceinline__ void unroll_for(F&& f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        unroll_for<N, F, I + 1>(static_cast<F&&>(f));
-    }
-}
-
-// row r of a staged face plane F (entries of (r / 2, bit position / 2), bits (r & 1) * 2 + (pos & 1))
-template <int STRIDE>
-__device__ __forceinline__ u64 face_row(const face_t* F, int r, int lane) {
-    const bool ok = STRIDE == CX || lane < 2 * STRIDE;
-    const u32 e = ok ? F[(r >> 1) * STRIDE + (lane >> 1)] : 0u;
-    return __ballot((e >> (FK_BITS + ((r & 1) << 1) + (lane & 1))) & 1u);
-}
-
-// lane L of w[0..3] = the (uniform) rows a, b split in 32-bit halves
-// (a select, not v_writelane inline asm: the asm form gave wrong rows in this kernel)
-template <int L>
-__device__ __forceinline__ void put_rows(u32 (&w)[4], u64 a, u64 b) {
-#ifdef CC_PUT_ASM
-    const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
-    asm("s_nop 3\n\tv_writelane_b32 %0, %1, %2" : "+v"(w[0]) : "s"(a0), "i"(L));
-    asm("v_writelane_b32 %0, %1, %2" : "+v"(w[1]) : "s"(a1), "i"(L));
-    asm("v_writelane_b32 %0, %1, %2" : "+v"(w[2]) : "s"(b0), "i"(L));
-    asm("v_writelane_b32 %0, %1, %2" : "+v"(w[3]) : "s"(b1), "i"(L));
-    return;
-#endif
-    if ((int)__lane_id() == L) { w[0] = (u32)a; w[1] = (u32)(a >> 32); w[2] = (u32)b; w[3] = (u32)(b >> 32); }
+// bits 2k, 2k+1 of the result := bits sh, sh+1 of face entry k of an 8-entry LDS word
+// (two 16-bit entries per u32, entry 2j in the low half)
+__device__ __forceinline__ u32 pack8(uint4 v, int sh) {
+    const u32 w[4] = {v.x, v.y, v.z, v.w};
+    u32 r = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r |= (((w[j] >> sh) & 3u) << (4 * j)) | (((w[j] >> (16 + sh)) & 3u) << (4 * j + 2));
+    return r;
 }
 
 // The three lower seams at once, one voxel row per lane: lanes 0-31 the z seam (rows y, bits x),
 // 32-47 the y seam (rows z, bits x), 48-63 the x seam (rows z, bits y).  mode[s]: 0 no seam,
 // 1 inside the block (all 9 (dr, dx): 26-connectivity), 2 block face ((0, 0): 6-connectivity).
+// Each lane packs its own row of both sides straight from the staged entries (voxel 2c + i of
+// row r is bit FK_BITS + 2 (r & 1) + i of entry (r / 2, c)), 16-B LDS reads.
 // EMIT(seam, kA, kB) once per run of contacts.
 template <class EM>
 __device__ __forceinline__ void seam_rows3(const face_t* S, const int mode[3], int lane, EM&& emit) {
-    u32 w4[4] = {0, 0, 0, 0};                          // this lane's row of both sides (lo, hi)
-    if (mode[0])
-        unroll_for<TY>([&](auto R) {
-            put_rows<decltype(R)::value>(w4, face_row<CX>(S + F_ZLO, R.value, lane), face_row<CX>(S + F_ZHI, R.value, lane));
-        });
-    if (mode[1])
-        unroll_for<TZ>([&](auto R) {
-            put_rows<32 + decltype(R)::value>(w4, face_row<CX>(S + F_YLO, R.value, lane), face_row<CX>(S + F_YHI, R.value, lane));
-        });
-    if (mode[2])
-        unroll_for<TZ>([&](auto R) {
-            put_rows<48 + decltype(R)::value>(w4, face_row<CY>(S + F_XLO, R.value, lane), face_row<CY>(S + F_XHI, R.value, lane));
-        });
-    const u32 alo = w4[0], ahi = w4[1], blo = w4[2], bhi = w4[3];
     const int seam = lane < 32 ? 0 : lane < 48 ? 1 : 2;
     const int r = lane - (seam == 0 ? 0 : seam == 1 ? 32 : 48), nr = seam == 0 ? TY : TZ;
     const int stride = seam == 2 ? CY : CX;
     const face_t* FA = S + (seam == 0 ? F_ZLO : seam == 1 ? F_YLO : F_XLO);
     const face_t* FB = S + (seam == 0 ? F_ZHI : seam == 1 ? F_YHI : F_XHI);
-    const int md = mode[seam];
-    const u64 A = ((u64)ahi << 32) | alo, B0 = ((u64)bhi << 32) | blo;
-    // rows r - 1 / r + 1 of the neighbour (all lanes take part in the shuffles: an inactive
-    // source lane would read as 0)
+    const int md = seam == 0 ? mode[0] : seam == 1 ? mode[1] : mode[2];
+    static_assert(CX % 8 == 0 && CY % 8 == 0 && F_YLO % 8 == 0 && F_XLO % 8 == 0 && F_ZHI % 8 == 0 &&
+                  F_YHI % 8 == 0 && F_XHI % 8 == 0, "16-B aligned face rows");
+    u64 A = 0, B0 = 0;
+    if (md) {
+        const uint4* pa = reinterpret_cast<const uint4*>(FA + (r >> 1) * stride);
+        const uint4* pb = reinterpret_cast<const uint4*>(FB + (r >> 1) * stride);
+        const int sh = FK_BITS + 2 * (r & 1);
+#pragma unroll
+        for (int q = 0; q < CX / 8; ++q) {
+            if (q < stride / 8) {
+                A |= (u64)pack8(pa[q], sh) << (16 * q);
+                B0 |= (u64)pack8(pb[q], sh) << (16 * q);
+            }
+        }
+    }
     const u64 Bm_ = __shfl(B0, lane > 0 ? lane - 1 : 0, 64), Bp_ = __shfl(B0, lane + 1 < 64 ? lane + 1 : 63, 64);
     const u64 Bm = r > 0 ? Bm_ : 0ull, Bp = r + 1 < nr ? Bp_ : 0ull;
     if (!md || !A) return;
@@ -1385,7 +1363,7 @@ template <int STOP = 0>
 __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* __restrict__ FACES, u64* PAIRS, u32* PC,
                                                          u8* big, u64* IPAIRS, u32* IPC, u8* iovf,
                                                          int64_t t_begin, int64_t t_end) {
-    __shared__ face_t Sall[SP_WAVES][FACE_STRIDE];
+    __shared__ alignas(16) face_t Sall[SP_WAVES][FACE_STRIDE];
     __shared__ u32 Hall[SP_WAVES][SEAM_HASH];
     __shared__ face_t Eall[SP_WAVES][EDGE_N];
     __shared__ u32 cnt[SP_WAVES][2];
