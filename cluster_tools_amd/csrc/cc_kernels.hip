@@ -1541,14 +1541,27 @@ __device__ __forceinline__ void lunion_key(lds_u32* par, const u64* key, u32 a, 
     }
 }
 
+// largest lt in [0, n) with off[lt] <= i (off: exclusive scan in LDS, off[n] > i): the tile that
+// holds flat element i (empty tiles share their offset with the next one and are skipped)
+__device__ __forceinline__ int flat_tile(const u32* off, int n, u32 i) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// The block's tiles are visited as flat index ranges (nodes, pairs) so that every global load of
+// a phase is in flight at once; the per-tile loops this replaces waited on one tile at a time.
 __global__ __launch_bounds__(SB_THREADS) void k_block_uf(Geom g, const u32* __restrict__ COUNT,
                                                          const u64* __restrict__ PAIRS, const u32* __restrict__ PC,
                                                          u32* P, const u64* __restrict__ KEY, u8* big) {
-    __shared__ u32 noff[SB_MAXT + 1];
+    __shared__ u32 noff[SB_MAXT + 1];      // nodes of the block's tiles, exclusive scan
+    __shared__ u32 poff[SB_MAXT + 1];      // intra pairs of the block's tiles, exclusive scan
     __shared__ u32 lpar[SB_LCAP];
     __shared__ u64 lkey[SB_LCAP];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr int NW = SB_THREADS / 64;
     const int64_t b = blockIdx.x;
     if (big[b]) return;
     const int bx = (int)(b % g.nb[2]), by = (int)((b / g.nb[2]) % g.nb[1]), bz = (int)(b / ((int64_t)g.nb[2] * g.nb[1]));
@@ -1563,62 +1576,54 @@ __global__ __launch_bounds__(SB_THREADS) void k_block_uf(Geom g, const u32* __re
         const int lx = lt % nx, ly = (lt / nx) % ny, lz = lt / (nx * ny);
         return ((int64_t)(iz0 + lz) * g.nt[1] + (iy0 + ly)) * g.nt[2] + (ix0 + lx);
     };
-    if (wave == 0) {                       // exclusive scan of the tiles' component counts
+    for (int lt = tid; lt < ntb; lt += SB_THREADS) {
+        const int64_t t = tile_of(lt);
+        noff[lt] = COUNT[t];
+        poff[lt] = PC[t];
+    }
+    __syncthreads();
+    if (wave < 2) {                        // wave 0 scans the node counts, wave 1 the pair counts
+        u32* arr = wave == 0 ? noff : poff;
         u32 run = 0;
         for (int c0 = 0; c0 < ntb; c0 += 64) {
             const int lt = c0 + lane;
-            const u32 v = lt < ntb ? COUNT[tile_of(lt)] : 0;
+            const u32 v = lt < ntb ? arr[lt] : 0;
             u32 x = v;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
                 const u32 y = __shfl_up(x, o, 64);
                 if (lane >= o) x += y;
             }
-            if (lt < ntb) noff[lt] = run + x - v;
+            if (lt < ntb) arr[lt] = run + x - v;
             run += __shfl(x, 63, 64);
         }
-        if (lane == 0) noff[ntb] = run;
+        if (lane == 0) arr[ntb] = run;
     }
     __syncthreads();
-    const u32 N = noff[ntb];
+    const u32 N = noff[ntb], M = poff[ntb];
     if (N > SB_LCAP) {
         if (tid == 0) big[b] = 1;
         return;
     }
-    for (int lt = wave; lt < ntb; lt += NW) {
-        const int64_t t = tile_of(lt);
-        const u32 o = noff[lt], n = noff[lt + 1] - o;
-        for (u32 k = lane; k < n; k += 64) {
-            lpar[o + k] = o + k;
-            lkey[o + k] = KEY[(u64)t * g.cap + k];
-        }
+    for (u32 i = tid; i < N; i += SB_THREADS) {
+        const int lt = flat_tile(noff, ntb, i);
+        lpar[i] = i;
+        lkey[i] = KEY[(u64)tile_of(lt) * g.cap + (i - noff[lt])];
     }
     __syncthreads();
     lds_u32* par = as_lds(lpar);
-    for (int lt = wave; lt < ntb; lt += NW) {
-        const int64_t t = tile_of(lt);
-        const u32 n = PC[t];
-        const u64* pl = PAIRS + t * TPC;
-        for (u32 i = lane; i < n; i += 64) {
-            const u64 pr = pl[i];
-            const u32 a = (u32)(pr >> 32), c = (u32)pr;
-            lunion_key(par, lkey, noff[a >> 12] + (a & 0xFFFu), noff[c >> 12] + (c & 0xFFFu));
-        }
+    for (u32 i = tid; i < M; i += SB_THREADS) {
+        const int lt = flat_tile(poff, ntb, i);
+        const u64 pr = PAIRS[tile_of(lt) * TPC + (i - poff[lt])];
+        const u32 a = (u32)(pr >> 32), c = (u32)pr;
+        lunion_key(par, lkey, noff[a >> 12] + (a & 0xFFFu), noff[c >> 12] + (c & 0xFFFu));
     }
     __syncthreads();
-    for (int lt = wave; lt < ntb; lt += NW) {
-        const int64_t t = tile_of(lt);
-        const u32 o = noff[lt], n = noff[lt + 1] - o;
-        for (u32 k = lane; k < n; k += 64) {
-            const u32 r = lfind_k(par, o + k);
-            if (r != o + k) {
-                int lo = 0, hi = ntb - 1;            // tile of local node r
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (noff[mid] <= r) lo = mid; else hi = mid - 1;
-                }
-                P[(u64)t * g.cap + k] = (u32)((u64)tile_of(lo) * g.cap + (r - noff[lo]));
-            }
+    for (u32 i = tid; i < N; i += SB_THREADS) {
+        const u32 r = lfind_k(par, i);
+        if (r != i) {
+            const int lt = flat_tile(noff, ntb, i), lo = flat_tile(noff, ntb, r);
+            P[(u64)tile_of(lt) * g.cap + (i - noff[lt])] = (u32)((u64)tile_of(lo) * g.cap + (r - noff[lo]));
         }
     }
 }
