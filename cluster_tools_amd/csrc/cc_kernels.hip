@@ -222,6 +222,9 @@ __device__ __forceinline__ u32 cube_k(const TileCCL& T, int c) { return cube_k(T
 // x extent re-load the last column (duplicates: harmless to min / max; the bit rows are masked
 // by the caller) and rows past the extent are skipped (f is not called for them).
 constexpr int RZ = 4;                       // planes per round
+#ifndef CC_MASK_RZ
+#define CC_MASK_RZ 2
+#endif
 constexpr int NWAVE = NTHREADS / 64;
 constexpr int RY = TY / NWAVE;              // rows per plane and wave
 static_assert(TZ * RY == 64, "one wave slot per row: a wave owns 64 rows of a tile");
@@ -232,24 +235,26 @@ template <bool HAS_MASK, class F>
 __device__ __forceinline__ void for_tile_rows(const Geom& g, const TileInfo& ti, const float* __restrict__ in,
                                               const u8* __restrict__ mask, F&& f) {
     const int lane = cc_tid() & 63, wave = wave_id();
+    // planes per round: RZ, or 2 with a mask (its bytes in flight too; RZ = 4 spilled)
+    constexpr int RZ_ = HAS_MASK ? CC_MASK_RZ : RZ;
     const int64_t sz = g.Y * g.X, sy = NWAVE * g.X;
     const int64_t o0 = ((int64_t)ti.z0 * g.Y + ti.y0 + wave) * g.X + ti.x0;
     if (ti.lz == TZ && ti.ly == TY && ti.lx == TX) {
         const float* pz = in + o0;
         const u8* mz = HAS_MASK ? mask + o0 : nullptr;
 #pragma unroll
-        for (int z0 = 0; z0 < TZ; z0 += RZ, pz += RZ * sz) {
-            float v[RZ][RY];
-            u8 mk[RZ][RY];
+        for (int z0 = 0; z0 < TZ; z0 += RZ_, pz += RZ_ * sz) {
+            float v[RZ_][RY];
+            u8 mk[RZ_][RY];
 #pragma unroll
-            for (int a = 0; a < RZ; ++a)
+            for (int a = 0; a < RZ_; ++a)
 #pragma unroll
                 for (int b = 0; b < RY; ++b) {
                     v[a][b] = pz[a * sz + b * sy + lane];
                     if (HAS_MASK) mk[a][b] = mz[(z0 + a) * sz + b * sy + lane];
                 }
 #pragma unroll
-            for (int a = 0; a < RZ; ++a)
+            for (int a = 0; a < RZ_; ++a)
 #pragma unroll
                 for (int b = 0; b < RY; ++b) f((z0 + a) * RY + b, v[a][b], HAS_MASK ? (u32)mk[a][b] : 1u);
         }
@@ -257,12 +262,12 @@ __device__ __forceinline__ void for_tile_rows(const Geom& g, const TileInfo& ti,
     }
     const int lx = lane < ti.lx ? lane : ti.lx - 1;
 #pragma unroll
-    for (int z0 = 0; z0 < TZ; z0 += RZ) {
+    for (int z0 = 0; z0 < TZ; z0 += RZ_) {
         if (z0 >= ti.lz) break;
-        float v[RZ][RY];
-        u8 mk[RZ][RY];
+        float v[RZ_][RY];
+        u8 mk[RZ_][RY];
 #pragma unroll
-        for (int a = 0; a < RZ; ++a)
+        for (int a = 0; a < RZ_; ++a)
 #pragma unroll
             for (int b = 0; b < RY; ++b) {
                 const int lz = z0 + a, ly = wave + NWAVE * b;
@@ -275,7 +280,7 @@ __device__ __forceinline__ void for_tile_rows(const Geom& g, const TileInfo& ti,
                 }
             }
 #pragma unroll
-        for (int a = 0; a < RZ; ++a)
+        for (int a = 0; a < RZ_; ++a)
 #pragma unroll
             for (int b = 0; b < RY; ++b) {
                 const int lz = z0 + a, ly = wave + NWAVE * b;
