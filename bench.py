@@ -79,11 +79,18 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
     assert world == args.gpus, 'launch N > 1 with torch.distributed.run (WORLD_SIZE must equal --gpus)'
-    torch.cuda.set_device(local_rank)
-    dev = torch.device('cuda', local_rank)
+    # CC_DIST_BACKEND=gloo: rehearsal of the N > 1 schedule with several ranks on one GPU (RCCL
+    # refuses two ranks on one device); collectives staged through host memory
+    backend = os.environ.get('CC_DIST_BACKEND', 'nccl')
+    gpu = local_rank if backend == 'nccl' else local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    dev = torch.device('cuda', gpu)
     if world > 1:
         os.environ.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
-        dist.init_process_group('nccl', device_id=dev)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     block_shape = tuple(int(v) for v in args.block_shape.split(','))
     if args.shape:
@@ -96,7 +103,7 @@ def main():
     workload = ('C3%s (1024,2048,2048) f32, 1 GPU' % (' + uint8 mask (C4 at N=1)' if args.mask else '') if world == 1 and not args.shape else
                 'C5-style z-slabs (256N,4096,4096) f32' if not args.shape else 'custom %s' % (gshape,))
 
-    ctx = _lib.Context(local_rank)
+    ctx = _lib.Context(gpu)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     z0 = slab[0] * rank
     x = ctx.generate_boundary_map(slab, origin=(z0, 0, 0), device=dev)
@@ -111,8 +118,9 @@ def main():
         def step():
             return ctx.label_volume(x, block_shape, args.threshold, args.mode, mask=mask, out=out)[1]
     else:
-        from cluster_tools_amd.distributed import ShardedLabeler
-        lab = ShardedLabeler(ctx, gshape, block_shape, z0, slab[0], dev)
+        from cluster_tools_amd.distributed import ShardedLabeler, StagedComm
+        comm = StagedComm(device=dev) if backend != 'nccl' else None
+        lab = ShardedLabeler(ctx, gshape, block_shape, z0, slab[0], dev, comm=comm)
 
         def step():
             return lab.label(x, args.threshold, args.mode, mask=mask, out=out)
@@ -143,7 +151,7 @@ def main():
     breakdown = ctx.profile()
     ctx.set_profiling(False)
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=dev if backend == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 

@@ -65,6 +65,46 @@ class TorchComm:
         return out, self.world * mx
 
 
+class StagedComm(TorchComm):
+    """TorchComm over a CPU-only backend ('gloo') for GPU tensors: each collective stages its
+    operands through host memory.  Only for rehearsing the multi-process schedule where RCCL
+    cannot run (several ranks sharing one GPU); the production path is TorchComm over 'nccl'."""
+
+    def allgather_int(self, v):
+        import torch
+        t = torch.tensor([int(v)], dtype=torch.int64)
+        out = torch.empty(self.world, dtype=torch.int64)
+        self.dist.all_gather_into_tensor(out, t, group=self.group)
+        return [int(a) for a in out.tolist()]
+
+    def shift_up(self, send, recv):
+        ops = []
+        hsend = send.cpu() if send is not None and self.rank + 1 < self.world else None
+        hrecv = recv.cpu() if recv is not None and self.rank > 0 else None
+        if hsend is not None:
+            ops.append(self.dist.P2POp(self.dist.isend, hsend, self.rank + 1, group=self.group))
+        if hrecv is not None:
+            ops.append(self.dist.P2POp(self.dist.irecv, hrecv, self.rank - 1, group=self.group))
+        if ops:
+            for r in self.dist.batch_isend_irecv(ops):
+                r.wait()
+        if hrecv is not None:
+            recv.copy_(hrecv)
+
+    def allgather_pairs(self, pairs, n):
+        import torch
+        counts = self.allgather_int(n)
+        mx = max(counts)
+        if mx == 0:
+            return None, 0
+        buf = torch.zeros((mx, 2), dtype=torch.int64)
+        if n:
+            buf[:n] = pairs[:n].cpu()
+        out = torch.empty((self.world * mx, 2), dtype=torch.int64)
+        self.dist.all_gather_into_tensor(out, buf, group=self.group)
+        return out.to(self.device), self.world * mx
+
+
 def check_slabs(global_shape, block_shape, z0, zs):
     Z = global_shape[0]
     if z0 % block_shape[0]:

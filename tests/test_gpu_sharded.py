@@ -32,3 +32,30 @@ def test_sharded_single_gpu_vs_oracle(n_slabs, shape, block_shape, mode):
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.parametrize('mode', ['greater', 'less'])
+def test_two_ranks_one_gpu_gloo(tmp_path, mode):
+    """The multi-process schedule (ShardedLabeler, one process per rank) with the real device
+    work: two ranks share cuda:0, collectives over gloo staged through host memory (RCCL refuses
+    two ranks on one device; the RCCL path differs only in TorchComm)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    shape, block_shape = (64, 150, 200), (16, 64, 64)
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+           '--master-addr', '127.0.0.1', '--master-port', str(port),
+           os.path.join(root, 'tests', '_sharded_worker.py'), str(tmp_path), mode,
+           ','.join(map(str, shape)), ','.join(map(str, block_shape))]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    got = np.concatenate([np.load(str(tmp_path / ('slab_%d.npy' % k))) for k in range(2)]).astype(np.uint64)
+    ref = O.label_volume(O.boundary_map(shape, n_threads=1), block_shape, 0.5, mode)
+    np.testing.assert_array_equal(got, ref['labels'])
+    for k in range(2):
+        assert int(np.load(str(tmp_path / ('nl_%d.npy' % k)))[0]) == ref['n_labels']
