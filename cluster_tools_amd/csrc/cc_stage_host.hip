@@ -176,37 +176,80 @@ int cc_shard_planes(cc_ctx* c, uint64_t* bottom, uint64_t* top) {
     })
 }
 
+}  // extern "C"
+
+template <class UT>
+static int64_t seam_pairs_impl(cc_ctx* c, const UT* upper, uint64_t ubase, const uint64_t* lower, int64_t n,
+                               uint64_t* pairs, int64_t cap) {
+    CC_REQUIRE(c && upper && lower && n >= 0, "bad arguments");
+    HIP_OK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const int64_t capn = std::max<int64_t>(1, n);
+    c->pairs.ensure(2 * capn * sizeof(u64));
+    c->pairs2.ensure(2 * capn * sizeof(u64));
+    c->counter.ensure(sizeof(unsigned long long));
+    u64* pa = c->pairs.as<u64>();
+    u64* pb = pa + capn;
+    u64* qa = c->pairs2.as<u64>();
+    u64* qb = qa + capn;
+    unsigned long long* cnt = (unsigned long long*)c->counter.p;
+    HIP_OK(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), s));
+    // plane width for the 'pair above' filter (any value is correct; the slab's X is exact)
+    const int64_t X = (c->run && state(c).hg.g.Y * state(c).hg.g.X == n) ? state(c).hg.g.X : n;
+    launch(c, "k_seam_pairs", [&] {
+        k_seam_pairs<UT><<<grid1d(n, SEAM_PAIR_THREADS), SEAM_PAIR_THREADS, 0, s>>>(n, X, upper, (u64)ubase, lower, pa,
+                                                                                  pb, cnt, (u64)capn);
+    });
+    unsigned long long n_raw = 0;
+    HIP_OK(hipMemcpyAsync(&n_raw, cnt, sizeof(n_raw), hipMemcpyDeviceToHost, s));
+    sync(c);
+    int64_t nu = 0;
+    launch(c, "seam_dedup", [&] { nu = dedup_pairs(c, pa, pb, qa, qb, (int64_t)n_raw); });
+    if (pairs && cap > 0 && nu > 0) {
+        const int64_t m = std::min<int64_t>(cap, nu);
+        launch(c, "k_interleave", [&] { k_interleave<<<grid1d(m), 256, 0, s>>>(m, qa, qb, pairs); });
+        sync(c);
+    }
+    return nu;
+}
+
+extern "C" {
+
 int64_t cc_seam_pairs(cc_ctx* c, const uint64_t* upper, const uint64_t* lower, int64_t n, uint64_t* pairs,
                       int64_t cap) {
     try {
-        CC_REQUIRE(c && upper && lower && n >= 0, "bad arguments");
-        HIP_OK(hipSetDevice(c->device));
-        hipStream_t s = c->stream;
-        const int64_t capn = std::max<int64_t>(1, n);
-        c->pairs.ensure(2 * capn * sizeof(u64));
-        c->pairs2.ensure(2 * capn * sizeof(u64));
-        c->counter.ensure(sizeof(unsigned long long));
-        u64* pa = c->pairs.as<u64>();
-        u64* pb = pa + capn;
-        u64* qa = c->pairs2.as<u64>();
-        u64* qb = qa + capn;
-        unsigned long long* cnt = (unsigned long long*)c->counter.p;
-        HIP_OK(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), s));
-        launch(c, "k_seam_pairs", [&] { k_seam_pairs<<<grid1d(n), 256, 0, s>>>(n, upper, lower, pa, pb, cnt, (u64)capn); });
-        unsigned long long n_raw = 0;
-        HIP_OK(hipMemcpyAsync(&n_raw, cnt, sizeof(n_raw), hipMemcpyDeviceToHost, s));
-        sync(c);
-        const int64_t nu = dedup_pairs(c, pa, pb, qa, qb, (int64_t)n_raw);
-        if (pairs && cap > 0 && nu > 0) {
-            const int64_t m = std::min<int64_t>(cap, nu);
-            launch(c, "k_interleave", [&] { k_interleave<<<grid1d(m), 256, 0, s>>>(m, qa, qb, pairs); });
-            sync(c);
-        }
-        return nu;
+        return seam_pairs_impl<u64>(c, upper, 0, lower, n, pairs, cap);
     } catch (const CCError& e) {
         g_err = e.msg;
         return -1;
     }
+}
+
+int64_t cc_seam_pairs32(cc_ctx* c, const uint32_t* upper32, uint64_t upper_base, const uint64_t* lower, int64_t n,
+                        uint64_t* pairs, int64_t cap) {
+    try {
+        return seam_pairs_impl<u32>(c, upper32, upper_base, lower, n, pairs, cap);
+    } catch (const CCError& e) {
+        g_err = e.msg;
+        return -1;
+    }
+}
+
+int cc_shard_top_plane32(cc_ctx* c, uint32_t* top32) {
+    CC_TRY({
+        CC_REQUIRE(c && top32, "NULL argument");
+        HIP_OK(hipSetDevice(c->device));
+        RunState& st = state(c);
+        CC_REQUIRE(st.stage == 2, "phase order: call cc_shard_assign first");
+        CC_REQUIRE(st.sum_v < 0xFFFFFFFEull, "slab id range does not fit the 32-bit plane form");
+        Geom& g = st.hg.g;
+        hipStream_t s = c->stream;
+        const unsigned nlayer = (unsigned)((int64_t)g.nt[1] * g.nt[2]);
+        launch(c, "k_plane_labels", [&] {
+            k_plane_labels<true, u32><<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(),
+                                                                 c->KR.as<u64>(), top32, (u64)st.base);
+        });
+    })
 }
 
 int cc_shard_finish(cc_ctx* c, const uint64_t* pairs, int64_t n_pairs, uint64_t* labels, cc_result* res) {

@@ -8,9 +8,10 @@ what crosses GPUs is O(planes), never O(volume):
   2. allgather(sum of values)   RCCL, 8 B per rank -> id base of each slab
                                 (replaces the file-based merge_offsets.py:83-131)
   3. cc_shard_assign            global ids; 6-connected unions across the slab's block faces
-  4. cc_shard_planes            bottom / top voxel planes as component ids (Y*X uint64)
+  4. cc_shard_planes            bottom voxel plane as component ids (Y*X uint64);
+     cc_shard_top_plane32       top plane as uint32 id - id_base + 1 (half the wire bytes)
   5. send top plane r -> r+1    RCCL point-to-point over one xGMI link
-  6. cc_seam_pairs on r+1       unique (id above, id below) pairs of the seam
+  6. cc_seam_pairs32 on r+1     unique (id above, id below) pairs of the seam
   7. allgather(pairs)           RCCL, padded to the largest count (RCCL has no allgatherv)
   8. cc_shard_finish            replicated union-find over all seam pairs (identical on every
                                 rank), LUT, final labels of the slab
@@ -138,8 +139,9 @@ class ShardedLabeler:
         Y, X = global_shape[1], global_shape[2]
         r, w = self.comm.rank, self.comm.world
         self.bottom = torch.empty((Y, X), dtype=torch.int64, device=device) if r > 0 else None
-        self.upper = torch.empty((Y, X), dtype=torch.int64, device=device) if r > 0 else None
-        self.top = torch.empty((Y, X), dtype=torch.int64, device=device) if r + 1 < w else None
+        # the plane crossing xGMI travels as uint32 (id - id_base + 1): half the bytes of the ids
+        self.upper = torch.empty((Y, X), dtype=torch.int32, device=device) if r > 0 else None
+        self.top = torch.empty((Y, X), dtype=torch.int32, device=device) if r + 1 < w else None
         self.pairs = torch.empty((Y * X, 2), dtype=torch.int64, device=device) if r > 0 else None
         self.sums = None
 
@@ -151,10 +153,15 @@ class ShardedLabeler:
         s = ctx.shard_begin(x, self.block_shape, threshold, mode, self.z0, mask)
         self.sums = comm.allgather_int(s)
         base = sum(self.sums[:comm.rank])
+        if max(self.sums) >= 2 ** 32 - 2:
+            raise RuntimeError('a slab holds more than 2^32 - 3 ids: the 32-bit seam plane cannot carry them')
         ctx.shard_assign(base)
-        ctx.shard_planes(self.bottom, self.top)
+        ctx.shard_planes(self.bottom, None)
+        if self.top is not None:
+            ctx.shard_top_plane32(self.top)
         comm.shift_up(self.top, self.upper)
-        n = ctx.seam_pairs(self.upper, self.bottom, self.pairs) if comm.rank > 0 else 0
+        n = (ctx.seam_pairs32(self.upper, sum(self.sums[:comm.rank - 1]), self.bottom, self.pairs)
+             if comm.rank > 0 else 0)
         allp, np_ = comm.allgather_pairs(self.pairs, n)
         res = ctx.shard_finish(allp, np_, out)
         res['n_labels'] = sum(self.sums) + 1

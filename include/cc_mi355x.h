@@ -152,6 +152,12 @@ int64_t cc_seam_pairs(cc_ctx* ctx, const uint64_t* upper_dev, const uint64_t* lo
                       uint64_t* pairs_dev, int64_t cap);
 int cc_shard_finish(cc_ctx* ctx, const uint64_t* pairs_dev, int64_t n_pairs, uint64_t* labels_dev,
                     cc_result* res);
+/* The top plane in the compact form sent over xGMI (half the bytes of cc_shard_planes' top):
+ * uint32 id - id_base + 1, 0 = background (requires the slab's sum of block values < 2^32 - 2),
+ * and cc_seam_pairs on it, given the sending slab's id_base. */
+int cc_shard_top_plane32(cc_ctx* ctx, uint32_t* top32_dev);
+int64_t cc_seam_pairs32(cc_ctx* ctx, const uint32_t* upper32_dev, uint64_t upper_id_base,
+                        const uint64_t* lower_dev, int64_t n, uint64_t* pairs_dev, int64_t cap);
 
 /* --- synthetic benchmark input (oracle/synth.py is its restatement) --- */
 int cc_generate_boundary_map(cc_ctx* ctx, float* out_dev, const int64_t shape[3],

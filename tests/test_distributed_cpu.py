@@ -24,7 +24,16 @@ class FakeShardCtx:
         return r['n_labels'] - 1
 
     def shard_assign(self, base):
+        self.base = base
         self.lab[self.lab != 0] += base
+
+    def shard_top_plane32(self, top32):
+        t = self.lab[-1]
+        top32.copy_(torch.from_numpy(np.where(t != 0, t - self.base + 1, 0).astype(np.int32)))
+
+    def seam_pairs32(self, upper32, upper_base, lower, pairs):
+        u = upper32.numpy().astype(np.int64)
+        return self.seam_pairs(torch.from_numpy(np.where(u != 0, u - 1 + upper_base, 0)), lower, pairs)
 
     def shard_planes(self, bottom=None, top=None):
         if bottom is not None:
