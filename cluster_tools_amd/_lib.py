@@ -23,7 +23,7 @@ EXPORTS = (
     'cc_merge_assignments', 'cc_write', 'cc_generate_boundary_map', 'cc_set_profiling',
     'cc_get_profile', 'cc_reset_profile', 'cc_shard_begin', 'cc_shard_assign', 'cc_shard_planes',
     'cc_seam_pairs', 'cc_shard_finish', 'cc_set_debug', 'cc_threshold', 'cc_shard_top_plane32',
-    'cc_seam_pairs32',
+    'cc_seam_pairs32', 'cc_shard_top_cubes32', 'cc_seam_pairs_cubes32',
 )
 
 
@@ -72,6 +72,8 @@ def load():
         'cc_threshold': (I, [P, P, P, P, ctypes.c_double, I, P]),
         'cc_shard_top_plane32': (I, [P, P]),
         'cc_seam_pairs32': (i64, [P, P, u64, P, i64, P, i64]),
+        'cc_shard_top_cubes32': (I, [P, P]),
+        'cc_seam_pairs_cubes32': (i64, [P, P, u64, P, i64, i64, P, i64]),
         'cc_shard_begin': (I, [P, P, P, P, P, ctypes.c_double, I, i64, P]),
         'cc_shard_assign': (I, [P, u64]),
         'cc_shard_planes': (I, [P, P, P]),
@@ -280,6 +282,15 @@ class Context:
         cap = 0 if pairs_dev is None else pairs_dev.shape[0]
         return _check(load().cc_seam_pairs32(self._h, _ptr(upper32_dev), int(upper_id_base), _ptr(lower_dev), n,
                                              _ptr(pairs_dev), cap))
+
+    def shard_top_cubes32(self, cubes_dev):
+        _check(load().cc_shard_top_cubes32(self._h, _ptr(cubes_dev)))
+
+    def seam_pairs_cubes32(self, upper_cubes_dev, upper_id_base, lower_dev, pairs_dev=None):
+        Y, X = lower_dev.shape
+        cap = 0 if pairs_dev is None else pairs_dev.shape[0]
+        return _check(load().cc_seam_pairs_cubes32(self._h, _ptr(upper_cubes_dev), int(upper_id_base),
+                                                   _ptr(lower_dev), int(Y), int(X), _ptr(pairs_dev), cap))
 
     def shard_finish(self, pairs_dev, n_pairs, out_dev):
         res = CCResult()

@@ -1793,9 +1793,33 @@ __global__ __launch_bounds__(NTHREADS) void k_plane_labels(Geom g, const face_t*
 // sees every pair at least once but only ~ the pair regions' corners (the unfiltered plane gave
 // millions of single-counter atomics, 3.2 ms for a 4096^2 seam).  Appends are wave-aggregated.
 constexpr int SEAM_PAIR_THREADS = 1024;
-// UT = u32: the upper plane in compact form (id - ubase + 1, 0 = background)
-template <class UT>
-__global__ __launch_bounds__(SEAM_PAIR_THREADS) void k_seam_pairs(int64_t n, int64_t X, const UT* upper, u64 ubase,
+// Readers of the upper plane for k_seam_pairs: raw(i) is compared between neighbours (0 =
+// background), id(raw) is the global id.
+struct UpperIds {                  // uint64 ids (single-process schedule, stage tests)
+    const u64* p;
+    __device__ __forceinline__ u64 raw(int64_t i) const { return p[i]; }
+    __device__ __forceinline__ u64 id(u64 r) const { return r; }
+};
+struct UpperIds32 {                // uint32 id - base + 1 per voxel
+    const u32* p;
+    u64 base;
+    __device__ __forceinline__ u64 raw(int64_t i) const { return p[i]; }
+    __device__ __forceinline__ u64 id(u64 r) const { return r - 1 + base; }
+};
+struct UpperCubes32 {              // per 2x2 cube: (id - base + 1) << 4 | 4 voxel bits (y&1)*2 + (x&1)
+    const u32* p;
+    u64 base;
+    u32 X, CXg;
+    __device__ __forceinline__ u64 raw(int64_t i) const {
+        const u32 ii = (u32)i, y = ii / X, x = ii - y * X;
+        const u32 c = p[(y >> 1) * CXg + (x >> 1)];
+        return ((c >> ((y & 1) * 2 + (x & 1))) & 1u) ? (u64)(c >> 4) : 0ull;
+    }
+    __device__ __forceinline__ u64 id(u64 r) const { return r - 1 + base; }
+};
+
+template <class UP>
+__global__ __launch_bounds__(SEAM_PAIR_THREADS) void k_seam_pairs(int64_t n, int64_t X, UP upper,
                                                                   const u64* lower, u64* pa, u64* pb,
                                                                   unsigned long long* counter, u64 cap) {
     // workgroup-aggregated append: one global atomic per 1024 voxels (one per wave still
@@ -1806,12 +1830,12 @@ __global__ __launch_bounds__(SEAM_PAIR_THREADS) void k_seam_pairs(int64_t n, int
     bool emit = false;
     u64 a = 0, b = 0;
     if (i < n) {
-        const UT u = upper[i];
+        const u64 u = upper.raw(i);
         b = lower[i];
         emit = u && b;
-        if (emit && i > 0 && upper[i - 1] == u && lower[i - 1] == b) emit = false;
-        if (emit && i >= X && upper[i - X] == u && lower[i - X] == b) emit = false;
-        a = sizeof(UT) == 4 ? (u64)u - 1 + ubase : (u64)u;
+        if (emit && i > 0 && upper.raw(i - 1) == u && lower[i - 1] == b) emit = false;
+        if (emit && i >= X && upper.raw(i - X) == u && lower[i - X] == b) emit = false;
+        a = upper.id(u);
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const u64 m = __ballot(emit);
@@ -1826,6 +1850,27 @@ __global__ __launch_bounds__(SEAM_PAIR_THREADS) void k_seam_pairs(int64_t n, int
     if (emit) {
         const unsigned long long pos = gbase + wcnt[wave] + __popcll(m & ((1ull << lane) - 1));
         if (pos < cap) { pa[pos] = a; pb[pos] = b; }
+    }
+}
+
+// The top voxel plane as one u32 per 2x2 cube of the global cube grid (ceil(Y/2) x ceil(X/2);
+// needs even tile origins, i.e. even block_shape[1:]): (id - sub + 1) << 4 | the cube's 4
+// face-voxel bits, a quarter of the voxel plane's bytes.  One workgroup per top-layer tile.
+__global__ __launch_bounds__(NTHREADS) void k_top_cubes(Geom g, const face_t* __restrict__ FACES, u32* P,
+                                                        const u64* __restrict__ KR, u32* cubes, u64 sub) {
+    const int64_t t = (int64_t)(g.nt[0] - 1) * g.nt[1] * g.nt[2] + blockIdx.x;
+    const TileInfo ti = tile_info(g, t);
+    const face_t* F = FACES + t * FACE_STRIDE + F_ZHI;
+    const u32 base = (u32)(t * g.cap);
+    const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2;
+    const int64_t CXg = (g.X + 1) / 2;
+    for (int e = threadIdx.x; e < ncy * CX; e += NTHREADS) {
+        const int cy = e / CX, cx = e % CX;
+        if (cx >= ncx) continue;
+        const u32 a = F[e];
+        u32 w = 0;
+        if (a) w = ((u32)(KR[gfind(P, base + (a & FK_MASK))] - sub + 1) << 4) | (a >> FK_BITS);
+        cubes[(int64_t)(ti.y0 / 2 + cy) * CXg + ti.x0 / 2 + cx] = w;
     }
 }
 

@@ -167,6 +167,7 @@ struct RunState {
     uint64_t base = 0;         // global id base of this slab
     int64_t n_map = 0;         // seam mapping size
     bool local_only = false;
+    int64_t bs[3] = {0, 0, 0};  // block_shape
     uint64_t n_fix = 0;        // tiles relabelled by k_fix
     int stage = 0;             // 1 local done, 2 rid done, 3 final done
 };
@@ -185,6 +186,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     st.hg = make_geom(shape, block_shape, zoff);
     upload_geom(c, st.hg);
     Geom& g = st.hg.g;
+    for (int a = 0; a < 3; ++a) st.bs[a] = block_shape[a];
     st.thr = (float)threshold;                // numpy: python float -> float32
     st.mode = mode;
     st.local_only = local_only;

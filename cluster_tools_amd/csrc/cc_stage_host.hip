@@ -178,10 +178,10 @@ int cc_shard_planes(cc_ctx* c, uint64_t* bottom, uint64_t* top) {
 
 }  // extern "C"
 
-template <class UT>
-static int64_t seam_pairs_impl(cc_ctx* c, const UT* upper, uint64_t ubase, const uint64_t* lower, int64_t n,
-                               uint64_t* pairs, int64_t cap) {
-    CC_REQUIRE(c && upper && lower && n >= 0, "bad arguments");
+template <class UP>
+static int64_t seam_pairs_impl(cc_ctx* c, UP upper, const uint64_t* lower, int64_t n, uint64_t* pairs,
+                               int64_t cap) {
+    CC_REQUIRE(c && upper.p && lower && n >= 0, "bad arguments");
     HIP_OK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const int64_t capn = std::max<int64_t>(1, n);
@@ -197,8 +197,8 @@ static int64_t seam_pairs_impl(cc_ctx* c, const UT* upper, uint64_t ubase, const
     // plane width for the 'pair above' filter (any value is correct; the slab's X is exact)
     const int64_t X = (c->run && state(c).hg.g.Y * state(c).hg.g.X == n) ? state(c).hg.g.X : n;
     launch(c, "k_seam_pairs", [&] {
-        k_seam_pairs<UT><<<grid1d(n, SEAM_PAIR_THREADS), SEAM_PAIR_THREADS, 0, s>>>(n, X, upper, (u64)ubase, lower, pa,
-                                                                                  pb, cnt, (u64)capn);
+        k_seam_pairs<UP><<<grid1d(n, SEAM_PAIR_THREADS), SEAM_PAIR_THREADS, 0, s>>>(n, X, upper, lower, pa, pb, cnt,
+                                                                                  (u64)capn);
     });
     unsigned long long n_raw = 0;
     HIP_OK(hipMemcpyAsync(&n_raw, cnt, sizeof(n_raw), hipMemcpyDeviceToHost, s));
@@ -218,7 +218,7 @@ extern "C" {
 int64_t cc_seam_pairs(cc_ctx* c, const uint64_t* upper, const uint64_t* lower, int64_t n, uint64_t* pairs,
                       int64_t cap) {
     try {
-        return seam_pairs_impl<u64>(c, upper, 0, lower, n, pairs, cap);
+        return seam_pairs_impl(c, UpperIds{upper}, lower, n, pairs, cap);
     } catch (const CCError& e) {
         g_err = e.msg;
         return -1;
@@ -228,11 +228,42 @@ int64_t cc_seam_pairs(cc_ctx* c, const uint64_t* upper, const uint64_t* lower, i
 int64_t cc_seam_pairs32(cc_ctx* c, const uint32_t* upper32, uint64_t upper_base, const uint64_t* lower, int64_t n,
                         uint64_t* pairs, int64_t cap) {
     try {
-        return seam_pairs_impl<u32>(c, upper32, upper_base, lower, n, pairs, cap);
+        return seam_pairs_impl(c, UpperIds32{upper32, upper_base}, lower, n, pairs, cap);
     } catch (const CCError& e) {
         g_err = e.msg;
         return -1;
     }
+}
+
+int64_t cc_seam_pairs_cubes32(cc_ctx* c, const uint32_t* upper_cubes, uint64_t upper_base, const uint64_t* lower,
+                              int64_t Y, int64_t X, uint64_t* pairs, int64_t cap) {
+    try {
+        CC_REQUIRE(Y >= 1 && X >= 1 && Y * X < (1LL << 32), "bad plane shape");
+        UpperCubes32 up{upper_cubes, upper_base, (u32)X, (u32)((X + 1) / 2)};
+        return seam_pairs_impl(c, up, lower, Y * X, pairs, cap);
+    } catch (const CCError& e) {
+        g_err = e.msg;
+        return -1;
+    }
+}
+
+int cc_shard_top_cubes32(cc_ctx* c, uint32_t* cubes) {
+    CC_TRY({
+        CC_REQUIRE(c && cubes, "NULL argument");
+        HIP_OK(hipSetDevice(c->device));
+        RunState& st = state(c);
+        CC_REQUIRE(st.stage == 2, "phase order: call cc_shard_assign first");
+        CC_REQUIRE(st.sum_v < (1ull << 28) - 2, "slab id range does not fit the 28-bit cube form");
+        Geom& g = st.hg.g;
+        for (int a = 1; a < 3; ++a)   // tile origins = block origins + multiples of TY / TX
+            CC_REQUIRE(g.nb[a] == 1 || st.bs[a] % 2 == 0, "cube form needs even tile origins (even block_shape[1:])");
+        hipStream_t s = c->stream;
+        const unsigned nlayer = (unsigned)((int64_t)g.nt[1] * g.nt[2]);
+        launch(c, "k_top_cubes", [&] {
+            k_top_cubes<<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), cubes,
+                                                     (u64)st.base);
+        });
+    })
 }
 
 int cc_shard_top_plane32(cc_ctx* c, uint32_t* top32) {

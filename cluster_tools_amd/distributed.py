@@ -9,9 +9,10 @@ what crosses GPUs is O(planes), never O(volume):
                                 (replaces the file-based merge_offsets.py:83-131)
   3. cc_shard_assign            global ids; 6-connected unions across the slab's block faces
   4. cc_shard_planes            bottom voxel plane as component ids (Y*X uint64);
-     cc_shard_top_plane32       top plane as uint32 id - id_base + 1 (half the wire bytes)
+     cc_shard_top_cubes32       top plane as one uint32 per 2x2 cube (1/4 of the voxel plane's
+                                bytes; cc_shard_top_plane32: one uint32 per voxel, odd blocks)
   5. send top plane r -> r+1    RCCL point-to-point over one xGMI link
-  6. cc_seam_pairs32 on r+1     unique (id above, id below) pairs of the seam
+  6. cc_seam_pairs_cubes32      on r+1: unique (id above, id below) pairs of the seam
   7. allgather(pairs)           RCCL, padded to the largest count (RCCL has no allgatherv)
   8. cc_shard_finish            replicated union-find over all seam pairs (identical on every
                                 rank), LUT, final labels of the slab
@@ -139,9 +140,14 @@ class ShardedLabeler:
         Y, X = global_shape[1], global_shape[2]
         r, w = self.comm.rank, self.comm.world
         self.bottom = torch.empty((Y, X), dtype=torch.int64, device=device) if r > 0 else None
-        # the plane crossing xGMI travels as uint32 (id - id_base + 1): half the bytes of the ids
-        self.upper = torch.empty((Y, X), dtype=torch.int32, device=device) if r > 0 else None
-        self.top = torch.empty((Y, X), dtype=torch.int32, device=device) if r + 1 < w else None
+        # the plane crossing xGMI: one uint32 per 2x2 cube ((id - id_base + 1) << 4 | voxel bits,
+        # 1/4 of the voxel plane's bytes) when the tile origins are even, else one uint32 per
+        # voxel (id - id_base + 1, half the bytes of the uint64 ids)
+        nby, nbx = -(-Y // block_shape[1]), -(-X // block_shape[2])
+        self.cubes = ((nby == 1 or block_shape[1] % 2 == 0) and (nbx == 1 or block_shape[2] % 2 == 0))
+        pshape = ((Y + 1) // 2, (X + 1) // 2) if self.cubes else (Y, X)
+        self.upper = torch.empty(pshape, dtype=torch.int32, device=device) if r > 0 else None
+        self.top = torch.empty(pshape, dtype=torch.int32, device=device) if r + 1 < w else None
         self.pairs = torch.empty((Y * X, 2), dtype=torch.int64, device=device) if r > 0 else None
         self.sums = None
 
@@ -153,15 +159,18 @@ class ShardedLabeler:
         s = ctx.shard_begin(x, self.block_shape, threshold, mode, self.z0, mask)
         self.sums = comm.allgather_int(s)
         base = sum(self.sums[:comm.rank])
-        if max(self.sums) >= 2 ** 32 - 2:
-            raise RuntimeError('a slab holds more than 2^32 - 3 ids: the 32-bit seam plane cannot carry them')
+        if max(self.sums) >= (2 ** 28 if self.cubes else 2 ** 32) - 2:
+            raise RuntimeError('a slab holds too many ids for the 32-bit seam plane')
         ctx.shard_assign(base)
         ctx.shard_planes(self.bottom, None)
         if self.top is not None:
-            ctx.shard_top_plane32(self.top)
+            (ctx.shard_top_cubes32 if self.cubes else ctx.shard_top_plane32)(self.top)
         comm.shift_up(self.top, self.upper)
-        n = (ctx.seam_pairs32(self.upper, sum(self.sums[:comm.rank - 1]), self.bottom, self.pairs)
-             if comm.rank > 0 else 0)
+        n = 0
+        if comm.rank > 0:
+            ubase = sum(self.sums[:comm.rank - 1])
+            n = (ctx.seam_pairs_cubes32(self.upper, ubase, self.bottom, self.pairs) if self.cubes
+                 else ctx.seam_pairs32(self.upper, ubase, self.bottom, self.pairs))
         allp, np_ = comm.allgather_pairs(self.pairs, n)
         res = ctx.shard_finish(allp, np_, out)
         res['n_labels'] = sum(self.sums) + 1

@@ -158,6 +158,15 @@ int cc_shard_finish(cc_ctx* ctx, const uint64_t* pairs_dev, int64_t n_pairs, uin
 int cc_shard_top_plane32(cc_ctx* ctx, uint32_t* top32_dev);
 int64_t cc_seam_pairs32(cc_ctx* ctx, const uint32_t* upper32_dev, uint64_t upper_id_base,
                         const uint64_t* lower_dev, int64_t n, uint64_t* pairs_dev, int64_t cap);
+/* The top plane as one uint32 per 2x2 cube of the global cube grid, ceil(Y/2) x ceil(X/2):
+ * (id - id_base + 1) << 4 | the cube's 4 voxel bits ((y & 1) * 2 + (x & 1)), 0 = background; a
+ * quarter of the voxel plane's bytes.  Needs even block_shape[1:] (or one block along the axis)
+ * and the slab's sum of block values < 2^28 - 2.  cc_seam_pairs_cubes32 forms the seam pairs
+ * from it (upper) and this slab's uint64 bottom plane (lower, Y x X). */
+int cc_shard_top_cubes32(cc_ctx* ctx, uint32_t* cubes_dev);
+int64_t cc_seam_pairs_cubes32(cc_ctx* ctx, const uint32_t* upper_cubes_dev, uint64_t upper_id_base,
+                              const uint64_t* lower_dev, int64_t Y, int64_t X, uint64_t* pairs_dev,
+                              int64_t cap);
 
 /* --- synthetic benchmark input (oracle/synth.py is its restatement) --- */
 int cc_generate_boundary_map(cc_ctx* ctx, float* out_dev, const int64_t shape[3],

@@ -31,6 +31,26 @@ class FakeShardCtx:
         t = self.lab[-1]
         top32.copy_(torch.from_numpy(np.where(t != 0, t - self.base + 1, 0).astype(np.int32)))
 
+    def shard_top_cubes32(self, cubes):
+        t = self.lab[-1]
+        Y, X = t.shape
+        p = np.zeros((2 * ((Y + 1) // 2), 2 * ((X + 1) // 2)), dtype=np.int64)
+        p[:Y, :X] = t
+        q = p.reshape(p.shape[0] // 2, 2, p.shape[1] // 2, 2)
+        ids = q.max(axis=(1, 3))          # the foreground voxels of a cube share one component
+        bits = sum(((q[:, j, :, i] != 0).astype(np.int64) << (2 * j + i)) for j in range(2) for i in range(2))
+        w = np.where(ids != 0, ((ids - self.base + 1) << 4) | bits, 0)
+        cubes.copy_(torch.from_numpy(w.astype(np.int32)))
+
+    def seam_pairs_cubes32(self, cubes, upper_base, lower, pairs):
+        c = cubes.numpy().astype(np.int64)
+        Y, X = lower.shape
+        yy, xx = np.meshgrid(np.arange(Y), np.arange(X), indexing='ij')
+        e = c[yy // 2, xx // 2]
+        on = (e >> ((yy & 1) * 2 + (xx & 1))) & 1
+        up = np.where(on != 0, (e >> 4) - 1 + upper_base, 0)
+        return self.seam_pairs(torch.from_numpy(up), lower, pairs)
+
     def seam_pairs32(self, upper32, upper_base, lower, pairs):
         u = upper32.numpy().astype(np.int64)
         return self.seam_pairs(torch.from_numpy(np.where(u != 0, u - 1 + upper_base, 0)), lower, pairs)

@@ -34,8 +34,9 @@ def test_sharded_single_gpu_vs_oracle(n_slabs, shape, block_shape, mode):
             c.close()
 
 
-@pytest.mark.parametrize('mode', ['greater', 'less'])
-def test_two_ranks_one_gpu_gloo(tmp_path, mode):
+@pytest.mark.parametrize('mode,block_shape', [('greater', (16, 64, 64)), ('less', (16, 64, 64)),
+                                              ('less', (16, 45, 63))])   # odd: per-voxel u32 plane
+def test_two_ranks_one_gpu_gloo(tmp_path, mode, block_shape):
     """The multi-process schedule (ShardedLabeler, one process per rank) with the real device
     work: two ranks share cuda:0, collectives over gloo staged through host memory (RCCL refuses
     two ranks on one device; the RCCL path differs only in TorchComm)."""
@@ -43,7 +44,7 @@ def test_two_ranks_one_gpu_gloo(tmp_path, mode):
     import socket
     import subprocess
     import sys
-    shape, block_shape = (64, 150, 200), (16, 64, 64)
+    shape = (64, 150, 200)
     with socket.socket() as s:
         s.bind(('127.0.0.1', 0))
         port = s.getsockname()[1]
