@@ -24,6 +24,7 @@ EXPORTS = (
     'cc_get_profile', 'cc_reset_profile', 'cc_shard_begin', 'cc_shard_assign', 'cc_shard_planes',
     'cc_seam_pairs', 'cc_shard_finish', 'cc_set_debug', 'cc_threshold', 'cc_shard_top_plane32',
     'cc_seam_pairs32', 'cc_shard_top_cubes32', 'cc_seam_pairs_cubes32',
+    'cc_evaluate', 'cc_get_overlaps',
 )
 
 
@@ -34,6 +35,18 @@ class CCResult(ctypes.Structure):
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+class CCEvalResult(ctypes.Structure):
+    _fields_ = [('n_points', ctypes.c_uint64), ('n_pairs', ctypes.c_uint64),
+                ('n_seg_ids', ctypes.c_uint64), ('n_gt_ids', ctypes.c_uint64),
+                ('vi_split', ctypes.c_double), ('vi_merge', ctypes.c_double),
+                ('adapted_rand_error', ctypes.c_double), ('rand_index', ctypes.c_double),
+                ('sum_sq_pairs', ctypes.c_double), ('sum_sq_gt', ctypes.c_double),
+                ('sum_sq_seg', ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: (float if t is ctypes.c_double else int)(getattr(self, k)) for k, t in self._fields_}
 
 
 _lib = None
@@ -79,6 +92,8 @@ def load():
         'cc_shard_planes': (I, [P, P, P]),
         'cc_seam_pairs': (i64, [P, P, P, i64, P, i64]),
         'cc_shard_finish': (I, [P, P, i64, P, ctypes.POINTER(CCResult)]),
+        'cc_evaluate': (I, [P, P, P, P, P, I, u64, ctypes.POINTER(CCEvalResult)]),
+        'cc_get_overlaps': (i64, [P, P, P, P, i64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -190,6 +205,36 @@ class Context:
         _check(load().cc_threshold(self._h, _ptr(inp), _ptr(shape), _ptr(bs), float(threshold),
                                    mode_id(mode), _ptr(out)))
         return out
+
+    def evaluate(self, seg, gt, block_shape, ignore_label=0):
+        """EvaluationWorkflow (evaluation/evaluation_workflow.py:46-84) on device: overlaps per
+        block (block_node_labels.py:133-166) + measures (measures.py:81-162).  `seg`, `gt` are
+        uint64 (torch int64 / uint64) CUDA tensors of one shape; ignore_label None counts every
+        gt voxel.  Returns the cc_eval_result fields as a dict."""
+        import torch
+        for a in (seg, gt):
+            assert hasattr(a, 'data_ptr') and a.is_cuda and a.element_size() == 8 and a.is_contiguous()
+            assert a.dtype in (torch.int64, torch.uint64)
+        assert seg.shape == gt.shape and seg.dim() == 3
+        shape, bs = _i64(seg.shape), _i64(block_shape)
+        assert len(bs) == 3
+        res = CCEvalResult()
+        use_ignore = ignore_label is not None
+        # the ctx runs on its own stream: seg / gt may still be in flight on torch's
+        torch.cuda.current_stream(seg.device).synchronize()
+        _check(load().cc_evaluate(self._h, _ptr(seg), _ptr(gt), _ptr(shape), _ptr(bs), int(use_ignore),
+                                  int(ignore_label) if use_ignore else 0, ctypes.byref(res)))
+        return res.as_dict()
+
+    def overlaps(self):
+        """Contingency table of the last evaluate(): (seg_ids, gt_ids, counts) uint64, sorted by
+        (seg id, gt id)."""
+        L = load()
+        n = _check(L.cc_get_overlaps(self._h, None, None, None, 0))
+        a, b, c = (np.empty(n, dtype=np.uint64) for _ in range(3))
+        _check(L.cc_get_overlaps(self._h, _ptr(a), _ptr(b), _ptr(c), n))
+        o = np.lexsort((b, a))
+        return a[o], b[o], c[o]
 
     def block_values(self, n_blocks):
         a = np.empty(n_blocks, dtype=np.uint64)

@@ -55,7 +55,9 @@ struct cc_ctx {
     // workspace
     DevBuf tiles, bstat, bparam, bits, faces, count, rc, roff, P, KR, FIN, keys, keys2, vals, vals2, seg,
         values, offsets, lut, cub_tmp, scalars, scalars2, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2,
-        flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf, spec;
+        flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf, spec,
+        ev_main, ev_z, ev_seg, ev_gt, ev_flag, ev_part;   // evaluation (cc_eval.hip)
+    int64_t ev_cap = 0;      // entries per evaluation hash table of the last cc_evaluate
     // last run
     int64_t n_blocks = 0;
     uint64_t n_labels = 0;
@@ -604,7 +606,8 @@ void cc_destroy(cc_ctx* c) {
                       &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
                       &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
-                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec};
+                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec,
+                      &c->ev_main, &c->ev_z, &c->ev_seg, &c->ev_gt, &c->ev_flag, &c->ev_part};
     for (DevBuf* b : bufs) b->release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
@@ -787,3 +790,4 @@ int cc_get_profile(cc_ctx* c, char* names, int names_cap, int64_t* counts, doubl
 }  // extern "C"
 
 #include "cc_stage_host.hip"
+#include "cc_eval.hip"

@@ -187,6 +187,30 @@ int cc_reset_profile(cc_ctx* ctx);
 #define CC_DEBUG_GLOBAL_STITCH 1
 int cc_set_debug(cc_ctx* ctx, int flags);
 
+/* --- segmentation evaluation ------------------------------------------------
+ * EvaluationWorkflow (evaluation/evaluation_workflow.py:46-84): overlaps of seg with gt per block
+ * of the evaluation grid (node_labels/block_node_labels.py:133-166: a block whose seg sums to 0 is
+ * skipped; voxels with gt == ignore_label are not counted when use_ignore), then the contingency
+ * table and the measures (evaluation/measures.py:81-162; a = gt sizes, b = seg sizes).
+ * seg_dev / gt_dev: uint64 device volumes (C-order, 16-byte aligned).  Ids: seg < 2^31,
+ * gt < 2^32 - 1 (error otherwise).  vi_* in bits (log2). */
+typedef struct {
+    uint64_t n_points;            /* measures.py:113                               */
+    uint64_t n_pairs;             /* contingency-table entries (seg id, gt id)      */
+    uint64_t n_seg_ids;           /* distinct seg ids counted (b_dict)              */
+    uint64_t n_gt_ids;            /* distinct gt ids counted (a_dict)               */
+    double   vi_split;            /* H(seg | gt)                                    */
+    double   vi_merge;            /* H(gt | seg)                                    */
+    double   adapted_rand_error;  /* 1 - 2 P R / (P + R)                            */
+    double   rand_index;          /* 1 - (sum a^2 + sum b^2 - 2 sum p^2) / N^2       */
+    double   sum_sq_pairs, sum_sq_gt, sum_sq_seg;
+} cc_eval_result;
+
+int cc_evaluate(cc_ctx* ctx, const uint64_t* seg_dev, const uint64_t* gt_dev, const int64_t shape[3],
+                const int64_t block_shape[3], int use_ignore, uint64_t ignore_label, cc_eval_result* out);
+/* contingency table of the last cc_evaluate (unordered); returns its size (copies min(size, cap)) */
+int64_t cc_get_overlaps(cc_ctx* ctx, uint64_t* seg_ids, uint64_t* gt_ids, uint64_t* counts, int64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

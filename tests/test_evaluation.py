@@ -1,0 +1,146 @@
+"""Segmentation evaluation (reference EvaluationWorkflow: node_labels/block_node_labels.py:133-166
+overlaps + evaluation/measures.py:81-162 measures).  CPU: the numpy oracle on hand-computed
+cases and the block-skip / ignore-label rules.  GPU: cc_evaluate against the oracle -- the
+contingency table bit-exact, the measures to 1e-9 -- on ragged shapes and block grids, table
+growth, and the partition-equality property at volume scale.
+
+The measure formulas restate elf (absent here): parity of those formulas is unpinned, see
+oracle/evaluation.py."""
+import numpy as np
+import pytest
+
+from oracle import evaluation as E
+
+RTOL = 1e-9
+
+
+def _vol(a):
+    return np.asarray(a, dtype=np.uint64).reshape(1, 1, -1)
+
+
+def test_oracle_hand_case():
+    seg, gt = _vol([1, 1, 2, 2]), _vol([1, 1, 1, 1])
+    m, ov = E.measures(seg, gt, (1, 1, 4), ignore_label=None)
+    assert ov == {(1, 1): 2, (2, 1): 2}
+    assert m['n_points'] == 4 and m['n_pairs'] == 2
+    assert m['vi_split'] == pytest.approx(1.0) and m['vi_merge'] == pytest.approx(0.0, abs=1e-15)
+    assert m['adapted_rand_error'] == pytest.approx(1.0 / 3.0)
+    assert m['rand_index'] == pytest.approx(0.5)
+
+
+def test_oracle_identical_partitions():
+    rng = np.random.default_rng(3)
+    seg = rng.integers(1, 20, size=(6, 7, 9)).astype(np.uint64)
+    perm = rng.permutation(np.arange(100, 120, dtype=np.uint64))
+    gt = perm[seg.astype(np.int64) - 1]
+    m, _ = E.measures(seg, gt, (4, 4, 4), ignore_label=None)
+    assert abs(m['vi_split']) < 1e-12 and abs(m['vi_merge']) < 1e-12
+    assert m['rand_index'] == pytest.approx(1.0) and abs(m['adapted_rand_error']) < 1e-12
+
+
+def test_oracle_block_skip_and_ignore():
+    # block 0 (x 0..1): seg all zero -> skipped (block_node_labels.py:141); block 1 keeps its
+    # seg-0 voxel; gt == 0 voxels are ignored
+    seg, gt = _vol([0, 0, 0, 5]), _vol([3, 4, 7, 0])
+    _, ov = E.measures(seg, gt, (1, 1, 2), ignore_label=0)
+    assert ov == {(0, 7): 1}
+    _, ov = E.measures(seg, gt, (1, 1, 2), ignore_label=None)
+    assert ov == {(0, 7): 1, (5, 0): 1}
+    _, ov = E.measures(seg, gt, (1, 1, 4), ignore_label=0)
+    assert ov == {(0, 3): 1, (0, 4): 1, (0, 7): 1}
+
+
+def _random_case(rng, shape, n_seg, n_gt, zero_frac, ignore_frac):
+    seg = rng.integers(1, n_seg + 1, size=shape).astype(np.uint64)
+    seg[rng.random(shape) < zero_frac] = 0
+    # whole zero slabs so that some blocks hold no seg at all
+    seg[: max(1, shape[0] // 3)] = 0
+    seg[:, :, : shape[2] // 2][rng.random(seg[:, :, : shape[2] // 2].shape) < 0.5] = 0
+    gt = rng.integers(1, n_gt + 1, size=shape).astype(np.uint64)
+    gt[rng.random(shape) < ignore_frac] = 0
+    return seg, gt
+
+
+CASES = [
+    ((3, 5, 7), (2, 2, 3), 4, 3, 0.3, 0.2),
+    ((9, 17, 33), (4, 8, 8), 6, 5, 0.2, 0.1),
+    ((16, 40, 72), (16, 16, 16), 30, 12, 0.1, 0.05),
+    ((5, 64, 130), (5, 64, 130), 500, 300, 0.0, 0.0),
+    ((20, 31, 45), (7, 10, 13), 1, 1, 0.5, 0.3),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', range(len(CASES)))
+@pytest.mark.parametrize('ignore', [0, None])
+def test_gpu_evaluate_matches_oracle(ctx, case, ignore):
+    import torch
+    shape, bs, ns, ng, zf, igf = CASES[case]
+    rng = np.random.default_rng(100 + case)
+    seg, gt = _random_case(rng, shape, ns, ng, zf, igf)
+    want, ov = E.measures(seg, gt, bs, ignore_label=ignore)
+    dseg = torch.from_numpy(seg.view(np.int64)).cuda()
+    dgt = torch.from_numpy(gt.view(np.int64)).cuda()
+    got = ctx.evaluate(dseg, dgt, bs, ignore_label=ignore)
+    for k in ('n_points', 'n_pairs', 'n_seg_ids', 'n_gt_ids'):
+        assert got[k] == want[k], k
+    s, g, c = ctx.overlaps()
+    assert {(int(a), int(b)): int(n) for a, b, n in zip(s, g, c)} == ov
+    if want['n_points']:
+        for k in ('vi_split', 'vi_merge', 'adapted_rand_error', 'rand_index'):
+            assert got[k] == pytest.approx(want[k], rel=RTOL, abs=1e-12), k
+
+
+@pytest.mark.gpu
+def test_gpu_evaluate_empty_and_errors(ctx):
+    import torch
+    z = torch.zeros((4, 8, 8), dtype=torch.int64, device='cuda')
+    got = ctx.evaluate(z, z, (2, 4, 4))
+    assert got['n_points'] == 0 and got['n_pairs'] == 0
+    big = torch.full((4, 8, 8), 1 << 40, dtype=torch.int64, device='cuda')
+    with pytest.raises(RuntimeError, match='segmentation id'):
+        ctx.evaluate(big, z + 1, (2, 4, 4))
+    with pytest.raises(RuntimeError, match='ground-truth id'):
+        ctx.evaluate(z + 1, big, (2, 4, 4))
+
+
+@pytest.mark.gpu
+def test_gpu_evaluate_table_growth(ctx):
+    """~400k distinct pairs: more than the first table (2^16 entries) holds."""
+    import torch
+    rng = np.random.default_rng(7)
+    shape = (32, 128, 128)
+    seg = rng.integers(1, 1 << 20, size=shape).astype(np.uint64)
+    gt = rng.integers(1, 1 << 20, size=shape).astype(np.uint64)
+    want, ov = E.measures(seg, gt, (32, 64, 64), ignore_label=0)
+    got = ctx.evaluate(torch.from_numpy(seg.view(np.int64)).cuda(),
+                       torch.from_numpy(gt.view(np.int64)).cuda(), (32, 64, 64))
+    assert got['n_pairs'] == want['n_pairs'] == len(ov)
+    for k in ('vi_split', 'vi_merge', 'adapted_rand_error', 'rand_index'):
+        assert got[k] == pytest.approx(want[k], rel=RTOL, abs=1e-12), k
+
+
+@pytest.mark.gpu
+def test_gpu_evaluate_cc_labels_at_scale(ctx):
+    """Property at volume scale: the CCL output against a permuted relabelling of itself is the
+    same partition (VI 0, RI 1, ARE 0); against the 'less' labelling with ignore label 0 the
+    counted voxels are the 'greater' background (n_points = voxels with gt != 0)."""
+    import torch
+    shape, bs = (256, 1024, 1024), (64, 512, 512)
+    inp = ctx.generate_boundary_map(shape)
+    seg, r = ctx.label_volume(inp, bs, 0.5, 'greater')
+    perm = torch.randperm(int(r['n_labels']) + 7, device='cuda')[: int(r['n_labels'])] + 1
+    perm[0] = 0
+    gt = perm[seg]
+    got = ctx.evaluate(seg, gt, bs, ignore_label=None)
+    assert got['n_points'] == seg.numel()
+    assert abs(got['vi_split']) < 1e-9 and abs(got['vi_merge']) < 1e-9
+    assert abs(got['rand_index'] - 1.0) < 1e-12 and abs(got['adapted_rand_error']) < 1e-12
+    assert got['n_pairs'] == got['n_seg_ids'] == got['n_gt_ids']
+    gt2, _ = ctx.label_volume(inp, bs, 0.5, 'less')
+    got = ctx.evaluate(seg, gt2, bs, ignore_label=0)
+    assert got['n_points'] == int((gt2 != 0).sum())   # every block holds seg (membranes)
+    # 'less' foreground is exactly the 'greater' background: every counted voxel has seg 0, so
+    # seg splits nothing and merges every gt object
+    assert got['n_seg_ids'] == 1 and got['n_pairs'] == got['n_gt_ids']
+    assert abs(got['vi_split']) < 1e-9 and got['vi_merge'] > 1.0 and 0.0 < got['rand_index'] < 1.0
