@@ -145,6 +145,13 @@ __device__ __forceinline__ u32 lfind(volatile lds_u32* par, u32 x) {
     return x;
 }
 
+// root of x without path compression (concurrent stores of ancestors by other threads allowed)
+__device__ __forceinline__ u32 lfind_ro(volatile lds_u32* par, u32 x) {
+    u32 p;
+    while ((p = par[x]) != x) x = p;
+    return x;
+}
+
 __device__ __forceinline__ void lunion(u32* par_, u32 a, u32 b) {
     lds_u32* par = as_lds(par_);
     volatile lds_u32* vp = par;

@@ -9,11 +9,11 @@
 //      the gt ids (a) and seg ids (b), n_points, then VI split / merge (log2) and the adapted rand
 //      error / rand index.
 //
-// Device layout: one pass over (seg, gt) uint64 volumes, 16 B/voxel, HBM-bound.  Every thread
-// takes 8 consecutive voxels (4 x 16-B loads per volume) and merges runs of equal (seg, gt)
-// before touching any table; a wave whose lanes all end on the same pair adds one wave sum.
-// Each workgroup owns a contiguous voxel range and a 2048-entry LDS hash table, flushed once to
-// the global open-addressing tables at the end.  Pairs of a seg-0 voxel are kept apart per block
+// Device layout: one pass over (seg, gt) uint64 volumes, 16 B/voxel, HBM-bound.  A wave takes
+// 512 voxels of one x-row as 8 coalesced loads of 64 voxels; runs of equal (seg, gt) keys among
+// the 64 lanes are found with one ballot and only each run's head lane touches a table.  Each
+// workgroup owns consecutive rows and a 2048-entry LDS hash table, flushed once to the global
+// open-addressing tables at the end.  Pairs of a seg-0 voxel are kept apart per block
 // (ZTAG keys: block id, gt id) because whether they count depends on the whole block (the
 // ws.sum() == 0 skip); k_ev_fold adds them for blocks that held any non-zero seg voxel.
 // Then k_ev_sizes builds the per-id size tables from the pair table and k_ev_reduce produces
@@ -30,7 +30,8 @@ constexpr u64 EV_ZTAG = 1ull << 63;
 constexpr int EV_LDS = 2048;       // LDS hash entries per workgroup
 constexpr int EV_LDS_PROBES = 32;
 constexpr int EV_PROBES = 4096;    // global probe limit before reporting the table as full
-constexpr int EV_V = 8;            // voxels per thread per step
+constexpr int EV_Q = 8;            // loads of 64 voxels per wave item
+constexpr int EV_ROW = 64 * EV_Q;  // voxels of one row per wave item
 constexpr u32 EV_ERR_SEG = 1, EV_ERR_GT = 2, EV_ERR_FULL = 4;
 
 __device__ __forceinline__ u64 ev_hash(u64 k) {
@@ -94,93 +95,64 @@ struct EvGrid {
     int64_t Y, X, bz, by, bx, nby, nbx;
 };
 
-__global__ __launch_bounds__(256) void k_ev_overlaps(const u64* __restrict__ seg, const u64* __restrict__ gt, int64_t n,
-                                                     int64_t per_wg, EvGrid gr, int use_ignore, u64 ignore, EvTabs t,
-                                                     u32* __restrict__ blk_flag) {
+// One wave item = 512 voxels of one x-row (8 loads of 64 consecutive uint64 per volume, each
+// instruction one contiguous 512-B span).  After each load, runs of equal keys across the 64
+// lanes are found with one ballot (run heads) and only the head lane of each run adds
+// (key, run length) to the LDS table.  A workgroup owns `rows_per_wg` consecutive rows.
+__global__ __launch_bounds__(256) void k_ev_overlaps(const u64* __restrict__ seg, const u64* __restrict__ gt,
+                                                     int64_t n_rows, int64_t rows_per_wg, EvGrid gr, int use_ignore,
+                                                     u64 ignore, EvTabs t, u32* __restrict__ blk_flag) {
     __shared__ u64 lk[EV_LDS];
     __shared__ u32 lc[EV_LDS];
     for (int e = threadIdx.x; e < EV_LDS; e += 256) { lk[e] = EV_EMPTY; lc[e] = 0; }
     __syncthreads();
-    const int64_t beg = (int64_t)blockIdx.x * per_wg, end = min(n, beg + per_wg);
-    const int lane = threadIdx.x & 63;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_wg, r1 = min(n_rows, r0 + rows_per_wg);
+    const int64_t nseg = (gr.X + EV_ROW - 1) / EV_ROW;
+    const int64_t items = (r1 - r0) * nseg;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     u32 err = 0, flagged = NONE;
-    // per_wg is a multiple of 256 * EV_V: every wave runs the same number of iterations
-    for (int64_t i0 = beg + (int64_t)threadIdx.x * EV_V; i0 - (int64_t)threadIdx.x * EV_V < end; i0 += 256 * EV_V) {
-        u64 rk = EV_EMPTY;
-        u32 rc = 0;
-        if (i0 < end) {
-            u64 sv[EV_V], gv[EV_V];
-            const int nv = (int)min<int64_t>(EV_V, end - i0);
-            if (nv == EV_V) {
+    for (int64_t it = wave; it < items; it += 4) {
+        const int64_t ri = it / nseg;
+        const int64_t row = r0 + ri;
+        const int64_t x0 = (it - ri * nseg) * EV_ROW;
+        const int64_t z = row / gr.Y, y = row - z * gr.Y;
+        const u64 rowbid = (u64)(((z / gr.bz) * gr.nby + y / gr.by) * gr.nbx);
+        const u64* sp = seg + row * gr.X;
+        const u64* gp = gt + row * gr.X;
+        u64 sv[EV_Q], gv[EV_Q];
 #pragma unroll
-                for (int q = 0; q < EV_V / 2; ++q) {
-                    typedef u64 v2u64 __attribute__((ext_vector_type(2)));
-                    const v2u64 a = __builtin_nontemporal_load((const v2u64*)(seg + i0) + q);
-                    const v2u64 b = __builtin_nontemporal_load((const v2u64*)(gt + i0) + q);
-                    sv[2 * q] = a.x; sv[2 * q + 1] = a.y;
-                    gv[2 * q] = b.x; gv[2 * q + 1] = b.y;
-                }
-            } else {
-#pragma unroll
-                for (int v = 0; v < EV_V; ++v) {
-                    sv[v] = v < nv ? seg[i0 + v] : 0;
-                    gv[v] = v < nv ? gt[i0 + v] : 0;
-                }
-            }
-            const int64_t zy = i0 / gr.X;
-            int64_t x = i0 - zy * gr.X;
-            int64_t z = zy / gr.Y;
-            int64_t y = zy - z * gr.Y;
-            int64_t zb = z / gr.bz, zr = z - zb * gr.bz, yb = y / gr.by, yr = y - yb * gr.by, xb = x / gr.bx, xr = x - xb * gr.bx;
-#pragma unroll
-            for (int v = 0; v < EV_V; ++v) {
-                if (v < nv) {
-                    const u64 s = sv[v], g = gv[v];
-                    const u32 bid = (u32)((zb * gr.nby + yb) * gr.nbx + xb);
-                    // block_node_labels.py:141: the block counts when its seg is not all 0,
-                    // whatever the gt holds there
-                    if (s != 0 && bid != flagged) {
-                        if (blk_flag[bid] == 0) blk_flag[bid] = 1;
-                        flagged = bid;
-                    }
-                    if (!(use_ignore && g == ignore)) {
-                        u64 key;
-                        if (s == 0) {
-                            key = EV_ZTAG | ((u64)bid << 32) | g;
-                        } else {
-                            key = (s << 32) | g;
-                            if (s >> 31) err |= EV_ERR_SEG;
-                        }
-                        if (g >= 0xFFFFFFFFull) err |= EV_ERR_GT;
-                        if (key != rk) {
-                            if (rc) ev_local(lk, lc, t, rk, rc);
-                            rk = key;
-                            rc = 0;
-                        }
-                        ++rc;
-                    }
-                    // next voxel along x (carry into y / z at row ends)
-                    if (++xr == gr.bx) { xr = 0; ++xb; }
-                    if (++x == gr.X) {
-                        x = 0; xb = 0; xr = 0;
-                        if (++yr == gr.by) { yr = 0; ++yb; }
-                        if (++y == gr.Y) {
-                            y = 0; yb = 0; yr = 0; ++z;
-                            if (++zr == gr.bz) { zr = 0; ++zb; }
-                        }
-                    }
-                }
-            }
+        for (int q = 0; q < EV_Q; ++q) {
+            const int64_t x = x0 + q * 64 + lane;
+            sv[q] = x < gr.X ? __builtin_nontemporal_load(sp + x) : 0;
+            gv[q] = x < gr.X ? __builtin_nontemporal_load(gp + x) : 0;
         }
-        // wave aggregation of the last run of every lane
-        const u64 k0 = (u64)__shfl((unsigned long long)rk, 0);
-        if (__all(rk == k0 || rc == 0)) {
-            u32 sum = rc;
+        int64_t xb = (x0 + lane) / gr.bx, xr = (x0 + lane) - xb * gr.bx;
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
-            if (lane == 0 && sum) ev_local(lk, lc, t, k0, sum);
-        } else if (rc) {
-            ev_local(lk, lc, t, rk, rc);
+        for (int q = 0; q < EV_Q; ++q) {
+            const bool valid = x0 + q * 64 + lane < gr.X;
+            const u64 s = sv[q], g = gv[q];
+            const u64 bid = rowbid + (u64)xb;
+            // block_node_labels.py:141: the block counts when its seg is not all 0, whatever the gt
+            if (valid && s != 0 && (u32)bid != flagged) {
+                if (blk_flag[bid] == 0) blk_flag[bid] = 1;
+                flagged = (u32)bid;
+            }
+            u64 key = EV_EMPTY;
+            if (valid && !(use_ignore && g == ignore)) {
+                key = s == 0 ? (EV_ZTAG | (bid << 32) | g) : ((s << 32) | g);
+                if (s >> 31) err |= EV_ERR_SEG;
+                if (g >= 0xFFFFFFFFull) err |= EV_ERR_GT;
+            }
+            const u64 prev = (u64)__shfl_up((unsigned long long)key, 1);
+            const bool head = lane == 0 || key != prev;
+            const u64 H = __ballot(head);
+            if (head && key != EV_EMPTY) {
+                const u64 above = lane == 63 ? 0 : H >> (lane + 1);
+                const u32 len = above ? (u32)__builtin_ctzll(above) + 1 : (u32)(64 - lane);
+                ev_local(lk, lc, t, key, len);
+            }
+            xr += 64;
+            while (xr >= gr.bx) { xr -= gr.bx; ++xb; }
         }
     }
     if (err) atomicOr(t.err, err);
@@ -203,14 +175,28 @@ __global__ __launch_bounds__(256) void k_ev_fold(EvTabs t, const u32* __restrict
 // size tables: seg id -> sum of its pair counts (b_dict), gt id -> (a_dict); measures.py:81-89
 __global__ __launch_bounds__(256) void k_ev_sizes(EvTabs t, u64* sk, u64* sc, u64* gk, u64* gc) {
     const u64 cap = t.mask + 1;
-    for (u64 e = (u64)blockIdx.x * 256 + threadIdx.x; e < cap; e += (u64)gridDim.x * 256) {
-        const u64 k = t.mk[e];
-        if (k == EV_EMPTY) continue;
-        const u64 c = t.mc[e];
-        bool ok = ev_insert(sk, sc, t.mask, k >> 32, c);
-        ok = ev_insert(gk, gc, t.mask, k & 0xFFFFFFFFull, c) && ok;
-        if (!ok) atomicOr(t.err, EV_ERR_FULL);
+    bool ok = true;
+    // wave-uniform trip count: the ballot below needs every lane
+    for (u64 e0 = (u64)blockIdx.x * 256 + (threadIdx.x & ~63u); e0 < cap; e0 += (u64)gridDim.x * 256) {
+        const u64 e = e0 + (threadIdx.x & 63);
+        const u64 k = e < cap ? t.mk[e] : EV_EMPTY;
+        const u64 c = k != EV_EMPTY ? t.mc[e] : 0;
+        const u64 sid = k != EV_EMPTY ? k >> 32 : EV_EMPTY;
+        if (k != EV_EMPTY) ok = ev_insert(gk, gc, t.mask, k & 0xFFFFFFFFull, c) && ok;
+        // seg ids repeat across many pairs (seg 0 against every gt object): one add per wave
+        // when every occupied slot of the wave holds the same seg id
+        const int first = __builtin_ctzll(__ballot(k != EV_EMPTY) | (1ull << 63));
+        const u64 s0 = (u64)__shfl((unsigned long long)sid, first);
+        if (__all(k == EV_EMPTY || sid == s0)) {
+            u64 sum = c;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) sum += (u64)__shfl_xor((unsigned long long)sum, o);
+            if ((int)(threadIdx.x & 63) == first && k != EV_EMPTY) ok = ev_insert(sk, sc, t.mask, s0, sum) && ok;
+        } else if (k != EV_EMPTY) {
+            ok = ev_insert(sk, sc, t.mask, sid, c) && ok;
+        }
     }
+    if (!ok) atomicOr(t.err, EV_ERR_FULL);
 }
 
 // per-workgroup partials of one table: {entries, sum c} (u64) and {sum c^2, sum c log2 c} (f64)
@@ -289,15 +275,14 @@ int cc_evaluate(cc_ctx* c, const uint64_t* seg, const uint64_t* gt, const int64_
         }
         const int64_t n_blocks = nb[0] * nb[1] * nb[2];
         CC_REQUIRE(n_blocks < (1LL << 31), "too many evaluation blocks (>= 2^31)");
-        const int64_t n = shape[0] * shape[1] * shape[2];
-        CC_REQUIRE(((uintptr_t)seg & 15) == 0 && ((uintptr_t)gt & 15) == 0, "seg / gt must be 16-byte aligned");
+        CC_REQUIRE(((uintptr_t)seg & 7) == 0 && ((uintptr_t)gt & 7) == 0, "seg / gt must be 8-byte aligned");
         EvGrid gr{shape[1], shape[2], block_shape[0], block_shape[1], block_shape[2], nb[1], nb[2]};
-        // one contiguous range of whole 2048-voxel steps per workgroup, ~4 workgroups per CU
-        const int64_t step = 256 * EV_V;
-        const int64_t steps = (n + step - 1) / step;
-        const int64_t n_wg = std::min<int64_t>(1024, steps);
-        const int64_t per_wg = ((steps + n_wg - 1) / n_wg) * step;
-        const unsigned grid = (unsigned)((n + per_wg - 1) / per_wg);
+        // rows of one workgroup: ~8192 workgroups on large volumes (LDS tables stay sparse)
+        const int64_t n_rows = shape[0] * shape[1];
+        const int64_t rows_per_wg = std::max<int64_t>(1, (n_rows + 8191) / 8192);
+        const int64_t n_wg = (n_rows + rows_per_wg - 1) / rows_per_wg;
+        CC_REQUIRE(n_wg < (1LL << 31), "too many rows");
+        const unsigned grid = (unsigned)n_wg;
         c->ev_flag.ensure(n_blocks * sizeof(u32) + 16);
         c->ev_part.ensure(4 * EV_REDUCE_WG * sizeof(u64));
         c->counter.ensure(sizeof(u32));
@@ -320,10 +305,10 @@ int cc_evaluate(cc_ctx* c, const uint64_t* seg, const uint64_t* gt, const int64_
             EvTabs t{mk, mk + cap, zk, zk + cap, (u64)cap - 1, c->counter.as<u32>()};
             u32* flag = c->ev_flag.as<u32>();
             launch(c, "k_ev_overlaps", [&] {
-                k_ev_overlaps<<<grid, 256, 0, s>>>(seg, gt, n, per_wg, gr, use_ignore ? 1 : 0, ignore_label, t, flag);
+                k_ev_overlaps<<<grid, 256, 0, s>>>(seg, gt, n_rows, rows_per_wg, gr, use_ignore ? 1 : 0, ignore_label, t, flag);
             });
             launch(c, "k_ev_fold", [&] { k_ev_fold<<<grid_stride(cap), 256, 0, s>>>(t, flag); });
-            launch(c, "k_ev_sizes", [&] { k_ev_sizes<<<grid_stride(cap), 256, 0, s>>>(t, sk, sk + cap, gk, gk + cap); });
+            launch(c, "k_ev_sizes", [&] { k_ev_sizes<<<std::min<unsigned>(2048, grid_stride(cap)), 256, 0, s>>>(t, sk, sk + cap, gk, gk + cap); });
             u32 herr = 0;
             HIP_OK(hipMemcpyAsync(&herr, c->counter.p, sizeof(u32), hipMemcpyDeviceToHost, s));
             sync(c);

@@ -174,13 +174,17 @@ __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T) {
     }
     __syncthreads();
     if (STOP == 2) return 0;
-    // 3. compress; count the roots of each quarter row
+    // 3. compress; count the roots of each quarter row.  The finds here must not compress
+    // paths: a compressing find of another thread could store an intermediate ancestor into
+    // par[r] after r's owner stored the root, and phase 5 would then read that ancestor's entry
+    // (mid-update) as the root's -- a run silently landing in another component of the tile.
+    // Without it every store to par[r] is the root itself, by r's owner only.
     const u32 r0 = T.roff[qrow];
     const u32 Brow = T.B[qrow];
     u32 n = 0;
     for (u32 m = Bq; m; m &= m - 1) {
         const u32 r = r0 + (u32)__popc(Brow & ((1u << __builtin_ctz(m)) - 1));
-        const u32 root = lfind(as_lds(par), r);
+        const u32 root = lfind_ro(as_lds(par), r);
         par[r] = root;
         n += (root == r);
     }

@@ -192,7 +192,7 @@ int cc_set_debug(cc_ctx* ctx, int flags);
  * of the evaluation grid (node_labels/block_node_labels.py:133-166: a block whose seg sums to 0 is
  * skipped; voxels with gt == ignore_label are not counted when use_ignore), then the contingency
  * table and the measures (evaluation/measures.py:81-162; a = gt sizes, b = seg sizes).
- * seg_dev / gt_dev: uint64 device volumes (C-order, 16-byte aligned).  Ids: seg < 2^31,
+ * seg_dev / gt_dev: uint64 device volumes (C-order, 8-byte aligned).  Ids: seg < 2^31,
  * gt < 2^32 - 1 (error otherwise).  vi_* in bits (log2). */
 typedef struct {
     uint64_t n_points;            /* measures.py:113                               */

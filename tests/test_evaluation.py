@@ -144,3 +144,20 @@ def test_gpu_evaluate_cc_labels_at_scale(ctx):
     # seg splits nothing and merges every gt object
     assert got['n_seg_ids'] == 1 and got['n_pairs'] == got['n_gt_ids']
     assert abs(got['vi_split']) < 1e-9 and got['vi_merge'] > 1.0 and 0.0 < got['rand_index'] < 1.0
+
+
+@pytest.mark.gpu
+def test_gpu_ccl_partition_deterministic_c3(ctx):
+    """Regression: at C3 'less' (150k components) a path-compression race in the tile CCL
+    (cc_kernels.hip tile_ccl phase 3) moved a handful of 7-60 voxel pieces to another component
+    of their tile in ~8 of 256 blocks per run.  Two runs must give the same partition: the
+    contingency table of run a against run b is a bijection (pairs == ids on both sides)."""
+    shape, bs = (1024, 2048, 2048), (64, 512, 512)
+    inp = ctx.generate_boundary_map(shape)
+    a, ra = ctx.label_volume(inp, bs, 0.5, 'less')
+    for _ in range(2):
+        b, rb = ctx.label_volume(inp, bs, 0.5, 'less')
+        r = ctx.evaluate(a, b, bs, ignore_label=None)
+        assert ra == rb
+        assert r['n_pairs'] == r['n_seg_ids'] == r['n_gt_ids'] == ra['n_components'] + 1
+        del b
