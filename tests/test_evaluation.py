@@ -161,3 +161,38 @@ def test_gpu_ccl_partition_deterministic_c3(ctx):
         assert ra == rb
         assert r['n_pairs'] == r['n_seg_ids'] == r['n_gt_ids'] == ra['n_components'] + 1
         del b
+
+
+@pytest.mark.gpu
+def test_gpu_evaluation_workflow(tmp_path):
+    """EvaluationWorkflow through the task API on N5 (evaluation_workflow.py:46-84 surface):
+    the output JSON carries the reference's four keys, equal to the oracle's measures."""
+    import json
+    import os
+    from cluster_tools_amd import luigi_compat as luigi, n5
+    from cluster_tools_amd.cluster_tasks import BaseClusterTask
+    from cluster_tools_amd.evaluation import EvaluationWorkflow
+    rng = np.random.default_rng(11)
+    shape, bs = (12, 40, 56), [6, 16, 32]
+    seg, gt = _random_case(rng, shape, 9, 7, 0.2, 0.1)
+    data = str(tmp_path / 'data.n5')
+    with n5.open_file(data) as f:
+        f.create_dataset('seg', data=seg, chunks=(6, 16, 16), compression='gzip')
+        f.create_dataset('gt', data=gt, chunks=(6, 16, 16), compression='gzip')
+    cfg = str(tmp_path / 'config')
+    os.makedirs(cfg)
+    g = BaseClusterTask.default_global_config()
+    g['block_shape'] = bs
+    with open(os.path.join(cfg, 'global.config'), 'w') as f:
+        json.dump(g, f)
+    out = str(tmp_path / 'scores.json')
+    t = EvaluationWorkflow(tmp_folder=str(tmp_path / 'tmp'), config_dir=cfg, target='local', max_jobs=1,
+                           seg_path=data, seg_key='seg', gt_path=data, gt_key='gt', output_path=out)
+    assert luigi.build([t], local_scheduler=True)
+    with open(out) as f:
+        got = json.load(f)
+    want, _ = E.measures(seg, gt, bs, ignore_label=0)
+    assert set(got) == {'vi-split', 'vi-merge', 'adapted-rand-error', 'rand-index'}
+    for k, w in (('vi-split', 'vi_split'), ('vi-merge', 'vi_merge'),
+                 ('adapted-rand-error', 'adapted_rand_error'), ('rand-index', 'rand_index')):
+        assert got[k] == pytest.approx(want[w], rel=RTOL, abs=1e-12), k
