@@ -60,3 +60,33 @@ def test_two_ranks_one_gpu_gloo(tmp_path, mode, block_shape):
     np.testing.assert_array_equal(got, ref['labels'])
     for k in range(2):
         assert int(np.load(str(tmp_path / ('nl_%d.npy' % k)))[0]) == ref['n_labels']
+
+
+@pytest.mark.parametrize('mode,masked', [('less', True), ('greater', False)])
+def test_sharded_c4_scale_pair_bijection(mode, masked):
+    """SURVEY.md §8d parity at scale for the sharded configs: C4 (C3 + ellipsoid mask, here over
+    4 z-slabs on one GPU) against the single-volume path.  The partitions are equal iff the
+    device contingency table (cc_evaluate) of the two labellings is a bijection:
+    |unique(a, b)| == |unique(a)| == |unique(b)|, and the raw labels are identical."""
+    import torch
+    from cluster_tools_amd import _lib
+    from cluster_tools_amd.distributed import label_slabs_single_process
+    from cluster_tools_amd.synthetic import ellipsoid_mask_device
+    shape, bs = (1024, 2048, 2048), (64, 512, 512)
+    ctxs = [_lib.Context(0) for _ in range(4)]
+    try:
+        x = ctxs[0].generate_boundary_map(shape)
+        mask = ellipsoid_mask_device(shape, 0, shape[0], x.device) if masked else None
+        torch.cuda.synchronize()          # the mask is built on torch's stream, the ctx has its own
+        a, ra = ctxs[0].label_volume(x, bs, 0.5, mode, mask=mask)
+        b, res, sums, _ = label_slabs_single_process(ctxs, x, bs, 0.5, mode, mask=mask)
+        del x, mask
+        torch.cuda.synchronize()
+        r = ctxs[0].evaluate(a, b, bs, ignore_label=None)
+        assert r['n_pairs'] == r['n_seg_ids'] == r['n_gt_ids'] == ra['n_components'] + 1
+        assert sum(q['n_components'] for q in res) == ra['n_components']
+        assert sum(sums) + 1 == ra['n_labels']
+        assert bool(torch.equal(a, b))
+    finally:
+        for c in ctxs:
+            c.close()
