@@ -196,3 +196,23 @@ def test_white_noise_large_block(ctx):
     inp = rng.random((64, 192, 256), dtype=np.float32)
     _check_against_oracle(ctx, inp, (64, 192, 256), 0.3, 'less')
     _check_against_oracle(ctx, inp, (32, 96, 128), 0.3, 'less')
+
+
+@pytest.mark.slow
+def test_c3_less_vs_oracle(ctx):
+    """BASELINE config 3 (1024 x 2048 x 2048, block 64 x 512 x 512) in 'less' mode (150 k
+    components: the case where a tile-CCL race once moved small pieces between components)
+    bit-exact against the C oracle; the labels are compared on the device."""
+    import os
+    import torch
+    shape, bs = (1024, 2048, 2048), (64, 512, 512)
+    x = ctx.generate_boundary_map(shape)
+    lab, res = ctx.label_volume(x, bs, 0.5, 'less')
+    inp = x.cpu().numpy()
+    del x
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    r = O.label_volume(inp, bs, 0.5, 'less', n_threads=threads)
+    del inp
+    assert res['n_labels'] == r['n_labels'] and res['max_id'] == r['max_id']
+    ref = torch.from_numpy(r.pop('labels').view(np.int64)).cuda()
+    assert bool(torch.equal(lab, ref))
