@@ -24,7 +24,7 @@ EXPORTS = (
     'cc_get_profile', 'cc_reset_profile', 'cc_shard_begin', 'cc_shard_assign', 'cc_shard_planes',
     'cc_seam_pairs', 'cc_shard_finish', 'cc_set_debug', 'cc_threshold', 'cc_shard_top_plane32',
     'cc_seam_pairs32', 'cc_shard_top_cubes32', 'cc_seam_pairs_cubes32',
-    'cc_evaluate', 'cc_get_overlaps',
+    'cc_evaluate', 'cc_get_overlaps', 'cc_relabel_consecutive',
 )
 
 
@@ -94,6 +94,7 @@ def load():
         'cc_shard_finish': (I, [P, P, i64, P, ctypes.POINTER(CCResult)]),
         'cc_evaluate': (I, [P, P, P, P, P, I, u64, ctypes.POINTER(CCEvalResult)]),
         'cc_get_overlaps': (i64, [P, P, P, P, i64]),
+        'cc_relabel_consecutive': (I, [P, P, P, i64, P, P, P, i64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -235,6 +236,34 @@ class Context:
         _check(L.cc_get_overlaps(self._h, _ptr(a), _ptr(b), _ptr(c), n))
         o = np.lexsort((b, a))
         return a[o], b[o], c[o]
+
+    def relabel_consecutive(self, labels, out=None):
+        """RelabelWorkflow (relabel_workflow.py:10-60, find_labeling.py:84-120) on device:
+        returns (relabelled tensor, assignments (n, 2) uint64 [old id, new id]).  `labels` is a
+        uint64 (torch int64 / uint64) CUDA tensor; out may be `labels` (in place)."""
+        import torch
+        assert hasattr(labels, 'data_ptr') and labels.is_cuda and labels.element_size() == 8
+        assert labels.is_contiguous() and labels.dtype in (torch.int64, torch.uint64)
+        if out is None:
+            out = torch.empty_like(labels)
+        assert out.shape == labels.shape and out.is_contiguous() and out.element_size() == 8
+        torch.cuda.current_stream(labels.device).synchronize()
+        L = load()
+        nu, st = np.zeros(1, dtype=np.uint64), np.zeros(1, dtype=np.uint64)
+        cap = 1 << 20
+        while True:
+            uniq = np.empty(cap, dtype=np.uint64)
+            _check(L.cc_relabel_consecutive(self._h, _ptr(labels), _ptr(out), labels.numel(), _ptr(nu), _ptr(st),
+                                            _ptr(uniq), cap))
+            if int(nu[0]) <= cap:
+                break
+            if out.data_ptr() == labels.data_ptr():    # the ids are already replaced
+                raise RuntimeError('relabel_consecutive in place: more than %d ids, pass out=' % cap)
+            cap = int(nu[0])
+        n = int(nu[0])
+        uniq = uniq[:n]
+        table = np.stack([uniq, np.arange(int(st[0]), int(st[0]) + n, dtype=np.uint64)], axis=1)
+        return out, table
 
     def block_values(self, n_blocks):
         a = np.empty(n_blocks, dtype=np.uint64)

@@ -58,6 +58,7 @@ struct cc_ctx {
         flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf, spec,
         ev_main, ev_z, ev_seg, ev_gt, ev_flag, ev_part;   // evaluation (cc_eval.hip)
     int64_t ev_cap = 0;      // entries per evaluation hash table of the last cc_evaluate
+    int64_t rl_cap = 0;      // id-set slots of the last cc_relabel_consecutive
     // last run
     int64_t n_blocks = 0;
     uint64_t n_labels = 0;
@@ -791,3 +792,4 @@ int cc_get_profile(cc_ctx* c, char* names, int names_cap, int64_t* counts, doubl
 
 #include "cc_stage_host.hip"
 #include "cc_eval.hip"
+#include "cc_relabel.hip"

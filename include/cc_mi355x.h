@@ -211,6 +211,16 @@ int cc_evaluate(cc_ctx* ctx, const uint64_t* seg_dev, const uint64_t* gt_dev, co
 /* contingency table of the last cc_evaluate (unordered); returns its size (copies min(size, cap)) */
 int64_t cc_get_overlaps(cc_ctx* ctx, uint64_t* seg_ids, uint64_t* gt_ids, uint64_t* counts, int64_t cap);
 
+/* --- consecutive relabelling --------------------------------------------------
+ * RelabelWorkflow (relabel/relabel_workflow.py:10-60; find_labeling.py:84-120): the sorted unique
+ * ids of labels_dev get new ids start, start + 1, ... (start = 0 when id 0 occurs, else 1); the
+ * volume mapped into out_dev (may alias labels_dev).  n uint64 device elements.  Returns the
+ * number of unique ids and start; copies min(n_unique, cap) sorted unique ids to uniques_host
+ * (nullable) -- the old ids of the assignment table, new id = index + start.  Id 2^64-1 is
+ * reserved (error). */
+int cc_relabel_consecutive(cc_ctx* ctx, const uint64_t* labels_dev, uint64_t* out_dev, int64_t n,
+                           uint64_t* n_unique, uint64_t* start_label, uint64_t* uniques_host, int64_t cap);
+
 #ifdef __cplusplus
 }
 #endif
