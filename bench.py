@@ -39,6 +39,8 @@ def parse():
     p.add_argument('--mode', default='greater')
     p.add_argument('--threshold', type=float, default=0.5)
     p.add_argument('--mask', action='store_true')
+    p.add_argument('--dither', action='store_true',
+                   help='continuous input: the synthetic map plus a deterministic sub-2^-8 dither (not quantized)')
     p.add_argument('--shape', default=None, help='override Z,Y,X (per-rank slab for N > 1)')
     p.add_argument('--block-shape', default='64,512,512')
     p.add_argument('--no-cpu-baseline', action='store_true')
@@ -56,7 +58,7 @@ def cpu_baseline(args, block_shape, shape_yx):
     threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or len(os.sched_getaffinity(0))
     threads = max(1, min(threads, 64))
     shape = (args.cpu_sample_z,) + tuple(shape_yx)
-    x = O.boundary_map(shape, n_threads=threads)
+    x = O.boundary_map(shape, n_threads=threads, dither=args.dither)
     t0 = time.perf_counter()
     r = O.label_volume(x, block_shape, args.threshold, args.mode, n_threads=threads, want_lut=False)
     dt = time.perf_counter() - t0
@@ -74,6 +76,7 @@ def main():
     import torch
     import torch.distributed as dist
     from cluster_tools_amd import _lib
+    lib_src = _lib.check_provenance()       # the library must be built from this tree's sources
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -99,14 +102,17 @@ def main():
         slab = (1024, 2048, 2048) if world == 1 else (256, 4096, 4096)
     gshape = (slab[0] * world,) + slab[1:]
     tag = ('c3' if world == 1 and not args.shape else 'c5slab' if not args.shape else 'custom') + \
-        ('_mask' if args.mask else '') + ('' if args.mode == 'greater' else '_' + args.mode)
-    workload = ('C3%s (1024,2048,2048) f32, 1 GPU' % (' + uint8 mask (C4 at N=1)' if args.mask else '') if world == 1 and not args.shape else
+        ('_mask' if args.mask else '') + ('_cont' if args.dither else '') + \
+        ('' if args.mode == 'greater' else '_' + args.mode)
+    workload = ('C3%s%s (1024,2048,2048) f32, 1 GPU' % (' + uint8 mask (C4 at N=1)' if args.mask else '',
+                                                       ' continuous (dithered)' if args.dither else '')
+                if world == 1 and not args.shape else
                 'C5-style z-slabs (256N,4096,4096) f32' if not args.shape else 'custom %s' % (gshape,))
 
     ctx = _lib.Context(gpu)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     z0 = slab[0] * rank
-    x = ctx.generate_boundary_map(slab, origin=(z0, 0, 0), device=dev)
+    x = ctx.generate_boundary_map(slab, origin=(z0, 0, 0), device=dev, dither=args.dither)
     mask = None
     if args.mask:
         from cluster_tools_amd.synthetic import ellipsoid_mask_device
@@ -189,7 +195,8 @@ def main():
         'metric': METRIC, 'value': round(value, 3), 'unit': 'Gvox/s', 'n_gpus': world,
         'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3),
         'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
-        'data': 'synthetic (integer-only jittered-Voronoi boundary map, SURVEY.md §8d, seed 0x5EED)',
+        'data': 'synthetic (integer-only jittered-Voronoi boundary map, SURVEY.md §8d, seed 0x5EED%s)'
+                % (', + sub-2^-8 dither: continuous float32' if args.dither else ''),
         'config': {'workload': workload, 'shape': list(gshape), 'slab': list(slab),
                    'block_shape': list(block_shape), 'threshold': args.threshold,
                    'threshold_mode': args.mode, 'mask': bool(args.mask),
@@ -200,6 +207,7 @@ def main():
         'kernels_ms_per_step': {k: round(v['total_ms'] / args.steps, 4) for k, v in
                                 sorted(breakdown.items(), key=lambda kv: -kv[1]['total_ms']) if v['count']},
         'result': res,
+        'lib': {'version': _lib.version(), 'src': lib_src},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         del x, out

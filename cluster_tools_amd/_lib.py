@@ -24,7 +24,7 @@ EXPORTS = (
     'cc_get_profile', 'cc_reset_profile', 'cc_shard_begin', 'cc_shard_assign', 'cc_shard_planes',
     'cc_seam_pairs', 'cc_shard_finish', 'cc_set_debug', 'cc_threshold', 'cc_shard_top_plane32',
     'cc_seam_pairs32', 'cc_shard_top_cubes32', 'cc_seam_pairs_cubes32',
-    'cc_evaluate', 'cc_get_overlaps', 'cc_relabel_consecutive',
+    'cc_evaluate', 'cc_get_overlaps', 'cc_relabel_consecutive', 'cc_n5_read', 'cc_n5_write',
 )
 
 
@@ -77,7 +77,7 @@ def load():
         'cc_block_faces': (i64, [P, P, P, P, P, P, i64]),
         'cc_merge_assignments': (I, [P, P, i64, u64, P]),
         'cc_write': (I, [P, P, P, P, P, P, u64]),
-        'cc_generate_boundary_map': (I, [P, P, P, P, u64]),
+        'cc_generate_boundary_map': (I, [P, P, P, P, u64, I]),
         'cc_set_profiling': (I, [P, I]),
         'cc_get_profile': (I, [P, ctypes.c_char_p, I, P, P, I]),
         'cc_reset_profile': (I, [P]),
@@ -95,6 +95,8 @@ def load():
         'cc_evaluate': (I, [P, P, P, P, P, I, u64, ctypes.POINTER(CCEvalResult)]),
         'cc_get_overlaps': (i64, [P, P, P, P, i64]),
         'cc_relabel_consecutive': (I, [P, P, P, i64, P, P, P, i64]),
+        'cc_n5_read': (I, [ctypes.c_char_p, I, P, P, I, I, P, P, P, I]),
+        'cc_n5_write': (I, [ctypes.c_char_p, I, P, P, I, I, I, P, P, P, I, I]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -102,6 +104,23 @@ def load():
         fn.argtypes = args
     _lib = L
     return L
+
+
+def version():
+    return load().cc_version().decode()
+
+
+def check_provenance():
+    """Raise unless the loaded library was built from this tree's sources: cc_version()
+    carries the SHA-256 prefix build.py embedded (binary provenance)."""
+    from . import build
+    v = version()
+    want = build.source_hash()
+    got = v.split('src=')[-1] if 'src=' in v else None
+    if got != want:
+        raise RuntimeError('%s was built from other sources (library src=%s, tree src=%s): rebuild with '
+                           '__graft_entry__.build()' % (LIB_PATH, got, want))
+    return want
 
 
 def _check(rc):
@@ -252,13 +271,13 @@ class Context:
         nu, st = np.zeros(1, dtype=np.uint64), np.zeros(1, dtype=np.uint64)
         cap = 1 << 20
         while True:
+            # a table larger than cap is reported (n_unique) before out is touched, so in-place
+            # calls are safe: the second call has the exact size
             uniq = np.empty(cap, dtype=np.uint64)
             _check(L.cc_relabel_consecutive(self._h, _ptr(labels), _ptr(out), labels.numel(), _ptr(nu), _ptr(st),
                                             _ptr(uniq), cap))
             if int(nu[0]) <= cap:
                 break
-            if out.data_ptr() == labels.data_ptr():    # the ids are already replaced
-                raise RuntimeError('relabel_consecutive in place: more than %d ids, pass out=' % cap)
             cap = int(nu[0])
         n = int(nu[0])
         uniq = uniq[:n]
@@ -320,13 +339,14 @@ class Context:
                                len(lut)))
         return labels_dev
 
-    def generate_boundary_map(self, shape, origin=(0, 0, 0), seed=0x5EED, out_dev=None, device=None):
+    def generate_boundary_map(self, shape, origin=(0, 0, 0), seed=0x5EED, out_dev=None, device=None, dither=False):
         import torch
         if out_dev is None:
             out_dev = torch.empty(tuple(int(s) for s in shape), dtype=torch.float32,
                                   device=device if device is not None else 'cuda:%d' % self.device)
         shape_a, origin_a = _i64(shape), _i64(origin)   # keep alive across the call
-        _check(load().cc_generate_boundary_map(self._h, _ptr(out_dev), _ptr(shape_a), _ptr(origin_a), int(seed)))
+        _check(load().cc_generate_boundary_map(self._h, _ptr(out_dev), _ptr(shape_a), _ptr(origin_a), int(seed),
+                                               int(bool(dither))))
         return out_dev
 
     # ---- z-slab shards (cluster_tools_amd/distributed.py drives these) ----
@@ -414,3 +434,30 @@ def merge_offsets(values):
     n_labels = np.zeros(1, dtype=np.uint64)
     _check(load().cc_merge_offsets(_ptr(values), len(values), _ptr(offsets), _ptr(empty), _ptr(n_labels)))
     return offsets, np.nonzero(empty)[0], int(n_labels[0])
+
+
+_COMPRESSION = {'raw': 0, 'gzip': 1}
+
+
+def n5_read(path, shape, chunks, elem_size, compression, begin, end, out, n_threads=8):
+    """cc_n5_read: region [begin, end) of an N5 dataset into the C-order host array `out`."""
+    if compression not in _COMPRESSION:
+        raise NotImplementedError('n5 compression %s' % compression)
+    assert out.flags.c_contiguous and out.dtype.itemsize == elem_size
+    sh, ch, b, e = (_i64(v) for v in (shape, chunks, begin, end))
+    _check(load().cc_n5_read(os.fsencode(path), len(sh), _ptr(sh), _ptr(ch), int(elem_size),
+                             _COMPRESSION[compression], _ptr(b), _ptr(e), _ptr(out), int(n_threads)))
+    return out
+
+
+def n5_write(path, shape, chunks, elem_size, compression, level, begin, end, data, n_threads=8,
+             skip_zero_chunks=False):
+    """cc_n5_write: the C-order host array `data` into region [begin, end) of an N5 dataset."""
+    if compression not in _COMPRESSION:
+        raise NotImplementedError('n5 compression %s' % compression)
+    data = np.ascontiguousarray(data)
+    assert data.dtype.itemsize == elem_size
+    sh, ch, b, e = (_i64(v) for v in (shape, chunks, begin, end))
+    _check(load().cc_n5_write(os.fsencode(path), len(sh), _ptr(sh), _ptr(ch), int(elem_size),
+                              _COMPRESSION[compression], int(level), _ptr(b), _ptr(e), _ptr(data),
+                              int(n_threads), int(bool(skip_zero_chunks))))

@@ -18,7 +18,7 @@ constexpr u64 GEN_NOISE_SALT = 0x5851F42D4C957F2Dull;
 // seeds of the 3x3x3 cells around a row's cells are shared by the row, so they are computed
 // once per block into LDS (the row spans at most 9 cells along x -> 3*3*11 seeds).
 __global__ __launch_bounds__(256) void k_generate(float* __restrict__ out, int64_t Z, int64_t Y, int64_t X,
-                                                  int64_t oz, int64_t oy, int64_t ox, u64 seed) {
+                                                  int64_t oz, int64_t oy, int64_t ox, u64 seed, int dither) {
     __shared__ int64_t sp[3][3][11][3];
     const int64_t nxb = (X + 255) / 256;
     const int64_t row = (int64_t)blockIdx.y * Y + blockIdx.x / nxb;   // grid (Y * nxb, Z)
@@ -59,7 +59,9 @@ __global__ __launch_bounds__(256) void k_generate(float* __restrict__ out, int64
     const u64 nh = splitmix64((seed + GEN_NOISE_SALT) ^ vkey);
     int64_t q = m + (int64_t)(nh % 33) - 16;
     q = q < 0 ? 0 : (q > 255 ? 255 : q);
-    out[((row / Y) * Y + (row % Y)) * X + xl] = (float)q / 256.0f;
+    // continuous variant: (q * 2^16 + 16-bit dither) / 2^24, exact in float32
+    const float v = dither ? (float)((u32)q * 65536u + (u32)((nh >> 16) & 0xFFFF)) / 16777216.0f : (float)q / 256.0f;
+    out[((row / Y) * Y + (row % Y)) * X + xl] = v;
 }
 
 }  // namespace cc

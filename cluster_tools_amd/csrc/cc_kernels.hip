@@ -740,9 +740,10 @@ __global__ void k_guess(int64_t nb, const u32* part, float thr, int mode, BlockP
         if (q[4 * p + 3] && q[4 * p + 2] == mx) nmx += q[4 * p + 3];
     }
     const bool nan = mx > 0xFF800000u || mn < 0x007FFFFFu;
-    BlockParam p = block_param(mn, mx, nan ? 1u : 0u, thr, mode);
-    if (nmn < 2 || nmx < 2) p.kind = BP_EMPTY;     // continuous values: no guess
-    guess[b] = widen(p, mode);
+    // On continuous data the sampled extremes are not the block's, so the guessed bound misses
+    // the exact one by a little: only tiles holding a voxel between the two are relabelled.
+    (void)nmn; (void)nmx;
+    guess[b] = widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
 }
 
 struct SpecArgs {
@@ -1368,17 +1369,24 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const face_t* S, 
 // STOP (ablation harness only; 0 in the library): 1 staged, 2 + z seam, 3 + y seam, 4 + x seam
 // Tiles [t_begin, t_end): the seams of a z-layer chunk only read faces of that chunk and the
 // layers below it, so the library runs them on a side stream behind the k_spec chunks.
+// list (nullable): the tiles are list[1 .. list[0]] instead of the range (seams redone after k_fix)
 template <int STOP = 0>
 __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* __restrict__ FACES, u64* PAIRS, u32* PC,
                                                          u8* big, u64* IPAIRS, u32* IPC, u8* iovf,
-                                                         int64_t t_begin, int64_t t_end) {
+                                                         int64_t t_begin, int64_t t_end, const u32* list) {
     __shared__ alignas(16) face_t Sall[SP_WAVES][FACE_STRIDE];
     __shared__ u32 Hall[SP_WAVES][SEAM_HASH];
     __shared__ face_t Eall[SP_WAVES][EDGE_N];
     __shared__ u32 cnt[SP_WAVES][2];
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t t = t_begin + (int64_t)blockIdx.x * SP_WAVES + w;
-    const bool valid = t < t_end;
+    const int64_t idx = (int64_t)blockIdx.x * SP_WAVES + w;
+    int64_t t = t_begin + idx;
+    bool valid = t < t_end;
+    if (list) {
+        const u32 nl = __builtin_amdgcn_readfirstlane(list[0]);
+        valid = idx < (int64_t)nl;
+        t = valid ? (int64_t)__builtin_amdgcn_readfirstlane(list[1 + idx]) : 0;
+    }
     face_t* S = Sall[w];
     u32* H = Hall[w];
     TileInfo ti;
@@ -1473,6 +1481,29 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* _
         if (n > TPC) big[ti.block] = 1;
         IPC[t] = ni < TPI ? ni : TPI;
         if (ni > TPI) iovf[t] = 1;
+    }
+}
+
+// Tiles whose seams read the faces of a relabelled tile (FIX[1 .. FIX[0]], k_fix): the tile itself
+// and the 13 tiles that have it as a lex-negative neighbour.  Each marked once (flag), listed in
+// LIST[1 .. LIST[0]] for k_seams.
+__global__ void k_mark_seams(Geom g, const u32* FIX, u32* flag, u32* LIST) {
+    const u32 n = FIX[0];
+    for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < 14 * n; i += gridDim.x * blockDim.x) {
+        const u32 f = FIX[1 + i / 14], d = i % 14;
+        const TileInfo ti = tile_info(g, f);
+        // d = 0: the tile; else the dependent at (+dz, dy, dx) over the 13 lex-positive offsets
+        int dz = 0, dy = 0, dx = 0;
+        if (d > 0) {
+            const int c = (int)d - 1;               // 0..12: (0,0,1), (0,1,-1..1), (1,-1..1,-1..1)
+            if (c == 0) { dx = 1; }
+            else if (c < 4) { dy = 1; dx = c - 2; }
+            else { dz = 1; dy = (c - 4) / 3 - 1; dx = (c - 4) % 3 - 1; }
+        }
+        const int iz = ti.iz + dz, iy = ti.iy + dy, ix = ti.ix + dx;
+        if (iz >= g.nt[0] || iy < 0 || iy >= g.nt[1] || ix < 0 || ix >= g.nt[2]) continue;
+        const u32 t = (u32)(((int64_t)iz * g.nt[1] + iy) * g.nt[2] + ix);
+        if (atomicExch(&flag[t], 1u) == 0u) LIST[1 + atomicAdd(LIST, 1u)] = t;
     }
 }
 
@@ -2009,7 +2040,7 @@ template __global__ void k_fix<false>(Geom, const u32*, const BlockParam*, const
                                       face_t*, u32*, u32*, u64*);
 template __global__ void k_fix<true>(Geom, const u32*, const BlockParam*, const float*, const u8*, float, int, u64*,
                                      face_t*, u32*, u32*, u64*);
-template __global__ void k_seams<0>(Geom, const face_t*, u64*, u32*, u8*, u64*, u32*, u8*, int64_t, int64_t);
+template __global__ void k_seams<0>(Geom, const face_t*, u64*, u32*, u8*, u64*, u32*, u8*, int64_t, int64_t, const u32*);
 template __global__ void k_stitch<false>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_stitch<true>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_finalize<false>(Geom, const u32*, u32*, const u64*, const u64*, const u64*, const u64*, int64_t, u64*);

@@ -55,7 +55,7 @@ struct cc_ctx {
     // workspace
     DevBuf tiles, bstat, bparam, bits, faces, count, rc, roff, P, KR, FIN, keys, keys2, vals, vals2, seg,
         values, offsets, lut, cub_tmp, scalars, scalars2, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2,
-        flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf, spec,
+        flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf, spec, mark,
         ev_main, ev_z, ev_seg, ev_gt, ev_flag, ev_part;   // evaluation (cc_eval.hip)
     int64_t ev_cap = 0;      // entries per evaluation hash table of the last cc_evaluate
     int64_t rl_cap = 0;      // id-set slots of the last cc_relabel_consecutive
@@ -259,7 +259,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             launch_on(c, q, "k_seams", [&] {
                 k_seams<0><<<(unsigned)((t1 - t0 + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, q>>>(
                     g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), c->big.as<u8>(), c->ipairs.as<u64>(),
-                    c->ipc.as<u32>(), c->iovf.as<u8>(), t0, t1);
+                    c->ipc.as<u32>(), c->iovf.as<u8>(), t0, t1, nullptr);
             });
         };
         clear_seams();
@@ -306,9 +306,21 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
                 if (mask) k_fix<true><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, in, mask, thr, mode, BITS, FACES, COUNT, P, KR);
                 else k_fix<false><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR);
             });
-            if (lds_seams) {            // relabelled faces: all seams again
-                clear_seams();
-                seams(s, 0, nt);
+            if (lds_seams) {
+                // relabelled faces: the seams of the relabelled tiles and of the tiles above /
+                // beside them again (their lists are overwritten; stale overflow flags only send
+                // work to the global fallback, which reads the current faces)
+                c->mark.ensure((size_t)(nt + 1 + std::min<int64_t>(nt, 14 * (int64_t)nfix)) * sizeof(u32));
+                u32* flag = c->mark.as<u32>();
+                u32* list = flag + nt;
+                HIP_OK(hipMemsetAsync(flag, 0, (nt + 1) * sizeof(u32), s));
+                launch(c, "k_mark_seams", [&] { k_mark_seams<<<grid1d(14 * (int64_t)nfix), 256, 0, s>>>(g, FIX, flag, list); });
+                const int64_t nl = std::min<int64_t>(nt, 14 * (int64_t)nfix);
+                launch(c, "k_seams", [&] {
+                    k_seams<0><<<(unsigned)((nl + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(
+                        g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), c->big.as<u8>(), c->ipairs.as<u64>(),
+                        c->ipc.as<u32>(), c->iovf.as<u8>(), 0, 0, list);
+                });
             }
         }
     }
@@ -577,7 +589,11 @@ static void run_pipeline(cc_ctx* c, const float* in, const uint8_t* mask, const 
 
 extern "C" {
 
-const char* cc_version(void) { return "cc_mi355x 0.1 gfx950"; }
+#ifndef CC_SRC_HASH
+#define CC_SRC_HASH "unknown"
+#endif
+// "src=" carries the SHA-256 prefix of the sources this library was built from (build.py)
+const char* cc_version(void) { return "cc_mi355x 0.2 gfx950 src=" CC_SRC_HASH; }
 
 const char* cc_last_error(void) { return g_err.c_str(); }
 
@@ -607,7 +623,7 @@ void cc_destroy(cc_ctx* c) {
                       &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
                       &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
-                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec,
+                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec, &c->mark,
                       &c->ev_main, &c->ev_z, &c->ev_seg, &c->ev_gt, &c->ev_flag, &c->ev_part};
     for (DevBuf* b : bufs) b->release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
@@ -793,3 +809,4 @@ int cc_get_profile(cc_ctx* c, char* names, int names_cap, int64_t* counts, doubl
 #include "cc_stage_host.hip"
 #include "cc_eval.hip"
 #include "cc_relabel.hip"
+#include "cc_n5_host.hpp"

@@ -173,6 +173,12 @@ int cc_relabel_consecutive(cc_ctx* c, const uint64_t* labels, uint64_t* out, int
             HIP_OK(hipMemcpyAsync(&first, sorted, sizeof(u64), hipMemcpyDeviceToHost, s));
             sync(c);
             const u64 start = first == 0 ? 0 : 1;
+            c->rl_cap = cap;
+            *n_unique = (uint64_t)nu;
+            *start_label = start;
+            // the table does not fit the caller's buffer: report its size and leave out_dev
+            // untouched (an in-place call must not lose the ids before the table is returned)
+            if (uniques_host && cap_host < nu) return 0;
             launch(c, "k_rl_assign", [&] {
                 k_rl_assign<<<grid1d(nu), 256, 0, s>>>(sorted, nu, start, keys, (u64)cap - 1, vals);
             });
@@ -181,9 +187,6 @@ int cc_relabel_consecutive(cc_ctx* c, const uint64_t* labels, uint64_t* out, int
                 HIP_OK(hipMemcpyAsync(uniques_host, sorted, std::min<int64_t>(cap_host, nu) * sizeof(u64),
                                       hipMemcpyDeviceToHost, s));
             sync(c);
-            c->rl_cap = cap;
-            *n_unique = (uint64_t)nu;
-            *start_label = start;
             return 0;
         }
     })

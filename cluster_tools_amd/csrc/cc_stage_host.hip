@@ -122,7 +122,7 @@ int cc_write(cc_ctx* c, uint64_t* labels, const int64_t shape[3], const int64_t 
 }
 
 int cc_generate_boundary_map(cc_ctx* c, float* out, const int64_t shape[3], const int64_t origin[3],
-                             uint64_t seed) {
+                             uint64_t seed, int dither) {
     CC_TRY({
         CC_REQUIRE(c && out && shape, "NULL argument");
         HIP_OK(hipSetDevice(c->device));
@@ -133,7 +133,7 @@ int cc_generate_boundary_map(cc_ctx* c, float* out, const int64_t shape[3], cons
         CC_REQUIRE(shape[1] * nxb < (1LL << 24) && shape[0] < 65536, "volume too large for the generator grid");
         const dim3 grid((unsigned)(shape[1] * nxb), (unsigned)shape[0]);
         launch(c, "k_generate", [&] {
-            k_generate<<<grid, 256, 0, c->stream>>>(out, shape[0], shape[1], shape[2], o[0], o[1], o[2], seed);
+            k_generate<<<grid, 256, 0, c->stream>>>(out, shape[0], shape[1], shape[2], o[0], o[1], o[2], seed, dither);
         });
         sync(c);
     })

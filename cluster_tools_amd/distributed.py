@@ -130,26 +130,56 @@ def slab_bounds(Z, bz, world):
 class ShardedLabeler:
     """This rank's share of a z-slab sharded labelling run (ctx: _lib.Context of this GPU)."""
 
-    def __init__(self, ctx, global_shape, block_shape, z0, zs, device, comm=None):
+    def __init__(self, ctx, global_shape, block_shape, z0, zs, device, comm=None, force_form=None):
         import torch
         check_slabs(global_shape, block_shape, z0, zs)
         self.ctx, self.device = ctx, device
         self.gshape, self.block_shape = tuple(global_shape), tuple(block_shape)
         self.z0, self.zs = z0, zs
         self.comm = comm if comm is not None else TorchComm(device=device)
+        # The library enqueues on the ctx's stream and returns; the collectives run behind torch's
+        # current stream (ProcessGroupNCCL orders its stream after it, StagedComm's .cpu() syncs
+        # it).  Binding the ctx to that stream orders the seam planes and pairs with the
+        # collectives in both directions.
+        if device is not None and torch.device(device).type == 'cuda':
+            ctx.set_stream(torch.cuda.current_stream(device).cuda_stream)
         Y, X = global_shape[1], global_shape[2]
         r, w = self.comm.rank, self.comm.world
         self.bottom = torch.empty((Y, X), dtype=torch.int64, device=device) if r > 0 else None
         # the plane crossing xGMI: one uint32 per 2x2 cube ((id - id_base + 1) << 4 | voxel bits,
         # 1/4 of the voxel plane's bytes) when the tile origins are even, else one uint32 per
-        # voxel (id - id_base + 1, half the bytes of the uint64 ids)
+        # voxel (id - id_base + 1, half the bytes of the uint64 ids); slabs with too many ids
+        # for these forms fall back to the next wider one (decided from the allgathered sums,
+        # so every rank picks the same form)
         nby, nbx = -(-Y // block_shape[1]), -(-X // block_shape[2])
-        self.cubes = ((nby == 1 or block_shape[1] % 2 == 0) and (nbx == 1 or block_shape[2] % 2 == 0))
-        pshape = ((Y + 1) // 2, (X + 1) // 2) if self.cubes else (Y, X)
-        self.upper = torch.empty(pshape, dtype=torch.int32, device=device) if r > 0 else None
-        self.top = torch.empty(pshape, dtype=torch.int32, device=device) if r + 1 < w else None
+        self.cubes_ok = ((nby == 1 or block_shape[1] % 2 == 0) and (nbx == 1 or block_shape[2] % 2 == 0))
         self.pairs = torch.empty((Y * X, 2), dtype=torch.int64, device=device) if r > 0 else None
+        self._planes = {}
         self.sums = None
+        self.form = None
+        self.force_form = force_form          # tests: a wider seam-plane form than the ids need
+
+    def _plane(self, form, which):
+        """send / receive buffer of a seam-plane form ('cubes32', 'voxel32', 'voxel64')."""
+        import torch
+        r, w = self.comm.rank, self.comm.world
+        if (which == 'top' and r + 1 >= w) or (which == 'upper' and r == 0):
+            return None
+        key = (form, which)
+        if key not in self._planes:
+            Y, X = self.gshape[1], self.gshape[2]
+            shape = ((Y + 1) // 2, (X + 1) // 2) if form == 'cubes32' else (Y, X)
+            dt = torch.int64 if form == 'voxel64' else torch.int32
+            self._planes[key] = torch.empty(shape, dtype=dt, device=self.device)
+        return self._planes[key]
+
+    @staticmethod
+    def seam_form(cubes_ok, max_sum):
+        if cubes_ok and max_sum < 2 ** 28 - 2:
+            return 'cubes32'
+        if max_sum < 2 ** 32 - 2:
+            return 'voxel32'
+        return 'voxel64'
 
     def label(self, x, threshold, mode='greater', mask=None, out=None):
         import torch
@@ -159,30 +189,40 @@ class ShardedLabeler:
         s = ctx.shard_begin(x, self.block_shape, threshold, mode, self.z0, mask)
         self.sums = comm.allgather_int(s)
         base = sum(self.sums[:comm.rank])
-        if max(self.sums) >= (2 ** 28 if self.cubes else 2 ** 32) - 2:
-            raise RuntimeError('a slab holds too many ids for the 32-bit seam plane')
+        form = self.form = self.force_form or self.seam_form(self.cubes_ok, max(self.sums))
         ctx.shard_assign(base)
-        ctx.shard_planes(self.bottom, None)
-        if self.top is not None:
-            (ctx.shard_top_cubes32 if self.cubes else ctx.shard_top_plane32)(self.top)
-        comm.shift_up(self.top, self.upper)
+        top, upper = self._plane(form, 'top'), self._plane(form, 'upper')
+        if form == 'voxel64':
+            ctx.shard_planes(self.bottom, top)
+        else:
+            ctx.shard_planes(self.bottom, None)
+            if top is not None:
+                (ctx.shard_top_cubes32 if form == 'cubes32' else ctx.shard_top_plane32)(top)
+        comm.shift_up(top, upper)
         n = 0
         if comm.rank > 0:
             ubase = sum(self.sums[:comm.rank - 1])
-            n = (ctx.seam_pairs_cubes32(self.upper, ubase, self.bottom, self.pairs) if self.cubes
-                 else ctx.seam_pairs32(self.upper, ubase, self.bottom, self.pairs))
+            if form == 'cubes32':
+                n = ctx.seam_pairs_cubes32(upper, ubase, self.bottom, self.pairs)
+            elif form == 'voxel32':
+                n = ctx.seam_pairs32(upper, ubase, self.bottom, self.pairs)
+            else:
+                n = ctx.seam_pairs(upper, self.bottom, self.pairs)
         allp, np_ = comm.allgather_pairs(self.pairs, n)
         res = ctx.shard_finish(allp, np_, out)
         res['n_labels'] = sum(self.sums) + 1
         res['max_id'] = res['n_labels'] - 1
         res['id_base'] = base
+        res['seam_form'] = form
         return res
 
 
-def label_slabs_single_process(ctxs, x, block_shape, threshold, mode='greater', mask=None, bounds=None):
+def label_slabs_single_process(ctxs, x, block_shape, threshold, mode='greater', mask=None, bounds=None,
+                               form=None):
     """The same schedule for several slabs on ONE device, phase by phase in one process (the
     collectives become list operations).  Used to test the sharded algorithm on one GPU.
-    ctxs: one _lib.Context per slab.  Returns (labels, per-slab results, luts)."""
+    ctxs: one _lib.Context per slab.  form: the seam-plane form ('cubes32', 'voxel32', 'voxel64';
+    default: what ShardedLabeler picks).  Returns (labels, per-slab results, sums, luts)."""
     import torch
     Z, Y, X = x.shape
     bounds = bounds or slab_bounds(Z, block_shape[0], len(ctxs))
@@ -191,20 +231,41 @@ def label_slabs_single_process(ctxs, x, block_shape, threshold, mode='greater', 
     for ctx, (z0, zs) in zip(ctxs, bounds):
         m = None if mask is None else mask[z0:z0 + zs]
         sums.append(ctx.shard_begin(x[z0:z0 + zs], block_shape, threshold, mode, z0, m))
+    nby, nbx = -(-Y // block_shape[1]), -(-X // block_shape[2])
+    cubes_ok = (nby == 1 or block_shape[1] % 2 == 0) and (nbx == 1 or block_shape[2] % 2 == 0)
+    form = form or ShardedLabeler.seam_form(cubes_ok, max(sums))
+    if form == 'cubes32' and not cubes_ok:
+        raise ValueError('cubes32 seam planes need even block_shape[1:]')
     tops, bottoms = [], []
     for r, ctx in enumerate(ctxs):
         ctx.shard_assign(sum(sums[:r]))
         b = torch.empty((Y, X), dtype=torch.int64, device=x.device) if r > 0 else None
-        t = torch.empty((Y, X), dtype=torch.int64, device=x.device) if r + 1 < len(ctxs) else None
-        ctx.shard_planes(b, t)
+        t = None
+        if r + 1 < len(ctxs):
+            if form == 'voxel64':
+                t = torch.empty((Y, X), dtype=torch.int64, device=x.device)
+            elif form == 'voxel32':
+                t = torch.empty((Y, X), dtype=torch.int32, device=x.device)
+            else:
+                t = torch.empty(((Y + 1) // 2, (X + 1) // 2), dtype=torch.int32, device=x.device)
+        ctx.shard_planes(b, t if form == 'voxel64' else None)
+        if t is not None and form != 'voxel64':
+            (ctx.shard_top_cubes32 if form == 'cubes32' else ctx.shard_top_plane32)(t)
         bottoms.append(b)
         tops.append(t)
+    torch.cuda.synchronize(x.device)     # each ctx has its own stream: tops complete before r + 1 reads
     allp = []
     for r, ctx in enumerate(ctxs):
         if r == 0:
             continue
         pairs = torch.empty((Y * X, 2), dtype=torch.int64, device=x.device)
-        n = ctx.seam_pairs(tops[r - 1], bottoms[r], pairs)
+        ubase = sum(sums[:r - 1])
+        if form == 'cubes32':
+            n = ctx.seam_pairs_cubes32(tops[r - 1], ubase, bottoms[r], pairs)
+        elif form == 'voxel32':
+            n = ctx.seam_pairs32(tops[r - 1], ubase, bottoms[r], pairs)
+        else:
+            n = ctx.seam_pairs(tops[r - 1], bottoms[r], pairs)
         allp.append(pairs[:n])
     allp = torch.cat(allp) if allp else torch.zeros((0, 2), dtype=torch.int64, device=x.device)
     res = []

@@ -15,14 +15,11 @@ z5py-written file exists in this container to check byte layouts against):
     truncated), followed by the big-endian C-order payload, gzip-compressed;
   * a missing chunk reads as the fill value 0.
 
-Chunk (de)compression runs in a thread pool (zlib releases the GIL).
+Chunk coding is native (cc_n5_read / cc_n5_write in libcc_mi355x.so: host C++ with zlib,
+chunks spread over host threads), as z5py's is in the reference; it needs no GPU.
 """
 import json
 import os
-import struct
-import zlib
-from concurrent.futures import ThreadPoolExecutor
-from itertools import product
 
 import numpy as np
 
@@ -75,7 +72,7 @@ class Attributes:
 
 
 class Dataset:
-    def __init__(self, path, n_threads=8):
+    def __init__(self, path, n_threads=None):
         self.path = path
         meta = _read_json(os.path.join(path, 'attributes.json'))
         self.shape = tuple(int(v) for v in meta['dimensions'][::-1])
@@ -84,56 +81,52 @@ class Dataset:
         self.compression = meta.get('compression', {'type': 'raw'}).get('type', 'raw')
         self.level = meta.get('compression', {}).get('level', 5)
         self.attrs = Attributes(path, reserved=True)
-        self.n_threads = n_threads
+        self.n_threads = n_threads or min(16, len(os.sched_getaffinity(0)))
         self.ndim = len(self.shape)
 
     @property
     def size(self):
         return int(np.prod(self.shape))
 
-    # ---- chunk level ----
-    def _chunk_path(self, cid):
-        return os.path.join(self.path, *[str(c) for c in cid[::-1]])
+    # ---- native codec (libcc_mi355x.so cc_n5_read / cc_n5_write, host C++ + zlib) ----
+    def _region(self, box):
+        return [b for b, _ in box], [e for _, e in box]
+
+    def read_region(self, box):
+        """C-order array of the region [(b, e), ...] (missing chunks read as 0)."""
+        from . import _lib
+        beg, end = self._region(box)
+        out = np.empty(tuple(e - b for b, e in box), dtype=self.dtype)
+        _lib.n5_read(self.path, self.shape, self.chunks, self.dtype.itemsize, self.compression, beg, end, out,
+                     self.n_threads)
+        return out
+
+    def write_region(self, box, value, skip_zero_chunks=False):
+        from . import _lib
+        beg, end = self._region(box)
+        value = np.ascontiguousarray(np.broadcast_to(np.asarray(value, dtype=self.dtype),
+                                                     tuple(e - b for b, e in box)))
+        _lib.n5_write(self.path, self.shape, self.chunks, self.dtype.itemsize, self.compression, self.level,
+                      beg, end, value, self.n_threads, skip_zero_chunks)
 
     def _chunk_box(self, cid):
         beg = [c * s for c, s in zip(cid, self.chunks)]
         end = [min(b + s, sh) for b, s, sh in zip(beg, self.chunks, self.shape)]
         return beg, end
 
+    def chunk_exists(self, cid):
+        return os.path.exists(os.path.join(self.path, *[str(c) for c in cid[::-1]]))
+
     def read_chunk(self, cid):
-        p = self._chunk_path(cid)
-        beg, end = self._chunk_box(cid)
-        shape = tuple(e - b for b, e in zip(beg, end))
-        if not os.path.exists(p):
+        """One chunk (None if its file is absent)."""
+        if not self.chunk_exists(cid):
             return None
-        with open(p, 'rb') as f:
-            buf = f.read()
-        mode, ndim = struct.unpack('>HH', buf[:4])
-        dims = struct.unpack('>' + 'I' * ndim, buf[4:4 + 4 * ndim])[::-1]
-        off = 4 + 4 * ndim + (4 if mode == 1 else 0)
-        raw = buf[off:]
-        if self.compression == 'gzip':
-            raw = zlib.decompress(raw, 47)          # gzip or zlib header, auto-detected
-        elif self.compression != 'raw':
-            raise NotImplementedError('n5 compression %s' % self.compression)
-        a = np.frombuffer(raw, dtype=self.dtype.newbyteorder('>')).reshape(dims)
-        a = a.astype(self.dtype, copy=False)
-        if tuple(dims) != shape:                     # z5py may store full-size edge chunks
-            a = a[tuple(slice(0, s) for s in shape)]
-        return a
+        beg, end = self._chunk_box(cid)
+        return self.read_region(list(zip(beg, end)))
 
     def write_chunk(self, cid, data):
-        p = self._chunk_path(cid)
-        os.makedirs(os.path.dirname(p), exist_ok=True)
-        data = np.ascontiguousarray(data, dtype=self.dtype.newbyteorder('>'))
-        head = struct.pack('>HH', 0, data.ndim) + struct.pack('>' + 'I' * data.ndim, *data.shape[::-1])
-        payload = data.tobytes()
-        if self.compression == 'gzip':
-            c = zlib.compressobj(self.level, zlib.DEFLATED, 31)
-            payload = c.compress(payload) + c.flush()
-        with open(p + '.tmp', 'wb') as f:
-            f.write(head + payload)
-        os.replace(p + '.tmp', p)
+        beg, end = self._chunk_box(cid)
+        self.write_region(list(zip(beg, end)), data)
 
     # ---- array level ----
     def _norm(self, key):
@@ -145,57 +138,18 @@ class Dataset:
         key = key + (slice(None),) * (self.ndim - len(key))
         out = []
         for k, s in zip(key, self.shape):
-            if isinstance(k, int):
-                k = slice(k, k + 1)
+            if isinstance(k, (int, np.integer)):
+                k = slice(int(k), int(k) + 1)
             b, e, st = k.indices(s)
             assert st == 1, 'strided n5 access is not supported'
-            out.append((b, e))
+            out.append((b, max(b, e)))
         return out
-
-    def _chunk_ids(self, box):
-        ranges = [range(b // c, (e - 1) // c + 1) if e > b else range(0) for (b, e), c in zip(box, self.chunks)]
-        return list(product(*ranges))
 
     def __getitem__(self, key):
-        box = self._norm(key)
-        out = np.zeros(tuple(e - b for b, e in box), dtype=self.dtype)
-
-        def one(cid):
-            a = self.read_chunk(cid)
-            if a is None:
-                return
-            cb, ce = self._chunk_box(cid)
-            src, dst = [], []
-            for (b, e), x0, x1 in zip(box, cb, ce):
-                lo, hi = max(b, x0), min(e, x1)
-                src.append(slice(lo - x0, hi - x0))
-                dst.append(slice(lo - b, hi - b))
-            out[tuple(dst)] = a[tuple(src)]
-        with ThreadPoolExecutor(self.n_threads) as tp:
-            list(tp.map(one, self._chunk_ids(box)))
-        return out
+        return self.read_region(self._norm(key))
 
     def __setitem__(self, key, value):
-        box = self._norm(key)
-        value = np.broadcast_to(np.asarray(value, dtype=self.dtype), tuple(e - b for b, e in box))
-
-        def one(cid):
-            cb, ce = self._chunk_box(cid)
-            src, dst, full = [], [], True
-            for (b, e), x0, x1 in zip(box, cb, ce):
-                lo, hi = max(b, x0), min(e, x1)
-                src.append(slice(lo - b, hi - b))
-                dst.append(slice(lo - x0, hi - x0))
-                full &= lo == x0 and hi == x1
-            if full:
-                chunk = value[tuple(src)]
-            else:
-                chunk = self.read_chunk(cid)
-                chunk = np.zeros(tuple(e - b for b, e in zip(cb, ce)), self.dtype) if chunk is None else chunk.copy()
-                chunk[tuple(dst)] = value[tuple(src)]
-            self.write_chunk(cid, chunk)
-        with ThreadPoolExecutor(self.n_threads) as tp:
-            list(tp.map(one, self._chunk_ids(box)))
+        self.write_region(self._norm(key), value)
 
 
 class Group:
@@ -236,6 +190,8 @@ class Group:
         chunks = tuple(int(c) for c in (chunks or shape))
         p = self._p(key)
         os.makedirs(p, exist_ok=True)
+        if compression not in ('gzip', 'raw', None):
+            raise NotImplementedError('n5 compression %s' % compression)
         comp = {'type': 'gzip', 'level': level} if compression == 'gzip' else {'type': 'raw'}
         meta = _read_json(os.path.join(p, 'attributes.json'))
         meta.update({'dimensions': list(shape[::-1]), 'blockSize': list(chunks[::-1]),

@@ -54,7 +54,8 @@ void        cc_destroy(cc_ctx* ctx);
 const char* cc_last_error(void);
 /* use an existing hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL -> ctx's own */
 int         cc_set_stream(cc_ctx* ctx, void* hip_stream);
-/* library version string, e.g. "cc_mi355x 0.1 gfx950" */
+/* library version string, e.g. "cc_mi355x 0.2 gfx950 src=0123456789abcdef": src = SHA-256 prefix of
+ * the sources (csrc/ files, this header) the library was built from (binary provenance, build.py) */
 const char* cc_version(void);
 
 /* --- fused path: block_components -> merge_offsets -> block_faces ->
@@ -168,9 +169,11 @@ int64_t cc_seam_pairs_cubes32(cc_ctx* ctx, const uint32_t* upper_cubes_dev, uint
                               const uint64_t* lower_dev, int64_t Y, int64_t X, uint64_t* pairs_dev,
                               int64_t cap);
 
-/* --- synthetic benchmark input (oracle/synth.py is its restatement) --- */
+/* --- synthetic benchmark input (oracle/synth.py is its restatement) ---
+ * dither = 0: q / 256 (quantized); dither = 1: (q * 2^16 + 16-bit hash dither) / 2^24, the
+ * continuous variant (block extremes and threshold crossings no longer on a 2^-8 grid). */
 int cc_generate_boundary_map(cc_ctx* ctx, float* out_dev, const int64_t shape[3],
-                             const int64_t origin[3], uint64_t seed);
+                             const int64_t origin[3], uint64_t seed, int dither);
 
 /* --- instrumentation ---------------------------------------------------------- */
 /* Per-kernel HIP-event timing on the stream each kernel runs on: enable = 0 off, 1 every launch
@@ -215,11 +218,28 @@ int64_t cc_get_overlaps(cc_ctx* ctx, uint64_t* seg_ids, uint64_t* gt_ids, uint64
  * RelabelWorkflow (relabel/relabel_workflow.py:10-60; find_labeling.py:84-120): the sorted unique
  * ids of labels_dev get new ids start, start + 1, ... (start = 0 when id 0 occurs, else 1); the
  * volume mapped into out_dev (may alias labels_dev).  n uint64 device elements.  Returns the
- * number of unique ids and start; copies min(n_unique, cap) sorted unique ids to uniques_host
- * (nullable) -- the old ids of the assignment table, new id = index + start.  Id 2^64-1 is
- * reserved (error). */
+ * number of unique ids and start; copies the sorted unique ids to uniques_host (nullable) -- the
+ * old ids of the assignment table, new id = index + start.  If uniques_host is given and
+ * cap < n_unique, only n_unique / start are returned and out_dev is NOT written (safe for in-place
+ * calls: call again with cap >= n_unique).  Id 2^64-1 is reserved (error). */
 int cc_relabel_consecutive(cc_ctx* ctx, const uint64_t* labels_dev, uint64_t* out_dev, int64_t n,
                            uint64_t* n_unique, uint64_t* start_label, uint64_t* uniques_host, int64_t cap);
+
+/* --- N5 chunk codec (host only, no GPU) ---------------------------------------
+ * Replaces z5py, which the reference reaches through elf.io.open_file (volume_utils.py:21-22) for
+ * every ds[bb] read / write of the path (block_components.py:151,180, write.py:185-202,
+ * merge_assignments.py:136-139).  N5 layout: chunk file <dataset>/<i_fastest>/.../<i_slowest>,
+ * big-endian header (u16 mode, u16 ndim, u32 dims fastest first) and big-endian C-order payload,
+ * raw (compression 0) or gzip (1, deflate `level`).  Region [begin, end) (NULL = whole dataset) of
+ * a dataset of `shape` / `chunks` (C order, ndim 1..4), elem_size 1/2/4/8 bytes, host buffers in
+ * C order over the region.  Chunks are coded on n_threads host threads.  Read: missing chunks
+ * read as 0.  Write: partially covered chunks are read, merged and rewritten; skip_zero_chunks: an
+ * all-zero chunk that has no file yet is not written (the reference never writes empty blocks). */
+int cc_n5_read(const char* dataset_path, int ndim, const int64_t* shape, const int64_t* chunks, int elem_size,
+               int compression, const int64_t* begin, const int64_t* end, void* out_host, int n_threads);
+int cc_n5_write(const char* dataset_path, int ndim, const int64_t* shape, const int64_t* chunks, int elem_size,
+                int compression, int level, const int64_t* begin, const int64_t* end, const void* in_host,
+                int n_threads, int skip_zero_chunks);
 
 #ifdef __cplusplus
 }

@@ -57,7 +57,8 @@ static inline int64_t fdiv(int64_t a, int64_t b) { /* floor division, b > 0 */
     return (a % b != 0 && a < 0) ? q - 1 : q;
 }
 
-static uint8_t boundary_q_at(int64_t z, int64_t y, int64_t x, uint64_t seed) {
+/* q, and in *dither the 16-bit dither of the continuous variant (bits 16..31 of the noise hash) */
+static uint8_t boundary_q_at(int64_t z, int64_t y, int64_t x, uint64_t seed, uint32_t* dither) {
     int64_t cz = fdiv(z, PITCH), cy = fdiv(y, PITCH), cx = fdiv(x, PITCH);
     int64_t d1 = (int64_t)1 << 62, d2 = (int64_t)1 << 62;
     for (int dz = -1; dz <= 1; ++dz)
@@ -78,6 +79,7 @@ static uint8_t boundary_q_at(int64_t z, int64_t y, int64_t x, uint64_t seed) {
     uint64_t vkey = ((uint64_t)z << 42) | ((uint64_t)y << 21) | (uint64_t)x;
     uint64_t nh = splitmix64((seed + NOISE_SALT) ^ vkey);
     int64_t n = (int64_t)(nh % 33) - 16;
+    *dither = (uint32_t)((nh >> 16) & 0xFFFF);
     int64_t q = m + n;
     if (q < 0) q = 0;
     if (q > 255) q = 255;
@@ -86,7 +88,7 @@ static uint8_t boundary_q_at(int64_t z, int64_t y, int64_t x, uint64_t seed) {
 
 typedef struct {
     float* out; uint8_t* outq;
-    int64_t Z, Y, X, oz, oy, ox; uint64_t seed; int tid, nt;
+    int64_t Z, Y, X, oz, oy, ox; uint64_t seed; int tid, nt, dither;
 } gen_arg_t;
 
 static void* gen_worker(void* p) {
@@ -94,23 +96,25 @@ static void* gen_worker(void* p) {
     for (int64_t z = a->tid; z < a->Z; z += a->nt)
         for (int64_t y = 0; y < a->Y; ++y)
             for (int64_t x = 0; x < a->X; ++x) {
-                uint8_t q = boundary_q_at(z + a->oz, y + a->oy, x + a->ox, a->seed);
+                uint32_t d;
+                uint8_t q = boundary_q_at(z + a->oz, y + a->oy, x + a->ox, a->seed, &d);
                 int64_t i = (z * a->Y + y) * a->X + x;
-                if (a->out) a->out[i] = (float)q / 256.0f;
+                /* quantized: q / 256; continuous (dither): (q * 2^16 + d) / 2^24, exact in float32 */
+                if (a->out) a->out[i] = a->dither ? (float)((uint32_t)q * 65536u + d) / 16777216.0f : (float)q / 256.0f;
                 if (a->outq) a->outq[i] = q;
             }
     return NULL;
 }
 
-/* out (float32) and/or outq (uint8 q) may be NULL. */
+/* out (float32) and/or outq (uint8 q) may be NULL; dither != 0: the continuous variant. */
 void oracle_boundary_map(float* out, uint8_t* outq, int64_t Z, int64_t Y, int64_t X,
-                         int64_t oz, int64_t oy, int64_t ox, uint64_t seed, int n_threads) {
+                         int64_t oz, int64_t oy, int64_t ox, uint64_t seed, int n_threads, int dither) {
     if (n_threads < 1) n_threads = 1;
     pthread_t th[256];
     gen_arg_t args[256];
     if (n_threads > 256) n_threads = 256;
     for (int t = 0; t < n_threads; ++t) {
-        args[t] = (gen_arg_t){out, outq, Z, Y, X, oz, oy, ox, seed, t, n_threads};
+        args[t] = (gen_arg_t){out, outq, Z, Y, X, oz, oy, ox, seed, t, n_threads, dither};
         pthread_create(&th[t], NULL, gen_worker, &args[t]);
     }
     for (int t = 0; t < n_threads; ++t) pthread_join(th[t], NULL);

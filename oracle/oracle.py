@@ -26,7 +26,8 @@ def lib():
         L = ctypes.CDLL(_LIB_PATH)
         P = ctypes.c_void_p
         i64 = ctypes.c_int64
-        L.oracle_boundary_map.argtypes = [P, P, i64, i64, i64, i64, i64, i64, ctypes.c_uint64, ctypes.c_int]
+        L.oracle_boundary_map.argtypes = [P, P, i64, i64, i64, i64, i64, i64, ctypes.c_uint64, ctypes.c_int,
+                                          ctypes.c_int]
         L.oracle_boundary_map.restype = None
         L.oracle_label_volume.argtypes = [P, P, P, P, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                           P, P, P, P, P, P, i64, P, ctypes.c_int, P]
@@ -41,13 +42,14 @@ def _ptr(a):
     return None if a is None else a.ctypes.data
 
 
-def boundary_map(shape, origin=(0, 0, 0), seed=0x5EED, n_threads=8, as_q=False):
-    """Synthetic boundary map (oracle/synth.py definition), float32 or uint8 q."""
+def boundary_map(shape, origin=(0, 0, 0), seed=0x5EED, n_threads=8, as_q=False, dither=False):
+    """Synthetic boundary map (oracle/synth.py definition), float32 or uint8 q; dither: the
+    continuous variant (q * 2^16 + 16-bit dither) / 2^24."""
     shape = tuple(int(s) for s in shape)
     out = np.empty(shape, dtype=np.uint8 if as_q else np.float32)
     args = (None, out) if as_q else (out, None)
     lib().oracle_boundary_map(_ptr(args[0]), _ptr(args[1]), *shape, *[int(o) for o in origin],
-                              ctypes.c_uint64(seed), int(n_threads))
+                              ctypes.c_uint64(seed), int(n_threads), int(bool(dither)))
     return out
 
 

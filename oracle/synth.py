@@ -15,7 +15,10 @@ Definition (integer-only so CPU and GPU agree bit for bit):
   * noise n = splitmix64((seed + NOISE_SALT) ^ vkey) % 33 - 16 with
     vkey = (z<<42)|(y<<21)|x (independent of the volume shape, so any sub-box of
     a volume equals the same sub-box generated on its own);
-  * q = clamp(m + n, 0, 255); value = float32(q) / 256 (exact).
+  * q = clamp(m + n, 0, 255); value = float32(q) / 256 (exact);
+  * continuous variant (dither=True): d = (nh >> 16) & 0xFFFF and value = float32(q * 2^16 + d)
+    / 2^24 (exact), i.e. q / 256 plus a deterministic sub-2^-8 dither, so block extremes and
+    threshold crossings are no longer quantized.
 """
 import numpy as np
 
@@ -34,8 +37,8 @@ def splitmix64(x):
     return z ^ (z >> np.uint64(31))
 
 
-def boundary_q(shape, origin=(0, 0, 0), seed=MASTER_SEED):
-    """uint8 membrane strength q for the box [origin, origin+shape)."""
+def boundary_q(shape, origin=(0, 0, 0), seed=MASTER_SEED, with_dither=False):
+    """uint8 membrane strength q for the box [origin, origin+shape) (and the uint16 dither)."""
     Z, Y, X = shape
     z = np.arange(origin[0], origin[0] + Z, dtype=np.int64)[:, None, None]
     y = np.arange(origin[1], origin[1] + Y, dtype=np.int64)[None, :, None]
@@ -65,11 +68,17 @@ def boundary_q(shape, origin=(0, 0, 0), seed=MASTER_SEED):
     with np.errstate(over='ignore'):
         nh = splitmix64((seed64 + np.uint64(NOISE_SALT)) ^ vkey)
     n = (nh % np.uint64(33)).astype(np.int64) - 16
-    return np.clip(m + n, 0, 255).astype(np.uint8)
+    q = np.clip(m + n, 0, 255).astype(np.uint8)
+    if with_dither:
+        return q, ((nh >> np.uint64(16)) & np.uint64(0xFFFF)).astype(np.uint32)
+    return q
 
 
-def boundary_map(shape, origin=(0, 0, 0), seed=MASTER_SEED):
-    """float32 boundary map in [0, 255/256]."""
+def boundary_map(shape, origin=(0, 0, 0), seed=MASTER_SEED, dither=False):
+    """float32 boundary map in [0, 255/256] (dither: the continuous variant, below 1)."""
+    if dither:
+        q, d = boundary_q(shape, origin, seed, with_dither=True)
+        return (q.astype(np.uint32) * np.uint32(65536) + d).astype(np.float32) / np.float32(1 << 24)
     return boundary_q(shape, origin, seed).astype(np.float32) / np.float32(256)
 
 

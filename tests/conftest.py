@@ -29,6 +29,17 @@ def load_golden(name):
     return out
 
 
+@pytest.fixture(scope='session', autouse=True)
+def _library_provenance():
+    """On a GPU box, refuse to test a libcc_mi355x.so built from other sources than this tree's
+    (cc_version() carries the source hash build.py embedded)."""
+    import torch
+    if torch.cuda.is_available():
+        from cluster_tools_amd import _lib
+        _lib.check_provenance()
+    yield
+
+
 @pytest.fixture(scope='session')
 def ctx():
     import torch

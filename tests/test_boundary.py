@@ -71,3 +71,9 @@ def test_device_mask_generator_matches_oracle(gshape, z0, nz):
     got = ellipsoid_mask_device(gshape, z0, nz, torch.device('cpu'), chunk=7).numpy()
     ref = ellipsoid_mask(gshape)[z0:z0 + nz]
     assert np.array_equal(got, ref)
+
+
+def test_binary_provenance():
+    """The library in the tree was built from the tree's sources (cc_version's src= hash)."""
+    from cluster_tools_amd import _lib, build
+    assert _lib.check_provenance() == build.source_hash()

@@ -97,7 +97,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, shape, block_shape, thr, mode, result_dir):
+def _worker(rank, world, port, shape, block_shape, thr, mode, result_dir, form=None):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
@@ -105,7 +105,7 @@ def _worker(rank, world, port, shape, block_shape, thr, mode, result_dir):
     x = O.boundary_map(shape, n_threads=1)
     z0, zs = slab_bounds(shape[0], block_shape[0], world)[rank]
     lab = ShardedLabeler(FakeShardCtx(), shape, block_shape, z0, zs, device=None,
-                         comm=TorchComm(device=None))
+                         comm=TorchComm(device=None), force_form=form)
     out = torch.empty((zs,) + tuple(shape[1:]), dtype=torch.int64)
     res = lab.label(torch.from_numpy(x[z0:z0 + zs].copy()), thr, mode, out=out)
     np.save(os.path.join(result_dir, 'slab_%d.npy' % rank), out.numpy())
@@ -117,15 +117,29 @@ def _worker(rank, world, port, shape, block_shape, thr, mode, result_dir):
     (2, (32, 70, 90), (16, 32, 32), 'greater'),
     (2, (32, 70, 90), (8, 40, 48), 'less'),
     (3, (40, 64, 64), (8, 32, 32), 'less'),
+    (2, (32, 70, 90), (16, 32, 32), 'voxel32'),     # seam-plane fallbacks for slabs with many ids
+    (3, (40, 64, 64), (8, 32, 32), 'voxel64'),
 ])
 def test_gloo_sharded_schedule_matches_oracle(tmp_path, world, shape, block_shape, mode):
     port = _free_port()
-    mp.spawn(_worker, args=(world, port, shape, block_shape, 0.5, mode, str(tmp_path)), nprocs=world, join=True)
+    form = None
+    if mode.startswith('voxel'):
+        form, mode = mode, 'less'
+    mp.spawn(_worker, args=(world, port, shape, block_shape, 0.5, mode, str(tmp_path), form), nprocs=world,
+             join=True)
     got = np.concatenate([np.load(str(tmp_path / ('slab_%d.npy' % r))) for r in range(world)]).astype(np.uint64)
     ref = O.label_volume(O.boundary_map(shape, n_threads=1), block_shape, 0.5, mode)
     np.testing.assert_array_equal(got, ref['labels'])
     for r in range(world):
         assert int(np.load(str(tmp_path / ('nl_%d.npy' % r)))[0]) == ref['n_labels']
+
+
+def test_seam_form_choice():
+    from cluster_tools_amd.distributed import ShardedLabeler as S
+    assert S.seam_form(True, 2 ** 28 - 3) == 'cubes32'
+    assert S.seam_form(True, 2 ** 28 - 2) == 'voxel32'
+    assert S.seam_form(False, 5) == 'voxel32'
+    assert S.seam_form(True, 2 ** 32 - 2) == 'voxel64'
 
 
 def test_slab_bounds():

@@ -53,3 +53,93 @@ def test_missing_chunks_read_as_zero(tmp_path):
         ds = f.require_dataset('seg', shape=(10, 10, 10), dtype='uint64', chunks=(5, 5, 5))
         ds[0:5, 0:5, 0:5] = 7
         assert ds[:].sum() == 7 * 125
+
+
+def _write_chunk_py(path, data, mode=0, full_dims=None):
+    """An N5 chunk written independently of the library (python gzip + struct, N5 spec)."""
+    import gzip as gz
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    dims = full_dims or data.shape
+    head = struct.pack('>HH', mode, data.ndim) + struct.pack('>' + 'I' * data.ndim, *dims[::-1])
+    if mode == 1:
+        head += struct.pack('>I', data.size)
+    with open(path, 'wb') as f:
+        f.write(head + gz.compress(np.ascontiguousarray(data, dtype=data.dtype.newbyteorder('>')).tobytes()))
+
+
+def test_native_reads_independently_written_chunks(tmp_path):
+    """Chunks written by python's gzip module (default mode, varlength mode, a full-size edge chunk)
+    decode through the native codec."""
+    p = str(tmp_path / 'z.n5')
+    with n5.open_file(p) as f:
+        ds = f.create_dataset('v', shape=(5, 6, 7), dtype='uint32', chunks=(4, 4, 4), compression='gzip')
+    a = (np.arange(5 * 6 * 7, dtype='uint32') * 2654435761 % 1000003).reshape(5, 6, 7)
+    root = os.path.join(p, 'v')
+    _write_chunk_py(os.path.join(root, '0', '0', '0'), a[0:4, 0:4, 0:4])
+    _write_chunk_py(os.path.join(root, '1', '0', '0'), a[0:4, 0:4, 4:7], mode=1)
+    full = np.zeros((4, 4, 4), dtype='uint32')
+    full[:1, :2, :3] = a[4:5, 4:6, 4:7]
+    _write_chunk_py(os.path.join(root, '1', '1', '1'), full, full_dims=(4, 4, 4))
+    got = ds[:]
+    ref = np.zeros_like(a)
+    ref[0:4, 0:4, 0:7] = a[0:4, 0:4, 0:7]
+    ref[4:5, 4:6, 4:7] = a[4:5, 4:6, 4:7]
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_one_and_four_dimensional_datasets(tmp_path):
+    p = str(tmp_path / 'w.n5')
+    lut = (np.arange(100003, dtype=np.uint64) * 7) ^ np.uint64(1 << 40)
+    x4 = np.random.default_rng(1).random((3, 9, 10, 11)).astype(np.float32)
+    with n5.open_file(p) as f:
+        f.create_dataset('assignments', data=lut, chunks=(65334,), compression='gzip')
+        f.create_dataset('raw4', data=x4, chunks=(1, 4, 5, 6), compression='raw')
+    with n5.open_file(p, 'r') as f:
+        np.testing.assert_array_equal(f['assignments'][:], lut)
+        np.testing.assert_array_equal(f['assignments'][65000:70000], lut[65000:70000])
+        np.testing.assert_array_equal(f['raw4'][1:3, 2:9, :, 5:11], x4[1:3, 2:9, :, 5:11])
+    # raw chunk payload is big-endian float32 after a 4 + 4*4 byte header
+    buf = open(os.path.join(p, 'raw4', '0', '0', '0', '0'), 'rb').read()
+    np.testing.assert_array_equal(np.frombuffer(buf[20:], dtype='>f4').reshape(1, 4, 5, 6), x4[0:1, 0:4, 0:5, 0:6])
+
+
+def test_skip_zero_chunks_and_overwrite(tmp_path):
+    """All-zero chunks are not created (the reference never writes empty blocks), but an existing
+    chunk that becomes zero is rewritten."""
+    p = str(tmp_path / 's.n5')
+    with n5.open_file(p) as f:
+        ds = f.create_dataset('seg', shape=(8, 8, 8), dtype='uint64', chunks=(4, 4, 4), compression='gzip')
+        a = np.zeros((8, 8, 8), dtype=np.uint64)
+        a[0, 0, 0] = 5
+        ds.write_region([(0, 8)] * 3, a, skip_zero_chunks=True)
+        assert ds.chunk_exists((0, 0, 0)) and not ds.chunk_exists((1, 1, 1))
+        ds.write_region([(0, 8)] * 3, np.zeros_like(a), skip_zero_chunks=True)
+        assert ds.chunk_exists((0, 0, 0))
+        assert ds[:].sum() == 0
+
+
+def test_threads_give_identical_files(tmp_path):
+    a = np.random.default_rng(2).integers(0, 50, (37, 41, 43)).astype(np.uint64)
+    blobs = []
+    for nt in (1, 7):
+        p = str(tmp_path / ('t%d.n5' % nt))
+        with n5.open_file(p) as f:
+            ds = f.create_dataset('seg', shape=a.shape, dtype='uint64', chunks=(8, 16, 16), compression='gzip')
+            ds.n_threads = nt
+            ds[:] = a
+            np.testing.assert_array_equal(ds[:], a)
+        blobs.append(open(os.path.join(p, 'seg', '2', '1', '4'), 'rb').read())
+    assert blobs[0] == blobs[1]
+
+
+def test_corrupt_chunk_raises(tmp_path):
+    import pytest
+    p = str(tmp_path / 'c.n5')
+    with n5.open_file(p) as f:
+        ds = f.create_dataset('seg', shape=(4, 4, 4), dtype='uint64', chunks=(4, 4, 4), compression='gzip')
+        ds[:] = 1
+    path = os.path.join(p, 'seg', '0', '0', '0')
+    buf = open(path, 'rb').read()
+    open(path, 'wb').write(buf[:-9])
+    with pytest.raises(RuntimeError):
+        n5.open_file(p, 'r')['seg'][:]

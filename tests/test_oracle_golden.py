@@ -50,6 +50,11 @@ def test_generator_c_matches_numpy():
     from oracle.synth import boundary_map
     for shape, origin in [((20, 37, 50), (0, 0, 0)), ((9, 40, 70), (31, 63, 95))]:
         np.testing.assert_array_equal(O.boundary_map(shape, origin, n_threads=2), boundary_map(shape, origin))
+        d = O.boundary_map(shape, origin, n_threads=2, dither=True)
+        np.testing.assert_array_equal(d, boundary_map(shape, origin, dither=True))
+        # the dither stays below one quantization step and does not move q
+        q = O.boundary_map(shape, origin, n_threads=2)
+        assert np.all((d >= q) & (d < q + np.float32(1 / 256)))
 
 
 def test_oracle_threads_invariant():

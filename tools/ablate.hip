@@ -81,7 +81,7 @@ int main(int argc, char** argv) {
         HIP_OK(hipMalloc(&out, nvox * 8));
         {
             const int64_t nxb = (shape[2] + 255) / 256;
-            k_generate<<<dim3((unsigned)(shape[1] * nxb), (unsigned)shape[0]), 256, 0, s>>>(in, shape[0], shape[1], shape[2], 0, 0, 0, 0x5EED);
+            k_generate<<<dim3((unsigned)(shape[1] * nxb), (unsigned)shape[0]), 256, 0, s>>>(in, shape[0], shape[1], shape[2], 0, 0, 0, 0x5EED, 0);
         }
         u32 *st, *COUNT, *P;
         face_t* FACES;
@@ -164,7 +164,7 @@ int main(int argc, char** argv) {
             HIP_OK(hipMemset(big, 0, nb));
             HIP_OK(hipMemset(iovf, 0, nt));
             const unsigned sg = (unsigned)((nt + SP_WAVES - 1) / SP_WAVES);
-#define SEAMS(V) k_seams<V><<<sg, SP_WAVES * 64, 0, s>>>(g, FACES, pairs, pc, big, ipairs, ipc, iovf, 0, nt)
+#define SEAMS(V) k_seams<V><<<sg, SP_WAVES * 64, 0, s>>>(g, FACES, pairs, pc, big, ipairs, ipc, iovf, 0, nt, nullptr)
             r.push_back({"k_seams_stage", time_ms(s, iters, [&] { SEAMS(1); })});
             r.push_back({"k_seams_z", time_ms(s, iters, [&] { SEAMS(2); })});
             r.push_back({"k_seams_zy", time_ms(s, iters, [&] { SEAMS(3); })});

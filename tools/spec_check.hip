@@ -33,7 +33,7 @@ int main(int argc, char** argv) {
         HIP_OK(hipMalloc(&in, nvox * 4));
         {
             const int64_t nxb = (shape[2] + 255) / 256;
-            k_generate<<<dim3((unsigned)(shape[1] * nxb), (unsigned)shape[0]), 256, 0, s>>>(in, shape[0], shape[1], shape[2], 0, 0, 0, 0x5EED);
+            k_generate<<<dim3((unsigned)(shape[1] * nxb), (unsigned)shape[0]), 256, 0, s>>>(in, shape[0], shape[1], shape[2], 0, 0, 0, 0x5EED, 0);
         }
         u32 *st, *COUNT[2], *P, *TB;
         face_t* FACES;
