@@ -6,11 +6,14 @@ One step = the full five-stage path (block_components -> merge_offsets -> block_
 merge_assignments -> write) over one synthetic volume that is already resident in HBM,
 ending with the final uint64 labels resident in HBM.
 
-Workloads:
-  N = 1  C3: (1024, 2048, 2048) float32, block (64, 512, 512), threshold 0.5 'greater'
-  N > 1  z-slab sharded, one process per GPU, weak scaling: each rank owns a
-         (256, 4096, 4096) slab of a (256 N, 4096, 4096) volume -- at N = 8 this is C5,
-         (2048, 4096, 4096).  Seams are stitched over RCCL (cluster_tools_amd/distributed.py).
+Workloads (--workload):
+  c3 (default at N = 1)  (1024, 2048, 2048) float32, block (64, 512, 512), threshold 0.5 'greater'
+  c4   C3 + the ellipsoid uint8 mask, strong-scaled: z-slabs of the one volume over N ranks
+  c5 (default at N > 1)  weak scaling: each rank owns a (256, 4096, 4096) slab of a
+       (256 N, 4096, 4096) volume -- at N = 8 this is C5, (2048, 4096, 4096)
+  c2   (512, 512, 512), block (128, 128, 128)
+  --dither: continuous input (the map plus a sub-2^-8 dither).  N > 1 runs one process per GPU;
+  seams are stitched over RCCL (cluster_tools_amd/distributed.py).
 Rank 0 prints one JSON line.
 """
 import argparse
@@ -29,6 +32,14 @@ B_ALG = 12.0                   # algorithmic bytes / voxel: f32 read + uint64 wr
 KERNEL_BYTES = {'k_spec': 4.0, 'k_pass2': 8.0}
 
 
+WORKLOADS = {
+    'c3': {'shape': (1024, 2048, 2048), 'block': (64, 512, 512), 'scaling': 'strong'},
+    'c4': {'shape': (1024, 2048, 2048), 'block': (64, 512, 512), 'scaling': 'strong', 'mask': True},
+    'c5': {'per_rank': (256, 4096, 4096), 'block': (64, 512, 512), 'scaling': 'weak'},
+    'c2': {'shape': (512, 512, 512), 'block': (128, 128, 128), 'scaling': 'strong'},
+}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
@@ -42,7 +53,10 @@ def parse():
     p.add_argument('--dither', action='store_true',
                    help='continuous input: the synthetic map plus a deterministic sub-2^-8 dither (not quantized)')
     p.add_argument('--shape', default=None, help='override Z,Y,X (per-rank slab for N > 1)')
-    p.add_argument('--block-shape', default='64,512,512')
+    p.add_argument('--workload', default=None, choices=sorted(WORKLOADS),
+                   help='c3 (default at N=1), c4 (C3 + mask, strong-scaled z-slabs), c5 (default at N>1: '
+                        '(256N,4096,4096), weak), c2 (512^3, block 128^3)')
+    p.add_argument('--block-shape', default=None)
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-sample-z', type=int, default=1024)
     p.add_argument('--traffic-json', default=None,
@@ -95,26 +109,38 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    block_shape = tuple(int(v) for v in args.block_shape.split(','))
+    # workloads: strong = the volume is fixed and split into z-slabs over the N
+    # ranks; weak = every rank owns a slab of the same size
+    wl = args.workload or ('c3' if world == 1 else 'c5')
+    spec = dict(WORKLOADS[wl])
+    if args.mask:
+        spec['mask'] = True
+    block_shape = tuple(int(v) for v in (args.block_shape or ','.join(map(str, spec['block']))).split(','))
+    from cluster_tools_amd.distributed import slab_bounds
     if args.shape:
         slab = tuple(int(v) for v in args.shape.split(','))
+        gshape, z0, scaling = (slab[0] * world,) + slab[1:], slab[0] * rank, 'weak'
+    elif spec['scaling'] == 'weak':
+        slab = spec['per_rank']
+        gshape, z0, scaling = (slab[0] * world,) + slab[1:], slab[0] * rank, 'weak'
     else:
-        slab = (1024, 2048, 2048) if world == 1 else (256, 4096, 4096)
-    gshape = (slab[0] * world,) + slab[1:]
-    tag = ('c3' if world == 1 and not args.shape else 'c5slab' if not args.shape else 'custom') + \
-        ('_mask' if args.mask else '') + ('_cont' if args.dither else '') + \
-        ('' if args.mode == 'greater' else '_' + args.mode)
-    workload = ('C3%s%s (1024,2048,2048) f32, 1 GPU' % (' + uint8 mask (C4 at N=1)' if args.mask else '',
-                                                       ' continuous (dithered)' if args.dither else '')
-                if world == 1 and not args.shape else
-                'C5-style z-slabs (256N,4096,4096) f32' if not args.shape else 'custom %s' % (gshape,))
+        gshape = spec['shape']
+        z0, zs = slab_bounds(gshape[0], block_shape[0], world)[rank]
+        slab, scaling = (zs,) + tuple(gshape[1:]), 'strong'
+    masked = bool(spec.get('mask'))
+    tag = (wl if not args.shape else 'custom') + ('_mask' if masked and wl != 'c4' else '') + \
+        ('_cont' if args.dither else '') + ('' if args.mode == 'greater' else '_' + args.mode) + \
+        ('' if world == 1 else '_n%d' % world)
+    workload = '%s%s%s %s f32, block %s, %s over %d GPU%s' % (
+        wl.upper() if not args.shape else 'custom', ' + uint8 ellipsoid mask' if masked else '',
+        ' continuous (dithered)' if args.dither else '', tuple(gshape), tuple(block_shape),
+        '%s-scaled z-slabs' % scaling if world > 1 else 'one volume', world, 's' if world > 1 else '')
 
     ctx = _lib.Context(gpu)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-    z0 = slab[0] * rank
     x = ctx.generate_boundary_map(slab, origin=(z0, 0, 0), device=dev, dither=args.dither)
     mask = None
-    if args.mask:
+    if masked:
         from cluster_tools_amd.synthetic import ellipsoid_mask_device
         mask = ellipsoid_mask_device(gshape, z0, slab[0], dev)
     out = torch.empty(slab, dtype=torch.int64, device=dev)
@@ -162,17 +188,17 @@ def main():
         dt = float(t.item())
 
     nvox_rank = int(np.prod(slab))
-    nvox_all = nvox_rank * world
+    nvox_all = int(np.prod(gshape))
     ms_per_step = dt / args.steps * 1e3
     value = nvox_all * args.steps / dt / 1e9
-    b_alg = B_ALG + (1.0 if args.mask else 0.0)
+    b_alg = B_ALG + (1.0 if masked else 0.0)
     # dominant kernel of this rank, timed by HIP events on the stream it runs on
     kern = {k: v for k, v in prof.items() if v['count']}
     dom = max(kern, key=lambda k: kern[k]['total_ms'])
     avg_ms = kern[dom]['total_ms'] / kern[dom]['count']
     step_ms = kern[dom]['total_ms'] / args.steps      # == avg_ms for a kernel launched once per step
     kb = KERNEL_BYTES.get(dom)
-    if dom == 'k_spec' and args.mask:
+    if dom == 'k_spec' and masked:
         kb += 1.0
     traffic = None
     tj = args.traffic_json or os.path.join(ROOT, 'profiles', 'traffic_%s.json' % tag)
@@ -194,12 +220,12 @@ def main():
     line = {
         'metric': METRIC, 'value': round(value, 3), 'unit': 'Gvox/s', 'n_gpus': world,
         'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3),
-        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'higher_is_better': True, 'scaling': scaling, 'vs_baseline': None, 'dtype': 'f32',
         'data': 'synthetic (integer-only jittered-Voronoi boundary map, SURVEY.md §8d, seed 0x5EED%s)'
                 % (', + sub-2^-8 dither: continuous float32' if args.dither else ''),
-        'config': {'workload': workload, 'shape': list(gshape), 'slab': list(slab),
+        'config': {'workload': workload, 'workload_id': wl, 'shape': list(gshape), 'slab': list(slab),
                    'block_shape': list(block_shape), 'threshold': args.threshold,
-                   'threshold_mode': args.mode, 'mask': bool(args.mask),
+                   'threshold_mode': args.mode, 'mask': masked, 'continuous': bool(args.dither),
                    'parallelism': 'z-slab x%d' % world if world > 1 else 'single GPU'},
         'roofline': roofline,
         'e2e_roofline': {'alg_bytes_per_voxel': b_alg, 'achieved_gbs_per_gpu': round(e2e_gbs, 1),

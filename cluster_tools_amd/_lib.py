@@ -25,13 +25,15 @@ EXPORTS = (
     'cc_seam_pairs', 'cc_shard_finish', 'cc_set_debug', 'cc_threshold', 'cc_shard_top_plane32',
     'cc_seam_pairs32', 'cc_shard_top_cubes32', 'cc_seam_pairs_cubes32',
     'cc_evaluate', 'cc_get_overlaps', 'cc_relabel_consecutive', 'cc_n5_read', 'cc_n5_write',
+    'cc_set_option',
 )
 
 
 class CCResult(ctypes.Structure):
     _fields_ = [('n_blocks', ctypes.c_int64), ('n_labels', ctypes.c_uint64),
                 ('max_id', ctypes.c_uint64), ('n_components', ctypes.c_uint64),
-                ('n_block_components', ctypes.c_uint64), ('n_relabelled_tiles', ctypes.c_uint64)]
+                ('n_block_components', ctypes.c_uint64), ('n_relabelled_tiles', ctypes.c_uint64),
+                ('identity_lut', ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
@@ -74,7 +76,8 @@ def load():
         'cc_get_lut': (i64, [P, P, i64]),
         'cc_block_components': (I, [P, P, P, P, P, ctypes.c_double, I, P, P, i64]),
         'cc_merge_offsets': (I, [P, i64, P, P, P]),
-        'cc_block_faces': (i64, [P, P, P, P, P, P, i64]),
+        'cc_block_faces': (i64, [P, P, P, P, P, P, i64, P]),
+        'cc_set_option': (I, [P, I, i64]),
         'cc_merge_assignments': (I, [P, P, i64, u64, P]),
         'cc_write': (I, [P, P, P, P, P, P, u64]),
         'cc_generate_boundary_map': (I, [P, P, P, P, u64, I]),
@@ -312,17 +315,20 @@ class Context:
                                           float(threshold), mode_id(mode), _ptr(out_dev), _ptr(values), nb))
         return out_dev, values
 
-    def block_faces(self, labels_dev, block_shape, offsets):
+    def block_faces(self, labels_dev, block_shape, offsets, with_block_flags=False):
+        """Deduplicated face pairs; with_block_flags: also the per-block 'has an upper-face pair'
+        flags (uint8[n_blocks])."""
         shape = _i64(labels_dev.shape)
         bs = _i64(block_shape)
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        flags = np.zeros(len(offsets), dtype=np.uint8) if with_block_flags else None
         n = _check(load().cc_block_faces(self._h, _ptr(labels_dev), _ptr(shape), _ptr(bs), _ptr(offsets),
-                                         None, 0))
+                                         None, 0, _ptr(flags)))
         pairs = np.empty((n, 2), dtype=np.uint64)
         if n:
             _check(load().cc_block_faces(self._h, _ptr(labels_dev), _ptr(shape), _ptr(bs), _ptr(offsets),
-                                         _ptr(pairs), n))
-        return pairs
+                                         _ptr(pairs), n, None))
+        return (pairs, flags) if with_block_flags else pairs
 
     def merge_assignments(self, pairs, n_labels):
         pairs = np.ascontiguousarray(pairs, dtype=np.uint64).reshape(-1, 2)
@@ -408,6 +414,11 @@ class Context:
     def set_profiling(self, on=True):
         """on: False/0 off, True/1 every launch, 2 only the volume-sized kernels (k_spec, k_pass2)."""
         _check(load().cc_set_profiling(self._h, int(on)))
+
+    def set_empty_job_quirk(self, max_jobs):
+        """CC_OPT_EMPTY_JOB_QUIRK: reproduce the reference's empty-job branch
+        (merge_assignments.py:115-123) for `max_jobs` face jobs; 0 = off."""
+        _check(load().cc_set_option(self._h, 1, int(max_jobs)))
 
     def set_debug(self, flags):
         """Test hook (include/cc_mi355x.h): 1 = global union-find for intra-block seams."""

@@ -1507,6 +1507,31 @@ __global__ void k_mark_seams(Geom g, const u32* FIX, u32* flag, u32* LIST) {
     }
 }
 
+// Emulation of the reference's "empty job" branch (merge_assignments.py:115-123 with
+// block_faces.py:169-176, opt-in): bflag[b] = 1 iff block b has a 6-connected face pair with one
+// of its upper neighbours, i.e. b contributes a pair to its block_faces job.  One wave per tile
+// with a lower block face: own lower face entries against the neighbour's upper face entries
+// (the same cube positions and bit layout on both sides).
+__global__ __launch_bounds__(256) void k_block_face_flags(Geom g, const face_t* __restrict__ FACES, u8* bflag) {
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= g.n_tiles) return;
+    const TileInfo ti = tile_info(g, t);
+    const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const int i = a == 0 ? ti.iz : a == 1 ? ti.iy : ti.ix;
+        if (i == 0 || g.tblk[a][i] == g.tblk[a][i - 1]) continue;
+        const int64_t tn = t - (a == 0 ? sz : a == 1 ? sy : 1);
+        const int lo = a == 0 ? F_ZLO : a == 1 ? F_YLO : F_XLO, hi = a == 0 ? F_ZHI : a == 1 ? F_YHI : F_XHI;
+        const int n = a == 0 ? F_Z : a == 1 ? F_Y : F_X;
+        bool hit = false;
+        for (int e = lane; e < n; e += 64)
+            hit |= ((FACES[t * FACE_STRIDE + lo + e] >> FK_BITS) & (FACES[tn * FACE_STRIDE + hi + e] >> FK_BITS)) != 0;
+        if (__ballot(hit) && lane == 0) bflag[tile_info(g, tn).block] = 1;
+    }
+}
+
 // Block-face unions from the k_seams lists, one wave per tile: node pairs -> current roots,
 // duplicate root pairs dropped per wave, union keyed by rid (the smaller rid becomes the root).
 __global__ __launch_bounds__(SP_WAVES * 64) void k_inter_union(Geom g, const u64* __restrict__ IPAIRS,

@@ -55,7 +55,7 @@ struct cc_ctx {
     // workspace
     DevBuf tiles, bstat, bparam, bits, faces, count, rc, roff, P, KR, FIN, keys, keys2, vals, vals2, seg,
         values, offsets, lut, cub_tmp, scalars, scalars2, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2,
-        flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf, spec, mark,
+        flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf, spec, mark, bflag,
         ev_main, ev_z, ev_seg, ev_gt, ev_flag, ev_part;   // evaluation (cc_eval.hip)
     int64_t ev_cap = 0;      // entries per evaluation hash table of the last cc_evaluate
     int64_t rl_cap = 0;      // id-set slots of the last cc_relabel_consecutive
@@ -69,6 +69,7 @@ struct cc_ctx {
     int prof = 0;          // 0 off, 1 every launch, 2 the volume-sized kernels only (cc_set_profiling)
     int debug = 0;         // CC_DEBUG_* test hooks
     int front_chunks = 1;  // z-layer chunks of the speculative front (CC_FRONT_CHUNKS)
+    int64_t quirk_jobs = 0;  // CC_OPT_EMPTY_JOB_QUIRK: emulate the reference's empty-job branch for max_jobs
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, ProfEntry> prof_acc;
@@ -172,6 +173,7 @@ struct RunState {
     bool local_only = false;
     int64_t bs[3] = {0, 0, 0};  // block_shape
     uint64_t n_fix = 0;        // tiles relabelled by k_fix
+    bool identity_lut = false; // the empty-job emulation dropped every block-face merge
     int stage = 0;             // 1 local done, 2 rid done, 3 final done
 };
 
@@ -415,7 +417,26 @@ static void phase_rid(cc_ctx* c, uint64_t base) {
             k_assign_rid<<<grid1d(nr), 256, 0, s>>>(nr, c->keys2.as<u64>(), c->vals2.as<u32>(), c->seg.as<u32>(),
                                                     offsets, c->KR.as<u64>());
         });
-    if (!st.local_only) {
+    st.identity_lut = false;
+    if (!st.local_only && c->quirk_jobs > 0) {
+        // reference empty-job branch (merge_assignments.py:115-123): block_faces job j owns blocks
+        // j :: n_jobs (cluster_tasks.py:331); if any job found no face pair, no merge happens
+        c->bflag.ensure(nb);
+        HIP_OK(hipMemsetAsync(c->bflag.p, 0, nb, s));
+        launch(c, "k_block_face_flags", [&] {
+            k_block_face_flags<<<(unsigned)((nt + 3) / 4), 256, 0, s>>>(g, c->faces.as<face_t>(), c->bflag.as<u8>());
+        });
+        std::vector<u8> fl(nb);
+        HIP_OK(hipMemcpyAsync(fl.data(), c->bflag.p, nb, hipMemcpyDeviceToHost, s));
+        sync(c);
+        const int64_t nj = std::min<int64_t>(nb, c->quirk_jobs);
+        for (int64_t j = 0; j < nj && !st.identity_lut; ++j) {
+            bool has = false;
+            for (int64_t b = j; b < nb && !has; b += nj) has = fl[b] != 0;
+            st.identity_lut = !has;
+        }
+    }
+    if (!st.local_only && !st.identity_lut) {
         const unsigned grid = (unsigned)((nt + SP_WAVES - 1) / SP_WAVES);
         launch(c, "k_inter_union", [&] {
             k_inter_union<<<grid, SP_WAVES * 64, 0, s>>>(g, c->ipairs.as<u64>(), c->ipc.as<u32>(), c->P.as<u32>(), c->KR.as<u64>());
@@ -561,6 +582,7 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
         res->n_components = st.local_only ? 0 : sc[1];
         res->n_block_components = (uint64_t)nr;
         res->n_relabelled_tiles = st.n_fix;
+        res->identity_lut = st.identity_lut ? 1 : 0;
     }
 }
 
@@ -623,7 +645,7 @@ void cc_destroy(cc_ctx* c) {
                       &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
                       &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
-                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec, &c->mark,
+                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec, &c->mark, &c->bflag,
                       &c->ev_main, &c->ev_z, &c->ev_seg, &c->ev_gt, &c->ev_flag, &c->ev_part};
     for (DevBuf* b : bufs) b->release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
@@ -768,6 +790,18 @@ int cc_set_profiling(cc_ctx* c, int enable) {
         CC_REQUIRE(c, "ctx is NULL");
         CC_REQUIRE(enable >= 0 && enable <= 2, "profiling level must be 0, 1 or 2");
         c->prof = enable;
+    })
+}
+
+int cc_set_option(cc_ctx* c, int option, int64_t value) {
+    CC_TRY({
+        CC_REQUIRE(c, "ctx is NULL");
+        if (option == CC_OPT_EMPTY_JOB_QUIRK) {
+            CC_REQUIRE(value >= 0, "max_jobs must be >= 0");
+            c->quirk_jobs = value;
+        } else {
+            CC_REQUIRE(false, "unknown option");
+        }
     })
 }
 

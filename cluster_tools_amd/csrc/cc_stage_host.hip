@@ -4,7 +4,7 @@
 extern "C" {
 
 int64_t cc_block_faces(cc_ctx* c, const uint64_t* labels, const int64_t shape[3], const int64_t block_shape[3],
-                       const uint64_t* offsets_host, uint64_t* pairs_host, int64_t cap) {
+                       const uint64_t* offsets_host, uint64_t* pairs_host, int64_t cap, uint8_t* block_has_pairs_host) {
     try {
         CC_REQUIRE(c && labels && shape && block_shape && offsets_host, "NULL argument");
         HIP_OK(hipSetDevice(c->device));
@@ -30,6 +30,12 @@ int64_t cc_block_faces(cc_ctx* c, const uint64_t* labels, const int64_t shape[3]
         u64* qb = qa + capn;
         unsigned long long* cnt = (unsigned long long*)c->counter.p;
         HIP_OK(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), s));
+        u8* bflag = nullptr;
+        if (block_has_pairs_host) {
+            c->bflag.ensure(n_blocks);
+            bflag = c->bflag.as<u8>();
+            HIP_OK(hipMemsetAsync(bflag, 0, n_blocks, s));
+        }
         for (int a = 0; a < 3; ++a) {
             const int64_t nplanes = (shape[a] - 1) / block_shape[a];
             const int64_t work = nplanes * (shape[0] * shape[1] * shape[2] / shape[a]);
@@ -37,11 +43,13 @@ int64_t cc_block_faces(cc_ctx* c, const uint64_t* labels, const int64_t shape[3]
             launch(c, "k_face_pairs", [&] {
                 k_face_pairs<<<grid1d(work), 256, 0, s>>>(a, shape[0], shape[1], shape[2], block_shape[0],
                                                           block_shape[1], block_shape[2], nb[0], nb[1], nb[2],
-                                                          labels, c->offsets.as<u64>(), pa, pb, cnt, (u64)capn);
+                                                          labels, c->offsets.as<u64>(), pa, pb, cnt, (u64)capn,
+                                                          bflag);
             });
         }
         unsigned long long n_raw = 0;
         HIP_OK(hipMemcpyAsync(&n_raw, cnt, sizeof(n_raw), hipMemcpyDeviceToHost, s));
+        if (bflag) HIP_OK(hipMemcpyAsync(block_has_pairs_host, bflag, n_blocks, hipMemcpyDeviceToHost, s));
         sync(c);
         const int64_t n = (int64_t)n_raw;
         if (n == 0) return 0;
@@ -153,6 +161,7 @@ int cc_shard_begin(cc_ctx* c, const float* in, const uint8_t* mask, const int64_
         CC_REQUIRE(c && in && slab_shape && block_shape && sum_values, "NULL argument");
         CC_REQUIRE(z_offset >= 0 && z_offset % block_shape[0] == 0,
                    "slab z offset must be a multiple of block_shape[0] (seams on block faces)");
+        CC_REQUIRE(c->quirk_jobs == 0, "the empty-job emulation is not available on the z-slab path");
         HIP_OK(hipSetDevice(c->device));
         phase_local(c, in, mask, slab_shape, block_shape, threshold, to_mode(mode), z_offset, false);
         *sum_values = read_sum_v(c);

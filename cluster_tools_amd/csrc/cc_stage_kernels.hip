@@ -11,7 +11,7 @@ namespace cc {
 __global__ void k_face_pairs(int axis, int64_t Z, int64_t Y, int64_t X, int64_t bz, int64_t by, int64_t bx,
                              int64_t nbz, int64_t nby, int64_t nbx, const u64* __restrict__ L,
                              const u64* __restrict__ off, u64* pa, u64* pb, unsigned long long* counter,
-                             u64 cap) {
+                             u64 cap, u8* bflag) {
     const int64_t S[3] = {Z, Y, X}, B[3] = {bz, by, bx};
     const int64_t nplanes = (S[axis] - 1) / B[axis];       // block faces with an upper neighbour
     const int64_t plane = (axis == 0 ? Y * X : axis == 1 ? Z * X : Z * Y);
@@ -33,6 +33,7 @@ __global__ void k_face_pairs(int axis, int64_t Z, int64_t Y, int64_t X, int64_t 
     const int64_t bb = ((q[0] / bz) * nby + q[1] / by) * nbx + q[2] / bx;
     const unsigned long long pos = atomicAdd(counter, 1ull);
     if (pos < cap) { pa[pos] = la + off[ba]; pb[pos] = lb + off[bb]; }
+    if (bflag) bflag[ba] = 1;      // block ba's face job has a pair (block_faces.py:116-137)
     (void)nbz;
 }
 

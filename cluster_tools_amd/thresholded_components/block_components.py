@@ -9,11 +9,16 @@ compute runs on the MI355X through libcc_mi355x:
   fused=True   (set by ThresholdedComponentsWorkflow) cc_label_volume: all five stages in this
                job; the output dataset receives the FINAL labels and the downstream tasks only
                emit their artefacts (cc_offsets.json, the assignments LUT, maxId, logs).
-One GPU job labels the whole volume; per-block results do not depend on the job split.
+               Task config 'gpus' > 1 shards the volume in z-slabs over that many GPUs
+               (sharded_job.py, one rank per GPU, RCCL).
+One job labels the whole volume; per-block results do not depend on the job split.  N5 chunks
+are coded natively (cc_n5_read / cc_n5_write on host threads); the fused job records its
+n5-read / H2D / device / D2H / n5-write split in <tmp>/cc_fused_timing.json.
 """
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -24,6 +29,7 @@ import cluster_tools_amd.utils.function_utils as fu
 
 FUSED_MARKER = 'cc_fused.json'
 FUSED_LUT = 'cc_fused_assignments.npy'
+FUSED_TIMING = 'cc_fused_timing.json'     # host / device split of the fused job (seconds)
 
 
 class BlockComponentsBase(Task):
@@ -47,8 +53,10 @@ class BlockComponentsBase(Task):
 
     @staticmethod
     def default_task_config():
+        # gpus: GPUs of this node for the fused job (> 1: z-slab sharding, one rank per GPU);
+        # dist_backend: 'nccl' (RCCL over xGMI) or 'gloo' (host-staged, rehearsal on one GPU)
         config = LocalTask.default_task_config()
-        config.update({'sigma_prefilter': 0})
+        config.update({'sigma_prefilter': 0, 'gpus': 1, 'dist_backend': 'nccl'})
         return config
 
     def requires(self):
@@ -78,6 +86,14 @@ class BlockComponentsBase(Task):
             raise NotImplementedError('sigma_prefilter > 0 is not supported on the MI355X path')
         chunks = tuple(max(1, min(ch, sh)) for ch, sh in zip(chunks, shape))
         compression = config.pop('compression', 'gzip')
+        # the reference empty-job branch (merge_assignments config, see merge_assignments.py) is
+        # applied here when the whole path runs fused in this job
+        from cluster_tools_amd.thresholded_components.merge_assignments import QUIRK_KEY
+        ma_cfg = os.path.join(self.config_dir, 'merge_assignments.config')
+        if self.fused and os.path.exists(ma_cfg):
+            with open(ma_cfg) as f:
+                if json.load(f).get(QUIRK_KEY, False):
+                    config['quirk_jobs'] = int(self.max_jobs)
         with vu.file_reader(self.output_path) as f:
             f.require_dataset(self.output_key, shape=shape, dtype='uint64', compression=compression, chunks=chunks)
         block_list = vu.blocks_in_volume(shape, block_shape, roi_begin, roi_end)
@@ -92,15 +108,134 @@ class BlockComponentsLocal(BlockComponentsBase, LocalTask):
     pass
 
 
-def _load(path, key, dtype=None):
+def _n_threads():
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def _read(path, key, box=None, dtype=None):
+    """Region of an N5 dataset through the native codec (whole dataset when box is None)."""
     with vu.file_reader(path, 'r') as f:
-        a = f[key][:]
+        ds = f[key]
+        ds.n_threads = _n_threads()
+        a = ds.read_region(box or [(0, s) for s in ds.shape])
     return a if dtype is None else a.astype(dtype, copy=False)
 
 
-def block_components(job_id, config_path):
+def _write_output(config, labels, box, n_threads=None):
+    """Final / block-local labels into the output dataset.  Chunks of empty blocks are not
+    created (the reference skips empty blocks, block_components.py:175-177, and they read as 0)."""
+    with vu.file_reader(config['output_path']) as f:
+        ds = f[config['output_key']]
+        ds.n_threads = n_threads or _n_threads()
+        ds.write_region(box, labels, skip_zero_chunks=True)
+
+
+def _write_fused_artefacts(tmp_folder, config, values, lut, res, timing):
+    np.save(os.path.join(tmp_folder, FUSED_LUT), lut)
+    with open(os.path.join(tmp_folder, FUSED_MARKER), 'w') as f:
+        json.dump({'output_path': os.path.abspath(config['output_path']),
+                   'output_key': config['output_key'], 'n_labels': int(res['n_labels']),
+                   'max_id': int(res['max_id']), 'n_components': int(res['n_components'])}, f)
+    with open(os.path.join(tmp_folder, FUSED_TIMING), 'w') as f:
+        json.dump(timing, f, indent=1)
+    fu.log('timing (s): ' + ', '.join('%s %.3f' % (k, v) for k, v in timing.items() if k.endswith('_s')))
+
+
+def _fused_single(config, shape, nb):
+    """All five stages on one GPU, with the host side split out: N5 read, H2D, device, D2H, N5
+    write (the PCIe-inclusive and codec-inclusive rates are reported beside the
+    device-resident one)."""
     import torch
     from cluster_tools_amd import _lib
+    timing = {'voxels': int(np.prod(shape)), 'gpus': 1}
+    t = time.perf_counter()
+    inp = _read(config['input_path'], config['input_key'], dtype=np.float32)
+    mask = None
+    if config.get('mask_path', ''):
+        vu.load_mask(config['mask_path'], config['mask_key'], shape)
+        mask = (_read(config['mask_path'], config['mask_key']) != 0).astype(np.uint8)
+    timing['n5_read_s'] = time.perf_counter() - t
+    device = int(os.environ.get('CC_DEVICE', '0'))
+    dev = torch.device('cuda', device)
+    torch.cuda.set_device(dev)
+    t = time.perf_counter()
+    x = torch.from_numpy(inp).to(dev)
+    m = None if mask is None else torch.from_numpy(mask).to(dev)
+    torch.cuda.synchronize(dev)
+    timing['h2d_s'] = time.perf_counter() - t
+    del inp, mask
+    with _lib.Context(device) as ctx:
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        ctx.set_empty_job_quirk(config.get('quirk_jobs', 0))
+        t = time.perf_counter()
+        labels_dev, res = ctx.label_volume(x, config['block_shape'], config['threshold'],
+                                           config['threshold_mode'], m)
+        torch.cuda.synchronize(dev)
+        timing['device_s'] = time.perf_counter() - t
+        values = ctx.block_values(nb)
+        lut = ctx.lut(res['n_labels'])
+    del x, m
+    t = time.perf_counter()
+    labels = labels_dev.cpu().numpy().view(np.uint64)
+    timing['d2h_s'] = time.perf_counter() - t
+    del labels_dev
+    t = time.perf_counter()
+    _write_output(config, labels, [(0, s) for s in shape])
+    timing['n5_write_s'] = time.perf_counter() - t
+    if res.get('identity_lut'):
+        fu.log('a block_faces job has no pairs: no merge (reference empty-job branch)')
+    return values, lut, res, timing
+
+
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        return sk.getsockname()[1]
+
+
+def _fused_sharded(config_path, config, shape, nb):
+    """config['gpus'] > 1: z-slab sharding over that many GPUs of this node.  This
+    job process has not touched a GPU; it starts one rank per GPU with torch.distributed.run
+    (cluster_tools_amd/thresholded_components/sharded_job.py; RCCL collectives, or gloo with
+    config['dist_backend'] = 'gloo' to rehearse on one device) and assembles the per-rank block
+    values and LUT parts into the reference's artefacts.  This replaces the reference's
+    ProcessPool of block jobs (cluster_tasks.py:301-335, 545-551) with one rank per GPU."""
+    import subprocess
+    from cluster_tools_amd.distributed import assemble_lut
+    bz = config['block_shape'][0]
+    world = max(1, min(int(config['gpus']), -(-shape[0] // bz)))
+    out_dir = os.path.join(config['tmp_folder'], 'cc_shards')
+    os.makedirs(out_dir, exist_ok=True)
+    for fn in os.listdir(out_dir):
+        os.remove(os.path.join(out_dir, fn))
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'sharded_job.py')
+    repo = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ)
+    env['PYTHONPATH'] = repo + (os.pathsep + env['PYTHONPATH'] if env.get('PYTHONPATH') else '')
+    env['HSA_ENABLE_IPC_MODE_LEGACY'] = '0'
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(world),
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), script, config_path, out_dir]
+    fu.log('z-slab sharded run on %i GPUs (%s)' % (world, config.get('dist_backend', 'nccl')))
+    t = time.perf_counter()
+    subprocess.run(cmd, check=True, env=env)
+    wall = time.perf_counter() - t
+    parts = [np.load(os.path.join(out_dir, 'rank_%i.npz' % r)) for r in range(world)]
+    sums = [int(p['sum']) for p in parts]
+    values = np.concatenate([p['values'] for p in parts])
+    assert len(values) == nb, (len(values), nb)
+    lut = assemble_lut([p['lut'] for p in parts], sums)
+    n_labels = sum(sums) + 1
+    res = {'n_labels': n_labels, 'max_id': n_labels - 1,
+           'n_components': int(sum(int(p['n_components']) for p in parts))}
+    timing = {'voxels': int(np.prod(shape)), 'gpus': world, 'ranks_wall_s': wall}
+    for k in parts[0].files:
+        if k.endswith('_s'):
+            timing[k] = max(float(p[k]) for p in parts)          # slowest rank per stage
+    return values, lut, res, timing
+
+
+def block_components(job_id, config_path):
     fu.log('start processing job %i' % job_id)
     fu.log('reading config from %s' % config_path)
     with open(config_path) as f:
@@ -111,37 +246,29 @@ def block_components(job_id, config_path):
     threshold, mode = config['threshold'], config['threshold_mode']
     fused = config.get('fused', False)
     fu.log('Applying threshold %f with mode %s' % (threshold, mode))
-
-    inp = _load(config['input_path'], config['input_key'], np.float32)
-    shape = inp.shape
-    mask = None
-    if config.get('mask_path', ''):
-        mds = vu.load_mask(config['mask_path'], config['mask_key'], shape)
-        mask = (mds[:] != 0).astype(np.uint8)
+    shape = tuple(vu.get_shape(config['input_path'], config['input_key']))
     nb = vu.Blocking([0, 0, 0], list(shape), block_shape).numberOfBlocks
 
-    with _lib.Context(int(os.environ.get('CC_DEVICE', '0'))) as ctx:
-        if fused:
-            labels, res = ctx.label_volume(inp, block_shape, threshold, mode, mask)
-            values = ctx.block_values(nb)
-            lut = ctx.lut(res['n_labels'])
-            np.save(os.path.join(tmp_folder, FUSED_LUT), lut)
-            with open(os.path.join(tmp_folder, FUSED_MARKER), 'w') as f:
-                json.dump({'output_path': os.path.abspath(config['output_path']),
-                           'output_key': config['output_key'], 'n_labels': res['n_labels'],
-                           'max_id': res['max_id'], 'n_components': res['n_components']}, f)
+    if fused:
+        if int(config.get('gpus', 1)) > 1:
+            values, lut, res, timing = _fused_sharded(config_path, config, shape, nb)
         else:
+            values, lut, res, timing = _fused_single(config, shape, nb)
+        _write_fused_artefacts(tmp_folder, config, values, lut, res, timing)
+    else:
+        import torch
+        from cluster_tools_amd import _lib
+        inp = _read(config['input_path'], config['input_key'], dtype=np.float32)
+        mask = None
+        if config.get('mask_path', ''):
+            vu.load_mask(config['mask_path'], config['mask_key'], shape)
+            mask = (_read(config['mask_path'], config['mask_key']) != 0).astype(np.uint8)
+        with _lib.Context(int(os.environ.get('CC_DEVICE', '0'))) as ctx:
             x = torch.from_numpy(inp).cuda()
             m = None if mask is None else torch.from_numpy(mask).cuda()
             lab_dev, values = ctx.block_components(x, block_shape, threshold, mode, m)
             labels = lab_dev.cpu().numpy().view(np.uint64)
-    with vu.file_reader(config['output_path']) as f:
-        ds = f[config['output_key']]
-        blocking = vu.Blocking([0, 0, 0], list(shape), block_shape)
-        for b in block_list:           # empty blocks are not written (block_components.py:175-177)
-            if values[b]:
-                bb = vu.block_to_bb(blocking.getBlock(b))
-                ds[bb] = labels[bb]
+        _write_output(config, labels, [(0, s) for s in shape])
     for b in block_list:
         fu.log_block_success(b)
     offsets = {b: int(values[b]) for b in block_list}

@@ -78,11 +78,16 @@ def block_faces(job_id, config_path):
         from cluster_tools_amd import _lib
         with vu.file_reader(config['input_path'], 'r') as f:
             seg = f[config['input_key']][:]
+        from cluster_tools_amd.thresholded_components.merge_assignments import FACE_FLAGS
         with _lib.Context(int(os.environ.get('CC_DEVICE', '0'))) as ctx:
-            pairs = ctx.block_faces(torch.from_numpy(seg.view(np.int64)).cuda(), config['block_shape'], offsets)
+            pairs, flags = ctx.block_faces(torch.from_numpy(seg.view(np.int64)).cuda(), config['block_shape'],
+                                           offsets, with_block_flags=True)
         if len(pairs):
             assert int(pairs.max()) < n_labels, '%i, %i' % (int(pairs.max()), n_labels)
         np.save(os.path.join(tmp_folder, 'cc_assignments_%i.npy' % job_id), pairs)
+        # which blocks contribute pairs: the reference's per-job files are empty exactly when none
+        # of a job's blocks does (merge_assignments.any_empty_job)
+        np.save(os.path.join(tmp_folder, FACE_FLAGS), flags)
     for b in block_list:
         fu.log_block_success(b)
     fu.log_job_success(job_id)

@@ -46,6 +46,8 @@ typedef struct {
     uint64_t n_block_components; /* sum over blocks of n_i (block-local comps) */
     uint64_t n_relabelled_tiles; /* tiles whose speculated foreground interval was not exact and
                                     were labelled again (instrumentation; results never depend on it) */
+    uint64_t identity_lut;  /* 1 if CC_OPT_EMPTY_JOB_QUIRK found an empty face job: no block-face
+                               merge, the LUT is the identity (merge_assignments.py:115-123) */
 } cc_result;
 
 /* --- context ----------------------------------------------------------- */
@@ -114,10 +116,12 @@ int cc_merge_offsets(const uint64_t* values_host, int64_t n_blocks, uint64_t* of
 /* block_faces (block_faces.py:87-177): from block-local labels (device) and offsets
  * (host), the deduplicated face pairs (label_a + off_a, label_b + off_b), sorted
  * lexicographically like np.unique(axis=0).  Writes at most cap pairs to pairs_host
- * ([cap][2]); returns the number of pairs (may exceed cap: call again with a larger cap). */
+ * ([cap][2]); returns the number of pairs (may exceed cap: call again with a larger cap).
+ * block_has_pairs_host (nullable, n_blocks bytes): 1 for every block with a pair on one of its
+ * upper faces (the block's face job emits it; used for the empty-job emulation). */
 int64_t cc_block_faces(cc_ctx* ctx, const uint64_t* labels_dev, const int64_t shape[3],
                        const int64_t block_shape[3], const uint64_t* offsets_host,
-                       uint64_t* pairs_host, int64_t cap);
+                       uint64_t* pairs_host, int64_t cap, uint8_t* block_has_pairs_host);
 
 /* merge_assignments (merge_assignments.py:105-130): union-find over ids 0..n_labels-1
  * merged by pairs (host, [n_pairs][2]); lut_host[n_labels] = min id of each set. */
@@ -185,6 +189,13 @@ int cc_set_profiling(cc_ctx* ctx, int enable);
 int cc_get_profile(cc_ctx* ctx, char* names, int names_cap, int64_t* counts, double* total_ms,
                    int cap);
 int cc_reset_profile(cc_ctx* ctx);
+/* Options.  CC_OPT_EMPTY_JOB_QUIRK = max_jobs (0 = off, the default): reproduce the reference's
+ * empty-job branch -- block_faces job j owns blocks j :: min(n_blocks, max_jobs)
+ * (cluster_tasks.py:301-335); if any job has no face pair (it saves [], block_faces.py:169-176),
+ * merge_assignments drops every merge and writes the identity LUT (merge_assignments.py:115-123).
+ * Fused single-volume path only. */
+#define CC_OPT_EMPTY_JOB_QUIRK 1
+int cc_set_option(cc_ctx* ctx, int option, int64_t value);
 /* Test hook: CC_DEBUG_GLOBAL_STITCH routes every block's intra-block seams through the global
  * union-find fallback instead of the per-block LDS path (both must give identical results). */
 #define CC_DEBUG_GLOBAL_STITCH 1

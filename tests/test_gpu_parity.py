@@ -7,14 +7,24 @@ from conftest import golden_index, load_golden
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
-CASES = sorted((k, v) for k, v in golden_index().items() if not v['quirk'])
+CASES = sorted(golden_index().items())
 IDS = [c[0] for c in CASES]
 
 
-def _check_against_oracle(ctx, inp, block_shape, thr, mode, mask=None, res=None, lab=None):
+def _quirk_jobs(meta):
+    """max_jobs of the golden's block_faces run when it exercises the reference's empty-job
+    branch (merge_assignments.py:115-123), else 0."""
+    return meta['n_jobs_block_faces'] if meta['quirk'] else 0
+
+
+def _check_against_oracle(ctx, inp, block_shape, thr, mode, mask=None, res=None, lab=None, quirk_jobs=0):
     if lab is None:
-        lab, res = ctx.label_volume(inp, block_shape, thr, mode, mask)
-    r = O.label_volume(inp, block_shape, thr, mode, mask, n_threads=8)
+        ctx.set_empty_job_quirk(quirk_jobs)
+        try:
+            lab, res = ctx.label_volume(inp, block_shape, thr, mode, mask)
+        finally:
+            ctx.set_empty_job_quirk(0)
+    r = O.label_volume(inp, block_shape, thr, mode, mask, n_threads=8, quirk_n_jobs=quirk_jobs)
     nb = len(r['values'])
     np.testing.assert_array_equal(lab, r['labels'])          # raw uint64, bit-exact
     np.testing.assert_array_equal(ctx.block_values(nb), r['values'])
@@ -29,7 +39,8 @@ def _check_against_oracle(ctx, inp, block_shape, thr, mode, mask=None, res=None,
 def test_fused_path_golden(ctx, name, meta):
     d = load_golden(name)
     lab, res, r = _check_against_oracle(ctx, d['input'], meta['block_shape'], float(d['threshold']),
-                                        meta['mode'], d.get('mask'))
+                                        meta['mode'], d.get('mask'), quirk_jobs=_quirk_jobs(meta))
+    assert res['identity_lut'] == int(bool(meta['quirk']))
     # against the reference itself (canonical relabel = the parity contract)
     np.testing.assert_array_equal(O.canon(lab), d['labels_canon'])
     np.testing.assert_array_equal(ctx.block_values(len(d['block_values'])), d['block_values'])
@@ -56,9 +67,16 @@ def test_stage_level_golden(ctx, name, meta):
     np.testing.assert_array_equal(offsets, d['offsets'])
     np.testing.assert_array_equal(empty, d['empty_blocks'])
     assert n_labels == int(d['n_labels'])
-    pairs = ctx.block_faces(local, meta['block_shape'], offsets)
+    pairs, flags = ctx.block_faces(local, meta['block_shape'], offsets, with_block_flags=True)
     np.testing.assert_array_equal(pairs, d['pairs'])
-    lut = ctx.merge_assignments(pairs, n_labels)
+    from cluster_tools_amd.thresholded_components.merge_assignments import any_empty_job
+    if meta['quirk']:
+        # every block_faces job of the reference run must be checked: one without pairs -> identity
+        assert any_empty_job(flags, _quirk_jobs(meta))
+        lut = np.arange(n_labels, dtype=np.uint64)
+    else:
+        assert not any_empty_job(flags, 1)
+        lut = ctx.merge_assignments(pairs, n_labels)
     np.testing.assert_array_equal(O.canon(lut), d['lut_canon'])
     ctx.write(local, meta['block_shape'], offsets, lut)
     np.testing.assert_array_equal(O.canon(local.cpu().numpy()), d['labels_canon'])
@@ -81,6 +99,16 @@ SYNTH = [
     ((33, 65, 129), (11, 13, 43), 'greater'),      # tiles smaller than TX, odd everything
     ((128, 128, 128), (128, 128, 128), 'greater'),
 ]
+
+
+@pytest.mark.parametrize('n_jobs', [1, 4, 27, 1000])
+def test_empty_job_emulation_vs_oracle(ctx, n_jobs):
+    """CC_OPT_EMPTY_JOB_QUIRK against the oracle's emulation for several max_jobs: the LUT is the
+    identity exactly when one of the min(n_blocks, max_jobs) face jobs has no pair."""
+    inp = O.boundary_map((40, 72, 88), origin=(5, 5, 5))
+    for mode in ('greater', 'less'):
+        _, res, r = _check_against_oracle(ctx, inp, (16, 32, 32), 0.5, mode, quirk_jobs=n_jobs)
+        assert res['identity_lut'] == int(np.array_equal(r['lut'], np.arange(r['n_labels'])))
 
 
 @pytest.mark.parametrize('shape,bs,mode', SYNTH)

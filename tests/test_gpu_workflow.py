@@ -13,6 +13,19 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
+def _build(tasks, tmp):
+    """luigi.build, printing the jobs' error logs when it fails (the job processes' tracebacks)."""
+    import glob
+    from cluster_tools_amd import luigi_compat as luigi
+    ok = luigi.build(tasks, local_scheduler=True)
+    if not ok:
+        for p in sorted(glob.glob(os.path.join(str(tmp), 'error_logs', '*.err'))):
+            txt = open(p).read()
+            if txt.strip():
+                print('==== %s\n%s' % (p, txt[-4000:]))
+    return ok
+
+
 def _setup(tmp_path, name, block_shape):
     from cluster_tools_amd import n5
     from cluster_tools_amd.cluster_tasks import BaseClusterTask
@@ -45,7 +58,7 @@ def test_workflow_fused(tmp_path, name):
                                       input_path=data, input_key='volumes/boundaries', output_path=data,
                                       output_key='data', assignment_key='assignments',
                                       threshold=float(d['threshold']), threshold_mode=meta['mode'], **kw)
-    assert luigi.build([t], local_scheduler=True)
+    assert _build([t], tmp_path / 'tmp')
     with n5.open_file(data, 'r') as f:
         seg = f['data'][:]
         lut = f['assignments'][:]
@@ -79,7 +92,7 @@ def test_stage_by_stage(tmp_path):
     common = dict(tmp_folder=tmp, config_dir=cfg, max_jobs=4)
     t1 = BlockComponentsLocal(input_path=data, input_key='volumes/boundaries', output_path=data, output_key='data',
                               threshold=0.5, threshold_mode='less', dependency=DummyTask(), **common)
-    assert luigi.build([t1], local_scheduler=True)
+    assert _build([t1], tmp)
     with n5.open_file(data, 'r') as f:
         np.testing.assert_array_equal(f['data'][:], d['local_labels'].astype(np.uint64))
     off_path = os.path.join(tmp, 'cc_offsets.json')
@@ -91,9 +104,112 @@ def test_stage_by_stage(tmp_path):
     t5 = WriteLocal(input_path=data, input_key='data', output_path=data, output_key='data',
                     assignment_path=data, assignment_key='assignments', identifier='thresholded_components',
                     offset_path=off_path, dependency=t4, **common)
-    assert luigi.build([t5], local_scheduler=True)
+    assert _build([t5], tmp)
     np.testing.assert_array_equal(np.load(os.path.join(tmp, 'cc_assignments_0.npy')), d['pairs'])
     with n5.open_file(data, 'r') as f:
         np.testing.assert_array_equal(O.canon(f['data'][:]), d['labels_canon'])
         np.testing.assert_array_equal(O.canon(f['assignments'][:]), d['lut_canon'])
         assert f['data'].attrs['maxId'] == int(d['max_id'])
+
+
+def _write_task_config(cfg, name, values):
+    with open(os.path.join(cfg, name + '.config'), 'w') as f:
+        json.dump(values, f)
+
+
+@pytest.mark.parametrize('name', ['bmap_quirk', 'bmap_greater', 'bmap_less'])
+def test_workflow_empty_job_emulation(tmp_path, name):
+    """merge_assignments config 'reference_empty_job_quirk' with the golden run's face-job count as
+    max_jobs: the fused job reproduces the reference's output (identity LUT for bmap_quirk)."""
+    from cluster_tools_amd import n5
+    from cluster_tools_amd.thresholded_components import ThresholdedComponentsWorkflow
+    from cluster_tools_amd.thresholded_components.merge_assignments import MergeAssignmentsLocal
+    from conftest import golden_index
+    meta = golden_index()[name]
+    d, data, cfg = _setup(tmp_path, name, meta['block_shape'])
+    c = MergeAssignmentsLocal.default_task_config()
+    c['reference_empty_job_quirk'] = True
+    _write_task_config(cfg, 'merge_assignments', c)
+    t = ThresholdedComponentsWorkflow(tmp_folder=str(tmp_path / 'tmp'), config_dir=cfg, target='local',
+                                      max_jobs=meta['n_jobs_block_faces'], input_path=data,
+                                      input_key='volumes/boundaries', output_path=data, output_key='data',
+                                      assignment_key='assignments', threshold=float(d['threshold']),
+                                      threshold_mode=meta['mode'])
+    assert _build([t], tmp_path / 'tmp')
+    with n5.open_file(data, 'r') as f:
+        np.testing.assert_array_equal(O.canon(f['data'][:]), d['labels_canon'])
+        np.testing.assert_array_equal(O.canon(f['assignments'][:]), d['lut_canon'])
+
+
+@pytest.mark.parametrize('name', ['bmap_less', 'bmap_mask', 'bmap_greater'])
+def test_workflow_sharded_two_ranks(tmp_path, name):
+    """block_components config gpus = 2: the fused job starts two z-slab ranks
+    (torch.distributed.run, gloo collectives staged through the host: both ranks share this one
+    GPU, which RCCL refuses) and assembles the reference's artefacts from them."""
+    from cluster_tools_amd import n5
+    from cluster_tools_amd.thresholded_components import ThresholdedComponentsWorkflow
+    from cluster_tools_amd.thresholded_components.block_components import BlockComponentsLocal
+    from conftest import golden_index
+    meta = golden_index()[name]
+    d, data, cfg = _setup(tmp_path, name, meta['block_shape'])
+    c = BlockComponentsLocal.default_task_config()
+    c.update({'gpus': 2, 'dist_backend': 'gloo'})
+    _write_task_config(cfg, 'block_components', c)
+    kw = dict(mask_path=data, mask_key='volumes/mask') if 'mask' in d else {}
+    t = ThresholdedComponentsWorkflow(tmp_folder=str(tmp_path / 'tmp'), config_dir=cfg, target='local', max_jobs=4,
+                                      input_path=data, input_key='volumes/boundaries', output_path=data,
+                                      output_key='data', assignment_key='assignments',
+                                      threshold=float(d['threshold']), threshold_mode=meta['mode'], **kw)
+    assert _build([t], tmp_path / 'tmp')
+    with n5.open_file(data, 'r') as f:
+        seg = f['data'][:]
+        np.testing.assert_array_equal(O.canon(seg), d['labels_canon'])
+        np.testing.assert_array_equal(O.canon(f['assignments'][:]), d['lut_canon'])
+        assert f['data'].attrs['maxId'] == int(d['max_id'])
+    ref = O.label_volume(d['input'], meta['block_shape'], float(d['threshold']), meta['mode'], d.get('mask'))
+    np.testing.assert_array_equal(seg, ref['labels'])          # raw ids too (min-id representatives)
+    off = json.load(open(str(tmp_path / 'tmp' / 'cc_offsets.json')))
+    np.testing.assert_array_equal(np.array(off['offsets'], dtype=np.uint64), d['offsets'])
+    timing = json.load(open(str(tmp_path / 'tmp' / 'cc_fused_timing.json')))
+    assert timing['gpus'] == 2
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize('mode', ['greater', 'less'])
+def test_workflow_c1(tmp_path, mode):
+    """BASELINE config 1 through the drop-in API: a CREMI-sized (125, 1250, 1250) float32 N5
+    dataset (synthetic: the CREMI sample is absent), block_shape [50, 512, 512] (the reference
+    default), threshold 0.5, target 'local'; the N5 output against the oracle, and the host /
+    device split recorded by the fused job."""
+    import torch
+    from cluster_tools_amd import n5, _lib
+    from cluster_tools_amd.cluster_tasks import BaseClusterTask
+    from cluster_tools_amd.thresholded_components import ThresholdedComponentsWorkflow
+    shape, bs = (125, 1250, 1250), [50, 512, 512]
+    with _lib.Context(0) as ctx:
+        x = ctx.generate_boundary_map(shape).cpu().numpy()
+    data = str(tmp_path / 'c1.n5')
+    with n5.open_file(data) as f:
+        f.create_dataset('volumes/raw/boundaries', data=x, chunks=(25, 256, 256), compression='gzip')
+    cfg = str(tmp_path / 'config')
+    os.makedirs(cfg)
+    g = BaseClusterTask.default_global_config()
+    assert g['block_shape'] == bs
+    with open(os.path.join(cfg, 'global.config'), 'w') as f:
+        json.dump(g, f)
+    t = ThresholdedComponentsWorkflow(tmp_folder=str(tmp_path / 'tmp'), config_dir=cfg, target='local', max_jobs=16,
+                                      input_path=data, input_key='volumes/raw/boundaries', output_path=data,
+                                      output_key='segmentation/cc', assignment_key='segmentation/assignments',
+                                      threshold=0.5, threshold_mode=mode)
+    assert _build([t], tmp_path / 'tmp')
+    ref = O.label_volume(x, bs, 0.5, mode, n_threads=16)
+    with n5.open_file(data, 'r') as f:
+        seg = f['segmentation/cc'][:]
+        assert f['segmentation/cc'].chunks == (25, 256, 256)
+        assert f['segmentation/cc'].attrs['maxId'] == ref['max_id']
+        np.testing.assert_array_equal(f['segmentation/assignments'][:], ref['lut'])
+    np.testing.assert_array_equal(seg, ref['labels'])
+    timing = json.load(open(str(tmp_path / 'tmp' / 'cc_fused_timing.json')))
+    for k in ('n5_read_s', 'h2d_s', 'device_s', 'd2h_s', 'n5_write_s'):
+        assert timing[k] > 0
+    print('C1 %s timing: %s' % (mode, timing))

@@ -6,9 +6,14 @@ roofline.traffic).
 
 Per kernel: dispatch count, average duration (from the kernel trace), and per-dispatch HBM
 bytes from the PMC passes, corrected as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE and
-WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B / lane)
-coalesced streaming read, so it is doubled ('fetch_bytes'); 'fetch_bytes_raw' keeps the
-uncorrected figure.  WRITE_SIZE is exact for 16-B-per-lane streaming stores.
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a coalesced streaming read
+of full 128-B lines (16 B / lane per the guide; the 4 B / lane, 256 B per wave-instruction f32
+rows of k_spec / k_pass2 read the same way: 9.1 GB raw for the 17.2 GB input), so those are
+doubled ('fetch_bytes'); 'fetch_bytes_raw' keeps the uncorrected figure.  Byte-wide reads (the
+uint8 mask, 64 B per wave-instruction) are counted exactly (raw k_spec<true> = 8.6 GB f32 / 2 +
+4.3 GB mask), so `--narrow KERNEL=BYTES` names the per-dispatch bytes of such reads: they are
+taken out of the raw figure before doubling and added back once.  WRITE_SIZE is exact for
+16-B-per-lane streaming stores.
 """
 import argparse
 import collections
@@ -63,14 +68,22 @@ def main():
     p.add_argument('--fetch')
     p.add_argument('--write')
     p.add_argument('-o', '--out', required=True)
+    p.add_argument('--narrow', action='append', default=[],
+                   help='KERNEL_PREFIX=BYTES: per-dispatch bytes of byte-wide reads (counted exactly)')
     a = p.parse_args()
+    narrow = {k: float(v) for k, v in (n.split('=') for n in a.narrow)}
     res = trace_stats(a.trace)
     fetch = counter(a.fetch, 'FETCH_SIZE') if a.fetch else {}
     write = counter(a.write, 'WRITE_SIZE') if a.write else {}
     for k, v in res.items():
         if k in fetch:
-            v['fetch_bytes_raw'] = fetch[k] * 1024
-            v['fetch_bytes'] = 2 * fetch[k] * 1024
+            raw = fetch[k] * 1024
+            nb = next((b for pre, b in narrow.items() if k.startswith(pre)), 0.0)
+            nb = min(nb, raw)
+            v['fetch_bytes_raw'] = raw
+            v['fetch_bytes'] = 2 * (raw - nb) + nb
+            if nb:
+                v['fetch_narrow_bytes'] = nb
         if k in write:
             v['write_bytes'] = write[k] * 1024
         if 'fetch_bytes' in v and 'write_bytes' in v:

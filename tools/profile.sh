@@ -14,6 +14,10 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetc
     python3 "$ROOT/bench.py" --no-cpu-baseline --steps 2 --warmup 1 "$@" > /dev/null 2> "$OUT/fetch.err"
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
     python3 "$ROOT/bench.py" --no-cpu-baseline --steps 2 --warmup 1 "$@" > /dev/null 2> "$OUT/write.err"
+# byte-wide mask reads are counted exactly by FETCH_SIZE (prof_summary.py --narrow): with --mask,
+# k_spec<true, ...> reads one mask byte per voxel of the workload
+NARROW=()
+case " $* " in *" --mask "*) NARROW=(--narrow "k_spec<true=${CC_NVOX:-4294967296}");; esac
 python3 "$ROOT/tools/prof_summary.py" --trace "$OUT/trace" --fetch "$OUT/fetch" --write "$OUT/write" \
-    -o "$OUT/summary.json" > "$OUT/summary.txt"
+    "${NARROW[@]}" -o "$OUT/summary.json" > "$OUT/summary.txt"
 cat "$OUT/summary.txt"
