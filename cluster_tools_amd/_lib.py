@@ -24,9 +24,11 @@ EXPORTS = (
     'cc_get_profile', 'cc_reset_profile', 'cc_shard_begin', 'cc_shard_assign', 'cc_shard_planes',
     'cc_seam_pairs', 'cc_shard_finish', 'cc_set_debug', 'cc_threshold', 'cc_shard_top_plane32',
     'cc_seam_pairs32', 'cc_shard_top_cubes32', 'cc_seam_pairs_cubes32',
-    'cc_evaluate', 'cc_get_overlaps', 'cc_relabel_consecutive', 'cc_n5_read', 'cc_n5_write',
-    'cc_set_option',
+    'cc_evaluate', 'cc_get_overlaps', 'cc_relabel_consecutive', 'cc_set_option',
 )
+# every symbol include/cc_n5.h declares (libcc_n5.so: host-only N5 codec)
+N5_LIB_PATH = os.path.join(_HERE, 'lib', 'libcc_n5.so')
+N5_EXPORTS = ('cc_n5_version', 'cc_n5_last_error', 'cc_n5_read', 'cc_n5_write')
 
 
 class CCResult(ctypes.Structure):
@@ -61,6 +63,13 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError('libcc_mi355x.so not built (%s): run __graft_entry__.build()' % LIB_PATH)
+    # One HIP runtime per process: torch bundles its own libamdhip64 (SONAME libamdhip64.so.7), and
+    # the library must bind to that one.  Loaded first, the library would pull /opt/rocm's copy and
+    # torch would then load a second runtime beside it (the second to initialise sees no device).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     P, i64, u64, I = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int
     sig = {
@@ -98,8 +107,6 @@ def load():
         'cc_evaluate': (I, [P, P, P, P, P, I, u64, ctypes.POINTER(CCEvalResult)]),
         'cc_get_overlaps': (i64, [P, P, P, P, i64]),
         'cc_relabel_consecutive': (I, [P, P, P, i64, P, P, P, i64]),
-        'cc_n5_read': (I, [ctypes.c_char_p, I, P, P, I, I, P, P, P, I]),
-        'cc_n5_write': (I, [ctypes.c_char_p, I, P, P, I, I, I, P, P, P, I, I]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -107,6 +114,38 @@ def load():
         fn.argtypes = args
     _lib = L
     return L
+
+
+_n5 = None
+
+
+def load_n5():
+    """The host-only N5 codec library (no GPU runtime)."""
+    global _n5
+    if _n5 is not None:
+        return _n5
+    if not os.path.exists(N5_LIB_PATH):
+        raise RuntimeError('libcc_n5.so not built (%s): run __graft_entry__.build()' % N5_LIB_PATH)
+    L = ctypes.CDLL(N5_LIB_PATH)
+    P, I = ctypes.c_void_p, ctypes.c_int
+    sig = {
+        'cc_n5_version': (ctypes.c_char_p, []),
+        'cc_n5_last_error': (ctypes.c_char_p, []),
+        'cc_n5_read': (I, [ctypes.c_char_p, I, P, P, I, I, P, P, P, I]),
+        'cc_n5_write': (I, [ctypes.c_char_p, I, P, P, I, I, I, P, P, P, I, I]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _n5 = L
+    return L
+
+
+def _check_n5(rc):
+    if rc < 0:
+        raise RuntimeError('libcc_n5: ' + load_n5().cc_n5_last_error().decode())
+    return rc
 
 
 def version():
@@ -117,12 +156,12 @@ def check_provenance():
     """Raise unless the loaded library was built from this tree's sources: cc_version()
     carries the SHA-256 prefix build.py embedded (binary provenance)."""
     from . import build
-    v = version()
     want = build.source_hash()
-    got = v.split('src=')[-1] if 'src=' in v else None
-    if got != want:
-        raise RuntimeError('%s was built from other sources (library src=%s, tree src=%s): rebuild with '
-                           '__graft_entry__.build()' % (LIB_PATH, got, want))
+    for path, v in ((LIB_PATH, version()), (N5_LIB_PATH, load_n5().cc_n5_version().decode())):
+        got = v.split('src=')[-1] if 'src=' in v else None
+        if got != want:
+            raise RuntimeError('%s was built from other sources (library src=%s, tree src=%s): rebuild with '
+                               '__graft_entry__.build()' % (path, got, want))
     return want
 
 
@@ -456,8 +495,8 @@ def n5_read(path, shape, chunks, elem_size, compression, begin, end, out, n_thre
         raise NotImplementedError('n5 compression %s' % compression)
     assert out.flags.c_contiguous and out.dtype.itemsize == elem_size
     sh, ch, b, e = (_i64(v) for v in (shape, chunks, begin, end))
-    _check(load().cc_n5_read(os.fsencode(path), len(sh), _ptr(sh), _ptr(ch), int(elem_size),
-                             _COMPRESSION[compression], _ptr(b), _ptr(e), _ptr(out), int(n_threads)))
+    _check_n5(load_n5().cc_n5_read(os.fsencode(path), len(sh), _ptr(sh), _ptr(ch), int(elem_size),
+                                   _COMPRESSION[compression], _ptr(b), _ptr(e), _ptr(out), int(n_threads)))
     return out
 
 
@@ -469,6 +508,6 @@ def n5_write(path, shape, chunks, elem_size, compression, level, begin, end, dat
     data = np.ascontiguousarray(data)
     assert data.dtype.itemsize == elem_size
     sh, ch, b, e = (_i64(v) for v in (shape, chunks, begin, end))
-    _check(load().cc_n5_write(os.fsencode(path), len(sh), _ptr(sh), _ptr(ch), int(elem_size),
-                              _COMPRESSION[compression], int(level), _ptr(b), _ptr(e), _ptr(data),
-                              int(n_threads), int(bool(skip_zero_chunks))))
+    _check_n5(load_n5().cc_n5_write(os.fsencode(path), len(sh), _ptr(sh), _ptr(ch), int(elem_size),
+                                    _COMPRESSION[compression], int(level), _ptr(b), _ptr(e), _ptr(data),
+                                    int(n_threads), int(bool(skip_zero_chunks))))

@@ -1,7 +1,8 @@
-"""Build libcc_mi355x.so in-tree (hipcc, gfx950).  Used by __graft_entry__.build().
+"""Build libcc_mi355x.so (hipcc, gfx950) and libcc_n5.so (host C++, zlib) in-tree.  Used by
+__graft_entry__.build().
 
-Binary provenance: the build embeds a SHA-256 of every source it is built from (csrc/*.hip,
-csrc/*.hpp, csrc/*.cpp and include/cc_mi355x.h) in cc_version() ("... src=<hash>").
+Binary provenance: the build embeds a SHA-256 of every source the libraries are built from
+(csrc/*.hip, csrc/*.hpp, csrc/*.cpp, include/*.h) in cc_version() / cc_n5_version() ("... src=<hash>").
 `source_hash()` recomputes it from the tree; `_lib.check_provenance()` compares the two, and
 bench.py / the GPU tests refuse a library built from other sources than the tree's.
 """
@@ -12,8 +13,9 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
-HEADER = os.path.join(os.path.dirname(HERE), 'include', 'cc_mi355x.h')
+INCLUDE = os.path.join(os.path.dirname(HERE), 'include')
 OUT = os.path.join(HERE, 'lib', 'libcc_mi355x.so')
+OUT_N5 = os.path.join(HERE, 'lib', 'libcc_n5.so')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = os.environ.get('CC_OFFLOAD_ARCH', 'gfx950')
 
@@ -22,10 +24,14 @@ def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(('.hip', '.hpp', '.cpp')))
 
 
+def headers():
+    return sorted(os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE) if f.endswith('.h'))
+
+
 def source_hash():
-    """SHA-256 (first 16 hex digits) over the names and bytes of the library's sources."""
+    """SHA-256 (first 16 hex digits) over the names and bytes of the libraries' sources."""
     h = hashlib.sha256()
-    for p in sources() + [HEADER]:
+    for p in sources() + headers():
         h.update(os.path.basename(p).encode() + b'\0')
         with open(p, 'rb') as f:
             h.update(f.read())
@@ -34,23 +40,26 @@ def source_hash():
 
 
 def needs_rebuild():
-    if not os.path.exists(OUT):
+    if not os.path.exists(OUT) or not os.path.exists(OUT_N5):
         return True
-    t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(s) > t for s in sources() + [HEADER])
+    t = min(os.path.getmtime(OUT), os.path.getmtime(OUT_N5))
+    return any(os.path.getmtime(s) > t for s in sources() + headers())
 
 
 def build(force=False, verbose=True):
     if not force and not needs_rebuild():
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    h = '-DCC_SRC_HASH="%s"' % source_hash()
+    cmd_n5 = [os.environ.get('CXX', 'g++'), '-O3', '-std=c++17', '-fPIC', '-shared', '-Wall', h,
+              '-o', OUT_N5 + '.tmp', os.path.join(CSRC, 'cc_n5.cpp'), '-lz', '-pthread']
     cmd = [HIPCC, '--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-shared',
-           '-Wall', '-Wno-unused-function', '-DCC_SRC_HASH="%s"' % source_hash(),
-           '-o', OUT + '.tmp', os.path.join(CSRC, 'cc_lib.hip'), '-lz']
-    if verbose:
-        print(' '.join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    os.replace(OUT + '.tmp', OUT)
+           '-Wall', '-Wno-unused-function', h, '-o', OUT + '.tmp', os.path.join(CSRC, 'cc_lib.hip')]
+    for c, out in ((cmd_n5, OUT_N5), (cmd, OUT)):
+        if verbose:
+            print(' '.join(c), file=sys.stderr)
+        subprocess.run(c, check=True)
+        os.replace(out + '.tmp', out)
     return OUT
 
 

@@ -1,4 +1,6 @@
-// cc_n5_host.hpp -- native N5 chunk codec (host C++, zlib), included by cc_lib.hip.
+// cc_n5.cpp -- native N5 chunk codec (host C++, zlib): libcc_n5.so, include/cc_n5.h.  Host only,
+// no HIP: it is built and loaded apart from the device library, so reading a dataset never
+// brings up a GPU runtime (one HIP runtime per process: torch's, which libcc_mi355x binds to).
 //
 // The reference reads and writes every dataset of the path through elf.io.open_file -> z5py
 // (C++): cluster_tools/utils/volume_utils.py:21-22 (file_reader), ds_in[bb] / ds_out[bb] in
@@ -14,10 +16,11 @@
 // A region read / write fans the chunks it touches out over n_threads host threads (each
 // chunk: file read, inflate, byte swap into the caller's C-order box -- or the reverse), the
 // work the Python reference did one chunk at a time under z5py.
-#pragma once
 #include <sys/stat.h>
 #include <unistd.h>
 #include <zlib.h>
+
+#include <stdint.h>
 
 #include <algorithm>
 #include <array>
@@ -30,6 +33,10 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include "../../include/cc_n5.h"
+
+static thread_local std::string g_err;
 
 namespace cc_n5 {
 
@@ -370,6 +377,13 @@ static Spec make_spec(int ndim, const int64_t* shape, const int64_t* chunks, int
 }  // namespace cc_n5
 
 extern "C" {
+
+#ifndef CC_SRC_HASH
+#define CC_SRC_HASH "unknown"
+#endif
+const char* cc_n5_version(void) { return "cc_n5 0.2 src=" CC_SRC_HASH; }
+
+const char* cc_n5_last_error(void) { return g_err.c_str(); }
 
 int cc_n5_read(const char* dataset_path, int ndim, const int64_t* shape, const int64_t* chunks, int elem_size,
                int compression, const int64_t* begin, const int64_t* end, void* out, int n_threads) {

@@ -209,8 +209,11 @@ def _fused_sharded(config_path, config, shape, nb):
     os.makedirs(out_dir, exist_ok=True)
     for fn in os.listdir(out_dir):
         os.remove(os.path.join(out_dir, fn))
-    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'sharded_job.py')
-    repo = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import cluster_tools_amd
+    pkg = os.path.dirname(os.path.abspath(cluster_tools_amd.__file__))
+    # (this module runs as a copy in the tmp folder: locate the package, not __file__)
+    script = os.path.join(pkg, 'thresholded_components', 'sharded_job.py')
+    repo = os.path.dirname(pkg)
     env = dict(os.environ)
     env['PYTHONPATH'] = repo + (os.pathsep + env['PYTHONPATH'] if env.get('PYTHONPATH') else '')
     env['HSA_ENABLE_IPC_MODE_LEGACY'] = '0'

@@ -236,22 +236,6 @@ int64_t cc_get_overlaps(cc_ctx* ctx, uint64_t* seg_ids, uint64_t* gt_ids, uint64
 int cc_relabel_consecutive(cc_ctx* ctx, const uint64_t* labels_dev, uint64_t* out_dev, int64_t n,
                            uint64_t* n_unique, uint64_t* start_label, uint64_t* uniques_host, int64_t cap);
 
-/* --- N5 chunk codec (host only, no GPU) ---------------------------------------
- * Replaces z5py, which the reference reaches through elf.io.open_file (volume_utils.py:21-22) for
- * every ds[bb] read / write of the path (block_components.py:151,180, write.py:185-202,
- * merge_assignments.py:136-139).  N5 layout: chunk file <dataset>/<i_fastest>/.../<i_slowest>,
- * big-endian header (u16 mode, u16 ndim, u32 dims fastest first) and big-endian C-order payload,
- * raw (compression 0) or gzip (1, deflate `level`).  Region [begin, end) (NULL = whole dataset) of
- * a dataset of `shape` / `chunks` (C order, ndim 1..4), elem_size 1/2/4/8 bytes, host buffers in
- * C order over the region.  Chunks are coded on n_threads host threads.  Read: missing chunks
- * read as 0.  Write: partially covered chunks are read, merged and rewritten; skip_zero_chunks: an
- * all-zero chunk that has no file yet is not written (the reference never writes empty blocks). */
-int cc_n5_read(const char* dataset_path, int ndim, const int64_t* shape, const int64_t* chunks, int elem_size,
-               int compression, const int64_t* begin, const int64_t* end, void* out_host, int n_threads);
-int cc_n5_write(const char* dataset_path, int ndim, const int64_t* shape, const int64_t* chunks, int elem_size,
-                int compression, int level, const int64_t* begin, const int64_t* end, const void* in_host,
-                int n_threads, int skip_zero_chunks);
-
 #ifdef __cplusplus
 }
 #endif

@@ -9,8 +9,8 @@ import pytest
 from conftest import ROOT
 
 
-def header_functions():
-    src = open(os.path.join(ROOT, 'include', 'cc_mi355x.h')).read()
+def header_functions(name='cc_mi355x.h'):
+    src = open(os.path.join(ROOT, 'include', name)).read()
     src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
     return sorted(set(re.findall(r'\b(cc_[a-z0-9_]+)\s*\(', src)))
 
@@ -23,6 +23,15 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(L, name), name
     assert set(declared) == set(_lib.EXPORTS)
+
+
+def test_n5_library_exports_every_declared_symbol():
+    from cluster_tools_amd import _lib
+    L = _lib.load_n5()
+    declared = header_functions('cc_n5.h')
+    for name in declared:
+        assert hasattr(L, name), name
+    assert set(declared) == set(_lib.N5_EXPORTS)
 
 
 def test_version_and_error_channel():
