@@ -272,7 +272,12 @@ class Context:
         """EvaluationWorkflow (evaluation/evaluation_workflow.py:46-84) on device: overlaps per
         block (block_node_labels.py:133-166) + measures (measures.py:81-162).  `seg`, `gt` are
         uint64 (torch int64 / uint64) CUDA tensors of one shape; ignore_label None counts every
-        gt voxel.  Returns the cc_eval_result fields as a dict."""
+        gt voxel.  Returns the cc_eval_result fields as a dict.
+
+        The device table packs (seg, gt) into one 64-bit key (seg < 2^31, gt < 2^32 - 1).  Volumes
+        with larger (e.g. sparse 64-bit) ids are first relabelled consecutively on the device
+        (relabel_consecutive: order-preserving, 0 stays 0, so the per-block `seg.sum() == 0` skip
+        and every measure are unchanged); overlaps() maps the ids back."""
         import torch
         for a in (seg, gt):
             assert hasattr(a, 'data_ptr') and a.is_cuda and a.element_size() == 8 and a.is_contiguous()
@@ -284,17 +289,36 @@ class Context:
         use_ignore = ignore_label is not None
         # the ctx runs on its own stream: seg / gt may still be in flight on torch's
         torch.cuda.current_stream(seg.device).synchronize()
+
+        def too_large(a, limit):
+            v = a.view(torch.int64)
+            return bool((v < 0).any()) or bool((v >= limit).any())
+        self._ev_tables = [None, None]
+        if too_large(seg, 2 ** 31):
+            seg, self._ev_tables[0] = self.relabel_consecutive(seg)
+        if too_large(gt, 2 ** 32 - 1):
+            gt, table = self.relabel_consecutive(gt)
+            self._ev_tables[1] = table
+            if use_ignore:       # the ignore label in the new id space (an unused id if absent)
+                k = np.searchsorted(table[:, 0], np.uint64(ignore_label))
+                present = k < len(table) and table[k, 0] == np.uint64(ignore_label)
+                ignore_label = int(table[k, 1]) if present else int(table[-1, 1]) + 1
+        torch.cuda.current_stream(seg.device).synchronize()
         _check(load().cc_evaluate(self._h, _ptr(seg), _ptr(gt), _ptr(shape), _ptr(bs), int(use_ignore),
                                   int(ignore_label) if use_ignore else 0, ctypes.byref(res)))
         return res.as_dict()
 
     def overlaps(self):
         """Contingency table of the last evaluate(): (seg_ids, gt_ids, counts) uint64, sorted by
-        (seg id, gt id)."""
+        (seg id, gt id), in the caller's id spaces."""
         L = load()
         n = _check(L.cc_get_overlaps(self._h, None, None, None, 0))
         a, b, c = (np.empty(n, dtype=np.uint64) for _ in range(3))
         _check(L.cc_get_overlaps(self._h, _ptr(a), _ptr(b), _ptr(c), n))
+        for k, arr in enumerate((a, b)):
+            table = getattr(self, '_ev_tables', [None, None])[k]
+            if table is not None:                      # back from the relabelled id space
+                arr[:] = table[(arr - table[0, 1]).astype(np.int64), 0]
         o = np.lexsort((b, a))
         return a[o], b[o], c[o]
 

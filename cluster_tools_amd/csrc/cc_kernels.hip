@@ -1795,8 +1795,11 @@ __global__ void k_lut(int64_t n, const u32* vals, u32* P, const u64* KR, u64 bas
     if (r == node && rep == KR[r]) atomicAdd((unsigned long long*)&scalars[1], 1ull);   // components owned here
 }
 
-// final label of every node.  FIN may alias KR when !LOCAL: roots keep their rid, so a
-// concurrent reader of a root's entry never sees an overwritten value.  LOCAL (stage-level
+// final label of every node.  FIN may alias KR when !LOCAL: a root's entry KR[root] = rid is
+// overwritten with apply_map(rid) while other waves may still read it.  That is safe because
+// apply_map is idempotent -- V[i] is the smallest id of its seam set, and that id is in U with
+// V = itself -- so a reader computes apply_map(rid) or apply_map(apply_map(rid)), the same value
+// (tests/test_gpu_sharded.py checks the sharded labels against the oracle).  LOCAL (stage-level
 // block_components) writes the block-local skimage label rid - offset into a separate FIN.
 template <bool LOCAL>
 __global__ __launch_bounds__(NTHREADS) void k_finalize(Geom g, const u32* COUNT, u32* P, const u64* KR,

@@ -97,11 +97,37 @@ def test_gpu_evaluate_empty_and_errors(ctx):
     z = torch.zeros((4, 8, 8), dtype=torch.int64, device='cuda')
     got = ctx.evaluate(z, z, (2, 4, 4))
     assert got['n_points'] == 0 and got['n_pairs'] == 0
-    big = torch.full((4, 8, 8), 1 << 40, dtype=torch.int64, device='cuda')
-    with pytest.raises(RuntimeError, match='segmentation id'):
-        ctx.evaluate(big, z + 1, (2, 4, 4))
-    with pytest.raises(RuntimeError, match='ground-truth id'):
-        ctx.evaluate(z + 1, big, (2, 4, 4))
+
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('ignore', [0, 5, None])
+def test_gpu_evaluate_sparse_64bit_ids(ctx, ignore):
+    """Ids beyond the device key packing (seg >= 2^31, gt >= 2^32 - 1, up to 2^64 - 2) are
+    relabelled consecutively on the device first: the measures equal those of the small-id
+    volumes, and overlaps() reports the caller's ids."""
+    import torch
+    rng = np.random.default_rng(21)
+    shape, bs = (9, 17, 33), (4, 8, 8)
+    seg, gt = _random_case(rng, shape, 6, 5, 0.2, 0.1)
+    want, ov = E.measures(seg, gt, bs, ignore_label=ignore)
+
+    def sparse(a):     # order-preserving, 0 -> 0, ignore label kept
+        b = a.astype(np.uint64) * np.uint64(0x0123456789ABC) + np.uint64(1 << 62)
+        b[a == 0] = 0
+        if ignore:
+            b[a == ignore] = ignore
+        return b
+    s64, g64 = sparse(seg), sparse(gt)
+    got = ctx.evaluate(torch.from_numpy(s64.view(np.int64)).cuda(), torch.from_numpy(g64.view(np.int64)).cuda(),
+                       bs, ignore_label=ignore)
+    for k in ('n_points', 'n_pairs', 'n_seg_ids', 'n_gt_ids'):
+        assert got[k] == want[k], k
+    for k in ('vi_split', 'vi_merge', 'adapted_rand_error', 'rand_index'):
+        assert got[k] == pytest.approx(want[k], rel=RTOL, abs=1e-12), k
+    _, ov64 = E.measures(s64, g64, bs, ignore_label=ignore)
+    sa, gb, cnt = ctx.overlaps()
+    assert {(int(a), int(b)): int(n) for a, b, n in zip(sa, gb, cnt)} == ov64
 
 
 @pytest.mark.gpu
