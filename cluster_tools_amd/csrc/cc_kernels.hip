@@ -526,7 +526,8 @@ struct Pass1LDS {
 
 template <int ABL>
 __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const TileInfo& ti, u64* BITS, face_t* FACES,
-                                             u32* COUNT, u32* P, u64* KEY, Pass1LDS& L, bool write);
+                                             u32* COUNT, u32* P, u64* KEY, Pass1LDS& L, bool write,
+                                             u8* fchg = nullptr);
 
 // Pass 1 of tile t (block parameters p): bit rows -> BITS, tile CCL -> COUNT, nodes (P, KEY),
 // face planes.  ABL (kernel ablation harness tools/ablate.hip only; 0 in the library): stop
@@ -535,19 +536,21 @@ template <bool HAS_MASK, int ABL = 0>
 __device__ __forceinline__ void pass1_tile(const Geom& g, int64_t t, const TileInfo& ti, const BlockParam& p,
                                            const float* __restrict__ in, const u8* __restrict__ mask, float thr,
                                            int mode, u64* BITS, face_t* FACES, u32* COUNT, u32* P, u64* KEY,
-                                           Pass1LDS& L, bool write = true) {
+                                           Pass1LDS& L, bool write = true, u8* fchg = nullptr) {
     const int tid = cc_tid();
     for (int i = tid; i < NROWS; i += NTHREADS) L.rows[i] = 0;
     __syncthreads();
     if (p.kind != BP_EMPTY) load_rows<HAS_MASK>(g, ti, in, mask, p, thr, mode, L.rows);
     __syncthreads();
-    pass1_finish<ABL>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, write);
+    pass1_finish<ABL>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, write, fchg);
 }
 
 // Pass 1 after the bit rows are in L.rows (and a barrier): BITS, tile CCL, COUNT, nodes, faces.
+// fchg (k_fix): fchg[t] = 1 when the new face planes differ from the ones in FACES (the seams
+// that read them must be redone; unchanged faces leave every seam list as it was).
 template <int ABL>
 __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const TileInfo& ti, u64* BITS, face_t* FACES,
-                                             u32* COUNT, u32* P, u64* KEY, Pass1LDS& L, bool write) {
+                                             u32* COUNT, u32* P, u64* KEY, Pass1LDS& L, bool write, u8* fchg) {
     u64* rows = L.rows;
     TileCCL& T = L.T;
     u32* key = L.key;
@@ -597,8 +600,15 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
     }
     u32* FW = (u32*)(FACES + t * FACE_STRIDE);          // two 16-bit entries per store
     static_assert(F_YLO == 2 * NTHREADS && FACE_STRIDE / 2 <= 2 * NTHREADS, "face words: z faces, then y / x");
-    FW[tid] = face_word(tid, rows, T, ti);
-    if (NTHREADS + tid < FACE_STRIDE / 2) FW[NTHREADS + tid] = face_word(NTHREADS + tid, rows, T, ti);
+    const u32 w0 = face_word(tid, rows, T, ti);
+    const bool two = NTHREADS + tid < FACE_STRIDE / 2;
+    const u32 w1 = two ? face_word(NTHREADS + tid, rows, T, ti) : 0u;
+    if (fchg) {
+        const bool diff = FW[tid] != w0 || (two && FW[NTHREADS + tid] != w1);
+        if (__syncthreads_or(diff) && tid == 0) fchg[t] = 1;
+    }
+    FW[tid] = w0;
+    if (two) FW[NTHREADS + tid] = w1;
 }
 
 // k_pass1: one workgroup per tile, block parameters precomputed (ablation harness; the library
@@ -653,7 +663,10 @@ __device__ __forceinline__ TileInfo uniform_ti(TileInfo ti) {
 // so those blocks skip the speculation (k_spec reads them for statistics only, k_fix labels them).
 // Results never depend on the guess; only the amount of k_fix work does.
 // ------------------------------------------------------------------------------------------
-constexpr int SAMPLE_DZ = 16, SAMPLE_DY = 32;     // one voxel row per 16 planes x 32 rows of a block
+// one voxel row per 4 planes x 16 rows of a block (1/64 of it: on continuous data the guessed
+// bounds miss the exact ones by about the extremes' sampling error, so a denser sample leaves
+// fewer tiles with a voxel in between; 1/512 left 8 % of the C3 tiles to k_fix)
+constexpr int SAMPLE_DZ = 4, SAMPLE_DY = 16;
 
 __device__ __forceinline__ void block_extent(const Geom& g, int64_t b, int e0[3], int el[3]) {
     const int bi[3] = {(int)(b / ((int64_t)g.nb[2] * g.nb[1])), (int)((b / g.nb[2]) % g.nb[1]), (int)(b % g.nb[2])};
@@ -834,15 +847,21 @@ __global__ void k_verify(Geom g, const BlockParam* guess, const BlockParam* bp, 
 // pass 1 with the exact parameters for the listed tiles, one workgroup per tile (the host reads
 // the count first: a fixed grid walking the list hoisted the tile set-up out of the loop and
 // spilled; a grid over all tiles paid ~2 us of dependent loads per returning workgroup)
+// fchg[t] = 1 when the tile's faces changed; tiles k_spec only read for statistics (no guess)
+// hold no faces from this run and are always flagged.
 template <bool HAS_MASK>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_fix(
-    Geom g, const u32* FIX, const BlockParam* bp, const float* __restrict__ in, const u8* __restrict__ mask,
-    float thr, int mode, u64* BITS, face_t* FACES, u32* COUNT, u32* P, u64* KEY) {
+    Geom g, const u32* FIX, const BlockParam* bp, const BlockParam* guess, const float* __restrict__ in,
+    const u8* __restrict__ mask, float thr, int mode, u64* BITS, face_t* FACES, u32* COUNT, u32* P, u64* KEY,
+    u8* fchg) {
     __shared__ Pass1LDS L;
     const int64_t t = __builtin_amdgcn_readfirstlane(FIX[1 + blockIdx.x]);
     const TileInfo ti = uniform_ti(tile_info(g, t));
     const BlockParam p = uniform_bp(bp[ti.block]);
-    pass1_tile<HAS_MASK>(g, t, ti, p, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L);
+    const bool fresh = __builtin_amdgcn_readfirstlane(guess[ti.block].kind) == BP_INTERVAL;
+    if (!fresh && cc_tid() == 0) fchg[t] = 1;
+    pass1_tile<HAS_MASK>(g, t, ti, p, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L, true,
+                         fresh ? fchg : nullptr);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1484,13 +1503,14 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* _
     }
 }
 
-// Tiles whose seams read the faces of a relabelled tile (FIX[1 .. FIX[0]], k_fix): the tile itself
-// and the 13 tiles that have it as a lex-negative neighbour.  Each marked once (flag), listed in
+// Tiles whose seams read the faces of a relabelled tile whose faces changed (FIX[1 .. FIX[0]],
+// k_fix, fchg): the tile itself and the 13 tiles that have it as a lex-negative neighbour.  Each marked once (flag), listed in
 // LIST[1 .. LIST[0]] for k_seams.
-__global__ void k_mark_seams(Geom g, const u32* FIX, u32* flag, u32* LIST) {
+__global__ void k_mark_seams(Geom g, const u32* FIX, const u8* fchg, u32* flag, u32* LIST) {
     const u32 n = FIX[0];
     for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < 14 * n; i += gridDim.x * blockDim.x) {
         const u32 f = FIX[1 + i / 14], d = i % 14;
+        if (!fchg[f]) continue;                    // same faces: every seam list still holds
         const TileInfo ti = tile_info(g, f);
         // d = 0: the tile; else the dependent at (+dz, dy, dx) over the 13 lex-positive offsets
         int dz = 0, dy = 0, dx = 0;
@@ -2064,10 +2084,10 @@ __global__ __launch_bounds__(NTHREADS) void k_threshold(Geom g, const BlockParam
     template __global__ void k_spec<M, S>(Geom, SpecArgs, const float*, const u8*, u64*, face_t*, u32*, u32*, u64*);
 CC_SPEC(false, 1) CC_SPEC(false, 2) CC_SPEC(false, 3) CC_SPEC(true, 1) CC_SPEC(true, 2) CC_SPEC(true, 3)
 #undef CC_SPEC
-template __global__ void k_fix<false>(Geom, const u32*, const BlockParam*, const float*, const u8*, float, int, u64*,
-                                      face_t*, u32*, u32*, u64*);
-template __global__ void k_fix<true>(Geom, const u32*, const BlockParam*, const float*, const u8*, float, int, u64*,
-                                     face_t*, u32*, u32*, u64*);
+template __global__ void k_fix<false>(Geom, const u32*, const BlockParam*, const BlockParam*, const float*, const u8*,
+                                      float, int, u64*, face_t*, u32*, u32*, u64*, u8*);
+template __global__ void k_fix<true>(Geom, const u32*, const BlockParam*, const BlockParam*, const float*, const u8*,
+                                     float, int, u64*, face_t*, u32*, u32*, u64*, u8*);
 template __global__ void k_seams<0>(Geom, const face_t*, u64*, u32*, u8*, u64*, u32*, u8*, int64_t, int64_t, const u32*);
 template __global__ void k_stitch<false>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_stitch<true>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);

@@ -298,25 +298,27 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             k_block_params<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, smin, smax, sflag, thr, mode, bp);
         });
         launch(c, "k_verify", [&] { k_verify<<<grid_stride(nt), 256, 0, s>>>(g, guess, bp, TB, mode, FIX); });
+        c->mark.ensure((size_t)(2 * nt + 1) * sizeof(u32) + nt);
+        u32* flag = c->mark.as<u32>();
+        u32* list = flag + nt;
+        u8* fchg = (u8*)(list + nt + 1);
         u32 nfix = 0;
         HIP_OK(hipMemcpyAsync(&nfix, FIX, sizeof(u32), hipMemcpyDeviceToHost, s));
         HIP_OK(hipStreamSynchronize(s));
         st.n_fix = nfix;
         if (lds_seams) stream_wait(c, c->side, s);
         if (nfix) {
+            HIP_OK(hipMemsetAsync(fchg, 0, nt, s));
             launch(c, "k_fix", [&] {
-                if (mask) k_fix<true><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, in, mask, thr, mode, BITS, FACES, COUNT, P, KR);
-                else k_fix<false><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR);
+                if (mask) k_fix<true><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, mask, thr, mode, BITS, FACES, COUNT, P, KR, fchg);
+                else k_fix<false><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR, fchg);
             });
             if (lds_seams) {
                 // relabelled faces: the seams of the relabelled tiles and of the tiles above /
                 // beside them again (their lists are overwritten; stale overflow flags only send
                 // work to the global fallback, which reads the current faces)
-                c->mark.ensure((size_t)(nt + 1 + std::min<int64_t>(nt, 14 * (int64_t)nfix)) * sizeof(u32));
-                u32* flag = c->mark.as<u32>();
-                u32* list = flag + nt;
                 HIP_OK(hipMemsetAsync(flag, 0, (nt + 1) * sizeof(u32), s));
-                launch(c, "k_mark_seams", [&] { k_mark_seams<<<grid1d(14 * (int64_t)nfix), 256, 0, s>>>(g, FIX, flag, list); });
+                launch(c, "k_mark_seams", [&] { k_mark_seams<<<grid1d(14 * (int64_t)nfix), 256, 0, s>>>(g, FIX, fchg, flag, list); });
                 const int64_t nl = std::min<int64_t>(nt, 14 * (int64_t)nfix);
                 launch(c, "k_seams", [&] {
                     k_seams<0><<<(unsigned)((nl + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(

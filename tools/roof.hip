@@ -1,0 +1,168 @@
+// tools/roof.hip -- HBM read / write ceilings on this box for the access shapes of the path
+// (timing only, not part of the library).  Each variant streams the same bytes as C3:
+//   rd_f4_uU      float4 per lane, U independent loads in flight per lane (grid-stride)
+//   rd_tile_rzR   the tile walk of k_spec / k_block_stats: lane = x, one 256-B row per load
+//                 instruction, R planes x 4 rows = 4R loads in flight per lane, 512-thread tiles
+//   rd_tile4_rzR  the same tile walk with float4 per lane (16 lanes per 64-float row, 4 rows per
+//                 load instruction), R planes x 4 row groups in flight
+//   wr_u2_uU      16-B uint64 pair stores per lane, U per lane per iteration
+// Run: tools/roof Z Y X [iters]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#define CHK(x)                                                                        \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess) {                                                       \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));              \
+            std::exit(1);                                                             \
+        }                                                                             \
+    } while (0)
+
+template <int U>
+__global__ __launch_bounds__(256) void rd_f4(const float4* __restrict__ in, int64_t n4, float* out) {
+    float acc = 0.f;
+    const int64_t stride = (int64_t)gridDim.x * 256 * U;
+    for (int64_t b = (int64_t)blockIdx.x * 256 * U + threadIdx.x; b < n4; b += stride) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = b + u * 256 < n4 ? in[b + u * 256] : make_float4(0, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w));
+    }
+    if (acc == 1234.5f) out[0] = acc;
+}
+
+// tiles of 16 x 32 x 64 voxels, one 512-thread workgroup per tile, wave w owns rows w + 8 b
+template <int RZ>
+__global__ __launch_bounds__(512) void rd_tile(const float* __restrict__ in, int64_t Y, int64_t X, int ntx, int nty,
+                                               float* out) {
+    const int t = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int tx = t % ntx, ty = (t / ntx) % nty, tz = t / (ntx * nty);
+    const float* p = in + (((int64_t)tz * 16) * Y + ty * 32 + wave) * X + tx * 64 + lane;
+    const int64_t sz = Y * X, sy = 8 * X;
+    float mx = -1e30f;
+#pragma unroll
+    for (int z0 = 0; z0 < 16; z0 += RZ) {
+        float v[RZ][4];
+#pragma unroll
+        for (int a = 0; a < RZ; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) v[a][b] = p[(z0 + a) * sz + b * sy];
+#pragma unroll
+        for (int a = 0; a < RZ; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) mx = fmaxf(mx, v[a][b]);
+    }
+    if (mx == 1234.5f) out[0] = mx;
+}
+
+// float4 lanes: lane l reads x = 4 (l % 16) .. + 3 of row group row 4 * (wave-slot) + l / 16
+template <int RZ>
+__global__ __launch_bounds__(512) void rd_tile4(const float* __restrict__ in, int64_t Y, int64_t X, int ntx, int nty,
+                                                float* out) {
+    const int t = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int tx = t % ntx, ty = (t / ntx) % nty, tz = t / (ntx * nty);
+    // wave w: rows y = 4 w + (lane / 16) of each plane (32 rows = 8 waves x 4)
+    const float* p = in + (((int64_t)tz * 16) * Y + ty * 32 + 4 * wave + (lane >> 4)) * X + tx * 64 + 4 * (lane & 15);
+    const int64_t sz = Y * X;
+    float mx = -1e30f;
+#pragma unroll
+    for (int z0 = 0; z0 < 16; z0 += RZ) {
+        float4 v[RZ];
+#pragma unroll
+        for (int a = 0; a < RZ; ++a) v[a] = *reinterpret_cast<const float4*>(p + (z0 + a) * sz);
+#pragma unroll
+        for (int a = 0; a < RZ; ++a) mx = fmaxf(mx, fmaxf(fmaxf(v[a].x, v[a].y), fmaxf(v[a].z, v[a].w)));
+    }
+    if (mx == 1234.5f) out[0] = mx;
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void wr_u2(ulonglong2* __restrict__ out, int64_t n2) {
+    const int64_t stride = (int64_t)gridDim.x * 256 * U;
+    for (int64_t b = (int64_t)blockIdx.x * 256 * U + threadIdx.x; b < n2; b += stride)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (b + u * 256 < n2) out[b + u * 256] = make_ulonglong2((unsigned long long)(b + u), 0);
+}
+
+// the k_pass2 shape: one 512-thread tile, each thread 16-B stores of (x, x+1) pairs of cube rows
+__global__ __launch_bounds__(512) void wr_tile(unsigned long long* __restrict__ out, int64_t Y, int64_t X, int ntx,
+                                               int nty) {
+    const int t = blockIdx.x;
+    const int tx = t % ntx, ty = (t / ntx) % nty, tz = t / (ntx * nty);
+    for (int c = threadIdx.x; c < 4096; c += 512) {
+        const int cz = c / 512, cy = (c / 32) % 16, cx = c % 32;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const int z = 2 * cz + (d >> 1), y = 2 * cy + (d & 1);
+            const int64_t idx = (((int64_t)tz * 16 + z) * Y + ty * 32 + y) * X + tx * 64 + 2 * cx;
+            *reinterpret_cast<ulonglong2*>(out + idx) = make_ulonglong2((unsigned long long)c, (unsigned long long)d);
+        }
+    }
+}
+
+template <class F>
+static double time_ms(hipStream_t s, int iters, F&& f) {
+    hipEvent_t a, b;
+    CHK(hipEventCreate(&a));
+    CHK(hipEventCreate(&b));
+    f();
+    CHK(hipGetLastError());
+    CHK(hipEventRecord(a, s));
+    for (int i = 0; i < iters; ++i) f();
+    CHK(hipEventRecord(b, s));
+    CHK(hipEventSynchronize(b));
+    float ms = 0;
+    CHK(hipEventElapsedTime(&ms, a, b));
+    return ms / iters;
+}
+
+int main(int argc, char** argv) {
+    const int64_t Z = argc > 1 ? atoll(argv[1]) : 1024, Y = argc > 2 ? atoll(argv[2]) : 2048,
+                  X = argc > 3 ? atoll(argv[3]) : 2048;
+    const int iters = argc > 4 ? atoi(argv[4]) : 10;
+    const int64_t n = Z * Y * X;
+    float* in;
+    unsigned long long* out;
+    float* dummy;
+    CHK(hipMalloc(&in, n * 4));
+    CHK(hipMalloc(&out, n * 8));
+    CHK(hipMalloc(&dummy, 64));
+    CHK(hipMemset(in, 0, n * 4));
+    hipStream_t s;
+    CHK(hipStreamCreate(&s));
+    const int ntx = (int)(X / 64), nty = (int)(Y / 32), ntz = (int)(Z / 16);
+    const unsigned nt = (unsigned)ntx * nty * ntz;
+    std::vector<std::pair<std::string, double>> r;
+    const unsigned g = 256 * 16;
+    r.push_back({"rd_f4_u1", time_ms(s, iters, [&] { rd_f4<1><<<g * 4, 256, 0, s>>>((const float4*)in, n / 4, dummy); })});
+    r.push_back({"rd_f4_u2", time_ms(s, iters, [&] { rd_f4<2><<<g * 2, 256, 0, s>>>((const float4*)in, n / 4, dummy); })});
+    r.push_back({"rd_f4_u4", time_ms(s, iters, [&] { rd_f4<4><<<g, 256, 0, s>>>((const float4*)in, n / 4, dummy); })});
+    r.push_back({"rd_f4_u8", time_ms(s, iters, [&] { rd_f4<8><<<g, 256, 0, s>>>((const float4*)in, n / 4, dummy); })});
+    r.push_back({"rd_f4_u8_g1k", time_ms(s, iters, [&] { rd_f4<8><<<1024, 256, 0, s>>>((const float4*)in, n / 4, dummy); })});
+    r.push_back({"rd_tile_rz2", time_ms(s, iters, [&] { rd_tile<2><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
+    r.push_back({"rd_tile_rz4", time_ms(s, iters, [&] { rd_tile<4><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
+    r.push_back({"rd_tile_rz8", time_ms(s, iters, [&] { rd_tile<8><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
+    r.push_back({"rd_tile_rz16", time_ms(s, iters, [&] { rd_tile<16><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
+    r.push_back({"rd_tile4_rz2", time_ms(s, iters, [&] { rd_tile4<2><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
+    r.push_back({"rd_tile4_rz4", time_ms(s, iters, [&] { rd_tile4<4><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
+    r.push_back({"rd_tile4_rz8", time_ms(s, iters, [&] { rd_tile4<8><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
+    r.push_back({"rd_tile4_rz16", time_ms(s, iters, [&] { rd_tile4<16><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
+    r.push_back({"wr_u2_u1", time_ms(s, iters, [&] { wr_u2<1><<<g * 8, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
+    r.push_back({"wr_u2_u4", time_ms(s, iters, [&] { wr_u2<4><<<g * 2, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
+    r.push_back({"wr_u2_u8", time_ms(s, iters, [&] { wr_u2<8><<<g, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
+    r.push_back({"wr_tile", time_ms(s, iters, [&] { wr_tile<<<nt, 512, 0, s>>>(out, Y, X, ntx, nty); })});
+    std::printf("{\"shape\": [%lld, %lld, %lld]", (long long)Z, (long long)Y, (long long)X);
+    for (auto& kv : r) std::printf(", \"%s\": %.4f", kv.first.c_str(), kv.second);
+    std::printf("}\n");
+    for (auto& kv : r)
+        std::printf("# %-16s %7.3f ms  %6.0f GB/s\n", kv.first.c_str(), kv.second,
+                    (kv.first[0] == 'r' ? 4.0 : 8.0) * n / kv.second / 1e6);
+    return 0;
+}
