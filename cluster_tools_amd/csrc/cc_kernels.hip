@@ -658,10 +658,10 @@ __device__ __forceinline__ TileInfo uniform_ti(TileInfo ti) {
 // lies between lg and lt nor between hg and ht -- decided from TB alone (spec_valid).  k_verify
 // k_verify lists the tiles that fail and k_fix relabels them from the input with the exact interval.
 // A one-sided interval is kept open to the end of the order (widen): it then differs from the
-// exact one only in its finite bound.  The guess is made only where the sample looks quantized
-// (its extremes occur more than once): on continuous data a sampled bound is almost never exact,
-// so those blocks skip the speculation (k_spec reads them for statistics only, k_fix labels them).
-// Results never depend on the guess; only the amount of k_fix work does.
+// exact one only in its finite bound.  On quantized data the sampled extremes are usually the
+// block's and the guess is exact; on continuous data it misses the exact bound by about the
+// extremes' sampling error, and only tiles holding a voxel in between are relabelled (1 % of the
+// C3 tiles with the dithered map).  Results never depend on the guess; only the k_fix work does.
 // ------------------------------------------------------------------------------------------
 // one voxel row per 4 planes x 16 rows of a block (1/64 of it: on continuous data the guessed
 // bounds miss the exact ones by about the extremes' sampling error, so a denser sample leaves
@@ -702,7 +702,7 @@ __device__ __forceinline__ u32 block_reduce(u32 v, u32* red, Op op) {
 }
 
 // k_sample: workgroup (b, part) reads every SAMPLE_PARTS-th sample row of block b and writes its
-// (min, count of min, max, count of max); k_guess combines the parts of each block.
+// (min, 0, max, 0); k_guess combines the parts of each block.
 constexpr int SAMPLE_PARTS = 8;
 
 __global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __restrict__ in, u32* part) {
@@ -714,31 +714,33 @@ __global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __rest
     block_extent(g, b, e0, el);
     const int nzs = max(1, el[0] / SAMPLE_DZ), nys = max(1, el[1] / SAMPLE_DY);
     const int zo = min(SAMPLE_DZ / 2, (el[0] - 1) / 2), yo = min(SAMPLE_DY / 2, (el[1] - 1) / 2);
+    // SAMPLE_U rows of the part in flight per thread (one row at a time was latency-bound)
+    constexpr int SAMPLE_U = 8;
+    const int nrows = nzs * nys;
     auto sweep = [&](auto&& f) {
-        for (int r = pt; r < nzs * nys; r += SAMPLE_PARTS) {
-            const int z = e0[0] + (r / nys) * SAMPLE_DZ + zo, y = e0[1] + (r % nys) * SAMPLE_DY + yo;
-            const float* row = in + ((int64_t)z * g.Y + y) * g.X + e0[2];
-#pragma unroll 4
-            for (int x = tid; x < el[2]; x += NTHREADS) f(f2ord(__float_as_uint(row[x])));
-        }
+        for (int r0 = pt; r0 < nrows; r0 += SAMPLE_PARTS * SAMPLE_U)
+            for (int x = tid; x < el[2]; x += NTHREADS) {
+                float v[SAMPLE_U];
+#pragma unroll
+                for (int u = 0; u < SAMPLE_U; ++u) {
+                    const int r = min(r0 + u * SAMPLE_PARTS, nrows - 1);    // repeats are harmless
+                    const int z = e0[0] + (r / nys) * SAMPLE_DZ + zo, y = e0[1] + (r % nys) * SAMPLE_DY + yo;
+                    v[u] = in[((int64_t)z * g.Y + y) * g.X + e0[2] + x];
+                }
+#pragma unroll
+                for (int u = 0; u < SAMPLE_U; ++u) f(f2ord(__float_as_uint(v[u])));
+            }
     };
-    // running (min, count of min) and (max, count of max) in one sweep
-    u32 mn = 0xFFFFFFFFu, mx = 0u, nmn = 0, nmx = 0;
+    u32 mn = 0xFFFFFFFFu, mx = 0u;
     sweep([&](u32 o) {
-        nmn = o < mn ? 1u : nmn + (o == mn);
-        nmx = o > mx ? 1u : nmx + (o == mx);
         mn = min(mn, o);
         mx = max(mx, o);
     });
-    const u32 bmn = block_reduce(mn, red, [](u32 a, u32 c) { return min(a, c); });
-    const u32 bmx = block_reduce(mx, red, [](u32 a, u32 c) { return max(a, c); });
-    nmn = block_reduce(mn == bmn ? nmn : 0u, red, [](u32 a, u32 c) { return a + c; });
-    nmx = block_reduce(mx == bmx ? nmx : 0u, red, [](u32 a, u32 c) { return a + c; });
-    mn = bmn;
-    mx = bmx;
+    mn = block_reduce(mn, red, [](u32 a, u32 c) { return min(a, c); });
+    mx = block_reduce(mx, red, [](u32 a, u32 c) { return max(a, c); });
     if (tid == 0) {
         u32* q = part + 4 * blockIdx.x;
-        q[0] = mn; q[1] = nmn; q[2] = mx; q[3] = nmx;
+        q[0] = mn; q[1] = 0; q[2] = mx; q[3] = 0;
     }
 }
 
@@ -746,16 +748,11 @@ __global__ void k_guess(int64_t nb, const u32* part, float thr, int mode, BlockP
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     const u32* q = part + 4 * SAMPLE_PARTS * b;
-    u32 mn = 0xFFFFFFFFu, mx = 0u, nmn = 0, nmx = 0;
+    u32 mn = 0xFFFFFFFFu, mx = 0u;
     for (int p = 0; p < SAMPLE_PARTS; ++p) { mn = min(mn, q[4 * p]); mx = max(mx, q[4 * p + 2]); }
-    for (int p = 0; p < SAMPLE_PARTS; ++p) {
-        if (q[4 * p + 1] && q[4 * p] == mn) nmn += q[4 * p + 1];
-        if (q[4 * p + 3] && q[4 * p + 2] == mx) nmx += q[4 * p + 3];
-    }
     const bool nan = mx > 0xFF800000u || mn < 0x007FFFFFu;
     // On continuous data the sampled extremes are not the block's, so the guessed bound misses
     // the exact one by a little: only tiles holding a voxel between the two are relabelled.
-    (void)nmn; (void)nmx;
     guess[b] = widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
 }
 

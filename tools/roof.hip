@@ -107,6 +107,23 @@ __global__ __launch_bounds__(512) void wr_tile(unsigned long long* __restrict__ 
     }
 }
 
+// the k_pass2 store shape over NT x-adjacent tiles per workgroup (NT * 512-B contiguous rows)
+template <int NT>
+__global__ __launch_bounds__(512) void wr_tile_w(unsigned long long* __restrict__ out, int64_t Y, int64_t X, int ntx,
+                                                 int nty) {
+    const int t = blockIdx.x;
+    const int tx = t % (ntx / NT), ty = (t / (ntx / NT)) % nty, tz = t / ((ntx / NT) * nty);
+    for (int c = threadIdx.x; c < 4096 * NT; c += 512) {
+        const int cz = c / (512 * NT), cy = (c / (32 * NT)) % 16, cx = c % (32 * NT);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const int z = 2 * cz + (d >> 1), y = 2 * cy + (d & 1);
+            const int64_t idx = (((int64_t)tz * 16 + z) * Y + ty * 32 + y) * X + (int64_t)tx * 64 * NT + 2 * cx;
+            *reinterpret_cast<ulonglong2*>(out + idx) = make_ulonglong2((unsigned long long)c, (unsigned long long)d);
+        }
+    }
+}
+
 template <class F>
 static double time_ms(hipStream_t s, int iters, F&& f) {
     hipEvent_t a, b;
@@ -158,6 +175,8 @@ int main(int argc, char** argv) {
     r.push_back({"wr_u2_u4", time_ms(s, iters, [&] { wr_u2<4><<<g * 2, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
     r.push_back({"wr_u2_u8", time_ms(s, iters, [&] { wr_u2<8><<<g, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
     r.push_back({"wr_tile", time_ms(s, iters, [&] { wr_tile<<<nt, 512, 0, s>>>(out, Y, X, ntx, nty); })});
+    r.push_back({"wr_tile_w2", time_ms(s, iters, [&] { wr_tile_w<2><<<nt / 2, 512, 0, s>>>(out, Y, X, ntx, nty); })});
+    r.push_back({"wr_tile_w4", time_ms(s, iters, [&] { wr_tile_w<4><<<nt / 4, 512, 0, s>>>(out, Y, X, ntx, nty); })});
     std::printf("{\"shape\": [%lld, %lld, %lld]", (long long)Z, (long long)Y, (long long)X);
     for (auto& kv : r) std::printf(", \"%s\": %.4f", kv.first.c_str(), kv.second);
     std::printf("}\n");
