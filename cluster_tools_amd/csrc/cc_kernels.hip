@@ -461,6 +461,16 @@ __device__ __forceinline__ void load_rows(const Geom& g, const TileInfo& ti, con
     if (r / TY < ti.lz && r % TY < ti.ly) rows[r] = split_row(((u64)mhi << 32) | mlo);
 }
 
+// bit i of x (i < 16) -> bit 2i
+__device__ __forceinline__ u32 spread2(u32 x) {
+    x &= 0xFFFFu;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x;
+}
+
 // voxel x of a split bit row
 __device__ __forceinline__ u32 vbit(u64 w, int x) { return (u32)(w >> ((x & 1) * 32 + (x >> 1))) & 1u; }
 // the two voxels (2cx, 2cx + 1) of cube column cx of a split row, as bits 0 / 1
@@ -778,27 +788,77 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         return;
     }
     const int tid = cc_tid(), lane = tid & 63, wave = wave_id();
-    for (int i = tid; i < NROWS; i += NTHREADS) L.rows[i] = 0;
-    __syncthreads();
     const u32 lo = p.lo, hi = p.hi;
-    const u64 lanes = ti.lx >= 64 ? ~0ull : ((1ull << ti.lx) - 1);
     u32 mn = 0xFFFFFFFFu, mx = 0u, A = 0u, B = 0xFFFFFFFFu, C = 0u, D = 0xFFFFFFFFu;
-    u32 mlo = 0, mhi = 0;                         // lane j: row mask of slot j (see load_rows)
-    for_tile_rows<HAS_MASK>(g, ti, in, mask, [&](int j, float x, u32 mk) {
+    // one voxel: statistics, nearest values around the guessed bounds, foreground predicate
+    auto voxel = [&](float x, u32 mk) -> bool {
         const u32 o = f2ord(__float_as_uint(x));
         mn = min(mn, o);
         mx = max(mx, o);
         const bool ge = o >= lo, le = o <= hi;
         const bool use = !HAS_MASK || mk != 0;
-        const bool fg = use && (SIDES == 1 ? ge : SIDES == 2 ? le : ge && le);
         if (SIDES & 1) { A = max(A, use && !ge ? o : 0u); B = min(B, use && ge ? o : 0xFFFFFFFFu); }
         if (SIDES & 2) { C = max(C, use && le ? o : 0u); D = min(D, use && !le ? o : 0xFFFFFFFFu); }
-        const u64 bal = __ballot(fg) & lanes;
-        const u32 blo = (u32)bal, bhi = (u32)(bal >> 32);
-        CC_WRITELANE2(mlo, mhi, blo, bhi, j);
-    });
-    const int r = slot_row(lane, wave);
-    if (r / TY < ti.lz && r % TY < ti.ly) L.rows[r] = split_row(((u64)mhi << 32) | mlo);
+        return use && (SIDES == 1 ? ge : SIDES == 2 ? le : ge && le);
+    };
+    const bool f4 = ti.lz == TZ && ti.ly == TY && ti.lx == TX && ((ti.x0 | (int)(g.X & 3)) & 3) == 0;
+    if (f4) {
+        // Full, 16-B aligned tile: float4 per lane (4 rows of 64 voxels per load instruction, a
+        // quarter of the load instructions of the lane = x walk).  Wave w owns rows y = 4w .. 4w+3
+        // of every plane; lane l holds x = 4 (l % 16) .. + 3 of row 4w + l / 16.  The four
+        // ballots of plane z (value j of every lane) are parked in lane z, then each lane m
+        // assembles tile row (z = m / 4, y = 4w + m % 4) in the split form from them.
+        const int i4 = 4 * (lane & 15);
+        const int64_t sz = g.Y * g.X;
+        const float* pz = in + ((int64_t)ti.z0 * g.Y + ti.y0 + 4 * wave + (lane >> 4)) * g.X + ti.x0 + i4;
+        const u8* mz = HAS_MASK ? mask + (pz - in) : nullptr;
+        constexpr int RZ4 = 4;
+        u32 R[8] = {0, 0, 0, 0, 0, 0, 0, 0};      // lane z: ballots (lo, hi) of values 0..3 of plane z
+#pragma unroll
+        for (int z0 = 0; z0 < TZ; z0 += RZ4) {
+            float4 v[RZ4];
+            uchar4 mk[RZ4];
+#pragma unroll
+            for (int a = 0; a < RZ4; ++a) {
+                v[a] = *reinterpret_cast<const float4*>(pz + (z0 + a) * sz);
+                if (HAS_MASK) mk[a] = *reinterpret_cast<const uchar4*>(mz + (z0 + a) * sz);
+            }
+#pragma unroll
+            for (int a = 0; a < RZ4; ++a) {
+                const u64 b0 = __ballot(voxel(v[a].x, HAS_MASK ? (u32)mk[a].x : 1u));
+                const u64 b1 = __ballot(voxel(v[a].y, HAS_MASK ? (u32)mk[a].y : 1u));
+                const u64 b2 = __ballot(voxel(v[a].z, HAS_MASK ? (u32)mk[a].z : 1u));
+                const u64 b3 = __ballot(voxel(v[a].w, HAS_MASK ? (u32)mk[a].w : 1u));
+                CC_WRITELANE2(R[0], R[1], (u32)b0, (u32)(b0 >> 32), z0 + a);
+                CC_WRITELANE2(R[2], R[3], (u32)b1, (u32)(b1 >> 32), z0 + a);
+                CC_WRITELANE2(R[4], R[5], (u32)b2, (u32)(b2 >> 32), z0 + a);
+                CC_WRITELANE2(R[6], R[7], (u32)b3, (u32)(b3 >> 32), z0 + a);
+            }
+        }
+        // row m = 4 z + q: bits 16 q .. 16 q + 15 of ballot j are voxels x = 4 i + j, i = 0..15
+        const int zz = lane >> 2, qq = lane & 3;
+        u32 seg[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const u32 blo = (u32)__shfl((int)R[2 * j], zz, 64), bhi = (u32)__shfl((int)R[2 * j + 1], zz, 64);
+            seg[j] = ((qq < 2 ? blo : bhi) >> (16 * (qq & 1))) & 0xFFFFu;
+        }
+        // split form: even voxels x = 4i (j = 0), 4i + 2 (j = 2) -> bits 2i, 2i + 1 of the low half
+        const u32 even = spread2(seg[0]) | (spread2(seg[2]) << 1), odd = spread2(seg[1]) | (spread2(seg[3]) << 1);
+        L.rows[zz * TY + 4 * wave + qq] = ((u64)odd << 32) | even;
+    } else {
+        for (int i = tid; i < NROWS; i += NTHREADS) L.rows[i] = 0;
+        __syncthreads();
+        const u64 lanes = ti.lx >= 64 ? ~0ull : ((1ull << ti.lx) - 1);
+        u32 mlo = 0, mhi = 0;                     // lane j: row mask of slot j (see load_rows)
+        for_tile_rows<HAS_MASK>(g, ti, in, mask, [&](int j, float x, u32 mk) {
+            const u64 bal = __ballot(voxel(x, mk)) & lanes;
+            const u32 blo = (u32)bal, bhi = (u32)(bal >> 32);
+            CC_WRITELANE2(mlo, mhi, blo, bhi, j);
+        });
+        const int r = slot_row(lane, wave);
+        if (r / TY < ti.lz && r % TY < ti.ly) L.rows[r] = split_row(((u64)mhi << 32) | mlo);
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         mn = min(mn, (u32)__shfl_xor(mn, o, 64));
