@@ -115,8 +115,14 @@ __device__ __forceinline__ u32 run_at(const TileCCL& T, int row, int cx0) {
 
 // Thread (row = tid / 4, q = tid % 4) owns the run starts in cubes [8q, 8q + 8) of cube row `row`,
 // so the per-run phases keep all 8 waves busy; tid order is run-id order.
+#ifndef CC_CCL_LIST
+#define CC_CCL_LIST 1
+#endif
+// list (nullable, LDS, capacity NRUN): phase 2 first lists its union pairs, then every thread takes
+// an equal share of the list (each thread's own contacts vary from none to dozens: processed in
+// place they leave most lanes idle and the barrier waiting for the busiest row)
 template <int STOP = 0>   // ablation harness only: return after phase STOP (1..3)
-__device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T) {
+__device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T, u32* list = nullptr) {
     const int tid = cc_tid();
     const int qrow = tid >> 2, q = tid & 3;
     u32* par = T.par;
@@ -137,6 +143,56 @@ __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T) {
     __syncthreads();
     if (STOP == 1) return 0;
     // 2. unions between runs of neighbouring cube rows: thread = (row, direction group)
+    if (CC_CCL_LIST && list) {
+        const int row = tid % NCROW, grp = tid / NCROW;          // grp is uniform per 2 waves
+        const int cz = row / CY, cy = row % CY;
+        const int dz = grp == 3 ? 0 : -1, dy = grp == 3 ? -1 : grp - 1;
+        const int bz = cz + dz, by = cy + dy;
+        const bool ok = bz >= 0 && by >= 0 && by < CY;
+        const int rowb = ok ? bz * CY + by : row;
+        u32 M[3] = {0u, 0u, 0u};
+        u32 BA = 0, BB = 0, ra0 = 0, rb0 = 0, cnt = 0;
+        if (ok) {
+            u64 a[4], b[4];
+            load_row4(rows, row, a);
+            load_row4(rows, rowb, b);
+            const int szs = dz < 0 ? 0 : 2, szn = dz < 0 ? 1 : 2;
+            const int sys = dy < 0 ? 0 : dy > 0 ? 1 : 2, syn = dy < 0 ? 1 : dy > 0 ? 0 : 2;
+            const u64 ua = pick_rows(a, szs, sys), ub = pick_rows(b, szn, syn);
+            const u32 ua0 = lo32(ua), ua1 = hi32(ua), ub0 = lo32(ub), ub1 = hi32(ub);
+            const u32 Ea = T.E[row], Eb = T.E[rowb];
+            BA = T.B[row]; BB = T.B[rowb]; ra0 = T.roff[row]; rb0 = T.roff[rowb];
+            const u32 C0 = (ua0 | ua1) & (ub0 | ub1);
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+                const u32 C = dx < 0 ? ua0 & (ub1 << 1) : dx > 0 ? ua1 & (ub0 >> 1) : C0;
+                const u32 ebs = dx < 0 ? Eb << 2 : dx > 0 ? Eb : Eb << 1;
+                u32 red = (C << 1) & (Ea << 1) & ebs;
+                if (dx > 0) red |= ((C0 >> 1) & Ea) | (C0 & Eb);
+                if (dx < 0) red |= ((C0 & Ea) << 1) | (C0 & (Eb << 1));
+                M[dx + 1] = C & ~red;
+                cnt += (u32)__popc(M[dx + 1]);
+            }
+        }
+        u32 total = 0;
+        u32 pos = block_excl_scan(cnt, T.scratch, &total);
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+            for (u32 m = M[d]; m; m &= m - 1) {
+                const int cx = __builtin_ctz(m);
+                const u32 ra = ra0 + (u32)__popc(BA & mask_le(cx)) - 1;
+                const u32 rb = rb0 + (u32)__popc(BB & mask_le(cx + d - 1)) - 1;
+                if (pos < (u32)NRUN) list[pos] = ra | (rb << 16);
+                else lunion(par, ra, rb);                    // list full: in place
+                ++pos;
+            }
+        __syncthreads();
+        const u32 nl = total < (u32)NRUN ? total : (u32)NRUN;
+        for (u32 i = tid; i < nl; i += NTHREADS) {
+            const u32 e = list[i];
+            lunion(par, e & 0xFFFFu, e >> 16);
+        }
+    } else
     for (int w = tid; w < NCROW * 4; w += NTHREADS) {
         const int row = w % NCROW, grp = w / NCROW;          // grp is uniform per 2 waves
         const int cz = row / CY, cy = row % CY;
@@ -568,8 +624,8 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
     if (write)
         for (int i = tid; i < NROWS; i += NTHREADS) BITS[t * NROWS + i] = rows[i];
     if (ABL == 1) return;
-    if (ABL >= 10) { tile_ccl<ABL - 10>(rows, T); return; }
-    const u32 R = tile_ccl(rows, T);
+    if (ABL >= 10) { tile_ccl<ABL - 10>(rows, T, key); return; }
+    const u32 R = tile_ccl(rows, T, key);
     if (ABL == 2) { if (tid == 0) COUNT[t] = R; return; }
     for (u32 k = tid; k < R; k += NTHREADS) key[k] = NONE;
     __syncthreads();
@@ -2075,7 +2131,7 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
     }
     for (int i = tid; i < NROWS; i += NTHREADS) rows[i] = BITS[t * NROWS + i];
     __syncthreads();
-    tile_ccl(rows, T);
+    tile_ccl(rows, T, (u32*)lab);
     const u32 base = (u32)(t * g.cap);
     for (u32 k = tid; k < R && k < LABCAP; k += NTHREADS) lab[k] = FIN[base + k];
     __syncthreads();

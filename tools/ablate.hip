@@ -149,6 +149,39 @@ int main(int argc, char** argv) {
                 else k_spec<false, 3><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS, FACES, COUNT, P, KEY);
             })});
         }
+        // compute-bound variants: every tile reads one of 8 tiles that stay in L2 (tile origins
+        // z = y = 0, x = 64 (ix % 8)); outputs per tile as usual
+        {
+            std::vector<int32_t> tab2 = hg.tab;
+            const int n0 = g.nt[0], n1 = g.nt[1], n2 = g.nt[2];
+            for (int i = 0; i < n0; ++i) tab2[i] = 0;
+            for (int i = 0; i < n1; ++i) tab2[3 * n0 + i] = 0;
+            for (int i = 0; i < n2; ++i) tab2[3 * n0 + 3 * n1 + i] = (i % 8) * 64;
+            int32_t* tabc;
+            HIP_OK(hipMalloc(&tabc, tab2.size() * 4));
+            HIP_OK(hipMemcpy(tabc, tab2.data(), tab2.size() * 4, hipMemcpyHostToDevice));
+            HostGeom hc = hg;
+            bind_geom_tables(hc, tabc);
+            Geom gc = hc.g;
+            u32 *fst, *TB;
+            BlockParam* guess;
+            HIP_OK(hipMalloc(&fst, 3 * nb * 4));
+            HIP_OK(hipMalloc(&TB, nt * 16));
+            HIP_OK(hipMalloc(&guess, nb * sizeof(BlockParam)));
+            HIP_OK(hipMemcpy(guess, bp, nb * sizeof(BlockParam), hipMemcpyDeviceToDevice));
+            SpecArgs sa;
+            sa.guess = guess; sa.smin = fst; sa.smax = fst + nb; sa.sflag = fst + 2 * nb; sa.TB = TB; sa.t0 = 0;
+            r.push_back({"k_spec_cached", time_ms(s, iters, [&] {
+                k_spec<false, 1><<<(unsigned)nt, NTHREADS, 0, s>>>(gc, sa, in, nullptr, BITS, FACES, COUNT, P, KEY);
+            })});
+            r.push_back({"k_block_stats_cached", time_ms(s, iters, [&] {
+                k_block_stats<<<(unsigned)nt, NTHREADS, 0, s>>>(gc, in, smin, smax, sflag);
+            })});
+#define P1C(A) k_pass1<false, A><<<(unsigned)nt, NTHREADS, 0, s>>>(gc, in, nullptr, bp, thr, mode, BITS, FACES, COUNT, P, KEY)
+            r.push_back({"k_pass1_abl1_cached", time_ms(s, iters, [&] { P1C(1); })});
+            r.push_back({"k_pass1_abl2_cached", time_ms(s, iters, [&] { P1C(2); })});
+            r.push_back({"k_pass1_full_cached", time_ms(s, iters, [&] { P1C(0); })});
+        }
         // seam kernel variants (FACES from the last full pass-1 run above)
         {
             P1(0);
