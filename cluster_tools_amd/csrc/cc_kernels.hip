@@ -121,8 +121,10 @@ __device__ __forceinline__ u32 run_at(const TileCCL& T, int row, int cx0) {
 // list (nullable, LDS, capacity NRUN): phase 2 first lists its union pairs, then every thread takes
 // an equal share of the list (each thread's own contacts vary from none to dozens: processed in
 // place they leave most lanes idle and the barrier waiting for the busiest row)
-template <int STOP = 0>   // ablation harness only: return after phase STOP (1..3)
-__device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T, u32* list = nullptr) {
+// firstv (nullable, LDS, may alias list): firstv[k] = the first voxel (tile raster index) of
+// component k, computed in phase 5 from each run's first voxel (pass 1's keys).
+template <int STOP = 0>   // ablation harness only: return after phase STOP (1..3; 4: pair list only)
+__device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T, u32* list = nullptr, u32* firstv = nullptr) {
     const int tid = cc_tid();
     const int qrow = tid >> 2, q = tid & 3;
     u32* par = T.par;
@@ -187,6 +189,7 @@ __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T, u32* list =
                 ++pos;
             }
         __syncthreads();
+        if (STOP == 4) return 0;       // ablation: the pair list without the unions
         const u32 nl = total < (u32)NRUN ? total : (u32)NRUN;
         for (u32 i = tid; i < nl; i += NTHREADS) {
             const u32 e = list[i];
@@ -255,13 +258,39 @@ __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T, u32* list =
             const u32 r = r0 + (u32)__popc(Brow & ((1u << __builtin_ctz(m)) - 1));
             if (par[r] == r) par[r] = r | (k++ << 16);
         }
+        if (firstv)
+            for (u32 i = tid; i < total; i += NTHREADS) firstv[i] = NONE;
     }
     __syncthreads();
-    // 5. every run carries its component's k
+    // 5. every run carries its component's k (and, for pass 1, offers its first voxel in raster
+    // order -- the first sub-row (lz, ly) with a voxel in the run's cubes, then its smallest x)
+    u64 a[4];
+    u32 E = 0;
+    if (firstv) {
+        load_row4(rows, qrow, a);
+        E = T.E[qrow];
+    }
+    const int cz = qrow / CY, cy = qrow % CY;
     for (u32 m = Bq; m; m &= m - 1) {
-        const u32 r = r0 + (u32)__popc(Brow & ((1u << __builtin_ctz(m)) - 1));
+        const int c0 = __builtin_ctz(m);
+        const u32 r = r0 + (u32)__popc(Brow & ((1u << c0) - 1));
         const u32 root = par[r] & 0xFFFFu;
-        if (root != r) par[r] = root | (par[root] & 0xFFFF0000u);
+        const u32 pk = par[root] & 0xFFFF0000u;
+        if (root != r) par[r] = root | pk;
+        if (firstv) {
+            const int c1 = c0 + __builtin_ctz(~(E >> c0));                    // end cube
+            const u32 M = mask_le(c1) & ~((1u << c0) - 1);
+            u32 idx = NONE;
+#pragma unroll
+            for (int j = 3; j >= 0; --j) {
+                const u32 ev = lo32(a[j]) & M, od = hi32(a[j]) & M;
+                if (ev | od) {
+                    const int xe = ev ? 2 * __builtin_ctz(ev) : TX, xo = od ? 2 * __builtin_ctz(od) + 1 : TX;
+                    idx = (u32)(((2 * cz + (j >> 1)) * TY + 2 * cy + (j & 1)) * TX + (xe < xo ? xe : xo));
+                }
+            }
+            atomicMin(&firstv[pk >> 16], idx);
+        }
     }
     __syncthreads();
     return total;
@@ -624,36 +653,9 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
     if (write)
         for (int i = tid; i < NROWS; i += NTHREADS) BITS[t * NROWS + i] = rows[i];
     if (ABL == 1) return;
-    if (ABL >= 10) { tile_ccl<ABL - 10>(rows, T, key); return; }
-    const u32 R = tile_ccl(rows, T, key);
+    if (ABL >= 10) { tile_ccl<ABL - 10>(rows, T, key, key); return; }
+    const u32 R = tile_ccl(rows, T, key, key);      // key[k] = first voxel of component k
     if (ABL == 2) { if (tid == 0) COUNT[t] = R; return; }
-    for (u32 k = tid; k < R; k += NTHREADS) key[k] = NONE;
-    __syncthreads();
-    // first voxel of each run in raster order: the first sub-row (lz, ly) with a voxel in the
-    // run's cubes, then its smallest x
-    {
-        const int row = tid >> 2, q = tid & 3;
-        const int cz = row / CY, cy = row % CY;
-        u64 a[4];
-        load_row4(rows, row, a);
-        const u32 Brow = T.B[row], E = T.E[row], r0 = T.roff[row];
-        for (u32 m = Brow & (0xFFu << (8 * q)); m; m &= m - 1) {
-            const int c0 = __builtin_ctz(m);                                  // start cube
-            const int c1 = c0 + __builtin_ctz(~(E >> c0));                    // end cube
-            const u32 M = mask_le(c1) & ~((1u << c0) - 1);
-            u32 idx = NONE;
-#pragma unroll
-            for (int j = 3; j >= 0; --j) {
-                const u32 ev = lo32(a[j]) & M, od = hi32(a[j]) & M;
-                if (ev | od) {
-                    const int xe = ev ? 2 * __builtin_ctz(ev) : TX, xo = od ? 2 * __builtin_ctz(od) + 1 : TX;
-                    idx = (u32)(((2 * cz + (j >> 1)) * TY + 2 * cy + (j & 1)) * TX + (xe < xo ? xe : xo));
-                }
-            }
-            atomicMin(&key[T.par[r0 + (u32)__popc(Brow & ((1u << c0) - 1))] >> 16], idx);
-        }
-    }
-    __syncthreads();
     if (tid == 0 && write) COUNT[t] = R;
     if (ABL == 3 || !write) return;
     const u32 base = (u32)(t * g.cap);

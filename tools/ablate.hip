@@ -179,7 +179,12 @@ int main(int argc, char** argv) {
             })});
 #define P1C(A) k_pass1<false, A><<<(unsigned)nt, NTHREADS, 0, s>>>(gc, in, nullptr, bp, thr, mode, BITS, FACES, COUNT, P, KEY)
             r.push_back({"k_pass1_abl1_cached", time_ms(s, iters, [&] { P1C(1); })});
+            r.push_back({"k_pass1_ph1_cached", time_ms(s, iters, [&] { P1C(11); })});
+            r.push_back({"k_pass1_ph2list_cached", time_ms(s, iters, [&] { P1C(14); })});
+            r.push_back({"k_pass1_ph2_cached", time_ms(s, iters, [&] { P1C(12); })});
+            r.push_back({"k_pass1_ph3_cached", time_ms(s, iters, [&] { P1C(13); })});
             r.push_back({"k_pass1_abl2_cached", time_ms(s, iters, [&] { P1C(2); })});
+            r.push_back({"k_pass1_abl3_cached", time_ms(s, iters, [&] { P1C(3); })});
             r.push_back({"k_pass1_full_cached", time_ms(s, iters, [&] { P1C(0); })});
         }
         // seam kernel variants (FACES from the last full pass-1 run above)
