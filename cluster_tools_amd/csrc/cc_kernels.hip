@@ -1603,9 +1603,18 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* _
     });
     if (STOP == 4) return;
     // edges and corners inside the block
+    // a lane's edge / corner neighbour is fixed: its direction code and block-local index are
+    // computed at the lane's first contact only
+    bool have_e = false;
+    u32 code_e = 0, lt_e = 0;
     seam_edges_rows(g, S, E, t, ti, lane, [&](int64_t t2, u32 k1, u32 k2) {
-        if (!fresh(dir_code(t2), k1, k2)) return;
-        append(false, ((u64)((lt_own << 12) | k1) << 32) | ((block_local(g, (u32)t2) << 12) | k2));
+        if (!have_e) {
+            code_e = dir_code(t2);
+            lt_e = block_local(g, (u32)t2);
+            have_e = true;
+        }
+        if (!fresh(code_e, k1, k2)) return;
+        append(false, ((u64)((lt_own << 12) | k1) << 32) | ((lt_e << 12) | k2));
     });
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
