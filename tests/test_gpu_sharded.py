@@ -62,15 +62,18 @@ def test_two_ranks_one_gpu_gloo(tmp_path, mode, block_shape):
         assert int(np.load(str(tmp_path / ('nl_%d.npy' % k)))[0]) == ref['n_labels']
 
 
-@pytest.mark.parametrize('mode,masked', [('less', True), ('greater', False)])
-def test_sharded_c4_scale_pair_bijection(mode, masked):
-    """SURVEY.md §8d parity at scale for the sharded configs: C4 (C3 + ellipsoid mask, here over
-    4 z-slabs on one GPU) against the single-volume path.  The partitions are equal iff the
-    device contingency table (cc_evaluate) of the two labellings is a bijection:
-    |unique(a, b)| == |unique(a)| == |unique(b)|, and the raw labels are identical."""
+@pytest.mark.parametrize('mode,masked,form', [('less', True, None), ('greater', False, None),
+                                              ('greater', True, 'voxel32')])
+def test_sharded_c4_scale_vs_oracle(mode, masked, form):
+    """SURVEY.md §8d parity at scale for the sharded configs: C4 (C3 + ellipsoid mask) over 4
+    z-slabs on one GPU, with the cubes32 seam planes the ranks exchange over xGMI (or the
+    per-voxel uint32 fallback), against the C oracle on the whole volume: raw labels identical
+    (compared on the device), the assembled LUT identical, and the device contingency table of
+    the two labellings a bijection (|unique(a, b)| == |unique(a)| == |unique(b)|)."""
+    import os
     import torch
     from cluster_tools_amd import _lib
-    from cluster_tools_amd.distributed import label_slabs_single_process
+    from cluster_tools_amd.distributed import label_slabs_single_process, assemble_lut
     from cluster_tools_amd.synthetic import ellipsoid_mask_device
     shape, bs = (1024, 2048, 2048), (64, 512, 512)
     ctxs = [_lib.Context(0) for _ in range(4)]
@@ -78,15 +81,20 @@ def test_sharded_c4_scale_pair_bijection(mode, masked):
         x = ctxs[0].generate_boundary_map(shape)
         mask = ellipsoid_mask_device(shape, 0, shape[0], x.device) if masked else None
         torch.cuda.synchronize()          # the mask is built on torch's stream, the ctx has its own
-        a, ra = ctxs[0].label_volume(x, bs, 0.5, mode, mask=mask)
-        b, res, sums, _ = label_slabs_single_process(ctxs, x, bs, 0.5, mode, mask=mask)
+        b, res, sums, luts = label_slabs_single_process(ctxs, x, bs, 0.5, mode, mask=mask, form=form)
+        inp = x.cpu().numpy()
+        hmask = None if mask is None else mask.cpu().numpy()
         del x, mask
-        torch.cuda.synchronize()
-        r = ctxs[0].evaluate(a, b, bs, ignore_label=None)
-        assert r['n_pairs'] == r['n_seg_ids'] == r['n_gt_ids'] == ra['n_components'] + 1
-        assert sum(q['n_components'] for q in res) == ra['n_components']
-        assert sum(sums) + 1 == ra['n_labels']
-        assert bool(torch.equal(a, b))
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        r = O.label_volume(inp, bs, 0.5, mode, hmask, n_threads=threads)
+        del inp, hmask
+        assert sum(sums) + 1 == r['n_labels']
+        np.testing.assert_array_equal(assemble_lut(luts, sums), r['lut'])
+        ref = torch.from_numpy(r.pop('labels').view(np.int64)).cuda()
+        assert bool(torch.equal(b, ref))
+        ev = ctxs[0].evaluate(ref, b, bs, ignore_label=None)
+        n_comp = sum(q['n_components'] for q in res)
+        assert ev['n_pairs'] == ev['n_seg_ids'] == ev['n_gt_ids'] == n_comp + 1
     finally:
         for c in ctxs:
             c.close()
