@@ -298,11 +298,9 @@ __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T, u32* list =
     return total;
 }
 
-// Pass 2's tile CCL: the runs again (phase 1 of tile_ccl: B, E, roff); each run's component index
-// k comes from KMAP, which pass 1 wrote (pass1_finish), already loaded into km (run tid + j *
-// NTHREADS) -- the union phases are not redone.
-constexpr int KM_PER_THREAD = NRUN / NTHREADS;
-__device__ __forceinline__ void tile_runs_kmap(const u64* rows, TileCCL& T, const u32 km[KM_PER_THREAD]) {
+// Pass 2's tile CCL: the runs again (phase 1 of tile_ccl: B, E, roff), then each run's component
+// index k from KMAP, which pass 1 wrote (pass1_finish) -- the union phases are not redone.
+__device__ __forceinline__ void tile_runs_kmap(const u64* rows, TileCCL& T, const uint16_t* __restrict__ km) {
     const int tid = cc_tid();
     const int qrow = tid >> 2, q = tid & 3;
     u64 a[4];
@@ -313,9 +311,7 @@ __device__ __forceinline__ void tile_runs_kmap(const u64* rows, TileCCL& T, cons
     u32 nrun = 0;
     const u32 off = block_excl_scan(q == 0 ? (u32)__popc(B) : 0u, T.scratch, &nrun);
     if (q == 0) { T.B[qrow] = B; T.E[qrow] = E; T.roff[qrow] = off; }
-#pragma unroll
-    for (int j = 0; j < KM_PER_THREAD; ++j)
-        if (tid + j * NTHREADS < (int)nrun) T.par[tid + j * NTHREADS] = km[j] << 16;
+    for (u32 i = tid; i < nrun; i += NTHREADS) T.par[i] = (u32)km[i] << 16;
     __syncthreads();
 }
 
@@ -686,7 +682,6 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
     if (write && KMAP) {
         uint16_t* km = KMAP + t * NRUN;
         for (u32 r = tid; r < T.nrun; r += NTHREADS) km[r] = (uint16_t)(T.par[r] >> 16);
-        if (tid == 0) KMAP[g.n_tiles * NRUN + t] = (uint16_t)T.nrun;     // run count, after the maps
     }
     if (ABL == 3 || !write) return;
     const u32 base = (u32)(t * g.cap);
@@ -2174,24 +2169,12 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
         }
         return;
     }
-    // every global load of the tile at once: its bit rows, its runs' component indices (pass 1)
-    // and its components' final labels -- one round trip instead of three dependent ones
-    const u32 base = (u32)(t * g.cap);
-    const u32 nr = KMAP[g.n_tiles * NRUN + t];
-    static_assert(NROWS == NTHREADS && LABCAP % NTHREADS == 0 && NRUN % NTHREADS == 0, "per-thread slots");
-    const u64 myrow = BITS[t * NROWS + tid];
-    u32 km[KM_PER_THREAD];
-    const uint16_t* kmt = KMAP + t * NRUN;
-#pragma unroll
-    for (int j = 0; j < KM_PER_THREAD; ++j) km[j] = tid + j * NTHREADS < (int)nr ? kmt[tid + j * NTHREADS] : 0u;
-    u64 f[LABCAP / NTHREADS];
-#pragma unroll
-    for (int j = 0; j < LABCAP / NTHREADS; ++j) f[j] = tid + j * NTHREADS < (int)R ? FIN[base + tid + j * NTHREADS] : 0ull;
-    rows[tid] = myrow;
-#pragma unroll
-    for (int j = 0; j < LABCAP / NTHREADS; ++j) lab[tid + j * NTHREADS] = f[j];
+    for (int i = tid; i < NROWS; i += NTHREADS) rows[i] = BITS[t * NROWS + i];
     __syncthreads();
-    tile_runs_kmap(rows, T, km);
+    tile_runs_kmap(rows, T, KMAP + t * NRUN);
+    const u32 base = (u32)(t * g.cap);
+    for (u32 k = tid; k < R && k < LABCAP; k += NTHREADS) lab[k] = FIN[base + k];
+    __syncthreads();
     for (int c = tid; c < NC; c += NTHREADS) {
         const int cz = c / (CY * CX), cy = (c / CX) % CY, cx = c % CX;
         if (cz >= ncz || cy >= ncy || cx >= ncx) continue;

@@ -206,7 +206,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     c->count.ensure(nt * sizeof(u32));
     c->P.ensure(nodes * sizeof(u32));
     c->KR.ensure(nodes * sizeof(u64));
-    c->kmap.ensure((size_t)nt * (NRUN + 1) * sizeof(uint16_t));     // maps, then the run counts
+    c->kmap.ensure((size_t)nt * NRUN * sizeof(uint16_t));
     c->seg.ensure(nb * 2 * sizeof(u32));
     c->values.ensure(nb * sizeof(u64));
     c->offsets.ensure(nb * sizeof(u64));

@@ -97,7 +97,7 @@ int main(int argc, char** argv) {
         HIP_OK(hipMalloc(&P, nodes * 4));
         HIP_OK(hipMalloc(&KEY, nodes * 8));
         HIP_OK(hipMalloc(&FIN, nodes * 8));
-        HIP_OK(hipMalloc(&KMAP, (size_t)nt * (NRUN + 1) * 2));
+        HIP_OK(hipMalloc(&KMAP, (size_t)nt * NRUN * 2));
         HIP_OK(hipMalloc(&dummy, 64));
         HIP_OK(hipMemset(FIN, 0, nodes * 8));
         u32 *smin = st, *smax = st + nb, *sflag = st + 2 * nb;
