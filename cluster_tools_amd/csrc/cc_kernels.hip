@@ -96,7 +96,6 @@ struct TileCCL {
     u32 roff[NCROW];       // run id of each cube row's first run
     u32 par[NRUN];         // union-find over run ids, then root | k << 16
     u32 scratch[8];
-    u32 nrun;              // runs of the tile
 };
 
 __device__ __forceinline__ void load_row4(const u64* rows, int row, u64 a[4]) {
@@ -140,7 +139,6 @@ __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T, u32* list =
         u32 nrun = 0;
         const u32 off = block_excl_scan(q == 0 ? (u32)__popc(B) : 0u, T.scratch, &nrun);
         if (q == 0) { T.B[qrow] = B; T.E[qrow] = E; T.roff[qrow] = off; }
-        if (tid == 0) T.nrun = nrun;
         for (u32 i = tid; i < nrun; i += NTHREADS) par[i] = i;
         Bq = B & (0xFFu << (8 * q));
     }
@@ -296,23 +294,6 @@ __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T, u32* list =
     }
     __syncthreads();
     return total;
-}
-
-// Pass 2's tile CCL: the runs again (phase 1 of tile_ccl: B, E, roff), then each run's component
-// index k from KMAP, which pass 1 wrote (pass1_finish) -- the union phases are not redone.
-__device__ __forceinline__ void tile_runs_kmap(const u64* rows, TileCCL& T, const uint16_t* __restrict__ km) {
-    const int tid = cc_tid();
-    const int qrow = tid >> 2, q = tid & 3;
-    u64 a[4];
-    load_row4(rows, qrow, a);
-    const u32 L = lo32(a[0] | a[1] | a[2] | a[3]), H = hi32(a[0] | a[1] | a[2] | a[3]);
-    const u32 E = H & (L >> 1);
-    const u32 B = (L | H) & ~(E << 1);
-    u32 nrun = 0;
-    const u32 off = block_excl_scan(q == 0 ? (u32)__popc(B) : 0u, T.scratch, &nrun);
-    if (q == 0) { T.B[qrow] = B; T.E[qrow] = E; T.roff[qrow] = off; }
-    for (u32 i = tid; i < nrun; i += NTHREADS) T.par[i] = (u32)km[i] << 16;
-    __syncthreads();
 }
 
 // component index k of an occupied cube
@@ -641,9 +622,7 @@ struct Pass1LDS {
 template <int ABL>
 __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const TileInfo& ti, u64* BITS, face_t* FACES,
                                              u32* COUNT, u32* P, u64* KEY, Pass1LDS& L, bool write,
-                                             uint16_t* KMAP, u8* fchg = nullptr);
-// KMAP: run -> component index of every tile (NRUN u16 slots per tile): pass 1 writes the tile's
-// runs, pass 2 reads them instead of redoing the union phases (tile_runs_kmap).
+                                             u8* fchg = nullptr);
 
 // Pass 1 of tile t (block parameters p): bit rows -> BITS, tile CCL -> COUNT, nodes (P, KEY),
 // face planes.  ABL (kernel ablation harness tools/ablate.hip only; 0 in the library): stop
@@ -652,13 +631,13 @@ template <bool HAS_MASK, int ABL = 0>
 __device__ __forceinline__ void pass1_tile(const Geom& g, int64_t t, const TileInfo& ti, const BlockParam& p,
                                            const float* __restrict__ in, const u8* __restrict__ mask, float thr,
                                            int mode, u64* BITS, face_t* FACES, u32* COUNT, u32* P, u64* KEY,
-                                           Pass1LDS& L, uint16_t* KMAP, bool write = true, u8* fchg = nullptr) {
+                                           Pass1LDS& L, bool write = true, u8* fchg = nullptr) {
     const int tid = cc_tid();
     for (int i = tid; i < NROWS; i += NTHREADS) L.rows[i] = 0;
     __syncthreads();
     if (p.kind != BP_EMPTY) load_rows<HAS_MASK>(g, ti, in, mask, p, thr, mode, L.rows);
     __syncthreads();
-    pass1_finish<ABL>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, write, KMAP, fchg);
+    pass1_finish<ABL>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, write, fchg);
 }
 
 // Pass 1 after the bit rows are in L.rows (and a barrier): BITS, tile CCL, COUNT, nodes, faces.
@@ -666,8 +645,7 @@ __device__ __forceinline__ void pass1_tile(const Geom& g, int64_t t, const TileI
 // that read them must be redone; unchanged faces leave every seam list as it was).
 template <int ABL>
 __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const TileInfo& ti, u64* BITS, face_t* FACES,
-                                             u32* COUNT, u32* P, u64* KEY, Pass1LDS& L, bool write, uint16_t* KMAP,
-                                             u8* fchg) {
+                                             u32* COUNT, u32* P, u64* KEY, Pass1LDS& L, bool write, u8* fchg) {
     u64* rows = L.rows;
     TileCCL& T = L.T;
     u32* key = L.key;
@@ -679,10 +657,6 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
     const u32 R = tile_ccl(rows, T, key, key);      // key[k] = first voxel of component k
     if (ABL == 2) { if (tid == 0) COUNT[t] = R; return; }
     if (tid == 0 && write) COUNT[t] = R;
-    if (write && KMAP) {
-        uint16_t* km = KMAP + t * NRUN;
-        for (u32 r = tid; r < T.nrun; r += NTHREADS) km[r] = (uint16_t)(T.par[r] >> 16);
-    }
     if (ABL == 3 || !write) return;
     const u32 base = (u32)(t * g.cap);
     for (u32 k = tid; k < R; k += NTHREADS) {
@@ -711,12 +685,11 @@ template <bool HAS_MASK, int ABL = 0>
 __global__ __launch_bounds__(NTHREADS) void k_pass1(Geom g, const float* __restrict__ in,
                                                     const u8* __restrict__ mask, const BlockParam* bp,
                                                     float thr, int mode, u64* BITS, face_t* FACES,
-                                                    u32* COUNT, u32* P, u64* KEY, uint16_t* KMAP) {
+                                                    u32* COUNT, u32* P, u64* KEY) {
     __shared__ Pass1LDS L;
     const int64_t t = blockIdx.x;
     const TileInfo ti = tile_info(g, t);
-    pass1_tile<HAS_MASK, ABL>(g, t, ti, uniform_bp(bp[ti.block]), in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L,
-                              KMAP);
+    pass1_tile<HAS_MASK, ABL>(g, t, ti, uniform_bp(bp[ti.block]), in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L);
 }
 
 // global tile id of local tile lt (z-major inside the block) of block b
@@ -856,7 +829,6 @@ struct SpecArgs {
     u32* smin; u32* smax; u32* sflag;
     u32* TB;                  // 4 per tile (see above)
     int64_t t0;               // first tile of this launch (the front runs in z-layer chunks)
-    uint16_t* KMAP;           // run -> component index per tile (read by pass 2)
 };
 
 // SIDES: bounds of the guessed interval that can move (1 lower: 'greater', 2 upper: 'less', 3 both)
@@ -967,7 +939,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         u32* tb = sa.TB + 4 * t;
         tb[0] = A; tb[1] = B; tb[2] = C; tb[3] = D;
     }
-    pass1_finish<0>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, true, sa.KMAP);
+    pass1_finish<0>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, true);
 }
 
 // are the bits computed with the guess G those of the exact parameters T? (see above)
@@ -996,14 +968,14 @@ template <bool HAS_MASK>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_fix(
     Geom g, const u32* FIX, const BlockParam* bp, const BlockParam* guess, const float* __restrict__ in,
     const u8* __restrict__ mask, float thr, int mode, u64* BITS, face_t* FACES, u32* COUNT, u32* P, u64* KEY,
-    u8* fchg, uint16_t* KMAP) {
+    u8* fchg) {
     __shared__ Pass1LDS L;
     const int64_t t = __builtin_amdgcn_readfirstlane(FIX[1 + blockIdx.x]);
     const TileInfo ti = uniform_ti(tile_info(g, t));
     const BlockParam p = uniform_bp(bp[ti.block]);
     const bool fresh = __builtin_amdgcn_readfirstlane(guess[ti.block].kind) == BP_INTERVAL;
     if (!fresh && cc_tid() == 0) fchg[t] = 1;
-    pass1_tile<HAS_MASK>(g, t, ti, p, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L, KMAP, true,
+    pass1_tile<HAS_MASK>(g, t, ti, p, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L, true,
                          fresh ? fchg : nullptr);
 }
 
@@ -2144,8 +2116,7 @@ __device__ __forceinline__ void store2(u64* __restrict__ out, int64_t idx, u64 v
 }
 
 __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restrict__ BITS, const u32* COUNT,
-                                                    const u64* __restrict__ FIN, u64* __restrict__ out,
-                                                    const uint16_t* __restrict__ KMAP) {
+                                                    const u64* __restrict__ FIN, u64* __restrict__ out) {
     __shared__ u64 rows[NROWS];             // split bit rows (see tile_ccl)
     __shared__ TileCCL T;
     __shared__ u64 lab[LABCAP];
@@ -2171,7 +2142,7 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
     }
     for (int i = tid; i < NROWS; i += NTHREADS) rows[i] = BITS[t * NROWS + i];
     __syncthreads();
-    tile_runs_kmap(rows, T, KMAP + t * NRUN);
+    tile_ccl(rows, T, (u32*)lab);
     const u32 base = (u32)(t * g.cap);
     for (u32 k = tid; k < R && k < LABCAP; k += NTHREADS) lab[k] = FIN[base + k];
     __syncthreads();
@@ -2197,6 +2168,110 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
                        (b & 1) ? v : 0, (b & 2) ? v : 0, two, vec);
             }
         }
+    }
+}
+
+// Persistent form of k_pass2: a fixed grid of workgroups walks the tiles; every global load of
+// the next tile (its bit rows, COUNT and the LDS-cached labels of its components) is issued
+// before the current tile's CCL, so those round trips hide behind the CCL and the stores instead
+// of opening every tile.  Workgroup b runs on XCD k = b % 8 and takes every W-th tile of XCD k's
+// contiguous share of the volume (W = workgroups per XCD), as xcd_order.
+constexpr int P2_LAB_PER_THREAD = LABCAP / NTHREADS;
+static_assert(NROWS == NTHREADS && LABCAP % NTHREADS == 0, "one bit row and LABCAP / NTHREADS labels per thread");
+
+__global__ __launch_bounds__(NTHREADS) void k_pass2p(Geom g, const u64* __restrict__ BITS, const u32* __restrict__ COUNT,
+                                                     const u64* __restrict__ FIN, u64* __restrict__ out) {
+    __shared__ u64 rows[NROWS];
+    __shared__ TileCCL T;
+    __shared__ u64 lab[LABCAP];
+    const int tid = threadIdx.x;
+    const u32 n = (u32)g.n_tiles, b = blockIdx.x, W = gridDim.x >> 3;     // gridDim.x: a multiple of 8
+    const u32 q = n >> 3, rem = n & 7, k8 = b & 7;
+    const u32 s0 = k8 * q + (k8 < rem ? k8 : rem), s1 = s0 + q + (k8 < rem ? 1u : 0u);
+    u32 t = s0 + (b >> 3);
+    if (t >= s1) return;
+    // prefetched state of tile t
+    u64 rnext = BITS[(int64_t)t * NROWS + tid];
+    u32 Rnext = COUNT[t];
+    u64 fnext[P2_LAB_PER_THREAD];
+    auto fetch_lab = [&](u32 tt, u32 R) {
+        const u32 base = tt * (u32)g.cap;
+#pragma unroll
+        for (int j = 0; j < P2_LAB_PER_THREAD; ++j) {
+            const u32 k = tid + j * NTHREADS;
+            fnext[j] = k < R ? FIN[base + k] : 0ull;
+        }
+    };
+    fetch_lab(t, Rnext);
+    while (true) {
+        const u32 tn = t + W;
+        const bool more = tn < s1;
+        const u64 rcur = rnext;
+        const u32 R = __builtin_amdgcn_readfirstlane(Rnext);
+        u64 fcur[P2_LAB_PER_THREAD];
+#pragma unroll
+        for (int j = 0; j < P2_LAB_PER_THREAD; ++j) fcur[j] = fnext[j];
+        if (more) {                     // next tile's loads in flight during this tile's work
+            rnext = BITS[(int64_t)tn * NROWS + tid];
+            Rnext = COUNT[tn];
+        }
+        const TileInfo ti = tile_info(g, t);
+        const bool vec = ((ti.x0 | (int)(g.X & 1)) & 1) == 0;
+        const int ncz = (ti.lz + 1) / 2, ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2;
+        const u32 base = t * (u32)g.cap;
+        // the next tile's labels: COUNT[tn] has had the CCL (or the setup) to arrive; the loads
+        // overlap this tile's stores
+        auto prefetch_lab = [&] {
+            if (more) fetch_lab(tn, __builtin_amdgcn_readfirstlane(Rnext));
+        };
+        if (R == 0) {
+            prefetch_lab();
+            for (int c = tid; c < NC; c += NTHREADS) {
+                const int cz = c / (CY * CX), cy = (c / CX) % CY, cx = c % CX;
+                if (cz >= ncz || cy >= ncy || cx >= ncx) continue;
+                const bool two = 2 * cx + 1 < ti.lx;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int z = 2 * cz + (d >> 1), y = 2 * cy + (d & 1);
+                    if (z < ti.lz && y < ti.ly)
+                        store2(out, ((int64_t)(ti.z0 + z) * g.Y + ti.y0 + y) * g.X + ti.x0 + 2 * cx, 0, 0, two, vec);
+                }
+            }
+        } else {
+            rows[tid] = rcur;
+            __syncthreads();
+            tile_ccl(rows, T, (u32*)lab);
+#pragma unroll
+            for (int j = 0; j < P2_LAB_PER_THREAD; ++j) lab[tid + j * NTHREADS] = fcur[j];
+            prefetch_lab();
+            __syncthreads();
+            for (int c = tid; c < NC; c += NTHREADS) {
+                const int cz = c / (CY * CX), cy = (c / CX) % CY, cx = c % CX;
+                if (cz >= ncz || cy >= ncy || cx >= ncx) continue;
+                const int r = (2 * cz) * TY + 2 * cy;
+                const u32 m = vpair(rows[r], cx) | (vpair(rows[r + 1], cx) << 2) | (vpair(rows[r + TY], cx) << 4) |
+                              (vpair(rows[r + TY + 1], cx) << 6);
+                u64 v = 0;
+                if (m) {
+                    const u32 k = cube_k(T, c);
+                    if (k < LABCAP) v = lab[k];
+                    else v = __builtin_nontemporal_load(FIN + base + k);
+                }
+                const bool two = 2 * cx + 1 < ti.lx;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int z = 2 * cz + (d >> 1), y = 2 * cy + (d & 1);
+                    if (z < ti.lz && y < ti.ly) {
+                        const u32 bb = m >> (2 * d);
+                        store2(out, ((int64_t)(ti.z0 + z) * g.Y + ti.y0 + y) * g.X + ti.x0 + 2 * cx,
+                               (bb & 1) ? v : 0, (bb & 2) ? v : 0, two, vec);
+                    }
+                }
+            }
+        }
+        if (!more) break;
+        __syncthreads();                // rows / T / lab are rewritten by the next tile
+        t = tn;
     }
 }
 
@@ -2238,9 +2313,9 @@ __global__ __launch_bounds__(NTHREADS) void k_threshold(Geom g, const BlockParam
 CC_SPEC(false, 1) CC_SPEC(false, 2) CC_SPEC(false, 3) CC_SPEC(true, 1) CC_SPEC(true, 2) CC_SPEC(true, 3)
 #undef CC_SPEC
 template __global__ void k_fix<false>(Geom, const u32*, const BlockParam*, const BlockParam*, const float*, const u8*,
-                                      float, int, u64*, face_t*, u32*, u32*, u64*, u8*, uint16_t*);
+                                      float, int, u64*, face_t*, u32*, u32*, u64*, u8*);
 template __global__ void k_fix<true>(Geom, const u32*, const BlockParam*, const BlockParam*, const float*, const u8*,
-                                     float, int, u64*, face_t*, u32*, u32*, u64*, u8*, uint16_t*);
+                                     float, int, u64*, face_t*, u32*, u32*, u64*, u8*);
 template __global__ void k_seams<0>(Geom, const face_t*, u64*, u32*, u8*, u64*, u32*, u8*, int64_t, int64_t, const u32*);
 template __global__ void k_stitch<false>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_stitch<true>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);

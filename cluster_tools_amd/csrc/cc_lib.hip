@@ -55,7 +55,7 @@ struct cc_ctx {
     // workspace
     DevBuf tiles, bstat, bparam, bits, faces, count, rc, roff, P, KR, FIN, keys, keys2, vals, vals2, seg,
         values, offsets, lut, cub_tmp, scalars, scalars2, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2,
-        flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf, spec, mark, bflag, kmap,
+        flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf, spec, mark, bflag,
         ev_main, ev_z, ev_seg, ev_gt, ev_flag, ev_part;   // evaluation (cc_eval.hip)
     int64_t ev_cap = 0;      // entries per evaluation hash table of the last cc_evaluate
     int64_t rl_cap = 0;      // id-set slots of the last cc_relabel_consecutive
@@ -70,6 +70,7 @@ struct cc_ctx {
     int debug = 0;         // CC_DEBUG_* test hooks
     int front_chunks = 1;  // z-layer chunks of the speculative front (CC_FRONT_CHUNKS)
     int64_t quirk_jobs = 0;  // CC_OPT_EMPTY_JOB_QUIRK: emulate the reference's empty-job branch for max_jobs
+    int64_t pass2_wgs = 0;   // k_pass2p grid (persistent pass 2); 0: one workgroup per tile (CC_PASS2_WGS)
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, ProfEntry> prof_acc;
@@ -206,7 +207,6 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     c->count.ensure(nt * sizeof(u32));
     c->P.ensure(nodes * sizeof(u32));
     c->KR.ensure(nodes * sizeof(u64));
-    c->kmap.ensure((size_t)nt * NRUN * sizeof(uint16_t));
     c->seg.ensure(nb * 2 * sizeof(u32));
     c->values.ensure(nb * sizeof(u64));
     c->offsets.ensure(nb * sizeof(u64));
@@ -245,7 +245,6 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         sa.guess = guess;
         sa.smin = smin; sa.smax = smax; sa.sflag = sflag;
         sa.TB = TB;
-        sa.KMAP = c->kmap.as<uint16_t>();
         // seam outputs (k_seams sets flags, so they are cleared first)
         c->big.ensure(nb);
         c->pairsl.ensure((size_t)nt * TPC * sizeof(u64));
@@ -312,8 +311,8 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         if (nfix) {
             HIP_OK(hipMemsetAsync(fchg, 0, nt, s));
             launch(c, "k_fix", [&] {
-                if (mask) k_fix<true><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, mask, thr, mode, BITS, FACES, COUNT, P, KR, fchg, sa.KMAP);
-                else k_fix<false><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR, fchg, sa.KMAP);
+                if (mask) k_fix<true><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, mask, thr, mode, BITS, FACES, COUNT, P, KR, fchg);
+                else k_fix<false><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR, fchg);
             });
             if (lds_seams) {
                 // relabelled faces: the seams of the relabelled tiles and of the tiles above /
@@ -567,7 +566,13 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
         c->lut_valid = true;
     }
     launch(c, "k_pass2", [&] {
-        k_pass2<<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, FIN, out, c->kmap.as<uint16_t>());
+        if (c->pass2_wgs > 0) {
+            // persistent: pass2_wgs workgroups per XCD-multiple (default 4 per CU)
+            const unsigned grid = (unsigned)std::min<int64_t>(c->pass2_wgs, (nt + 7) / 8 * 8);
+            k_pass2p<<<(grid + 7) / 8 * 8, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, FIN, out);
+        } else {
+            k_pass2<<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, FIN, out);
+        }
     });
 
     u64 sc[4] = {0, 0, 0, 0};
@@ -638,6 +643,12 @@ int cc_create(int device, cc_ctx** out) {
         HIP_OK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         c->stream = c->own_stream;
         if (const char* e = std::getenv("CC_FRONT_CHUNKS")) c->front_chunks = std::max(1, atoi(e));
+        {
+            hipDeviceProp_t prop;
+            HIP_OK(hipGetDeviceProperties(&prop, device));
+            c->pass2_wgs = 4 * (int64_t)prop.multiProcessorCount;
+            if (const char* e = std::getenv("CC_PASS2_WGS")) c->pass2_wgs = atoll(e);
+        }
         *out = c;
     })
 }
@@ -651,7 +662,7 @@ void cc_destroy(cc_ctx* c) {
                       &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
                       &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
-                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec, &c->mark, &c->bflag, &c->kmap,
+                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec, &c->mark, &c->bflag,
                       &c->ev_main, &c->ev_z, &c->ev_seg, &c->ev_gt, &c->ev_flag, &c->ev_part};
     for (DevBuf* b : bufs) b->release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }

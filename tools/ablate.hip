@@ -86,7 +86,6 @@ int main(int argc, char** argv) {
         u32 *st, *COUNT, *P;
         face_t* FACES;
         u64 *BITS, *KEY, *FIN;
-        uint16_t* KMAP;
         BlockParam* bp;
         float* dummy;
         HIP_OK(hipMalloc(&st, nb * 12));
@@ -97,7 +96,6 @@ int main(int argc, char** argv) {
         HIP_OK(hipMalloc(&P, nodes * 4));
         HIP_OK(hipMalloc(&KEY, nodes * 8));
         HIP_OK(hipMalloc(&FIN, nodes * 8));
-        HIP_OK(hipMalloc(&KMAP, (size_t)nt * NRUN * 2));
         HIP_OK(hipMalloc(&dummy, 64));
         HIP_OK(hipMemset(FIN, 0, nodes * 8));
         u32 *smin = st, *smax = st + nb, *sflag = st + 2 * nb;
@@ -116,7 +114,7 @@ int main(int argc, char** argv) {
         r.push_back({"copy_read", time_ms(s, iters, [&] { k_read<<<big, 256, 0, s>>>((const float4*)in, nvox / 4, dummy); })});
         r.push_back({"copy_write", time_ms(s, iters, [&] { k_write<<<big, 256, 0, s>>>((ulonglong2*)out, nvox / 2); })});
         r.push_back({"k_block_stats", time_ms(s, iters, stats)});
-#define P1(A) k_pass1<false, A><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, nullptr, bp, thr, mode, BITS, FACES, COUNT, P, KEY, KMAP)
+#define P1(A) k_pass1<false, A><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, nullptr, bp, thr, mode, BITS, FACES, COUNT, P, KEY)
         r.push_back({"k_pass1_abl1_load_bits", time_ms(s, iters, [&] { P1(1); })});
         r.push_back({"k_pass1_ccl_ph1_runs", time_ms(s, iters, [&] { P1(11); })});
         r.push_back({"k_pass1_ccl_ph2_unions", time_ms(s, iters, [&] { P1(12); })});
@@ -143,7 +141,6 @@ int main(int argc, char** argv) {
             HIP_OK(hipMemcpy(guess, hb.data(), nb * sizeof(BlockParam), hipMemcpyHostToDevice));
             SpecArgs sa;
             sa.guess = guess; sa.smin = fst; sa.smax = fst + nb; sa.sflag = fst + 2 * nb; sa.TB = TB; sa.t0 = 0;
-            sa.KMAP = KMAP;
             r.push_back({"k_spec", time_ms(s, iters, [&] {
                 HIP_OK(hipMemsetAsync(fst, 0xFF, nb * 4, s));
                 HIP_OK(hipMemsetAsync(fst + nb, 0, 2 * nb * 4, s));
@@ -174,14 +171,13 @@ int main(int argc, char** argv) {
             HIP_OK(hipMemcpy(guess, bp, nb * sizeof(BlockParam), hipMemcpyDeviceToDevice));
             SpecArgs sa;
             sa.guess = guess; sa.smin = fst; sa.smax = fst + nb; sa.sflag = fst + 2 * nb; sa.TB = TB; sa.t0 = 0;
-            sa.KMAP = KMAP;
             r.push_back({"k_spec_cached", time_ms(s, iters, [&] {
                 k_spec<false, 1><<<(unsigned)nt, NTHREADS, 0, s>>>(gc, sa, in, nullptr, BITS, FACES, COUNT, P, KEY);
             })});
             r.push_back({"k_block_stats_cached", time_ms(s, iters, [&] {
                 k_block_stats<<<(unsigned)nt, NTHREADS, 0, s>>>(gc, in, smin, smax, sflag);
             })});
-#define P1C(A) k_pass1<false, A><<<(unsigned)nt, NTHREADS, 0, s>>>(gc, in, nullptr, bp, thr, mode, BITS, FACES, COUNT, P, KEY, KMAP)
+#define P1C(A) k_pass1<false, A><<<(unsigned)nt, NTHREADS, 0, s>>>(gc, in, nullptr, bp, thr, mode, BITS, FACES, COUNT, P, KEY)
             r.push_back({"k_pass1_abl1_cached", time_ms(s, iters, [&] { P1C(1); })});
             r.push_back({"k_pass1_ph1_cached", time_ms(s, iters, [&] { P1C(11); })});
             r.push_back({"k_pass1_ph2list_cached", time_ms(s, iters, [&] { P1C(14); })});
@@ -213,7 +209,7 @@ int main(int argc, char** argv) {
             r.push_back({"k_seams_zyx", time_ms(s, iters, [&] { SEAMS(4); })});
             r.push_back({"k_seams_full", time_ms(s, iters, [&] { SEAMS(0); })});
         }
-        r.push_back({"k_pass2", time_ms(s, iters, [&] { k_pass2<<<(unsigned)nt, NTHREADS, 0, s>>>(g, BITS, COUNT, FIN, out, KMAP); })});
+        r.push_back({"k_pass2", time_ms(s, iters, [&] { k_pass2<<<(unsigned)nt, NTHREADS, 0, s>>>(g, BITS, COUNT, FIN, out); })});
         std::printf("{\"shape\": [%lld, %lld, %lld], \"block\": [%lld, %lld, %lld], \"mode\": %d, \"tiles\": %lld",
                     (long long)shape[0], (long long)shape[1], (long long)shape[2], (long long)bs[0], (long long)bs[1],
                     (long long)bs[2], mode, (long long)nt);

@@ -56,7 +56,7 @@ int main(int argc, char** argv) {
         HIP_OK(hipMemset(smax, 0, 2 * nb * 4));
         k_block_stats<<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, smin, smax, sflag);
         k_block_params<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, smin, smax, sflag, thr, mode, bp);
-        k_pass1<false, 0><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, nullptr, bp, thr, mode, BITS[0], FACES, COUNT[0], P, KEY, nullptr);
+        k_pass1<false, 0><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, nullptr, bp, thr, mode, BITS[0], FACES, COUNT[0], P, KEY);
         u32* part;
         HIP_OK(hipMalloc(&part, nb * SAMPLE_PARTS * 16));
         k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, part);
@@ -74,7 +74,6 @@ int main(int argc, char** argv) {
         }
         HIP_OK(hipMemcpy(guess, hb.data(), nb * sizeof(BlockParam), hipMemcpyHostToDevice));
         SpecArgs sa;
-        sa.KMAP = nullptr;
         sa.guess = guess; sa.smin = smin; sa.smax = smax; sa.sflag = sflag; sa.TB = TB; sa.t0 = 0;
         if (mode == 0) k_spec<false, 1><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS[1], FACES, COUNT[1], P, KEY);
         else if (mode == 1) k_spec<false, 2><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS[1], FACES, COUNT[1], P, KEY);
