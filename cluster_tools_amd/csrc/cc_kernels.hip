@@ -2171,110 +2171,6 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
     }
 }
 
-// Persistent form of k_pass2: a fixed grid of workgroups walks the tiles; every global load of
-// the next tile (its bit rows, COUNT and the LDS-cached labels of its components) is issued
-// before the current tile's CCL, so those round trips hide behind the CCL and the stores instead
-// of opening every tile.  Workgroup b runs on XCD k = b % 8 and takes every W-th tile of XCD k's
-// contiguous share of the volume (W = workgroups per XCD), as xcd_order.
-constexpr int P2_LAB_PER_THREAD = LABCAP / NTHREADS;
-static_assert(NROWS == NTHREADS && LABCAP % NTHREADS == 0, "one bit row and LABCAP / NTHREADS labels per thread");
-
-__global__ __launch_bounds__(NTHREADS) void k_pass2p(Geom g, const u64* __restrict__ BITS, const u32* __restrict__ COUNT,
-                                                     const u64* __restrict__ FIN, u64* __restrict__ out) {
-    __shared__ u64 rows[NROWS];
-    __shared__ TileCCL T;
-    __shared__ u64 lab[LABCAP];
-    const int tid = threadIdx.x;
-    const u32 n = (u32)g.n_tiles, b = blockIdx.x, W = gridDim.x >> 3;     // gridDim.x: a multiple of 8
-    const u32 q = n >> 3, rem = n & 7, k8 = b & 7;
-    const u32 s0 = k8 * q + (k8 < rem ? k8 : rem), s1 = s0 + q + (k8 < rem ? 1u : 0u);
-    u32 t = s0 + (b >> 3);
-    if (t >= s1) return;
-    // prefetched state of tile t
-    u64 rnext = BITS[(int64_t)t * NROWS + tid];
-    u32 Rnext = COUNT[t];
-    u64 fnext[P2_LAB_PER_THREAD];
-    auto fetch_lab = [&](u32 tt, u32 R) {
-        const u32 base = tt * (u32)g.cap;
-#pragma unroll
-        for (int j = 0; j < P2_LAB_PER_THREAD; ++j) {
-            const u32 k = tid + j * NTHREADS;
-            fnext[j] = k < R ? FIN[base + k] : 0ull;
-        }
-    };
-    fetch_lab(t, Rnext);
-    while (true) {
-        const u32 tn = t + W;
-        const bool more = tn < s1;
-        const u64 rcur = rnext;
-        const u32 R = __builtin_amdgcn_readfirstlane(Rnext);
-        u64 fcur[P2_LAB_PER_THREAD];
-#pragma unroll
-        for (int j = 0; j < P2_LAB_PER_THREAD; ++j) fcur[j] = fnext[j];
-        if (more) {                     // next tile's loads in flight during this tile's work
-            rnext = BITS[(int64_t)tn * NROWS + tid];
-            Rnext = COUNT[tn];
-        }
-        const TileInfo ti = tile_info(g, t);
-        const bool vec = ((ti.x0 | (int)(g.X & 1)) & 1) == 0;
-        const int ncz = (ti.lz + 1) / 2, ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2;
-        const u32 base = t * (u32)g.cap;
-        // the next tile's labels: COUNT[tn] has had the CCL (or the setup) to arrive; the loads
-        // overlap this tile's stores
-        auto prefetch_lab = [&] {
-            if (more) fetch_lab(tn, __builtin_amdgcn_readfirstlane(Rnext));
-        };
-        if (R == 0) {
-            prefetch_lab();
-            for (int c = tid; c < NC; c += NTHREADS) {
-                const int cz = c / (CY * CX), cy = (c / CX) % CY, cx = c % CX;
-                if (cz >= ncz || cy >= ncy || cx >= ncx) continue;
-                const bool two = 2 * cx + 1 < ti.lx;
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int z = 2 * cz + (d >> 1), y = 2 * cy + (d & 1);
-                    if (z < ti.lz && y < ti.ly)
-                        store2(out, ((int64_t)(ti.z0 + z) * g.Y + ti.y0 + y) * g.X + ti.x0 + 2 * cx, 0, 0, two, vec);
-                }
-            }
-        } else {
-            rows[tid] = rcur;
-            __syncthreads();
-            tile_ccl(rows, T, (u32*)lab);
-#pragma unroll
-            for (int j = 0; j < P2_LAB_PER_THREAD; ++j) lab[tid + j * NTHREADS] = fcur[j];
-            prefetch_lab();
-            __syncthreads();
-            for (int c = tid; c < NC; c += NTHREADS) {
-                const int cz = c / (CY * CX), cy = (c / CX) % CY, cx = c % CX;
-                if (cz >= ncz || cy >= ncy || cx >= ncx) continue;
-                const int r = (2 * cz) * TY + 2 * cy;
-                const u32 m = vpair(rows[r], cx) | (vpair(rows[r + 1], cx) << 2) | (vpair(rows[r + TY], cx) << 4) |
-                              (vpair(rows[r + TY + 1], cx) << 6);
-                u64 v = 0;
-                if (m) {
-                    const u32 k = cube_k(T, c);
-                    if (k < LABCAP) v = lab[k];
-                    else v = __builtin_nontemporal_load(FIN + base + k);
-                }
-                const bool two = 2 * cx + 1 < ti.lx;
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int z = 2 * cz + (d >> 1), y = 2 * cy + (d & 1);
-                    if (z < ti.lz && y < ti.ly) {
-                        const u32 bb = m >> (2 * d);
-                        store2(out, ((int64_t)(ti.z0 + z) * g.Y + ti.y0 + y) * g.X + ti.x0 + 2 * cx,
-                               (bb & 1) ? v : 0, (bb & 2) ? v : 0, two, vec);
-                    }
-                }
-            }
-        }
-        if (!more) break;
-        __syncthreads();                // rows / T / lab are rewritten by the next tile
-        t = tn;
-    }
-}
-
 // ------------------------------------------------------------------------------------------
 // k_threshold: the reference Threshold task (thresholded_components/threshold.py:131-171):
 // per-block normalize (volume_utils.py:98-105) and compare, written as uint8.  One workgroup

@@ -70,7 +70,6 @@ struct cc_ctx {
     int debug = 0;         // CC_DEBUG_* test hooks
     int front_chunks = 1;  // z-layer chunks of the speculative front (CC_FRONT_CHUNKS)
     int64_t quirk_jobs = 0;  // CC_OPT_EMPTY_JOB_QUIRK: emulate the reference's empty-job branch for max_jobs
-    int64_t pass2_wgs = 0;   // k_pass2p grid (persistent pass 2); 0: one workgroup per tile (CC_PASS2_WGS)
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, ProfEntry> prof_acc;
@@ -565,15 +564,7 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
         launch(c, "k_finalize", [&] { k_finalize<false><<<grid1d(nt, WAVES), NTHREADS, 0, s>>>(g, COUNT, P, KR, offsets, U, V, m, KR); });
         c->lut_valid = true;
     }
-    launch(c, "k_pass2", [&] {
-        if (c->pass2_wgs > 0) {
-            // persistent: pass2_wgs workgroups per XCD-multiple (default 4 per CU)
-            const unsigned grid = (unsigned)std::min<int64_t>(c->pass2_wgs, (nt + 7) / 8 * 8);
-            k_pass2p<<<(grid + 7) / 8 * 8, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, FIN, out);
-        } else {
-            k_pass2<<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, FIN, out);
-        }
-    });
+    launch(c, "k_pass2", [&] { k_pass2<<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, FIN, out); });
 
     u64 sc[4] = {0, 0, 0, 0};
     HIP_OK(hipMemcpyAsync(sc, scalars, 4 * sizeof(u64), hipMemcpyDeviceToHost, s));
@@ -643,12 +634,6 @@ int cc_create(int device, cc_ctx** out) {
         HIP_OK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         c->stream = c->own_stream;
         if (const char* e = std::getenv("CC_FRONT_CHUNKS")) c->front_chunks = std::max(1, atoi(e));
-        {
-            hipDeviceProp_t prop;
-            HIP_OK(hipGetDeviceProperties(&prop, device));
-            c->pass2_wgs = 4 * (int64_t)prop.multiProcessorCount;
-            if (const char* e = std::getenv("CC_PASS2_WGS")) c->pass2_wgs = atoll(e);
-        }
         *out = c;
     })
 }
