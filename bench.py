@@ -90,7 +90,9 @@ def main():
     import torch
     import torch.distributed as dist
     from cluster_tools_amd import _lib
-    lib_src = _lib.check_provenance()       # the library must be built from this tree's sources
+    # the library must be built from this tree's sources (CC_LIB_PATH: another build for same-box
+    # A/B timing, tools/ab_build.sh -- the line is then marked as such)
+    lib_src = _lib.check_provenance() if not os.environ.get('CC_LIB_PATH') else 'override:' + _lib.LIB_PATH
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
