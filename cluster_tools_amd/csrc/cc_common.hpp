@@ -105,16 +105,6 @@ __device__ __forceinline__ TileInfo tile_info(const Geom& g, int64_t t) {
     return ti;
 }
 
-// XCD-aware work order: workgroups are dispatched round-robin over the 8 XCDs (b % 8), so
-// workgroup b takes item start_k + b / 8 of XCD k = b % 8's contiguous share of the n items.
-// Each XCD then streams one contiguous part of the volume: tools/roof.hip measured the tile-shaped
-// uint64 stores of k_pass2 at 5.30 -> 4.84 ms and the tile reads at 2.86 -> 2.70 ms for C3.  The
-// map is a bijection for any n; results never depend on it (only speed does).
-__device__ __forceinline__ u32 xcd_order(u32 b, u32 n) {
-    const u32 q = n >> 3, rem = n & 7, k = b & 7;
-    return k * q + (k < rem ? k : rem) + (b >> 3);
-}
-
 // IEEE-754 total order for non-NaN floats as unsigned ints (-0 < +0).
 __device__ __host__ __forceinline__ u32 f2ord(u32 u) { return (u & 0x80000000u) ? ~u : (u | 0x80000000u); }
 __device__ __host__ __forceinline__ u32 ord2f(u32 o) { return (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o; }

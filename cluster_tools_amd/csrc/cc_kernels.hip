@@ -838,7 +838,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     u32* COUNT, u32* P, u64* KEY) {
     __shared__ Pass1LDS L;
     __shared__ u32 red[6][NTHREADS / 64];
-    const int64_t t = sa.t0 + xcd_order(blockIdx.x, gridDim.x);
+    const int64_t t = sa.t0 + blockIdx.x;
     const TileInfo ti = tile_info(g, t);
     const BlockParam p = uniform_bp(sa.guess[ti.block]);
     if (p.kind != BP_INTERVAL) {                   // no guess: statistics only, k_fix labels the tile
@@ -1513,7 +1513,7 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* _
     __shared__ face_t Eall[SP_WAVES][EDGE_N];
     __shared__ u32 cnt[SP_WAVES][2];
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t idx = (int64_t)xcd_order(blockIdx.x, gridDim.x) * SP_WAVES + w;
+    const int64_t idx = (int64_t)blockIdx.x * SP_WAVES + w;
     int64_t t = t_begin + idx;
     bool valid = t < t_end;
     if (list) {
@@ -2120,7 +2120,7 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
     __shared__ u64 rows[NROWS];             // split bit rows (see tile_ccl)
     __shared__ TileCCL T;
     __shared__ u64 lab[LABCAP];
-    const int64_t t = xcd_order(blockIdx.x, gridDim.x);
+    const int64_t t = blockIdx.x;
     const TileInfo ti = tile_info(g, t);
     const int tid = threadIdx.x;
     const u32 R = COUNT[t];

@@ -62,18 +62,10 @@ __global__ __launch_bounds__(512) void rd_tile(const float* __restrict__ in, int
 }
 
 // float4 lanes: lane l reads x = 4 (l % 16) .. + 3 of row group row 4 * (wave-slot) + l / 16
-// XCD-aware order: workgroup b runs on XCD b % 8 (round-robin dispatch); SW = 1 gives XCD k the
-// contiguous tile range [k nt / 8, (k + 1) nt / 8), SW = 2 gives it every 8th z-layer... (layers k, k + 8, ...)
-__device__ __forceinline__ int swz(int b, int nt, int SW, int layer) {
-    if (SW == 1) return (b % 8) * (nt / 8) + b / 8;
-    if (SW == 2) { const int L = nt / layer; const int l = b / layer, i = b % layer; return ((l % 8) * (L / 8) + l / 8) * layer + i; }
-    return b;
-}
-
-template <int RZ, int SW = 0>
+template <int RZ>
 __global__ __launch_bounds__(512) void rd_tile4(const float* __restrict__ in, int64_t Y, int64_t X, int ntx, int nty,
                                                 float* out) {
-    const int t = swz(blockIdx.x, gridDim.x, SW, ntx * nty), lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int t = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int tx = t % ntx, ty = (t / ntx) % nty, tz = t / (ntx * nty);
     // wave w: rows y = 4 w + (lane / 16) of each plane (32 rows = 8 waves x 4)
     const float* p = in + (((int64_t)tz * 16) * Y + ty * 32 + 4 * wave + (lane >> 4)) * X + tx * 64 + 4 * (lane & 15);
@@ -100,10 +92,9 @@ __global__ __launch_bounds__(256) void wr_u2(ulonglong2* __restrict__ out, int64
 }
 
 // the k_pass2 shape: one 512-thread tile, each thread 16-B stores of (x, x+1) pairs of cube rows
-template <int SW = 0>
 __global__ __launch_bounds__(512) void wr_tile(unsigned long long* __restrict__ out, int64_t Y, int64_t X, int ntx,
                                                int nty) {
-    const int t = swz(blockIdx.x, gridDim.x, SW, ntx * nty);
+    const int t = blockIdx.x;
     const int tx = t % ntx, ty = (t / ntx) % nty, tz = t / (ntx * nty);
     for (int c = threadIdx.x; c < 4096; c += 512) {
         const int cz = c / 512, cy = (c / 32) % 16, cx = c % 32;
@@ -183,13 +174,7 @@ int main(int argc, char** argv) {
     r.push_back({"wr_u2_u1", time_ms(s, iters, [&] { wr_u2<1><<<g * 8, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
     r.push_back({"wr_u2_u4", time_ms(s, iters, [&] { wr_u2<4><<<g * 2, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
     r.push_back({"wr_u2_u8", time_ms(s, iters, [&] { wr_u2<8><<<g, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
-    r.push_back({"wr_tile", time_ms(s, iters, [&] { wr_tile<0><<<nt, 512, 0, s>>>(out, Y, X, ntx, nty); })});
-    r.push_back({"wr_tile_xcd1", time_ms(s, iters, [&] { wr_tile<1><<<nt, 512, 0, s>>>(out, Y, X, ntx, nty); })});
-    r.push_back({"wr_tile_xcd2", time_ms(s, iters, [&] { wr_tile<2><<<nt, 512, 0, s>>>(out, Y, X, ntx, nty); })});
-    r.push_back({"rd_tile4_xcd1", time_ms(s, iters, [&] { rd_tile4<4, 1><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
-    r.push_back({"rd_tile4_xcd2", time_ms(s, iters, [&] { rd_tile4<4, 2><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
-    r.push_back({"wr_tile_again", time_ms(s, iters, [&] { wr_tile<0><<<nt, 512, 0, s>>>(out, Y, X, ntx, nty); })});
-    r.push_back({"wr_u2_u1_again", time_ms(s, iters, [&] { wr_u2<1><<<g * 8, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
+    r.push_back({"wr_tile", time_ms(s, iters, [&] { wr_tile<<<nt, 512, 0, s>>>(out, Y, X, ntx, nty); })});
     r.push_back({"wr_tile_w2", time_ms(s, iters, [&] { wr_tile_w<2><<<nt / 2, 512, 0, s>>>(out, Y, X, ntx, nty); })});
     r.push_back({"wr_tile_w4", time_ms(s, iters, [&] { wr_tile_w<4><<<nt / 4, 512, 0, s>>>(out, Y, X, ntx, nty); })});
     std::printf("{\"shape\": [%lld, %lld, %lld]", (long long)Z, (long long)Y, (long long)X);
