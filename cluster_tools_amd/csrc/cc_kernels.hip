@@ -1415,7 +1415,8 @@ __device__ __forceinline__ void stage_edges(const Geom& g, const face_t* __restr
 //   lane 0/1 (-1,-1,0)/(-1,+1,0): own ZLO row y = 0 / ly-1 against the neighbour's ZHI row, bits x
 //   lane 2/3 (-1,0,-1)/(-1,0,+1): own ZLO column x = 0 / lx-1, bits y
 //   lane 4/5 (0,-1,-1)/(0,-1,+1): own YLO column x = 0 / lx-1, bits z
-// EMIT(lane code, tn, ka, kb) once per run of contacts (26-connectivity along the edge).
+// EMIT(oz, oy, ox, ka, kb) once per run of contacts (26-connectivity along the edge), the
+// neighbour tile being t + oz sz + oy sy + ox.
 template <class EM>
 __device__ __forceinline__ void seam_edges_rows(const Geom& g, const face_t* S, const face_t* E, int64_t t,
                                                 const TileInfo& ti, int lane, EM&& emit) {
@@ -1462,7 +1463,8 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const face_t* S, 
 #pragma unroll
         for (int i = 0; i < 6; ++i) if (i == e) { a = A[i]; b = B[i]; }
         const int s = (e & 1) ? 1 : -1;
-        const int64_t tn = e < 2 ? t - sz + s * sy : e < 4 ? t - sz + s : t - sy + s;
+        // neighbour offset (oz, oy, ox): tn = t + oz sz + oy sy + ox
+        const int oz = e < 4 ? -1 : 0, oy = e < 2 ? s : e < 4 ? 0 : -1, ox = e < 2 ? 0 : s;
         u32 la = NONE, lb = NONE;
         if (a && b) {
 #pragma unroll
@@ -1484,7 +1486,7 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const face_t* S, 
                     ka &= FK_MASK; kb &= FK_MASK;
                     if (ka == la && kb == lb) continue;
                     la = ka; lb = kb;
-                    emit(tn, ka, kb);
+                    emit(oz, oy, ox, ka, kb);
                 }
             }
         }
@@ -1495,7 +1497,7 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const face_t* S, 
             const int jo = s1 < 0 ? 0 : (ti.ly - 1) & 1, io = s2 < 0 ? 0 : (ti.lx - 1) & 1;
             const u32 a = S[F_ZLO + cyo * CX + cxo], b = E[112 + c];
             if (((a >> FK_BITS) & fsel(jo, io)) && ((b >> FK_BITS) & fsel(ypar(s1), xpar(s2))))
-                emit(t - sz + s1 * sy + s2, a & FK_MASK, b & FK_MASK);
+                emit(-1, s1, s2, a & FK_MASK, b & FK_MASK);
         }
     }
 }
@@ -1534,11 +1536,16 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* _
     if (lane < 2) cnt[w][lane] = 0;
     __syncthreads();
     if (!valid) return;
-    const u32 lt_own = block_local(g, (u32)t);
+    // block-local index of the own tile and the tile strides inside its block (a neighbour in
+    // the same block at offset (oz, oy, ox) is lt_own + oz bny bnx + oy bnx + ox)
+    const int bz = g.tblk[0][ti.iz], by = g.tblk[1][ti.iy], bx = g.tblk[2][ti.ix];
+    const u32 bnx = (u32)g.btn[2][bx], bnyx = (u32)g.btn[1][by] * bnx;
+    const u32 lt_own = (u32)(ti.iz - g.bt0[0][bz]) * bnyx + (u32)(ti.iy - g.bt0[1][by]) * bnx + (u32)(ti.ix - g.bt0[2][bx]);
     const u32 capu = (u32)g.cap;
     u64* out = PAIRS + t * TPC;
     u64* iout = IPAIRS + t * TPI;
     // wave-aggregated append of one pair per active lane to the intra (0) or inter (1) list
+    // (used for the pairs beyond a lane's register stash only)
     auto append = [&](bool to_inter, u64 v) {
         const u64 act = __ballot(1), mi = __ballot(to_inter), ma = act & ~mi;
         u32 base_a = 0, base_i = 0;
@@ -1557,25 +1564,28 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* _
             if (pos < TPC) out[pos] = v;
         }
     };
-    if (STOP == 1) return;
-    const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
-    // exact code of a lower neighbour tile (the 13 lex-negative offsets)
-    auto dir_code = [&](int64_t tn) -> u32 {
-        const int64_t d = t - tn;
-        u32 c = 0;
-#pragma unroll
-        for (int dz = 0; dz <= 1; ++dz)
-#pragma unroll
-            for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-                for (int dx = -1; dx <= 1; ++dx) {
-                    const int code = dz * 9 + (dy + 1) * 3 + (dx + 1);   // d = dz sz - dy sy - dx
-                    if (d == dz * sz - dy * sy - dx) c = (u32)code;
-                }
-        return c;
+    // per-lane stash of the first STASH pairs in registers, written out by one set of ballots at
+    // the end (the contact loops are divergent: a wave-wide append per contact costs a ballot /
+    // atomic / readfirstlane round on the scalar unit every iteration)
+    constexpr int STASH = 4;
+    u64 st0 = 0, st1 = 0, st2 = 0, st3 = 0;
+    int ns = 0;
+    u32 kinds = 0;                                            // bit j: slot j goes to the inter list
+    auto push = [&](bool to_inter, u64 v) {
+        if (ns < STASH) {
+            st0 = ns == 0 ? v : st0; st1 = ns == 1 ? v : st1;
+            st2 = ns == 2 ? v : st2; st3 = ns == 3 ? v : st3;
+            kinds |= (u32)to_inter << ns;
+            ++ns;
+        } else {
+            append(to_inter, v);
+        }
     };
+    if (STOP == 1) return;
     // first sighting of (neighbour, ka, kb) in this tile? (LDS hash set; a full set lets
-    // duplicates through, which the consumers tolerate)
+    // duplicates through, which the consumers tolerate).  code: the neighbour's direction,
+    // dz * 9 + (dy + 1) * 3 + (dx + 1) for the neighbour t - dz sz + dy sy + dx (distinct
+    // directions are distinct tiles)
     auto fresh = [&](u32 code, u32 ka, u32 kb) -> bool {
         const u32 key = (code << 24) | ((ka & 0xFFFu) << 12) | (kb & 0xFFFu);
         u32 h = (key * 0x9E3779B1u) >> (32 - SEAM_HASH_BITS);
@@ -1587,6 +1597,7 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* _
         }
         return true;
     };
+    const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
     // the three lower seams: neighbour tile, mode (0 none, 1 intra 26-conn, 2 block face 6-conn)
     int mode[3] = {0, 0, 0};
     if (ti.iz > 0) mode[0] = g.tblk[0][ti.iz] == g.tblk[0][ti.iz - 1] ? 1 : 2;
@@ -1594,34 +1605,48 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* _
     if (ti.ix > 0) mode[2] = g.tblk[2][ti.ix] == g.tblk[2][ti.ix - 1] ? 1 : 2;
     const int myseam = lane < 32 ? 0 : lane < 48 ? 1 : 2;
     const int64_t tn_l = t - (myseam == 0 ? sz : myseam == 1 ? sy : 1);
-    const u32 code_l = myseam == 0 ? dir_code(t - sz) : myseam == 1 ? dir_code(t - sy) : dir_code(t - 1);
-    const u32 ltn_l = mode[myseam] == 1 ? block_local(g, (u32)tn_l) : 0u;
+    const u32 code_l = myseam == 0 ? 13u : myseam == 1 ? 1u : 3u;    // (-1,0,0) / (0,-1,0) / (0,0,-1)
+    const u32 ltn_l = lt_own - (myseam == 0 ? bnyx : myseam == 1 ? bnx : 1u);
     seam_rows3(S, mode, lane, [&](int seam, u32 ka, u32 kb) {
         if (!fresh(code_l, ka, kb)) return;
-        if (mode[seam] == 1) append(false, ((u64)((lt_own << 12) | ka) << 32) | ((ltn_l << 12) | kb));
-        else append(true, ((u64)((u32)t * capu + ka) << 32) | ((u32)tn_l * capu + kb));
+        if (mode[seam] == 1) push(false, ((u64)((lt_own << 12) | ka) << 32) | ((ltn_l << 12) | kb));
+        else push(true, ((u64)((u32)t * capu + ka) << 32) | ((u32)tn_l * capu + kb));
     });
-    if (STOP == 4) return;
-    // edges and corners inside the block
-    // a lane's edge / corner neighbour is fixed: its direction code and block-local index are
-    // computed at the lane's first contact only
-    bool have_e = false;
-    u32 code_e = 0, lt_e = 0;
-    seam_edges_rows(g, S, E, t, ti, lane, [&](int64_t t2, u32 k1, u32 k2) {
-        if (!have_e) {
-            code_e = dir_code(t2);
-            lt_e = block_local(g, (u32)t2);
-            have_e = true;
-        }
-        if (!fresh(code_e, k1, k2)) return;
-        append(false, ((u64)((lt_own << 12) | k1) << 32) | ((lt_e << 12) | k2));
-    });
+    if (STOP != 4) {
+        // edges and corners inside the block
+        seam_edges_rows(g, S, E, t, ti, lane, [&](int oz, int oy, int ox, u32 k1, u32 k2) {
+            const u32 code = (u32)(-oz * 9 + (oy + 1) * 3 + (ox + 1));
+            if (!fresh(code, k1, k2)) return;
+            const u32 lt_e = lt_own + (u32)(oz * (int)bnyx + oy * (int)bnx + ox);
+            push(false, ((u64)((lt_own << 12) | k1) << 32) | ((lt_e << 12) | k2));
+        });
+    }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the stashes: slot-major, lane order inside a slot, behind the overflow appends
+    u32 na = __builtin_amdgcn_readfirstlane(cnt[w][0]), ni = __builtin_amdgcn_readfirstlane(cnt[w][1]);
+    const u64 below = (1ull << lane) - 1;
+#pragma unroll
+    for (int j = 0; j < STASH; ++j) {
+        const bool has = j < ns, inter = (kinds >> j) & 1u;
+        const u64 mi = __ballot(has && inter), ma = __ballot(has && !inter);
+        if (!(mi | ma)) break;
+        const u64 v = j == 0 ? st0 : j == 1 ? st1 : j == 2 ? st2 : st3;
+        if (has) {
+            if (inter) {
+                const u32 pos = ni + (u32)__popcll(mi & below);
+                if (pos < TPI) iout[pos] = v;
+            } else {
+                const u32 pos = na + (u32)__popcll(ma & below);
+                if (pos < TPC) out[pos] = v;
+            }
+        }
+        na += (u32)__popcll(ma);
+        ni += (u32)__popcll(mi);
+    }
     if (lane == 0) {
-        const u32 n = cnt[w][0], ni = cnt[w][1];
-        PC[t] = n < TPC ? n : TPC;
-        if (n > TPC) big[ti.block] = 1;
+        PC[t] = na < TPC ? na : TPC;
+        if (na > TPC) big[ti.block] = 1;
         IPC[t] = ni < TPI ? ni : TPI;
         if (ni > TPI) iovf[t] = 1;
     }
