@@ -1457,47 +1457,45 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const face_t* S, 
             B[e] = __ballot((eb >> (FK_BITS + (p & 1) * 2 + xpar(s))) & 1u);
         }
     }
+    // one candidate row pair per lane: the edges on lanes 0-5, the corners on lanes 6-9 (a single
+    // bit each side); contact p of own row -> own entry S[ab + (p >> 1) as], neighbour entry
+    // E[bb + (q >> 1)]; one emit site (the loops stay rolled: a copy of the emit path per
+    // direction would blow the kernel past the instruction cache)
+    u64 a = 0, b = 0;
+    int ab = 0, as = 0, bb = 0, oz = 0, oy = 0, ox = 0;
     if (lane < 6) {
         const int e = lane;
-        u64 a = 0, b = 0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) if (i == e) { a = A[i]; b = B[i]; }
         const int s = (e & 1) ? 1 : -1;
         // neighbour offset (oz, oy, ox): tn = t + oz sz + oy sy + ox
-        const int oz = e < 4 ? -1 : 0, oy = e < 2 ? s : e < 4 ? 0 : -1, ox = e < 2 ? 0 : s;
-        u32 la = NONE, lb = NONE;
-        if (a && b) {
-#pragma unroll
-            for (int d = -1; d <= 1; ++d) {
-                const u64 C = a & (d > 0 ? b >> 1 : d < 0 ? b << 1 : b);
-                for (u64 m = C & ~(C << 1); m; m &= m - 1) {
-                    const int p = __builtin_ctzll(m), q = p + d;
-                    u32 ka, kb;
-                    if (e < 2) {
-                        ka = S[F_ZLO + (s < 0 ? 0 : ncy - 1) * CX + (p >> 1)];
-                        kb = E[(e ? 32 : 0) + (q >> 1)];
-                    } else if (e < 4) {
-                        ka = S[F_ZLO + (p >> 1) * CX + (s < 0 ? 0 : ncx - 1)];
-                        kb = E[(e == 3 ? 80 : 64) + (q >> 1)];
-                    } else {
-                        ka = S[F_YLO + (p >> 1) * CX + (s < 0 ? 0 : ncx - 1)];
-                        kb = E[(e == 5 ? 104 : 96) + (q >> 1)];
-                    }
-                    ka &= FK_MASK; kb &= FK_MASK;
-                    if (ka == la && kb == lb) continue;
-                    la = ka; lb = kb;
-                    emit(oz, oy, ox, ka, kb);
-                }
-            }
-        }
+        oz = e < 4 ? -1 : 0; oy = e < 2 ? s : e < 4 ? 0 : -1; ox = e < 2 ? 0 : s;
+        if (e < 2) { ab = F_ZLO + (s < 0 ? 0 : ncy - 1) * CX; as = 1; bb = e ? 32 : 0; }
+        else if (e < 4) { ab = F_ZLO + (s < 0 ? 0 : ncx - 1); as = CX; bb = e == 3 ? 80 : 64; }
+        else { ab = F_YLO + (s < 0 ? 0 : ncx - 1); as = CX; bb = e == 5 ? 104 : 96; }
     } else if (lane < 10 && zok) {                          // corners (-1, s1, s2)
         const int c = lane - 6, s1 = (c & 2) ? 1 : -1, s2 = (c & 1) ? 1 : -1;
         if (yok(s1) && xok(s2)) {
             const int cyo = s1 < 0 ? 0 : ncy - 1, cxo = s2 < 0 ? 0 : ncx - 1;
             const int jo = s1 < 0 ? 0 : (ti.ly - 1) & 1, io = s2 < 0 ? 0 : (ti.lx - 1) & 1;
-            const u32 a = S[F_ZLO + cyo * CX + cxo], b = E[112 + c];
-            if (((a >> FK_BITS) & fsel(jo, io)) && ((b >> FK_BITS) & fsel(ypar(s1), xpar(s2))))
-                emit(-1, s1, s2, a & FK_MASK, b & FK_MASK);
+            ab = F_ZLO + cyo * CX + cxo; bb = 112 + c;
+            oz = -1; oy = s1; ox = s2;
+            const bool hit = ((S[ab] >> FK_BITS) & fsel(jo, io)) && ((E[bb] >> FK_BITS) & fsel(ypar(s1), xpar(s2)));
+            a = b = hit ? 1ull : 0ull;
+        }
+    }
+    if (a && b) {
+        u32 la = NONE, lb = NONE;
+#pragma unroll 1
+        for (int d = -1; d <= 1; ++d) {
+            const u64 C = a & (d > 0 ? b >> 1 : d < 0 ? b << 1 : b);
+            for (u64 m = C & ~(C << 1); m; m &= m - 1) {
+                const int p = __builtin_ctzll(m), q = p + d;
+                const u32 ka = S[ab + (p >> 1) * as] & FK_MASK, kb = E[bb + (q >> 1)] & FK_MASK;
+                if (ka == la && kb == lb) continue;
+                la = ka; lb = kb;
+                emit(oz, oy, ox, ka, kb);
+            }
         }
     }
 }
@@ -1607,9 +1605,10 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* _
     const int64_t tn_l = t - (myseam == 0 ? sz : myseam == 1 ? sy : 1);
     const u32 code_l = myseam == 0 ? 13u : myseam == 1 ? 1u : 3u;    // (-1,0,0) / (0,-1,0) / (0,0,-1)
     const u32 ltn_l = lt_own - (myseam == 0 ? bnyx : myseam == 1 ? bnx : 1u);
-    seam_rows3(S, mode, lane, [&](int seam, u32 ka, u32 kb) {
+    const int md_l = myseam == 0 ? mode[0] : myseam == 1 ? mode[1] : mode[2];
+    seam_rows3(S, mode, lane, [&](int, u32 ka, u32 kb) {
         if (!fresh(code_l, ka, kb)) return;
-        if (mode[seam] == 1) push(false, ((u64)((lt_own << 12) | ka) << 32) | ((ltn_l << 12) | kb));
+        if (md_l == 1) push(false, ((u64)((lt_own << 12) | ka) << 32) | ((ltn_l << 12) | kb));
         else push(true, ((u64)((u32)t * capu + ka) << 32) | ((u32)tn_l * capu + kb));
     });
     if (STOP != 4) {
