@@ -4,10 +4,11 @@
 // Replaces the reference RelabelWorkflow (relabel/relabel_workflow.py:10-60): FindUniques
 // (find_uniques.py, np.unique per block), FindLabeling (find_labeling.py:84-120: sorted uniques,
 // new ids consecutive from 0 when 0 occurs, else from 1; the (old, new) assignment table) and
-// Write (write.py, apply the table).  Device: one pass inserts every x-run of equal ids into an
-// HBM open-addressing set (run heads by one ballot per 64 voxels; a hit on an existing key is a
-// plain load, no atomic), the set is compacted and radix-sorted, every sorted id's slot receives
-// its new id, and one more pass maps the volume (16 B/voxel: 8 read + 8 write).
+// Write (write.py, apply the table).  Device: one pass inserts the head id of every run of equal
+// ids into a per-workgroup LDS set and the ids new to the workgroup into an HBM open-addressing
+// set (keeping each workgroup's id list), the HBM set is compacted and radix-sorted, every
+// sorted id's slot receives its new id, and one more pass maps the volume from per-workgroup
+// LDS tables (24 B/voxel over both passes: 8 read, then 8 read + 8 write).
 
 namespace cc {
 
@@ -21,7 +22,16 @@ __device__ __forceinline__ u64 rl_slot(const u64* keys, u64 mask, u64 key) {
     return ~0ull;
 }
 
-constexpr int RL_Q = 4;     // 64-voxel groups per wave iteration (loads in flight)
+constexpr int RL_Q = 8;      // loads per lane per wave iteration (RL_Q * VW voxels in flight)
+constexpr int RL_WG = 512;   // threads per workgroup
+typedef unsigned long long rl_u64x2 __attribute__((ext_vector_type(2)));
+constexpr int RL_LDS_BITS = 11;
+static_assert((1 << RL_LDS_BITS) == EV_LDS, "LDS set size");
+
+// slot of an id in a workgroup's LDS set (any hash will do: the set is private to the kernel)
+__device__ __forceinline__ u32 rl_lhash(u64 k) {
+    return ((u32)k ^ (u32)(k >> 32) * 0x85EBCA6Bu) * 0x9E3779B1u >> (32 - RL_LDS_BITS);
+}
 
 // global set insert; false when EV_PROBES slots were taken
 __device__ __forceinline__ bool rl_insert(u64* keys, u64 mask, u64 key) {
@@ -34,49 +44,114 @@ __device__ __forceinline__ bool rl_insert(u64* keys, u64 mask, u64 key) {
     return false;
 }
 
+// VW consecutive ids per lane (one 8 VW-byte load), run heads: a voxel whose left neighbour
+// (in the same lane or the lane below) holds another id; lane 0's first voxel is always a head
+template <int VW>
+struct RlVec {
+    u64 v[VW];
+    __device__ __forceinline__ void load(const u64* p, int64_t i, int64_t end) {
+        if constexpr (VW == 2) {
+            if (i + 1 < end) {
+                const rl_u64x2 t = __builtin_nontemporal_load(reinterpret_cast<const rl_u64x2*>(p + i));
+                v[0] = t.x; v[1] = t.y;
+            } else {
+                v[0] = i < end ? p[i] : EV_EMPTY;
+                v[1] = EV_EMPTY;
+            }
+        } else {
+            v[0] = i < end ? __builtin_nontemporal_load(p + i) : EV_EMPTY;
+        }
+    }
+};
+
+// run-head mask of a lane's RL_Q x VW ids (bit q VW + j): the id differs from its left neighbour
+// (same lane or the lane below; lane 0's first id always), ids 2^64 - 1 past the end excluded;
+// e_or |= EV_ERR_GT for a reserved id inside the range
+template <int VW>
+__device__ __forceinline__ u32 rl_heads(const RlVec<VW>* x, int64_t base, int64_t end, int lane, u32& e_or) {
+    u32 hm = 0;
+#pragma unroll
+    for (int q = 0; q < RL_Q; ++q) {
+        const int64_t i = base + (q * 64 + lane) * VW;
+        const u64 prev = (u64)__shfl_up((unsigned long long)x[q].v[VW - 1], 1);
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+            const u64 key = x[q].v[j];
+            if (i + j < end && key == EV_EMPTY) e_or |= EV_ERR_GT;
+            const u64 left = j ? x[q].v[j - 1] : prev;
+            if ((key != left || (j == 0 && lane == 0)) && key != EV_EMPTY) hm |= 1u << (q * VW + j);
+        }
+    }
+    return hm;
+}
+
+template <int VW>
+__device__ __forceinline__ u64 rl_pick(const RlVec<VW>* x, int b) {
+    u64 k = 0;
+#pragma unroll
+    for (int q = 0; q < RL_Q; ++q)
+#pragma unroll
+        for (int j = 0; j < VW; ++j) if (q * VW + j == b) k = x[q].v[j];
+    return k;
+}
+
 // Each workgroup owns a contiguous voxel range and an LDS set: only ids new to the workgroup
 // reach the HBM set.  (Global inserts per x-run measured 6.4-7 s at C3: ~67 M waves probing the
-// background id's slot, with agent-scope loads or with CAS on stale L2 lines alike.)
-__global__ __launch_bounds__(256) void k_rl_unique(const u64* __restrict__ lab, int64_t n, int64_t per_wg, u64* keys,
-                                                   u64 mask, u32* err) {
+// background id's slot, with agent-scope loads or with CAS on stale L2 lines alike.)  The
+// workgroup's set is kept as a list (WGL[wg * EV_LDS ..], WGN[wg]; ~0u when the LDS set
+// overflowed) so that k_rl_apply can map the same range from LDS alone.
+template <int VW>
+__global__ __launch_bounds__(RL_WG) void k_rl_unique(const u64* __restrict__ lab, int64_t n, int64_t per_wg,
+                                                     u64* keys, u64 mask, u32* err, u64* WGL, u32* WGN) {
     __shared__ u64 lk[EV_LDS];
-    for (int e = threadIdx.x; e < EV_LDS; e += 256) lk[e] = EV_EMPTY;
+    __shared__ u32 ln, lovf;
+    for (int e = threadIdx.x; e < EV_LDS; e += RL_WG) lk[e] = EV_EMPTY;
+    if (threadIdx.x == 0) { ln = 0; lovf = 0; }
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int64_t beg = (int64_t)blockIdx.x * per_wg, end = min(n, beg + per_wg);
-    u32 e_or = 0;
-    for (int64_t base = beg + (threadIdx.x & ~63) * RL_Q; base < end; base += 256 * RL_Q) {
-        u64 v[RL_Q];
-#pragma unroll
-        for (int q = 0; q < RL_Q; ++q) {
-            const int64_t i = base + q * 64 + lane;
-            v[q] = i < end ? __builtin_nontemporal_load(lab + i) : EV_EMPTY;
-            if (i < end && v[q] == EV_EMPTY) e_or |= EV_ERR_GT;
-        }
-#pragma unroll
-        for (int q = 0; q < RL_Q; ++q) {
-            const u64 prev = (u64)__shfl_up((unsigned long long)v[q], 1);
-            if ((lane == 0 || v[q] != prev) && v[q] != EV_EMPTY) {
-                const u64 key = v[q];
-                u32 h = (u32)ev_hash(key) & (EV_LDS - 1);
-                int probe = 0;
-                for (; probe < EV_LDS_PROBES; ++probe) {
-                    u64 k = lk[h];
-                    if (k == EV_EMPTY) {
-                        k = atomicCAS((unsigned long long*)&lk[h], (unsigned long long)EV_EMPTY, (unsigned long long)key);
-                        if (k == EV_EMPTY) {                  // new to this workgroup
-                            if (!rl_insert(keys, mask, key)) e_or |= EV_ERR_FULL;
-                            break;
-                        }
-                    }
-                    if (k == key) break;
-                    h = (h + 1) & (EV_LDS - 1);
+    u32 e_or = 0, ovf = 0;
+    u64 r0 = EV_EMPTY, r1 = EV_EMPTY;                 // this lane's last two head ids (runs alternate)
+    auto head = [&](u64 key) {
+        if (key == r0 || key == r1) return;
+        r1 = r0; r0 = key;
+        u32 h = rl_lhash(key);
+        int probe = 0;
+#pragma unroll 1
+        for (; probe < EV_LDS_PROBES; ++probe) {
+            u64 k = lk[h];
+            if (k == EV_EMPTY) {
+                k = atomicCAS((unsigned long long*)&lk[h], (unsigned long long)EV_EMPTY, (unsigned long long)key);
+                if (k == EV_EMPTY) {                  // new to this workgroup
+                    if (!rl_insert(keys, mask, key)) e_or |= EV_ERR_FULL;
+                    return;
                 }
-                if (probe == EV_LDS_PROBES && !rl_insert(keys, mask, key)) e_or |= EV_ERR_FULL;
             }
+            if (k == key) return;
+            h = (h + 1) & (EV_LDS - 1);
         }
+        ovf = 1;                                      // LDS set crowded: straight to HBM
+        if (!rl_insert(keys, mask, key)) e_or |= EV_ERR_FULL;
+    };
+    for (int64_t base = beg + (int64_t)(threadIdx.x & ~63) * RL_Q * VW; base < end; base += (int64_t)RL_WG * RL_Q * VW) {
+        RlVec<VW> x[RL_Q];
+#pragma unroll
+        for (int q = 0; q < RL_Q; ++q) x[q].load(lab, base + (q * 64 + lane) * VW, end);
+        const u32 hm = rl_heads<VW>(x, base, end, lane, e_or);
+        // one insert site for all the lane's heads (an inlined copy per voxel spilled SGPRs)
+        for (u32 m = hm; m; m &= m - 1) head(rl_pick<VW>(x, __builtin_ctz(m)));
     }
     if (e_or) atomicOr(err, e_or);
+    if (ovf) lovf = 1;
+    __syncthreads();
+    if (lovf) {
+        if (threadIdx.x == 0) WGN[blockIdx.x] = ~0u;
+        return;
+    }
+    for (int e = threadIdx.x; e < EV_LDS; e += RL_WG)
+        if (lk[e] != EV_EMPTY) WGL[(int64_t)blockIdx.x * EV_LDS + atomicAdd(&ln, 1u)] = lk[e];
+    __syncthreads();
+    if (threadIdx.x == 0) WGN[blockIdx.x] = ln;
 }
 
 __global__ __launch_bounds__(256) void k_rl_compact(const u64* __restrict__ keys, u64 cap, u64* out, u32* count) {
@@ -94,29 +169,92 @@ __global__ __launch_bounds__(256) void k_rl_assign(const u64* __restrict__ sorte
     vals[rl_slot(keys, mask, sorted[i])] = (u64)i + start;
 }
 
-// out[i] = new id of lab[i]; run heads look the id up, the rest of the run takes the head's value
-__global__ __launch_bounds__(256) void k_rl_apply(const u64* lab, int64_t n, const u64* __restrict__ keys, u64 mask,
-                                                  const u64* __restrict__ vals, u64* out) {
-    const int lane = threadIdx.x & 63;
-    const int64_t stride = (int64_t)gridDim.x * 256 * RL_Q;
-    for (int64_t base = (int64_t)blockIdx.x * 256 * RL_Q + (threadIdx.x & ~63) * RL_Q; base < n; base += stride) {
-        u64 v[RL_Q];
-#pragma unroll
-        for (int q = 0; q < RL_Q; ++q) {
-            const int64_t i = base + q * 64 + lane;
-            v[q] = i < n ? __builtin_nontemporal_load(lab + i) : EV_EMPTY;
+// out[i] = new id of lab[i] over k_rl_unique's workgroup ranges: the workgroup's id list -> LDS
+// table (id -> new id), then run heads look their id up in LDS and the rest of a run takes the
+// head's value (ballot + shuffle).  A workgroup whose LDS set overflowed looks up in HBM.
+template <int VW>
+__global__ __launch_bounds__(RL_WG) void k_rl_apply(const u64* lab, int64_t n, int64_t per_wg,
+                                                    const u64* __restrict__ keys, u64 mask,
+                                                    const u64* __restrict__ vals, const u64* __restrict__ WGL,
+                                                    const u32* __restrict__ WGN, u64* out) {
+    __shared__ u64 lk[EV_LDS], lv[EV_LDS];
+    for (int e = threadIdx.x; e < EV_LDS; e += RL_WG) lk[e] = EV_EMPTY;
+    const u32 nl = WGN[blockIdx.x];
+    const bool global = nl == ~0u;
+    __syncthreads();
+    if (!global) {
+        for (u32 e = threadIdx.x; e < nl; e += RL_WG) {
+            const u64 key = WGL[(int64_t)blockIdx.x * EV_LDS + e];
+            const u64 val = vals[rl_slot(keys, mask, key)];
+            u32 h = rl_lhash(key);
+            while (atomicCAS((unsigned long long*)&lk[h], (unsigned long long)EV_EMPTY, (unsigned long long)key) != EV_EMPTY)
+                h = (h + 1) & (EV_LDS - 1);       // the ids are distinct and nl <= EV_LDS
+            lv[h] = val;
         }
+    }
+    __syncthreads();
+    u64 mk0 = EV_EMPTY, mv0 = 0, mk1 = EV_EMPTY, mv1 = 0;   // this lane's last two (id, new id)
+    auto lookup = [&](u64 key) -> u64 {
+        if (key == mk0) return mv0;
+        if (key == mk1) return mv1;
+        u64 v = 0;
+        if (global) {
+            v = vals[rl_slot(keys, mask, key)];
+        } else {
+            u32 h = rl_lhash(key);
+            int probe = 0;
+            for (; probe < EV_LDS; ++probe) {        // always found: the list holds every id of the range
+                if (lk[h] == key) break;
+                h = (h + 1) & (EV_LDS - 1);
+            }
+            v = probe < EV_LDS ? lv[h] : vals[rl_slot(keys, mask, key)];
+        }
+        mk1 = mk0; mv1 = mv0; mk0 = key; mv0 = v;
+        return v;
+    };
+    const int lane = threadIdx.x & 63;
+    const int64_t beg = (int64_t)blockIdx.x * per_wg, end = min(n, beg + per_wg);
+    for (int64_t base = beg + (int64_t)(threadIdx.x & ~63) * RL_Q * VW; base < end; base += (int64_t)RL_WG * RL_Q * VW) {
+        RlVec<VW> x[RL_Q];
+#pragma unroll
+        for (int q = 0; q < RL_Q; ++q) x[q].load(lab, base + (q * 64 + lane) * VW, end);
+        u32 e_or = 0;
+        const u32 hm = rl_heads<VW>(x, base, end, lane, e_or);
 #pragma unroll
         for (int q = 0; q < RL_Q; ++q) {
-            const int64_t i = base + q * 64 + lane;
-            const u64 prev = (u64)__shfl_up((unsigned long long)v[q], 1);
-            const bool head = lane == 0 || v[q] != prev;
-            const u64 H = __ballot(head);
-            u64 nv = 0;
-            if (head && v[q] != EV_EMPTY) nv = vals[rl_slot(keys, mask, v[q])];
-            const int hl = 63 - __builtin_clzll(H & (lane == 63 ? ~0ull : ((2ull << lane) - 1)));
-            nv = (u64)__shfl((unsigned long long)nv, hl);
-            if (i < n) __builtin_nontemporal_store(nv, out + i);
+            const int64_t i = base + (q * 64 + lane) * VW;
+            const u32 hq = (hm >> (q * VW)) & ((1u << VW) - 1);
+            // one lookup site per group of 64 lanes
+            u64 nv[VW];
+#pragma unroll
+            for (int j = 0; j < VW; ++j) nv[j] = 0;
+            for (u32 m = hq; m; m &= m - 1) {
+                const int b = __builtin_ctz(m);
+                u64 key = x[q].v[0];
+#pragma unroll
+                for (int j = 1; j < VW; ++j) if (j == b) key = x[q].v[j];
+                const u64 v = lookup(key);
+#pragma unroll
+                for (int j = 0; j < VW; ++j) if (j == b) nv[j] = v;
+            }
+            // voxel 0 of a lane without a head there: the last value of the nearest lane below
+            // holding a head (every voxel in between has the same id)
+            const u64 H = __ballot(hq != 0);
+            const u64 below = lane ? H & ((1ull << lane) - 1) : 0ull;
+            const int hl = below ? 63 - __builtin_clzll(below) : 0;
+            u64 lastv = 0;
+#pragma unroll
+            for (int j = 0; j < VW; ++j) if ((hq >> j) & 1u) lastv = nv[j];
+            const u64 from = (u64)__shfl((unsigned long long)lastv, hl);
+#pragma unroll
+            for (int j = 0; j < VW; ++j)
+                if (!((hq >> j) & 1u)) nv[j] = j ? nv[j - 1] : from;
+            if constexpr (VW == 2) {
+                if (i + 1 < end) __builtin_nontemporal_store(rl_u64x2{nv[0], nv[1]}, reinterpret_cast<rl_u64x2*>(out + i));
+                else if (i < end) out[i] = nv[0];
+            } else {
+                if (i < end) __builtin_nontemporal_store(nv[0], out + i);
+            }
         }
     }
 }
@@ -134,11 +272,15 @@ int cc_relabel_consecutive(cc_ctx* c, const uint64_t* labels, uint64_t* out, int
         *n_unique = 0;
         *start_label = 1;
         if (n == 0) return 0;
-        const unsigned grid = std::min<unsigned>(4096, grid_stride((n + RL_Q - 1) / RL_Q));
-        // k_rl_unique: contiguous ranges of whole 256 * RL_Q steps, ~8192 workgroups
-        const int64_t step = 256 * RL_Q, steps = (n + step - 1) / step;
+        // both passes: contiguous ranges of whole RL_WG * RL_Q * VW steps, ~8192 workgroups;
+        // 16-B accesses when both arrays are 16-B aligned
+        const bool vw2 = ((uintptr_t)labels % 16 == 0) && ((uintptr_t)out % 16 == 0);
+        const int64_t step = (int64_t)RL_WG * RL_Q * (vw2 ? 2 : 1), steps = (n + step - 1) / step;
         const int64_t per_wg = ((steps + 8191) / 8192) * step;
         const unsigned ugrid = (unsigned)((n + per_wg - 1) / per_wg);
+        c->rl_wg.ensure((size_t)ugrid * (EV_LDS * sizeof(u64) + sizeof(u32)));
+        u64* WGL = c->rl_wg.as<u64>();
+        u32* WGN = reinterpret_cast<u32*>(WGL + (size_t)ugrid * EV_LDS);
         c->counter.ensure(2 * sizeof(u32));
         int64_t cap = std::max<int64_t>(c->rl_cap, 1 << 16);   // grown tables are kept for the next call
         for (;;) {
@@ -148,7 +290,10 @@ int cc_relabel_consecutive(cc_ctx* c, const uint64_t* labels, uint64_t* out, int
             HIP_OK(hipMemsetAsync(keys, 0xFF, cap * sizeof(u64), s));
             HIP_OK(hipMemsetAsync(c->counter.p, 0, 2 * sizeof(u32), s));
             u32* err = c->counter.as<u32>();
-            launch(c, "k_rl_unique", [&] { k_rl_unique<<<ugrid, 256, 0, s>>>(labels, n, per_wg, keys, (u64)cap - 1, err); });
+            launch(c, "k_rl_unique", [&] {
+                if (vw2) k_rl_unique<2><<<ugrid, RL_WG, 0, s>>>(labels, n, per_wg, keys, (u64)cap - 1, err, WGL, WGN);
+                else k_rl_unique<1><<<ugrid, RL_WG, 0, s>>>(labels, n, per_wg, keys, (u64)cap - 1, err, WGL, WGN);
+            });
             u32 h[2] = {0, 0};
             c->ev_gt.ensure(cap * 2 * sizeof(u64));      // compacted ids | sorted ids
             u64* comp = c->ev_gt.as<u64>();
@@ -182,7 +327,10 @@ int cc_relabel_consecutive(cc_ctx* c, const uint64_t* labels, uint64_t* out, int
             launch(c, "k_rl_assign", [&] {
                 k_rl_assign<<<grid1d(nu), 256, 0, s>>>(sorted, nu, start, keys, (u64)cap - 1, vals);
             });
-            launch(c, "k_rl_apply", [&] { k_rl_apply<<<grid, 256, 0, s>>>(labels, n, keys, (u64)cap - 1, vals, out); });
+            launch(c, "k_rl_apply", [&] {
+                if (vw2) k_rl_apply<2><<<ugrid, RL_WG, 0, s>>>(labels, n, per_wg, keys, (u64)cap - 1, vals, WGL, WGN, out);
+                else k_rl_apply<1><<<ugrid, RL_WG, 0, s>>>(labels, n, per_wg, keys, (u64)cap - 1, vals, WGL, WGN, out);
+            });
             if (uniques_host && cap_host > 0)
                 HIP_OK(hipMemcpyAsync(uniques_host, sorted, std::min<int64_t>(cap_host, nu) * sizeof(u64),
                                       hipMemcpyDeviceToHost, s));

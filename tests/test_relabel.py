@@ -16,7 +16,7 @@ def test_oracle_start_label():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('case', ['zeros_runs', 'no_zero_sparse', 'many_ids', 'tiny'])
+@pytest.mark.parametrize('case', ['zeros_runs', 'no_zero_sparse', 'many_ids', 'tiny', 'runs_big', 'unaligned_odd'])
 def test_gpu_relabel_matches_oracle(ctx, case):
     import torch
     rng = np.random.default_rng(5)
@@ -27,10 +27,19 @@ def test_gpu_relabel_matches_oracle(ctx, case):
         lab[:, :, :30] = lab[0, 0, 0]
     elif case == 'many_ids':       # > the first table (2^16 slots)
         lab = rng.integers(0, 1 << 40, size=(16, 128, 128), dtype=np.int64).astype(np.uint64)
+    elif case == 'runs_big':       # several workgroup ranges, runs crossing lanes and ranges
+        lab = np.repeat(rng.integers(0, 3000, size=(40, 64, 32)), 37, axis=2).astype(np.uint64)
+    elif case == 'unaligned_odd':  # 8-B but not 16-B aligned, odd length: the one-id-per-lane path
+        lab = np.repeat(rng.integers(0, 900, size=(9, 31, 29)), 3, axis=2).astype(np.uint64)
     else:
         lab = np.array([[[3]]], dtype=np.uint64)
     want, wa = R.relabel_consecutive(lab)
     d = torch.from_numpy(lab.view(np.int64)).cuda()
+    if case == 'unaligned_odd':
+        buf = torch.empty(d.numel() + 1, dtype=torch.int64, device='cuda')
+        buf[1:] = d.reshape(-1)
+        d = buf[1:].view(d.shape)
+        assert d.data_ptr() % 16 == 8
     out, table = ctx.relabel_consecutive(d)
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), want)
     np.testing.assert_array_equal(table, wa)
