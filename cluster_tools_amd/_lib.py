@@ -24,8 +24,11 @@ EXPORTS = (
     'cc_get_profile', 'cc_reset_profile', 'cc_shard_begin', 'cc_shard_assign', 'cc_shard_planes',
     'cc_seam_pairs', 'cc_shard_finish', 'cc_set_debug', 'cc_threshold', 'cc_shard_top_plane32',
     'cc_seam_pairs32', 'cc_shard_top_cubes32', 'cc_seam_pairs_cubes32',
-    'cc_evaluate', 'cc_get_overlaps', 'cc_relabel_consecutive', 'cc_set_option',
+    'cc_evaluate', 'cc_get_overlaps', 'cc_relabel_consecutive', 'cc_set_option', 'cc_channel_mean',
 )
+# CC_DTYPE_* of include/cc_mi355x.h (cc_channel_mean)
+DTYPES = {'float32': 0, 'float64': 1, 'uint8': 2, 'int8': 3, 'uint16': 4, 'int16': 5, 'uint32': 6,
+          'int32': 7, 'uint64': 8, 'int64': 9}
 # every symbol include/cc_n5.h declares (libcc_n5.so: host-only N5 codec)
 N5_LIB_PATH = os.path.join(_HERE, 'lib', 'libcc_n5.so')
 N5_EXPORTS = ('cc_n5_version', 'cc_n5_last_error', 'cc_n5_read', 'cc_n5_write')
@@ -107,6 +110,7 @@ def load():
         'cc_evaluate': (I, [P, P, P, P, P, I, u64, ctypes.POINTER(CCEvalResult)]),
         'cc_get_overlaps': (i64, [P, P, P, P, i64]),
         'cc_relabel_consecutive': (I, [P, P, P, i64, P, P, P, i64]),
+        'cc_channel_mean': (I, [P, P, I, P, P, i64, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -252,6 +256,41 @@ class Context:
             _check(L.cc_label_volume_host(self._h, _ptr(inp), _ptr(mask), _ptr(shape), _ptr(bs),
                                           float(threshold), mode_id(mode), _ptr(out), ctypes.byref(res)))
         return out, res.as_dict()
+
+    def torch_device(self):
+        import torch
+        return torch.device('cuda', self.device)
+
+    def channel_mean(self, inp4, channel, out=None, shape4=None, dtype=None):
+        """Multi-channel input (block_components.py:150-159, threshold.py:139-148): the mean of
+        the listed channels of a (C, Z, Y, X) volume as the float32 (Z, Y, X) CUDA tensor the
+        reference normalizes (np.mean(axis=0) accumulation: float32 for float32 input, float64
+        otherwise).  `inp4` is a contiguous CUDA tensor, a CUDA byte tensor holding the raw
+        (C, Z, Y, X) data of numpy dtype `dtype` and shape `shape4` (unsigned dtypes need no torch
+        support), or a numpy array (uploaded as raw bytes); `channel` is an int or a list of ints
+        (order and repeats kept)."""
+        import torch
+        if shape4 is not None:
+            assert hasattr(inp4, 'data_ptr') and inp4.is_cuda and inp4.is_contiguous()
+            dt, shape, dev, buf = np.dtype(dtype).name, tuple(int(v) for v in shape4), inp4.device, inp4
+            assert len(shape) == 4 and inp4.numel() * inp4.element_size() == int(np.prod(shape)) * np.dtype(dtype).itemsize
+        elif hasattr(inp4, 'data_ptr'):
+            assert inp4.is_cuda and inp4.is_contiguous() and inp4.dim() == 4
+            dt, shape, dev, buf = str(inp4.dtype).replace('torch.', ''), tuple(inp4.shape), inp4.device, inp4
+        else:
+            a = np.ascontiguousarray(inp4)
+            assert a.ndim == 4
+            dt, shape, dev = a.dtype.name, a.shape, torch.device('cuda', self.device)
+            buf = torch.from_numpy(a.reshape(-1).view(np.uint8)).to(dev)
+        if dt not in DTYPES:
+            raise TypeError('channel_mean: unsupported dtype %s' % dt)
+        chans = _i64([channel] if isinstance(channel, (int, np.integer)) else list(channel))
+        if out is None:
+            out = torch.empty(shape[1:], dtype=torch.float32, device=dev)
+        assert out.dtype == torch.float32 and tuple(out.shape) == tuple(shape[1:]) and out.is_contiguous()
+        _check(load().cc_channel_mean(self._h, _ptr(buf), DTYPES[dt], _ptr(_i64(shape)), _ptr(chans),
+                                      len(chans), _ptr(out)))
+        return out
 
     def threshold(self, inp, block_shape, threshold, mode='greater', out=None):
         """Threshold task (threshold.py:131-171): per-block normalize + compare -> uint8.

@@ -846,3 +846,4 @@ int cc_get_profile(cc_ctx* c, char* names, int names_cap, int64_t* counts, doubl
 #include "cc_stage_host.hip"
 #include "cc_eval.hip"
 #include "cc_relabel.hip"
+#include "cc_prefilter.hip"

@@ -79,9 +79,15 @@ class BlockComponentsBase(Task):
         chunks = config.pop('chunks', None)
         if chunks is None:
             chunks = tuple(bs // 2 for bs in block_shape)
-        if self.channel is not None:
-            raise NotImplementedError('channel != None (4-D input) is not supported on the MI355X path')
-        assert len(shape) == 3, str(len(shape))
+        if self.channel is None:
+            assert len(shape) == 3, str(len(shape))
+        else:
+            # 4-D (C, Z, Y, X) input: the listed channels are averaged (block_components.py:75-89)
+            assert len(shape) == 4, str(len(shape))
+            chans = channel_list(self.channel)
+            assert all(0 <= c < shape[0] for c in chans), (shape[0], chans)
+            shape = shape[1:]
+            config.update({'channel': self.channel})
         if config.get('sigma_prefilter', 0) > 0:
             raise NotImplementedError('sigma_prefilter > 0 is not supported on the MI355X path')
         chunks = tuple(max(1, min(ch, sh)) for ch, sh in zip(chunks, shape))
@@ -121,6 +127,45 @@ def _read(path, key, box=None, dtype=None):
     return a if dtype is None else a.astype(dtype, copy=False)
 
 
+def channel_list(channel):
+    """The reference's `channel` (int or list of ints, block_components.py:152) as a list; a
+    JSON / luigi round trip may hand it over as a string."""
+    if isinstance(channel, str):
+        channel = json.loads(channel)
+    if isinstance(channel, (int, np.integer)):
+        return [int(channel)]
+    return [int(c) for c in channel]
+
+
+def read_input(config, box=None):
+    """Host side of the job input: the float32 volume (3-D input; normalize's astype('float32'),
+    volume_utils.py:99, done on the host), or for 4-D input with config['channel'] the distinct
+    listed channels of the region in the dataset's dtype plus the list as indices into that stack
+    (averaged on the device by to_device)."""
+    channel = config.get('channel')
+    if channel is None:
+        return _read(config['input_path'], config['input_key'], box, dtype=np.float32), None
+    chans = channel_list(channel)
+    distinct = sorted(set(chans))
+    with vu.file_reader(config['input_path'], 'r') as f:
+        ds = f[config['input_key']]
+        ds.n_threads = _n_threads()
+        box = box or [(0, s) for s in ds.shape[1:]]
+        stack = np.empty((len(distinct),) + tuple(e - b for b, e in box), dtype=ds.dtype)
+        for i, c in enumerate(distinct):
+            stack[i] = ds.read_region([(c, c + 1)] + list(box))[0]
+    return stack, [distinct.index(c) for c in chans]
+
+
+def to_device(ctx, host, chans, dev):
+    """float32 device volume for the labelling: upload, and for a channel stack the mean of the
+    listed channels (cc_channel_mean: np.mean(axis=0) as block_components.py:150-159 does it)."""
+    import torch
+    if chans is None:
+        return torch.from_numpy(host).to(dev)
+    return ctx.channel_mean(host, chans)
+
+
 def _write_output(config, labels, box, n_threads=None):
     """Final / block-local labels into the output dataset.  Chunks of empty blocks are not
     created (the reference skips empty blocks, block_components.py:175-177, and they read as 0)."""
@@ -149,7 +194,7 @@ def _fused_single(config, shape, nb):
     from cluster_tools_amd import _lib
     timing = {'voxels': int(np.prod(shape)), 'gpus': 1}
     t = time.perf_counter()
-    inp = _read(config['input_path'], config['input_key'], dtype=np.float32)
+    inp, chans = read_input(config)
     mask = None
     if config.get('mask_path', ''):
         vu.load_mask(config['mask_path'], config['mask_key'], shape)
@@ -158,16 +203,22 @@ def _fused_single(config, shape, nb):
     device = int(os.environ.get('CC_DEVICE', '0'))
     dev = torch.device('cuda', device)
     torch.cuda.set_device(dev)
-    t = time.perf_counter()
-    x = torch.from_numpy(inp).to(dev)
-    m = None if mask is None else torch.from_numpy(mask).to(dev)
-    torch.cuda.synchronize(dev)
-    timing['h2d_s'] = time.perf_counter() - t
-    del inp, mask
     with _lib.Context(device) as ctx:
         ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         ctx.set_empty_job_quirk(config.get('quirk_jobs', 0))
         t = time.perf_counter()
+        if chans is None:
+            x = torch.from_numpy(inp).to(dev)
+        else:
+            x = torch.from_numpy(inp.reshape(-1).view(np.uint8)).to(dev)
+        m = None if mask is None else torch.from_numpy(mask).to(dev)
+        torch.cuda.synchronize(dev)
+        timing['h2d_s'] = time.perf_counter() - t
+        stack_shape, stack_dtype = inp.shape, inp.dtype
+        del inp, mask
+        t = time.perf_counter()
+        if chans is not None:
+            x = ctx.channel_mean(x, chans, shape4=stack_shape, dtype=stack_dtype)
         labels_dev, res = ctx.label_volume(x, config['block_shape'], config['threshold'],
                                            config['threshold_mode'], m)
         torch.cuda.synchronize(dev)
@@ -250,6 +301,8 @@ def block_components(job_id, config_path):
     fused = config.get('fused', False)
     fu.log('Applying threshold %f with mode %s' % (threshold, mode))
     shape = tuple(vu.get_shape(config['input_path'], config['input_key']))
+    if config.get('channel') is not None:
+        shape = shape[1:]
     nb = vu.Blocking([0, 0, 0], list(shape), block_shape).numberOfBlocks
 
     if fused:
@@ -261,14 +314,14 @@ def block_components(job_id, config_path):
     else:
         import torch
         from cluster_tools_amd import _lib
-        inp = _read(config['input_path'], config['input_key'], dtype=np.float32)
+        inp, chans = read_input(config)
         mask = None
         if config.get('mask_path', ''):
             vu.load_mask(config['mask_path'], config['mask_key'], shape)
             mask = (_read(config['mask_path'], config['mask_key']) != 0).astype(np.uint8)
         with _lib.Context(int(os.environ.get('CC_DEVICE', '0'))) as ctx:
-            x = torch.from_numpy(inp).cuda()
-            m = None if mask is None else torch.from_numpy(mask).cuda()
+            x = to_device(ctx, inp, chans, ctx.torch_device())
+            m = None if mask is None else torch.from_numpy(mask).to(x.device)
             lab_dev, values = ctx.block_components(x, block_shape, threshold, mode, m)
             labels = lab_dev.cpu().numpy().view(np.uint64)
         _write_output(config, labels, [(0, s) for s in shape])

@@ -40,6 +40,8 @@ def main(config_path, out_dir):
         dist.init_process_group(backend)
 
     shape = tuple(vu.get_shape(config['input_path'], config['input_key']))
+    if config.get('channel') is not None:
+        shape = shape[1:]            # 4-D (C, Z, Y, X) input, channels averaged on the device
     bs = tuple(config['block_shape'])
     bounds = slab_bounds(shape[0], bs[0], world)
     z0, zs = bounds[rank]
@@ -48,20 +50,27 @@ def main(config_path, out_dir):
     timing = {}
 
     t = time.perf_counter()
-    inp = bc._read(config['input_path'], config['input_key'], box, dtype=np.float32)
+    inp, chans = bc.read_input(config, box)
     mask = None
     if config.get('mask_path', ''):
         vu.load_mask(config['mask_path'], config['mask_key'], shape)
         mask = (bc._read(config['mask_path'], config['mask_key'], box) != 0).astype(np.uint8)
     timing['n5_read_s'] = time.perf_counter() - t
     t = time.perf_counter()
-    x = torch.from_numpy(inp).to(dev)
+    x = torch.from_numpy(inp if chans is None else inp.reshape(-1).view(np.uint8)).to(dev)
     m = None if mask is None else torch.from_numpy(mask).to(dev)
     torch.cuda.synchronize(dev)
     timing['h2d_s'] = time.perf_counter() - t
+    stack_shape, stack_dtype = inp.shape, inp.dtype
     del inp, mask
 
     ctx = _lib.Context(gpu)
+    if chans is not None:
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        t = time.perf_counter()
+        x = ctx.channel_mean(x, chans, shape4=stack_shape, dtype=stack_dtype)
+        torch.cuda.synchronize(dev)
+        timing['channel_mean_s'] = time.perf_counter() - t
     comm = StagedComm(device=dev) if backend != 'nccl' else None
     lab = ShardedLabeler(ctx, shape, bs, z0, zs, dev, comm=comm)
     out = torch.empty(tuple(x.shape), dtype=torch.int64, device=dev)

@@ -7,7 +7,8 @@ output_path / output_key / threshold / threshold_mode / channel / dependency, th
 clipped to the shape, the job config per LocalTask and the "processed job" log contract.  The
 job's compute (per-block normalize + float32 compare, threshold.py:131-171) runs on the MI355X
 through cc_threshold (k_block_stats -> k_block_params -> k_threshold); one GPU job thresholds
-the whole volume and writes the listed blocks.  channel (4-D input) and sigma_prefilter > 0 are
+the whole volume and writes the listed blocks.  channel (4-D input): the listed channels are
+averaged on the device first (cc_channel_mean, threshold.py:139-148).  sigma_prefilter > 0 is
 rejected, as for BlockComponents.
 """
 import json
@@ -60,9 +61,14 @@ class ThresholdBase(Task):
         chunks = config.pop('chunks', None)
         if chunks is None:
             chunks = tuple(bs // 2 for bs in block_shape)
-        if self.channel is not None:
-            raise NotImplementedError('channel != None (4-D input) is not supported on the MI355X path')
-        assert len(shape) == 3, str(len(shape))
+        if self.channel is None:
+            assert len(shape) == 3, str(len(shape))
+        else:
+            assert len(shape) == 4, str(len(shape))
+            from cluster_tools_amd.thresholded_components.block_components import channel_list
+            assert all(0 <= c < shape[0] for c in channel_list(self.channel)), (shape[0], self.channel)
+            shape = shape[1:]
+            config.update({'channel': self.channel})
         if config.get('sigma_prefilter', 0) > 0:
             raise NotImplementedError('sigma_prefilter > 0 is not supported on the MI355X path')
         chunks = tuple(max(1, min(ch, sh)) for ch, sh in zip(chunks, shape))
@@ -92,11 +98,12 @@ def threshold(job_id, config_path):
     block_shape = config['block_shape']
     thr, mode = config['threshold'], config['threshold_mode']
     fu.log('Applying threshold %f with mode %s' % (thr, mode))
-    with vu.file_reader(config['input_path'], 'r') as f:
-        inp = np.ascontiguousarray(f[config['input_key']][:], dtype=np.float32)
-    shape = inp.shape
+    from cluster_tools_amd.thresholded_components.block_components import read_input, to_device
+    inp, chans = read_input(config)
+    shape = inp.shape if chans is None else inp.shape[1:]
     with _lib.Context(int(os.environ.get('CC_DEVICE', '0'))) as ctx:
-        out = ctx.threshold(torch.from_numpy(inp).cuda(), block_shape, thr, mode).cpu().numpy()
+        x = to_device(ctx, inp, chans, ctx.torch_device())
+        out = ctx.threshold(x, block_shape, thr, mode).cpu().numpy()
     blocking = vu.Blocking([0, 0, 0], list(shape), block_shape)
     with vu.file_reader(config['output_path']) as f:
         ds = f[config['output_key']]

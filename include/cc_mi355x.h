@@ -104,9 +104,28 @@ int cc_block_components(cc_ctx* ctx, const float* in_dev, const uint8_t* mask_de
 /* Threshold task (thresholded_components/threshold.py:131-171, _threshold_block): per
  * reference block normalize (volume_utils.py:98-105) then `> / < / ==` threshold (float32), the
  * result as uint8 0/1 of the same shape.  in_dev / out_dev are device pointers (C-order).
- * channel / sigma_prefilter are not supported (rejected by the Python task). */
+ * Multi-channel input: cc_channel_mean first. */
 int cc_threshold(cc_ctx* ctx, const float* in_dev, const int64_t shape[3], const int64_t block_shape[3],
                  double threshold, int mode, uint8_t* out_dev);
+
+/* Multi-channel input (the `channel` parameter of BlockComponents / Threshold,
+ * block_components.py:150-159, threshold.py:139-148): out_dev[Z*Y*X] (float32) = the mean of the
+ * listed channels of in_dev (C, Z, Y, X) = shape4, in list order (repeats allowed), computed as
+ * np.mean(stack, axis=0) in the reference: sequential sum over the list, float32 accumulation and
+ * division for float32 input, float64 for every other dtype, then the cast to float32 of
+ * vu.normalize (volume_utils.py:99).  The result feeds cc_label_volume / cc_threshold. */
+#define CC_DTYPE_FLOAT32 0
+#define CC_DTYPE_FLOAT64 1
+#define CC_DTYPE_UINT8   2
+#define CC_DTYPE_INT8    3
+#define CC_DTYPE_UINT16  4
+#define CC_DTYPE_INT16   5
+#define CC_DTYPE_UINT32  6
+#define CC_DTYPE_INT32   7
+#define CC_DTYPE_UINT64  8
+#define CC_DTYPE_INT64   9
+int cc_channel_mean(cc_ctx* ctx, const void* in_dev, int dtype, const int64_t shape4[4],
+                    const int64_t* channels, int64_t n_channels, float* out_dev);
 
 /* merge_offsets (merge_offsets.py:104-120): exclusive scan of values; writes offsets
  * and empty flags; returns n_labels through *n_labels. Host arrays. */

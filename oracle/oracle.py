@@ -222,3 +222,21 @@ def threshold_volume(inp, block_shape, threshold, mode='greater'):
                         raise RuntimeError('Thresholding Mode %s not supported' % mode)
                     out[bb] = r.astype(np.uint8)
     return out
+
+
+def channel_mean(inp4, channel):
+    """Multi-channel input restated (TEST INFRASTRUCTURE ONLY): the selected channels of a
+    (C, Z, Y, X) array averaged as block_components.py:150-159 / threshold.py:139-148 do it --
+    np.mean(axis=0) of a stack in the dataset's dtype.  numpy reduces over the outer axis
+    element by element in channel-list order (sum_0 = x_c0, sum_k = sum_{k-1} + x_ck), in float32
+    for float32 input and in float64 for integer / float64 input, then divides by the channel
+    count in that type; vu.normalize (volume_utils.py:99) casts the mean to float32 after.
+    Written as explicit loops so the order is stated, not inherited from np.mean."""
+    x = np.asarray(inp4)
+    chans = [channel] if isinstance(channel, (int, np.integer)) else [int(c) for c in channel]
+    acc_t = np.float32 if x.dtype == np.float32 else np.float64
+    acc = x[chans[0]].astype(acc_t)
+    for c in chans[1:]:
+        acc = (acc + x[c].astype(acc_t)).astype(acc_t)
+    acc = (acc / acc_t(len(chans))).astype(acc_t)
+    return acc.astype(np.float32)

@@ -86,8 +86,10 @@ def n_blocks_of(shape, block_shape):
     return int(np.prod([-(-s // b) for s, b in zip(shape, block_shape)]))
 
 
-def run_reference(inp, block_shape, threshold, mode, mask=None, n_jobs_bc=2, n_jobs_bf=1):
-    """Run the five reference stages in a scratch folder; return artefacts."""
+def run_reference(inp, block_shape, threshold, mode, mask=None, n_jobs_bc=2, n_jobs_bf=1, channel=None):
+    """Run the five reference stages in a scratch folder; return artefacts.  channel (int or
+    list): inp is 4-D (C, Z, Y, X) and block_components averages those channels
+    (block_components.py:150-159)."""
     tmp = tempfile.mkdtemp(prefix='golden_')
     try:
         in_path = os.path.join(tmp, 'in.h5')
@@ -96,7 +98,7 @@ def run_reference(inp, block_shape, threshold, mode, mask=None, n_jobs_bc=2, n_j
             f.create_dataset('raw', data=inp)
             if mask is not None:
                 f.create_dataset('mask', data=mask)
-        shape = inp.shape
+        shape = inp.shape if channel is None else inp.shape[1:]
         # output dataset as BlockComponentsBase.run_impl creates it (block_components.py:99-106)
         chunks = tuple(max(1, min(bs // 2, sh)) for bs, sh in zip(block_shape, shape))
         with h5py.File(out_path, 'w') as f:
@@ -121,6 +123,8 @@ def run_reference(inp, block_shape, threshold, mode, mask=None, n_jobs_bc=2, n_j
                'threshold': float(threshold), 'threshold_mode': mode}
         if mask is not None:
             cfg.update({'mask_path': in_path, 'mask_key': 'mask'})
+        if channel is not None:
+            cfg['channel'] = channel
         for j, p in enumerate(job_cfgs('block_components', n_bc, cfg)):
             ref_bc.block_components(j, p)
         # per-block values v_i (n_i + 1 or 0) before merge_offsets deletes the files

@@ -124,6 +124,46 @@ __global__ __launch_bounds__(512) void wr_tile_w(unsigned long long* __restrict_
     }
 }
 
+// tile shape sweep: TZ x TY x 64 tiles (TZ * TY = 512 rows, 256 KB of uint64 per workgroup), the
+// k_pass2 thread mapping (cube = 2 x 2 voxel rows x 2 voxels, 16-B stores); ZORD: tiles walked
+// z-fastest instead of x-fastest
+template <int TZ, int TY, bool ZORD = false>
+__global__ __launch_bounds__(512) void wr_tile_s(unsigned long long* __restrict__ out, int64_t Y, int64_t X, int ntx,
+                                                 int nty, int ntz) {
+    const int t = blockIdx.x;
+    int tx, ty, tz;
+    if (ZORD) { tz = t % ntz; ty = (t / ntz) % nty; tx = t / (ntz * nty); }
+    else { tx = t % ntx; ty = (t / ntx) % nty; tz = t / (ntx * nty); }
+    constexpr int CYN = TY / 2, NC = (TZ / 2 > 0 ? TZ / 2 : 1) * CYN * 32;
+    for (int c = threadIdx.x; c < NC; c += 512) {
+        const int cz = c / (CYN * 32), cy = (c / 32) % CYN, cx = c % 32;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const int z = (TZ == 1 ? 0 : 2 * cz + (d >> 1)), y = 2 * cy + (d & 1);
+            if (TZ == 1 && (d >> 1)) continue;
+            const int64_t idx = (((int64_t)tz * TZ + z) * Y + (int64_t)ty * TY + y) * X + tx * 64 + 2 * cx;
+            *reinterpret_cast<ulonglong2*>(out + idx) = make_ulonglong2((unsigned long long)c, (unsigned long long)d);
+        }
+    }
+}
+
+// read-side sweep: float4 lanes over TZ x TY x 64 tiles (k_spec's load shape)
+template <int TZ, int TY>
+__global__ __launch_bounds__(512) void rd_tile4_s(const float* __restrict__ in, int64_t Y, int64_t X, int ntx, int nty,
+                                                  float* out) {
+    const int t = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int tx = t % ntx, ty = (t / ntx) % nty, tz = t / (ntx * nty);
+    float mx = -1e30f;
+    // 512 rows of 64 floats; one load instruction = 4 rows (16 lanes each); wave w takes row groups w, w + 8, ...
+    for (int gi = wave; gi < TZ * TY / 4; gi += 8) {
+        const int row = gi * 4 + (lane >> 4), z = row / TY, y = row % TY;
+        const float4 v = *reinterpret_cast<const float4*>(in + (((int64_t)tz * TZ + z) * Y + (int64_t)ty * TY + y) * X +
+                                                          tx * 64 + 4 * (lane & 15));
+        mx = fmaxf(mx, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+    }
+    if (mx == 1234.5f) out[0] = mx;
+}
+
 template <class F>
 static double time_ms(hipStream_t s, int iters, F&& f) {
     hipEvent_t a, b;
@@ -177,6 +217,24 @@ int main(int argc, char** argv) {
     r.push_back({"wr_tile", time_ms(s, iters, [&] { wr_tile<<<nt, 512, 0, s>>>(out, Y, X, ntx, nty); })});
     r.push_back({"wr_tile_w2", time_ms(s, iters, [&] { wr_tile_w<2><<<nt / 2, 512, 0, s>>>(out, Y, X, ntx, nty); })});
     r.push_back({"wr_tile_w4", time_ms(s, iters, [&] { wr_tile_w<4><<<nt / 4, 512, 0, s>>>(out, Y, X, ntx, nty); })});
+    const int64_t nrow = (Y / 64) * 0 + 1;
+    (void)nrow;
+#define WS(TZ, TY, ZO, NAME)                                                                                        \
+    r.push_back({NAME, time_ms(s, iters, [&] {                                                                      \
+                     wr_tile_s<TZ, TY, ZO><<<nt, 512, 0, s>>>(out, Y, X, ntx, (int)(Y / TY), (int)(Z / TZ));        \
+                 })});
+    WS(16, 32, false, "wr_s16x32")
+    WS(16, 32, true, "wr_s16x32_zord")
+    WS(8, 64, false, "wr_s8x64")
+    WS(4, 128, false, "wr_s4x128")
+    WS(2, 256, false, "wr_s2x256")
+    WS(1, 512, false, "wr_s1x512")
+#define RS(TZ, TY, NAME)                                                                                            \
+    r.push_back({NAME, time_ms(s, iters, [&] { rd_tile4_s<TZ, TY><<<nt, 512, 0, s>>>(in, Y, X, ntx, (int)(Y / TY), dummy); })});
+    RS(16, 32, "rd_s16x32")
+    RS(8, 64, "rd_s8x64")
+    RS(4, 128, "rd_s4x128")
+    RS(1, 512, "rd_s1x512")
     std::printf("{\"shape\": [%lld, %lld, %lld]", (long long)Z, (long long)Y, (long long)X);
     for (auto& kv : r) std::printf(", \"%s\": %.4f", kv.first.c_str(), kv.second);
     std::printf("}\n");
