@@ -25,6 +25,7 @@ EXPORTS = (
     'cc_seam_pairs', 'cc_shard_finish', 'cc_set_debug', 'cc_threshold', 'cc_shard_top_plane32',
     'cc_seam_pairs32', 'cc_shard_top_cubes32', 'cc_seam_pairs_cubes32',
     'cc_evaluate', 'cc_get_overlaps', 'cc_relabel_consecutive', 'cc_set_option', 'cc_channel_mean',
+    'cc_gaussian_smooth_blocks', 'cc_gaussian_taps',
 )
 # CC_DTYPE_* of include/cc_mi355x.h (cc_channel_mean)
 DTYPES = {'float32': 0, 'float64': 1, 'uint8': 2, 'int8': 3, 'uint16': 4, 'int16': 5, 'uint32': 6,
@@ -111,6 +112,8 @@ def load():
         'cc_get_overlaps': (i64, [P, P, P, P, i64]),
         'cc_relabel_consecutive': (I, [P, P, P, i64, P, P, P, i64]),
         'cc_channel_mean': (I, [P, P, I, P, P, i64, P]),
+        'cc_gaussian_smooth_blocks': (I, [P, P, P, P, ctypes.c_double, P]),
+        'cc_gaussian_taps': (I, [ctypes.c_double, P, I]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -154,6 +157,13 @@ def _check_n5(rc):
 
 def version():
     return load().cc_version().decode()
+
+
+def gaussian_taps(sigma):
+    """The 2r + 1 float32 taps of the sigma_prefilter kernel (cc_gaussian_taps)."""
+    buf = np.zeros(129, dtype=np.float32)
+    r = _check(load().cc_gaussian_taps(float(sigma), _ptr(buf), len(buf)))
+    return buf[:2 * r + 1].copy()
 
 
 def check_provenance():
@@ -290,6 +300,20 @@ class Context:
         assert out.dtype == torch.float32 and tuple(out.shape) == tuple(shape[1:]) and out.is_contiguous()
         _check(load().cc_channel_mean(self._h, _ptr(buf), DTYPES[dt], _ptr(_i64(shape)), _ptr(chans),
                                       len(chans), _ptr(out)))
+        return out
+
+    def gaussian_smooth_blocks(self, inp, block_shape, sigma, out=None):
+        """sigma_prefilter (block_components.py:160-163): per block normalize + Gaussian smoothing
+        (vigra.filters.gaussianSmoothing restated, reflected block borders) of a float32 CUDA
+        volume; the labelling / threshold calls apply the second normalize.  out may be inp."""
+        import torch
+        assert hasattr(inp, 'data_ptr') and inp.is_cuda and inp.dtype == torch.float32 and inp.is_contiguous()
+        shape, bs = _i64(inp.shape), _i64(block_shape)
+        assert len(shape) == 3 and len(bs) == 3
+        if out is None:
+            out = torch.empty_like(inp)
+        assert out.dtype == torch.float32 and out.shape == inp.shape and out.is_contiguous()
+        _check(load().cc_gaussian_smooth_blocks(self._h, _ptr(inp), _ptr(shape), _ptr(bs), float(sigma), _ptr(out)))
         return out
 
     def threshold(self, inp, block_shape, threshold, mode='greater', out=None):

@@ -57,7 +57,8 @@ struct cc_ctx {
         values, offsets, lut, cub_tmp, scalars, scalars2, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2,
         flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf, spec, mark, bflag,
         ev_main, ev_z, ev_seg, ev_gt, ev_flag, ev_part,   // evaluation (cc_eval.hip)
-        rl_wg;                                            // relabel: per-workgroup id lists
+        rl_wg,                                            // relabel: per-workgroup id lists
+        gs1, gs2, gs_tab;                                 // Gaussian prefilter temporaries (cc_prefilter.hip)
     int64_t ev_cap = 0;      // entries per evaluation hash table of the last cc_evaluate
     int64_t rl_cap = 0;      // id-set slots of the last cc_relabel_consecutive
     // last run
@@ -649,7 +650,8 @@ void cc_destroy(cc_ctx* c) {
                       &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
                       &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec, &c->mark, &c->bflag,
-                      &c->ev_main, &c->ev_z, &c->ev_seg, &c->ev_gt, &c->ev_flag, &c->ev_part, &c->rl_wg};
+                      &c->ev_main, &c->ev_z, &c->ev_seg, &c->ev_gt, &c->ev_flag, &c->ev_part, &c->rl_wg,
+                      &c->gs1, &c->gs2, &c->gs_tab};
     for (DevBuf* b : bufs) b->release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);

@@ -106,3 +106,271 @@ int cc_channel_mean(cc_ctx* c, const void* in_dev, int dtype, const int64_t shap
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// sigma_prefilter (block_components.py:161-163, threshold.py:151-153): per block
+//   vu.normalize -> vu.apply_filter(., 'gaussianSmoothing', sigma) -> vu.normalize
+// The reference filters each block on its own (no halo).  Its filter is fastfilters' or, when
+// fastfilters is absent, vigra.filters.gaussianSmoothing (volume_utils.py:13-18, 80-94); neither
+// library is available here, so the arithmetic below restates vigra's separable Gaussian
+// (Kernel1D::initGaussian + separableConvolveMultiArray with BORDER_TREATMENT_REFLECT) in float32
+// as oracle/oracle.py:gaussian_smooth_blocks does: taps g(x) = norm * exp(x^2 * (-0.5/s/s)) for
+// x = -r..r, r = (int)(3 sigma + 0.5) (>= 1), divided by their sum; axes z, y, x in turn, each
+// output sum_i k[x - i] * src[reflect(i)] accumulated from 0 in increasing i with separate float32
+// multiply and add (no FMA: hipcc contracts a * b + c by default, so the sums run under
+// `fp contract(off)`); float32 between the axes.  Parity with vigra / fastfilters is
+// unpinned.  The second normalize is the labelling path's own.
+//
+// Layout: three streaming passes over the volume (z with the first normalize folded into the
+// loads, then y, then x); each workgroup stages its lines with the halo (reflected inside the
+// block) in LDS.  Traffic 8 B/voxel per pass (24 in all) + the block statistics read.
+// ------------------------------------------------------------------------------------------
+namespace cc {
+
+constexpr int GS_RMAX = 64;
+struct GaussTaps {
+    int32_t r;
+    float k[2 * GS_RMAX + 1];      // k[j] = tap of offset j - r
+};
+// tiles of one axis: outputs [a0, a0 + n) of the block segment [b0, b0 + w) along the axis
+struct AxSeg {
+    int32_t a0, b0, w, n;
+    int32_t blk, pad[3];           // block index along the axis
+};
+struct NormP {                     // vu.normalize of one block: y = x - mn; if (m > 0) y = y / m
+    float mn, m;
+    int32_t nan, pad;
+};
+constexpr int GS_ZY_OUT = 64;      // outputs per z / y tile (x: 64 lanes)
+constexpr int GS_X_OUT = 256;      // outputs per x tile (one row per wave)
+
+__global__ void k_norm_params(int64_t nb, const u32* smin, const u32* smax, const u32* sflag, NormP* np) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    NormP p;
+    p.mn = __uint_as_float(ord2f(smin[b]));
+    const float mx = __uint_as_float(ord2f(smax[b]));
+    // numpy: max(x - mn) is NaN when some x - mn is (x = mn = +-inf), else fl(mx - mn)
+    p.m = isinf(p.mn) ? __uint_as_float(0x7FC00000u) : mx - p.mn;
+    p.nan = (int32_t)(sflag[b] & 1u);
+    p.pad = 0;
+    np[b] = p;
+}
+
+__device__ __forceinline__ float gs_norm(float x, const NormP& p) {
+    if (p.nan) return __uint_as_float(0x7FC00000u);
+    float y = x - p.mn;
+    if (p.m > 0.0f) y = y / p.m;
+    return y;
+}
+
+__device__ __forceinline__ int gs_reflect(int rel, int w) {
+    rel = rel < 0 ? -rel : rel;
+    return rel >= w ? 2 * (w - 1) - rel : rel;
+}
+
+// z (AX = 0) or y (AX = 1) lines: 64 x-adjacent lines x GS_ZY_OUT outputs per workgroup, at a fixed
+// y (AX = 0) or z (AX = 1).  NORM: the first pass normalizes every loaded value with its block's
+// parameters.
+template <int AX, bool NORM>
+__global__ __launch_bounds__(256) void k_gauss_zy(const float* __restrict__ in, float* __restrict__ out, int64_t Z,
+                                                  int64_t Y, int64_t X, int64_t by, int64_t bx, int nby, int nbx,
+                                                  const AxSeg* __restrict__ segs, int64_t other, int64_t nxt,
+                                                  const NormP* __restrict__ np, GaussTaps tp) {
+    extern __shared__ float gbuf[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t id = blockIdx.x;
+    const int64_t xt = id % nxt, rest = id / nxt;
+    const int64_t o = rest % other, sg = rest / other;
+    const AxSeg S = segs[sg];
+    const int r = tp.r;
+    const int64_t x = xt * 64 + lane;
+    const bool xin = x < X;
+    const int64_t xs = xin ? x : X - 1;
+    NormP P{0.f, 0.f, 0, 0};
+    if (NORM) {       // AX = 0: the segment's z block, the tile's y block, the lane's x block
+        static_assert(!NORM || AX == 0, "the first (normalizing) pass runs along z");
+        P = np[((int64_t)S.blk * nby + o / by) * nbx + xs / bx];
+    }
+    for (int p = wave; p < S.n + 2 * r; p += 4) {
+        const int64_t c = S.b0 + gs_reflect(S.a0 - S.b0 - r + p, S.w);
+        const int64_t idx = AX == 0 ? (c * Y + o) * X + xs : (o * Y + c) * X + xs;
+        float v = in[idx];
+        if (NORM) v = gs_norm(v, P);
+        gbuf[p * 64 + lane] = v;
+    }
+    __syncthreads();
+    if (!xin) return;
+    for (int q = wave; q < S.n; q += 4) {
+#pragma clang fp contract(off)
+        float sum = 0.0f;
+        for (int j = 0; j <= 2 * r; ++j) { const float t = tp.k[2 * r - j] * gbuf[(q + j) * 64 + lane]; sum = sum + t; }
+        const int64_t c = S.a0 + q;
+        out[AX == 0 ? (c * Y + o) * X + x : (o * Y + c) * X + x] = sum;
+    }
+}
+
+// x lines: one row per wave, GS_X_OUT outputs of one block segment per workgroup row
+__global__ __launch_bounds__(256) void k_gauss_x(const float* __restrict__ in, float* __restrict__ out, int64_t rows,
+                                                 int64_t X, const AxSeg* __restrict__ segs, GaussTaps tp) {
+    extern __shared__ float gbuf[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = tp.r;
+    const AxSeg S = segs[blockIdx.y];
+    const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+    const bool ok = row < rows;                   // wave-uniform
+    float* b = gbuf + wave * (GS_X_OUT + 2 * GS_RMAX);
+    const float* src = in + (ok ? row : 0) * X;
+    if (ok)
+        for (int p = lane; p < S.n + 2 * r; p += 64) b[p] = src[S.b0 + gs_reflect(S.a0 - S.b0 - r + p, S.w)];
+    __syncthreads();
+    if (!ok) return;
+    for (int q = lane; q < S.n; q += 64) {
+#pragma clang fp contract(off)
+        float sum = 0.0f;
+        for (int j = 0; j <= 2 * r; ++j) { const float t = tp.k[2 * r - j] * b[q + j]; sum = sum + t; }
+        out[row * X + S.a0 + q] = sum;
+    }
+}
+
+}  // namespace cc
+
+namespace cc {
+
+// vigra Kernel1D<float>::initGaussian(sigma, 1.0) restated (see above): float arithmetic, expf
+static int gauss_taps(double sigma, GaussTaps& t) {
+    int radius = (int)(3.0 * sigma + 0.5);
+    if (radius == 0) radius = 1;
+    if (radius > GS_RMAX) return -1;
+    const float s = (float)sigma;
+    const float sigma2 = -0.5f / s / s;
+    const float norm = (float)(1.0 / (std::sqrt(2.0 * M_PI) * (double)s));
+    float sum = 0.0f;
+    float x = -(float)radius;
+    for (int i = 0; i <= 2 * radius; ++i, x += 1.0f) {
+        const float x2 = x * x;
+        t.k[i] = norm * std::exp(x2 * sigma2);
+    }
+    for (int i = 0; i <= 2 * radius; ++i) sum += t.k[i];
+    const float f = 1.0f / sum;
+    for (int i = 0; i <= 2 * radius; ++i) t.k[i] = t.k[i] * f;
+    for (int i = 2 * radius + 1; i <= 2 * GS_RMAX; ++i) t.k[i] = 0.0f;
+    t.r = radius;
+    return radius;
+}
+
+// tiles of `out_per` outputs inside each block segment of an axis of length n, blocks of bs
+static void axis_segs(int64_t n, int64_t bs, int out_per, std::vector<AxSeg>& v) {
+    for (int64_t b0 = 0, bi = 0; b0 < n; b0 += bs, ++bi) {
+        const int64_t w = std::min(bs, n - b0);
+        for (int64_t a0 = b0; a0 < b0 + w; a0 += out_per) {
+            AxSeg S{};
+            S.a0 = (int32_t)a0; S.b0 = (int32_t)b0; S.w = (int32_t)w;
+            S.n = (int32_t)std::min<int64_t>(out_per, b0 + w - a0);
+            S.blk = (int32_t)bi;
+            v.push_back(S);
+        }
+    }
+}
+
+}  // namespace cc
+
+extern "C" {
+
+int cc_gaussian_taps(double sigma, float* taps, int cap) {
+    CC_TRY({
+        CC_REQUIRE(sigma > 0 && taps, "sigma must be > 0");
+        GaussTaps t;
+        const int r = gauss_taps(sigma, t);
+        CC_REQUIRE(r > 0, "sigma too large (kernel radius > 64)");
+        CC_REQUIRE(cap >= 2 * r + 1, "taps buffer too small");
+        for (int i = 0; i <= 2 * r; ++i) taps[i] = t.k[i];
+        return r;
+    });
+}
+
+int cc_gaussian_smooth_blocks(cc_ctx* c, const float* in, const int64_t shape[3], const int64_t block_shape[3],
+                              double sigma, float* out) {
+    CC_TRY({
+        CC_REQUIRE(c && in && out && shape && block_shape, "NULL argument");
+        CC_REQUIRE(sigma > 0, "sigma must be > 0");
+        GaussTaps tp;
+        const int r = gauss_taps(sigma, tp);
+        CC_REQUIRE(r > 0, "sigma too large (kernel radius > 64)");
+        for (int a = 0; a < 3; ++a) {
+            CC_REQUIRE(shape[a] >= 1 && block_shape[a] >= 1, "bad shape / block_shape");
+            CC_REQUIRE(shape[a] < (1ll << 31), "axis too long");
+            // vigra convolveLine: "kernel longer than line" unless every line (block extent) > r
+            const int64_t last = shape[a] - (shape[a] - 1) / block_shape[a] * block_shape[a];
+            CC_REQUIRE(std::min(block_shape[a], shape[a]) > r && last > r,
+                       "sigma_prefilter: kernel longer than a block line (block extent <= 3 sigma)");
+        }
+        HIP_OK(hipSetDevice(c->device));
+        const int64_t Z = shape[0], Y = shape[1], X = shape[2], n = Z * Y * X;
+        hipStream_t s = c->stream;
+        // block statistics (ordered min / max, NaN flag) -> normalize parameters
+        RunState& st = state(c);
+        st = RunState();
+        st.hg = make_geom(shape, block_shape, 0);
+        upload_geom(c, st.hg);
+        Geom& g = st.hg.g;
+        const int64_t nt = g.n_tiles, nb = g.n_blocks;
+        c->bstat.ensure(nb * 3 * sizeof(u32));
+        u32* smin = c->bstat.as<u32>();
+        u32* smax = smin + nb;
+        u32* sflag = smax + nb;
+        HIP_OK(hipMemsetAsync(smin, 0xFF, nb * sizeof(u32), s));
+        HIP_OK(hipMemsetAsync(smax, 0x00, 2 * nb * sizeof(u32), s));
+        launch(c, "k_block_stats", [&] { k_block_stats<<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, smin, smax, sflag); });
+        std::vector<AxSeg> sz, sy, sx;
+        axis_segs(Z, block_shape[0], GS_ZY_OUT, sz);
+        axis_segs(Y, block_shape[1], GS_ZY_OUT, sy);
+        axis_segs(X, block_shape[2], GS_X_OUT, sx);
+        CC_REQUIRE(sx.size() < 65536, "too many x segments");
+        const size_t nseg = sz.size() + sy.size() + sx.size();
+        c->gs_tab.ensure(nseg * sizeof(AxSeg) + nb * sizeof(NormP));
+        AxSeg* dseg = c->gs_tab.as<AxSeg>();
+        NormP* np = (NormP*)(dseg + nseg);
+        std::vector<AxSeg> all(sz);
+        all.insert(all.end(), sy.begin(), sy.end());
+        all.insert(all.end(), sx.begin(), sx.end());
+        HIP_OK(hipMemcpyAsync(dseg, all.data(), nseg * sizeof(AxSeg), hipMemcpyHostToDevice, s));
+        launch(c, "k_norm_params", [&] { k_norm_params<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, smin, smax, sflag, np); });
+        c->gs1.ensure(n * sizeof(float));
+        c->gs2.ensure(n * sizeof(float));
+        float* A = c->gs1.as<float>();
+        float* B = c->gs2.as<float>();
+        const int64_t nxt = (X + 63) / 64;
+        const int nby = (int)g.nb[1], nbx = (int)g.nb[2];
+        const size_t lds_zy = (size_t)(GS_ZY_OUT + 2 * r) * 64 * sizeof(float);
+        {
+            const int64_t grid = (int64_t)sz.size() * Y * nxt;
+            CC_REQUIRE(grid < (1ll << 31), "volume too large for the z pass grid");
+            launch(c, "k_gauss_z", [&] {
+                k_gauss_zy<0, true><<<(unsigned)grid, 256, lds_zy, s>>>(in, A, Z, Y, X, block_shape[1], block_shape[2],
+                                                                        nby, nbx, dseg, Y, nxt, np, tp);
+            });
+        }
+        {
+            const int64_t grid = (int64_t)sy.size() * Z * nxt;
+            CC_REQUIRE(grid < (1ll << 31), "volume too large for the y pass grid");
+            launch(c, "k_gauss_y", [&] {
+                k_gauss_zy<1, false><<<(unsigned)grid, 256, lds_zy, s>>>(A, B, Z, Y, X, block_shape[1], block_shape[2],
+                                                                         nby, nbx, dseg + sz.size(), Z, nxt, np, tp);
+            });
+        }
+        {
+            const int64_t rows = Z * Y, gx = (rows + 3) / 4;
+            CC_REQUIRE(gx < (1ll << 31), "volume too large for the x pass grid");
+            const size_t lds_x = (size_t)4 * (GS_X_OUT + 2 * GS_RMAX) * sizeof(float);
+            launch(c, "k_gauss_x", [&] {
+                k_gauss_x<<<dim3((unsigned)gx, (unsigned)sx.size()), 256, lds_x, s>>>(B, out, rows, X,
+                                                                                   dseg + sz.size() + sy.size(), tp);
+            });
+        }
+        sync(c);
+        st.stage = 0;
+    });
+}
+
+}  // extern "C"

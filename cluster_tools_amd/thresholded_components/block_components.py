@@ -3,7 +3,8 @@
 
 Task parameters, configs, output dataset (uint64, chunks block//2, gzip), the per-job offsets
 JSON and the log contract are the reference's (block_components.py:21-119,236-291).  The job's
-compute runs on the MI355X through libcc_mi355x:
+compute runs on the MI355X through libcc_mi355x (4-D input with `channel`: cc_channel_mean first;
+sigma_prefilter > 0: cc_gaussian_smooth_blocks first):
   fused=False  cc_block_components: block-local 26-connected labels in skimage numbering and
                the per-block values (n_i + 1 or 0), exactly what the reference job writes;
   fused=True   (set by ThresholdedComponentsWorkflow) cc_label_volume: all five stages in this
@@ -88,8 +89,6 @@ class BlockComponentsBase(Task):
             assert all(0 <= c < shape[0] for c in chans), (shape[0], chans)
             shape = shape[1:]
             config.update({'channel': self.channel})
-        if config.get('sigma_prefilter', 0) > 0:
-            raise NotImplementedError('sigma_prefilter > 0 is not supported on the MI355X path')
         chunks = tuple(max(1, min(ch, sh)) for ch, sh in zip(chunks, shape))
         compression = config.pop('compression', 'gzip')
         # the reference empty-job branch (merge_assignments config, see merge_assignments.py) is
@@ -157,13 +156,23 @@ def read_input(config, box=None):
     return stack, [distinct.index(c) for c in chans]
 
 
-def to_device(ctx, host, chans, dev):
+def to_device(ctx, host, chans, dev, config=None):
     """float32 device volume for the labelling: upload, and for a channel stack the mean of the
-    listed channels (cc_channel_mean: np.mean(axis=0) as block_components.py:150-159 does it)."""
+    listed channels (cc_channel_mean: np.mean(axis=0) as block_components.py:150-159 does it);
+    then the sigma_prefilter front (prefilter)."""
     import torch
-    if chans is None:
-        return torch.from_numpy(host).to(dev)
-    return ctx.channel_mean(host, chans)
+    x = torch.from_numpy(host).to(dev) if chans is None else ctx.channel_mean(host, chans)
+    return prefilter(ctx, x, config)
+
+
+def prefilter(ctx, x, config):
+    """config['sigma_prefilter'] > 0: per block normalize -> Gaussian smoothing in place
+    (block_components.py:160-163; cc_gaussian_smooth_blocks, the filter restating vigra's).  The
+    second normalize is the labelling's own."""
+    sigma = float((config or {}).get('sigma_prefilter', 0) or 0)
+    if sigma > 0:
+        x = ctx.gaussian_smooth_blocks(x, config['block_shape'], sigma, out=x)
+    return x
 
 
 def _write_output(config, labels, box, n_threads=None):
@@ -219,6 +228,7 @@ def _fused_single(config, shape, nb):
         t = time.perf_counter()
         if chans is not None:
             x = ctx.channel_mean(x, chans, shape4=stack_shape, dtype=stack_dtype)
+        x = prefilter(ctx, x, config)
         labels_dev, res = ctx.label_volume(x, config['block_shape'], config['threshold'],
                                            config['threshold_mode'], m)
         torch.cuda.synchronize(dev)
@@ -320,7 +330,7 @@ def block_components(job_id, config_path):
             vu.load_mask(config['mask_path'], config['mask_key'], shape)
             mask = (_read(config['mask_path'], config['mask_key']) != 0).astype(np.uint8)
         with _lib.Context(int(os.environ.get('CC_DEVICE', '0'))) as ctx:
-            x = to_device(ctx, inp, chans, ctx.torch_device())
+            x = to_device(ctx, inp, chans, ctx.torch_device(), config)
             m = None if mask is None else torch.from_numpy(mask).to(x.device)
             lab_dev, values = ctx.block_components(x, block_shape, threshold, mode, m)
             labels = lab_dev.cpu().numpy().view(np.uint64)

@@ -65,12 +65,15 @@ def main(config_path, out_dir):
     del inp, mask
 
     ctx = _lib.Context(gpu)
-    if chans is not None:
+    if chans is not None or float(config.get('sigma_prefilter', 0) or 0) > 0:
+        # input preparation (channel mean, sigma_prefilter: block-local, so slab-local)
         ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         t = time.perf_counter()
-        x = ctx.channel_mean(x, chans, shape4=stack_shape, dtype=stack_dtype)
+        if chans is not None:
+            x = ctx.channel_mean(x, chans, shape4=stack_shape, dtype=stack_dtype)
+        x = bc.prefilter(ctx, x, config)
         torch.cuda.synchronize(dev)
-        timing['channel_mean_s'] = time.perf_counter() - t
+        timing['prefilter_s'] = time.perf_counter() - t
     comm = StagedComm(device=dev) if backend != 'nccl' else None
     lab = ShardedLabeler(ctx, shape, bs, z0, zs, dev, comm=comm)
     out = torch.empty(tuple(x.shape), dtype=torch.int64, device=dev)

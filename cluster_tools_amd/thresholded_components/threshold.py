@@ -8,8 +8,8 @@ clipped to the shape, the job config per LocalTask and the "processed job" log c
 job's compute (per-block normalize + float32 compare, threshold.py:131-171) runs on the MI355X
 through cc_threshold (k_block_stats -> k_block_params -> k_threshold); one GPU job thresholds
 the whole volume and writes the listed blocks.  channel (4-D input): the listed channels are
-averaged on the device first (cc_channel_mean, threshold.py:139-148).  sigma_prefilter > 0 is
-rejected, as for BlockComponents.
+averaged on the device first (cc_channel_mean, threshold.py:139-148); sigma_prefilter > 0: per block
+normalize + Gaussian smoothing first (cc_gaussian_smooth_blocks, threshold.py:150-153).
 """
 import json
 import os
@@ -69,8 +69,6 @@ class ThresholdBase(Task):
             assert all(0 <= c < shape[0] for c in channel_list(self.channel)), (shape[0], self.channel)
             shape = shape[1:]
             config.update({'channel': self.channel})
-        if config.get('sigma_prefilter', 0) > 0:
-            raise NotImplementedError('sigma_prefilter > 0 is not supported on the MI355X path')
         chunks = tuple(max(1, min(ch, sh)) for ch, sh in zip(chunks, shape))
         compression = config.pop('compression', 'gzip')
         with vu.file_reader(self.output_path) as f:
@@ -102,7 +100,7 @@ def threshold(job_id, config_path):
     inp, chans = read_input(config)
     shape = inp.shape if chans is None else inp.shape[1:]
     with _lib.Context(int(os.environ.get('CC_DEVICE', '0'))) as ctx:
-        x = to_device(ctx, inp, chans, ctx.torch_device())
+        x = to_device(ctx, inp, chans, ctx.torch_device(), config)
         out = ctx.threshold(x, block_shape, thr, mode).cpu().numpy()
     blocking = vu.Blocking([0, 0, 0], list(shape), block_shape)
     with vu.file_reader(config['output_path']) as f:

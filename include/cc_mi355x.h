@@ -127,6 +127,19 @@ int cc_threshold(cc_ctx* ctx, const float* in_dev, const int64_t shape[3], const
 int cc_channel_mean(cc_ctx* ctx, const void* in_dev, int dtype, const int64_t shape4[4],
                     const int64_t* channels, int64_t n_channels, float* out_dev);
 
+/* sigma_prefilter (block_components.py:161-163, threshold.py:151-153): out_dev = per block of
+ * block_shape, gaussianSmoothing(normalize(block), sigma) with the block's own borders (reflected,
+ * no halo), as float32; the labelling / threshold entry points then apply the second normalize.
+ * The filter restates vigra.filters.gaussianSmoothing (the reference's fallback when fastfilters is
+ * absent): taps of Kernel1D::initGaussian in float32 (radius (int)(3 sigma + 0.5)), separable
+ * z -> y -> x, BORDER_TREATMENT_REFLECT, float32 sums without FMA (parity with vigra unpinned).
+ * Error when a block line is not longer than the radius (vigra: "kernel longer than line") or the
+ * radius exceeds 64.  in_dev and out_dev may alias.  cc_gaussian_taps writes the 2r + 1 taps and
+ * returns r. */
+int cc_gaussian_smooth_blocks(cc_ctx* ctx, const float* in_dev, const int64_t shape[3],
+                              const int64_t block_shape[3], double sigma, float* out_dev);
+int cc_gaussian_taps(double sigma, float* taps, int cap);
+
 /* merge_offsets (merge_offsets.py:104-120): exclusive scan of values; writes offsets
  * and empty flags; returns n_labels through *n_labels. Host arrays. */
 int cc_merge_offsets(const uint64_t* values_host, int64_t n_blocks, uint64_t* offsets_host,

@@ -240,3 +240,86 @@ def channel_mean(inp4, channel):
         acc = (acc + x[c].astype(acc_t)).astype(acc_t)
     acc = (acc / acc_t(len(chans))).astype(acc_t)
     return acc.astype(np.float32)
+
+
+def gaussian_taps(sigma):
+    """vigra Kernel1D<float>::initGaussian(sigma, 1.0) restated (TEST INFRASTRUCTURE ONLY; the
+    reference's sigma_prefilter filter when fastfilters is absent, volume_utils.py:13-18,80-94;
+    vigra is absent here, so this restatement is UNPINNED against vigra itself): radius
+    (int)(3 sigma + 0.5) (at least 1); tap(x) = norm * expf(x*x * sigma2) for x = -r..r in float32,
+    sigma2 = -0.5f / s / s, norm = float(1 / (sqrt(2 pi) * s)); then every tap times 1 / (sum of
+    the taps, float32 left to right).  expf is libm's (the same function the library's host code
+    calls).  Returns (taps float32[2r + 1], r)."""
+    import ctypes
+    import math
+    libm = ctypes.CDLL('libm.so.6')
+    expf = libm.expf
+    expf.restype, expf.argtypes = ctypes.c_float, [ctypes.c_float]
+    f32 = np.float32
+    radius = max(1, int(3.0 * sigma + 0.5))
+    s = f32(sigma)
+    sigma2 = f32(f32(f32(-0.5) / s) / s)
+    norm = f32(1.0 / (math.sqrt(2.0 * math.pi) * float(s)))
+    taps = []
+    x = f32(-radius)
+    for _ in range(2 * radius + 1):
+        x2 = f32(x * x)
+        taps.append(f32(norm * f32(expf(float(f32(x2 * sigma2))))))
+        x = f32(x + f32(1.0))
+    total = f32(0.0)
+    for v in taps:
+        total = f32(total + v)
+    fct = f32(f32(1.0) / total)
+    return np.array([f32(v * fct) for v in taps], dtype=np.float32), radius
+
+
+def gaussian_smooth(arr, sigma):
+    """vigra.filters.gaussianSmoothing(arr, sigma) of a 3-D float32 array restated (TEST
+    INFRASTRUCTURE ONLY, unpinned against vigra): separable, axes 0, 1, 2 in turn; per line
+    out[x] = sum over i = x - r .. x + r (increasing) of tap[x - i] * src[reflect(i)], accumulated
+    from 0 with separate float32 multiply and add, float32 between the axes; reflect mirrors
+    without repeating the edge (BORDER_TREATMENT_REFLECT); every line must be longer than r
+    (vigra's convolveLine precondition)."""
+    taps, r = gaussian_taps(sigma)
+    y = np.asarray(arr, dtype=np.float32)
+    for ax in range(3):
+        w = y.shape[ax]
+        if w <= r:
+            raise ValueError('convolveLine(): kernel longer than line')
+        pad = [(r, r) if a == ax else (0, 0) for a in range(3)]
+        p = np.pad(y, pad, mode='reflect')
+        acc = np.zeros_like(y)
+        for j in range(2 * r + 1):
+            sl = [slice(None)] * 3
+            sl[ax] = slice(j, j + w)
+            acc = (acc + (taps[2 * r - j] * p[tuple(sl)]).astype(np.float32)).astype(np.float32)
+        y = acc
+    return y
+
+
+def normalize_block(x):
+    """vu.normalize (volume_utils.py:98-105), numpy as the reference runs it."""
+    y = np.asarray(x).astype('float32')
+    with np.errstate(invalid='ignore', divide='ignore'):
+        y -= y.min()
+        m = y.max()
+        if m > 0:
+            y /= m
+    return y
+
+
+def gaussian_smooth_blocks(inp, block_shape, sigma):
+    """The sigma_prefilter front of block_components.py:160-163 per block (TEST INFRASTRUCTURE
+    ONLY): normalize -> gaussian_smooth (restated vigra) -> (the second normalize is part of the
+    labelling / threshold that follows)."""
+    x = np.asarray(inp, dtype=np.float32)
+    out = np.empty_like(x)
+    grids = [range(0, s, b) for s, b in zip(x.shape, block_shape)]
+    for z0 in grids[0]:
+        for y0 in grids[1]:
+            for x0 in grids[2]:
+                bb = (slice(z0, z0 + block_shape[0]), slice(y0, y0 + block_shape[1]),
+                      slice(x0, x0 + block_shape[2]))
+                with np.errstate(invalid='ignore', over='ignore'):
+                    out[bb] = gaussian_smooth(normalize_block(x[bb]), sigma)
+    return out

@@ -86,7 +86,7 @@ def n_blocks_of(shape, block_shape):
     return int(np.prod([-(-s // b) for s, b in zip(shape, block_shape)]))
 
 
-def run_reference(inp, block_shape, threshold, mode, mask=None, n_jobs_bc=2, n_jobs_bf=1, channel=None):
+def run_reference(inp, block_shape, threshold, mode, mask=None, n_jobs_bc=2, n_jobs_bf=1, channel=None, extra=None):
     """Run the five reference stages in a scratch folder; return artefacts.  channel (int or
     list): inp is 4-D (C, Z, Y, X) and block_components averages those channels
     (block_components.py:150-159)."""
@@ -125,6 +125,7 @@ def run_reference(inp, block_shape, threshold, mode, mask=None, n_jobs_bc=2, n_j
             cfg.update({'mask_path': in_path, 'mask_key': 'mask'})
         if channel is not None:
             cfg['channel'] = channel
+        cfg.update(extra or {})          # e.g. sigma_prefilter (make_golden_sigma.py)
         for j, p in enumerate(job_cfgs('block_components', n_bc, cfg)):
             ref_bc.block_components(j, p)
         # per-block values v_i (n_i + 1 or 0) before merge_offsets deletes the files

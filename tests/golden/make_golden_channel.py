@@ -34,13 +34,13 @@ from cluster_tools.thresholded_components import threshold as ref_th  # noqa: E4
 from oracle.synth import boundary_q, ellipsoid_mask  # noqa: E402
 
 
-def run_reference_threshold(inp, block_shape, threshold, mode, channel, n_jobs=2):
+def run_reference_threshold(inp, block_shape, threshold, mode, channel, n_jobs=2, extra=None):
     tmp = tempfile.mkdtemp(prefix='golden_chthr_')
     try:
         in_path, out_path = os.path.join(tmp, 'in.h5'), os.path.join(tmp, 'out.h5')
         with h5py.File(in_path, 'w') as f:
             f.create_dataset('raw', data=inp)
-        shape = inp.shape[1:]
+        shape = inp.shape[1:] if channel is not None else inp.shape
         with h5py.File(out_path, 'w') as f:
             f.create_dataset('thr', shape=shape, dtype='uint8')
         nb = make_golden.n_blocks_of(shape, block_shape)
@@ -50,7 +50,7 @@ def run_reference_threshold(inp, block_shape, threshold, mode, channel, n_jobs=2
                 json.dump({'input_path': in_path, 'input_key': 'raw', 'output_path': out_path,
                            'output_key': 'thr', 'block_list': list(range(nb))[j::n_jobs],
                            'block_shape': list(block_shape), 'threshold': float(threshold),
-                           'threshold_mode': mode, 'channel': channel}, fh)
+                           'threshold_mode': mode, 'channel': channel, **(extra or {})}, fh)
             ref_th.threshold(j, p)
         with h5py.File(out_path, 'r') as f:
             return f['thr'][:]

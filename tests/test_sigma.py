@@ -1,0 +1,144 @@
+"""sigma_prefilter > 0 (reference block_components.py:160-163, threshold.py:150-153: per block
+normalize -> gaussianSmoothing -> normalize).  The filter restates vigra.filters.gaussianSmoothing
+(oracle.gaussian_smooth; vigra / fastfilters are absent, so the filter arithmetic is UNPINNED
+against them); the goldens (tests/golden/make_golden_sigma.py) run the reference's own jobs with
+that restatement plugged in, which pins everything around the filter.  The device path
+(cc_gaussian_smooth_blocks) must equal the restatement bit for bit."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_golden
+from oracle import oracle as O
+
+with open(os.path.join(GOLDEN, 'index_sigma.json')) as _f:
+    INDEX = json.load(_f)
+CASES = sorted(INDEX)
+
+
+def _case(name):
+    d = load_golden('sigma_' + name)
+    meta = INDEX[name]
+    x = d['input'] if meta['channel'] is None else O.channel_mean(d['input'], meta['channel'])
+    return d, meta, x
+
+
+@pytest.mark.parametrize('name', CASES)
+def test_oracle_matches_reference(name):
+    d, meta, x = _case(name)
+    bs, thr = meta['block_shape'], float(d['threshold'])
+    s = O.gaussian_smooth_blocks(x, bs, meta['sigma'])
+    np.testing.assert_array_equal(O.threshold_volume(s, bs, thr, meta['mode']), d['thr_expected'])
+    r = O.label_volume(s, bs, thr, meta['mode'], d.get('mask'), n_threads=3, want_local=True)
+    np.testing.assert_array_equal(r['local'], d['local_labels'].astype(np.uint64))
+    np.testing.assert_array_equal(r['values'], d['block_values'])
+    np.testing.assert_array_equal(O.canon(r['labels']), d['labels_canon'])
+    np.testing.assert_array_equal(O.canon(r['lut']), d['lut_canon'])
+    assert r['max_id'] == int(d['max_id'])
+
+
+def test_taps_shape():
+    for sigma, r in ((0.1, 1), (0.5, 2), (1.0, 3), (2.0, 6), (21.0, 63)):
+        k, rr = O.gaussian_taps(sigma)
+        assert rr == r and len(k) == 2 * r + 1
+        np.testing.assert_array_equal(k, k[::-1])
+        assert abs(float(k.sum(dtype=np.float64)) - 1.0) < 1e-5
+
+
+def test_filter_rejects_short_lines():
+    with pytest.raises(ValueError):
+        O.gaussian_smooth(np.zeros((3, 10, 10), np.float32), 1.0)      # r = 3 >= 3 planes
+
+
+@pytest.mark.gpu
+def test_gpu_taps_equal_restatement():
+    from cluster_tools_amd import _lib
+    for sigma in (0.3, 0.7, 1.0, 1.5, 2.0, 3.3, 10.0, 21.0):
+        np.testing.assert_array_equal(_lib.gaussian_taps(sigma), O.gaussian_taps(sigma)[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', CASES)
+def test_gpu_matches_reference(ctx, name):
+    import torch
+    d, meta, x = _case(name)
+    bs, thr = meta['block_shape'], float(d['threshold'])
+    xd = torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    s = ctx.gaussian_smooth_blocks(xd, bs, meta['sigma'])
+    np.testing.assert_array_equal(s.cpu().numpy(), O.gaussian_smooth_blocks(x, bs, meta['sigma']))
+    np.testing.assert_array_equal(ctx.threshold(s, bs, thr, meta['mode']).cpu().numpy(), d['thr_expected'])
+    m = torch.from_numpy(d['mask']).cuda() if 'mask' in d else None
+    lab, res = ctx.label_volume(s, bs, thr, meta['mode'], m)
+    np.testing.assert_array_equal(O.canon(lab.cpu().numpy()), d['labels_canon'])
+    np.testing.assert_array_equal(ctx.block_values(len(d['block_values'])), d['block_values'])
+    np.testing.assert_array_equal(O.canon(ctx.lut(res['n_labels'])), d['lut_canon'])
+    assert res['max_id'] == int(d['max_id'])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape,bs,sigma', [((70, 140, 300), (32, 64, 128), 1.3),      # ragged blocks / tiles (last block lines > r)
+                                            ((40, 64, 520), (40, 64, 520), 4.0),       # x segments > 256
+                                            ((33, 65, 129), (11, 13, 43), 1.0),        # odd everything
+                                            ((24, 40, 70), (24, 40, 70), 7.5)])        # r = 23
+def test_gpu_smooth_vs_oracle(ctx, shape, bs, sigma):
+    import torch
+    x = O.boundary_map(shape, origin=(3, 5, 7), dither=True)
+    got = ctx.gaussian_smooth_blocks(torch.from_numpy(x).cuda(), bs, sigma).cpu().numpy()
+    np.testing.assert_array_equal(got, O.gaussian_smooth_blocks(x, bs, sigma))
+    # in place
+    xd = torch.from_numpy(x).cuda()
+    ctx.gaussian_smooth_blocks(xd, bs, sigma, out=xd)
+    np.testing.assert_array_equal(xd.cpu().numpy(), got)
+
+
+@pytest.mark.gpu
+def test_gpu_rejects_short_lines(ctx):
+    import torch
+    x = torch.zeros((20, 20, 20), dtype=torch.float32, device='cuda')
+    with pytest.raises(RuntimeError):
+        ctx.gaussian_smooth_blocks(x, (10, 10, 10), 3.2)          # r = 10: a 10-voxel block line is too short
+    with pytest.raises(RuntimeError):
+        ctx.gaussian_smooth_blocks(x, (20, 20, 20), 30.0)         # r > 64
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['bmap_s07_mask', 'bmap_s2_less'])
+def test_workflow_sigma_n5(tmp_path, name):
+    """ThresholdedComponentsWorkflow with sigma_prefilter in the block_components task config, and
+    the Threshold task with it in its config, on N5."""
+    from cluster_tools_amd import luigi_compat as luigi, n5
+    from cluster_tools_amd.cluster_tasks import BaseClusterTask
+    from cluster_tools_amd.thresholded_components import ThresholdedComponentsWorkflow
+    from cluster_tools_amd.thresholded_components.threshold import ThresholdLocal
+    d, meta, x = _case(name)
+    data = str(tmp_path / 'data.n5')
+    with n5.open_file(data) as f:
+        f.create_dataset('raw', data=d['input'], chunks=(8, 16, 16), compression='gzip')
+        if 'mask' in d:
+            f.create_dataset('mask', data=d['mask'], chunks=(8, 16, 16), compression='gzip')
+    cfg = str(tmp_path / 'config')
+    os.makedirs(cfg)
+    g = BaseClusterTask.default_global_config()
+    g['block_shape'] = list(meta['block_shape'])
+    with open(os.path.join(cfg, 'global.config'), 'w') as f:
+        json.dump(g, f)
+    for task in ('block_components', 'threshold'):
+        with open(os.path.join(cfg, task + '.config'), 'w') as f:
+            json.dump({'sigma_prefilter': meta['sigma']}, f)
+    kw = dict(mask_path=data, mask_key='mask') if 'mask' in d else {}
+    t = ThresholdedComponentsWorkflow(tmp_folder=str(tmp_path / 'tmp'), config_dir=cfg, target='local', max_jobs=2,
+                                      input_path=data, input_key='raw', output_path=data, output_key='seg',
+                                      assignment_key='assignments', threshold=float(d['threshold']),
+                                      threshold_mode=meta['mode'], **kw)
+    assert luigi.build([t], local_scheduler=True)
+    th = ThresholdLocal(tmp_folder=str(tmp_path / 'tmp_thr'), config_dir=cfg, max_jobs=2, input_path=data,
+                        input_key='raw', output_path=data, output_key='thr', threshold=float(d['threshold']),
+                        threshold_mode=meta['mode'])
+    assert luigi.build([th], local_scheduler=True)
+    with n5.open_file(data, 'r') as f:
+        np.testing.assert_array_equal(O.canon(f['seg'][:]), d['labels_canon'])
+        np.testing.assert_array_equal(O.canon(f['assignments'][:]), d['lut_canon'])
+        assert f['seg'].attrs['maxId'] == int(d['max_id'])
+        np.testing.assert_array_equal(f['thr'][:], d['thr_expected'])
