@@ -1343,21 +1343,34 @@ __device__ __forceinline__ void seam_rows3(const face_t* S, const int mode[3], i
             }
         }
     }
-    const u64 Bm_ = __shfl(B0, lane > 0 ? lane - 1 : 0, 64), Bp_ = __shfl(B0, lane + 1 < 64 ? lane + 1 : 63, 64);
+    const int lm = lane > 0 ? lane - 1 : 0, lp = lane + 1 < 64 ? lane + 1 : 63;
+    const u64 Bm_ = __shfl(B0, lm, 64), Bp_ = __shfl(B0, lp, 64);
+    const u64 Am_ = __shfl(A, lm, 64), Ap_ = __shfl(A, lp, 64);
     const u64 Bm = r > 0 ? Bm_ : 0ull, Bp = r + 1 < nr ? Bp_ : 0ull;
+    const u64 Am = r > 0 ? Am_ : 0ull, Ap = r + 1 < nr ? Ap_ : 0ull;
     if (!md || !A) return;
     const bool full26 = md == 1;
     u32 la = NONE, lb = NONE;                                         // last pair emitted by this lane
+    // bit x := bit x + dx
+    auto sh = [](u64 v, int dx) { return dx > 0 ? v >> 1 : dx < 0 ? v << 1 : v; };
 #pragma unroll
     for (int dr = -1; dr <= 1; ++dr) {
         if (dr && !full26) continue;
         const u64 B = dr < 0 ? Bm : dr > 0 ? Bp : B0;
         if (!B) continue;
+        const u64 Ad = dr < 0 ? Am : Ap;
         const int rb = r + dr;
 #pragma unroll
         for (int dx = -1; dx <= 1; ++dx) {
             if (dx && !full26) continue;
-            const u64 C = A & (dx > 0 ? B >> 1 : dx < 0 ? B << 1 : B);
+            // contact A_r[x] - B_{r+dr}[x+dx].  Voxels next to each other on one side of the seam
+            // are one component of that tile, so the pair is also given by a contact of smaller
+            // |dr| + |dx| when A_r[x+dx] or B_{r+dr}[x] is set (dx != 0: the (dr, 0) contact) or
+            // A_{r+dr}[x] or B_r[x+dx] is set (dr != 0: the (0, dx) contact); by induction every
+            // pair keeps a contact that is not dropped, and (0, 0) contacts never are.
+            u64 C = A & sh(B, dx);
+            if (dx) C &= ~(sh(A, dx) | B);
+            if (dr) C &= ~(Ad | sh(B0, dx));
             for (u64 m = C & ~(C << 1); m; m &= m - 1) {
                 const int x = __builtin_ctzll(m);
                 const u32 ka = FA[(r >> 1) * stride + (x >> 1)] & FK_MASK;
@@ -1488,7 +1501,10 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const face_t* S, 
         u32 la = NONE, lb = NONE;
 #pragma unroll 1
         for (int d = -1; d <= 1; ++d) {
-            const u64 C = a & (d > 0 ? b >> 1 : d < 0 ? b << 1 : b);
+            u64 C = a & (d > 0 ? b >> 1 : d < 0 ? b << 1 : b);
+            // a diagonal contact a[p] - b[p + d] whose pair a (0) contact also gives (a[p + d] or
+            // b[p] set: neighbours along the line are one component of their tile) is dropped
+            if (d) C &= ~((d > 0 ? a >> 1 : a << 1) | b);
             for (u64 m = C & ~(C << 1); m; m &= m - 1) {
                 const int p = __builtin_ctzll(m), q = p + d;
                 const u32 ka = S[ab + (p >> 1) * as] & FK_MASK, kb = E[bb + (q >> 1)] & FK_MASK;
