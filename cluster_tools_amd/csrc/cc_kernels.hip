@@ -800,10 +800,34 @@ __global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __rest
             }
     };
     u32 mn = 0xFFFFFFFFu, mx = 0u;
-    sweep([&](u32 o) {
+    auto f = [&](u32 o) {
         mn = min(mn, o);
         mx = max(mx, o);
-    });
+    };
+    if (((g.X | e0[2] | el[2]) & 3) == 0) {
+        // 16-B aligned rows: float4 per lane, 4 rows per workgroup pass, SAMPLE_U of them in
+        // flight (the scalar walk waited on 8 dependent rounds of 8 rows per part)
+        const int slot = tid >> 7, x4 = 4 * (tid & 127);
+        const int nj = (nrows - pt + SAMPLE_PARTS - 1) / SAMPLE_PARTS;      // rows of this part
+        for (int j0 = 0; j0 < nj; j0 += 4 * SAMPLE_U)
+            for (int x = x4; x < el[2]; x += 512) {
+                float4 v[SAMPLE_U];
+#pragma unroll
+                for (int u = 0; u < SAMPLE_U; ++u) {
+                    const int j = min(j0 + 4 * u + slot, nj - 1);             // repeats are harmless
+                    const int r = pt + SAMPLE_PARTS * j;
+                    const int z = e0[0] + (r / nys) * SAMPLE_DZ + zo, y = e0[1] + (r % nys) * SAMPLE_DY + yo;
+                    v[u] = *reinterpret_cast<const float4*>(in + ((int64_t)z * g.Y + y) * g.X + e0[2] + x);
+                }
+#pragma unroll
+                for (int u = 0; u < SAMPLE_U; ++u) {
+                    f(f2ord(__float_as_uint(v[u].x))); f(f2ord(__float_as_uint(v[u].y)));
+                    f(f2ord(__float_as_uint(v[u].z))); f(f2ord(__float_as_uint(v[u].w)));
+                }
+            }
+    } else {
+        sweep(f);
+    }
     mn = block_reduce(mn, red, [](u32 a, u32 c) { return min(a, c); });
     mx = block_reduce(mx, red, [](u32 a, u32 c) { return max(a, c); });
     if (tid == 0) {
@@ -832,7 +856,9 @@ struct SpecArgs {
 };
 
 // SIDES: bounds of the guessed interval that can move (1 lower: 'greater', 2 upper: 'less', 3 both)
-template <bool HAS_MASK, int SIDES>
+// ABL (kernel ablation harness tools/ablate.hip only; 0 in the library): 99 stop once the bit rows
+// are in LDS (loads, ballots, statistics), else as pass1_finish's ABL
+template <bool HAS_MASK, int SIDES, int ABL = 0>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_spec(
     Geom g, SpecArgs sa, const float* __restrict__ in, const u8* __restrict__ mask, u64* BITS, face_t* FACES,
     u32* COUNT, u32* P, u64* KEY) {
@@ -939,7 +965,8 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         u32* tb = sa.TB + 4 * t;
         tb[0] = A; tb[1] = B; tb[2] = C; tb[3] = D;
     }
-    pass1_finish<0>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, true);
+    if (ABL == 99) return;
+    pass1_finish<ABL % 99>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, true);
 }
 
 // are the bits computed with the guess G those of the exact parameters T? (see above)

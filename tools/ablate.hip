@@ -148,6 +148,12 @@ int main(int argc, char** argv) {
                 else if (mode == 1) k_spec<false, 2><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS, FACES, COUNT, P, KEY);
                 else k_spec<false, 3><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS, FACES, COUNT, P, KEY);
             })});
+#define SPS(A) k_spec<false, 1, A><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS, FACES, COUNT, P, KEY)
+            r.push_back({"k_spec_rows", time_ms(s, iters, [&] { SPS(99); })});
+            r.push_back({"k_spec_bits", time_ms(s, iters, [&] { SPS(1); })});
+            r.push_back({"k_spec_ph2", time_ms(s, iters, [&] { SPS(12); })});
+            r.push_back({"k_spec_ccl", time_ms(s, iters, [&] { SPS(2); })});
+            r.push_back({"k_spec_keys", time_ms(s, iters, [&] { SPS(3); })});
         }
         // compute-bound variants: every tile reads one of 8 tiles that stay in L2 (tile origins
         // z = y = 0, x = 64 (ix % 8)); outputs per tile as usual
@@ -174,6 +180,14 @@ int main(int argc, char** argv) {
             r.push_back({"k_spec_cached", time_ms(s, iters, [&] {
                 k_spec<false, 1><<<(unsigned)nt, NTHREADS, 0, s>>>(gc, sa, in, nullptr, BITS, FACES, COUNT, P, KEY);
             })});
+#define SPC(A) k_spec<false, 1, A><<<(unsigned)nt, NTHREADS, 0, s>>>(gc, sa, in, nullptr, BITS, FACES, COUNT, P, KEY)
+            r.push_back({"k_spec_rows_cached", time_ms(s, iters, [&] { SPC(99); })});
+            r.push_back({"k_spec_bits_cached", time_ms(s, iters, [&] { SPC(1); })});
+            r.push_back({"k_spec_ph1_cached", time_ms(s, iters, [&] { SPC(11); })});
+            r.push_back({"k_spec_ph2_cached", time_ms(s, iters, [&] { SPC(12); })});
+            r.push_back({"k_spec_ph3_cached", time_ms(s, iters, [&] { SPC(13); })});
+            r.push_back({"k_spec_ccl_cached", time_ms(s, iters, [&] { SPC(2); })});
+            r.push_back({"k_spec_keys_cached", time_ms(s, iters, [&] { SPC(3); })});
             r.push_back({"k_block_stats_cached", time_ms(s, iters, [&] {
                 k_block_stats<<<(unsigned)nt, NTHREADS, 0, s>>>(gc, in, smin, smax, sflag);
             })});
