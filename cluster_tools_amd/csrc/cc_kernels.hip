@@ -848,6 +848,24 @@ __global__ void k_guess(int64_t nb, const u32* part, float thr, int mode, BlockP
     guess[b] = widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
 }
 
+// One launch for the front's initial state (it replaced nine memsets of ~4 us each): ordered
+// block min = ~0, max / NaN flag = 0, scalars, the k_fix count, seam overflow flags (+ their
+// "any" flags at big[nb] / iovf[nt]; fill = 1 sends everything to the global stitch), the
+// inter-pair counts, the root segments and the scan's extra element.
+__global__ __launch_bounds__(256) void k_clear_front(int64_t nb, int64_t nt, u32* smin, u32* smax_flag,
+                                                     u64* scalars, u32* FIX, u8* big, u8* iovf, u32* ipc,
+                                                     u32* seg, u32* rc_end, u8 fill) {
+    CC_FOR(i, (nt + 1 > 2 * nb + 1 ? nt + 1 : 2 * nb + 1)) {
+        if (i < nb) smin[i] = 0xFFFFFFFFu;
+        if (i < 2 * nb) { smax_flag[i] = 0u; seg[i] = 0u; }
+        if (i <= nb) big[i] = fill;
+        if (i <= nt) iovf[i] = fill;
+        if (i < nt) ipc[i] = 0u;
+        if (i < 4) scalars[i] = 0ull;
+        if (i == 0) { FIX[0] = 0u; rc_end[0] = 0u; }
+    }
+}
+
 struct SpecArgs {
     const BlockParam* guess;
     u32* smin; u32* smax; u32* sflag;
@@ -1688,9 +1706,9 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* _
     }
     if (lane == 0) {
         PC[t] = na < TPC ? na : TPC;
-        if (na > TPC) big[ti.block] = 1;
+        if (na > TPC) { big[ti.block] = 1; big[g.n_blocks] = 1; }
         IPC[t] = ni < TPI ? ni : TPI;
-        if (ni > TPI) iovf[t] = 1;
+        if (ni > TPI) { iovf[t] = 1; iovf[g.n_tiles] = 1; }
     }
 }
 
@@ -1767,28 +1785,35 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_stitch(Geom g, const face_t* 
                                                           const u64* __restrict__ K, const u8* __restrict__ big,
                                                           const u8* __restrict__ only) {
     __shared__ u32 Sall[SP_WAVES][FACE_STRIDE];
+    // the common case is nothing to do: big[n_blocks] / only[n_tiles] are "any block / tile
+    // flagged" (set with the per-block / per-tile flags), so a small grid reads one flag and
+    // leaves; otherwise it walks every tile
+    if (INTER ? (only && !only[g.n_tiles]) : !big[g.n_blocks]) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t t = (int64_t)blockIdx.x * SP_WAVES + w;
-    bool active = t < g.n_tiles;
     u32* S = Sall[w];
-    TileInfo ti;
-    if (active) {
-        ti = tile_info(g, t);
-        if (INTER)
-            active = (!only || only[t]) && ((ti.iz > 0 && g.tblk[0][ti.iz] != g.tblk[0][ti.iz - 1]) ||
-                     (ti.iy > 0 && g.tblk[1][ti.iy] != g.tblk[1][ti.iy - 1]) ||
-                     (ti.ix > 0 && g.tblk[2][ti.ix] != g.tblk[2][ti.ix - 1]));
-        else
-            active = big[ti.block] != 0;
-        if (active) stage_faces(g, FACES, t, ti, S, lane, 64);
-    }
-    __syncthreads();
-    if (!active) return;
     const u32 capu = (u32)g.cap;
-    stitch_tile<INTER>(g, FACES, S, t, ti, lane, 64, [&](int64_t t1, u32 e1, int64_t t2, u32 e2) {
-        const u32 a = (u32)(t1 * capu) + (e1 & FK_MASK), b = (u32)(t2 * capu) + (e2 & FK_MASK);
-        if (wave_first(((u64)a << 32) | b)) gunion(P, K, a, b);
-    });
+    for (int64_t t0 = (int64_t)blockIdx.x * SP_WAVES; t0 < g.n_tiles; t0 += (int64_t)gridDim.x * SP_WAVES) {
+        const int64_t t = t0 + w;
+        bool active = t < g.n_tiles;
+        TileInfo ti;
+        if (active) {
+            ti = tile_info(g, t);
+            if (INTER)
+                active = (!only || only[t]) && ((ti.iz > 0 && g.tblk[0][ti.iz] != g.tblk[0][ti.iz - 1]) ||
+                         (ti.iy > 0 && g.tblk[1][ti.iy] != g.tblk[1][ti.iy - 1]) ||
+                         (ti.ix > 0 && g.tblk[2][ti.ix] != g.tblk[2][ti.ix - 1]));
+            else
+                active = big[ti.block] != 0;
+            if (active) stage_faces(g, FACES, t, ti, S, lane, 64);
+        }
+        __syncthreads();
+        if (active)
+            stitch_tile<INTER>(g, FACES, S, t, ti, lane, 64, [&](int64_t t1, u32 e1, int64_t t2, u32 e2) {
+                const u32 a = (u32)(t1 * capu) + (e1 & FK_MASK), b = (u32)(t2 * capu) + (e2 & FK_MASK);
+                if (wave_first(((u64)a << 32) | b)) gunion(P, K, a, b);
+            });
+        __syncthreads();
+    }
 }
 
 __device__ __forceinline__ u32 lfind_k(lds_u32* par, u32 x) {
@@ -1845,7 +1870,7 @@ __global__ __launch_bounds__(SB_THREADS) void k_block_uf(Geom g, const u32* __re
     const int nz = g.btn[0][bz], ny = g.btn[1][by], nx = g.btn[2][bx];
     const int ntb = nz * ny * nx;
     if (ntb > SB_MAXT) {
-        if (tid == 0) big[b] = 1;
+        if (tid == 0) { big[b] = 1; big[g.n_blocks] = 1; }
         return;
     }
     auto tile_of = [&](int lt) -> int64_t {
@@ -1878,7 +1903,7 @@ __global__ __launch_bounds__(SB_THREADS) void k_block_uf(Geom g, const u32* __re
     __syncthreads();
     const u32 N = noff[ntb], M = poff[ntb];
     if (N > SB_LCAP) {
-        if (tid == 0) big[b] = 1;
+        if (tid == 0) { big[b] = 1; big[g.n_blocks] = 1; }
         return;
     }
     for (u32 i = tid; i < N; i += SB_THREADS) {

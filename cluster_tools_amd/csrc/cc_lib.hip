@@ -217,9 +217,6 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     u32* smin = c->bstat.as<u32>();
     u32* smax = smin + nb;
     u32* sflag = smax + nb;
-    HIP_OK(hipMemsetAsync(smin, 0xFF, nb * sizeof(u32), s));
-    HIP_OK(hipMemsetAsync(smax, 0x00, 2 * nb * sizeof(u32), s));
-    HIP_OK(hipMemsetAsync(c->scalars.p, 0, 4 * sizeof(u64), s));
 
     BlockParam* bp = c->bparam.as<BlockParam>();
     u64* BITS = c->bits.as<u64>();
@@ -237,7 +234,21 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         u32* TB = c->spec.as<u32>();
         u32* SPART = TB + 4 * nt;
         u32* FIX = SPART + 4 * SAMPLE_PARTS * nb;
-        HIP_OK(hipMemsetAsync(FIX, 0, sizeof(u32), s));
+        // seam outputs and flags (big[nb] / iovf[nt]: "any" flags of the global-stitch fallback)
+        c->big.ensure(nb + 1);
+        c->pairsl.ensure((size_t)nt * TPC * sizeof(u64));
+        c->pc.ensure(nt * sizeof(u32));
+        c->ipairs.ensure((size_t)nt * TPI * sizeof(u64));
+        c->ipc.ensure(nt * sizeof(u32));
+        c->iovf.ensure(nt + 1);
+        c->rc.ensure((nt + 1) * sizeof(u32));
+        c->roff.ensure((nt + 1) * sizeof(u32));
+        const bool lds_seams = !(c->debug & CC_DEBUG_GLOBAL_STITCH);
+        launch(c, "k_clear_front", [&] {
+            k_clear_front<<<grid1d(std::max(nt + 1, 2 * nb + 1)), 256, 0, s>>>(
+                nb, nt, smin, smax, c->scalars.as<u64>(), FIX, c->big.as<u8>(), c->iovf.as<u8>(), c->ipc.as<u32>(),
+                c->seg.as<u32>(), c->rc.as<u32>() + nt, lds_seams ? 0 : 1);
+        });
         launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART); });
         launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, mode, guess); });
         if (const char* e = std::getenv("CC_SPEC"); e && std::string(e) == "0")     // test hook: no guesses
@@ -246,19 +257,6 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         sa.guess = guess;
         sa.smin = smin; sa.smax = smax; sa.sflag = sflag;
         sa.TB = TB;
-        // seam outputs (k_seams sets flags, so they are cleared first)
-        c->big.ensure(nb);
-        c->pairsl.ensure((size_t)nt * TPC * sizeof(u64));
-        c->pc.ensure(nt * sizeof(u32));
-        c->ipairs.ensure((size_t)nt * TPI * sizeof(u64));
-        c->ipc.ensure(nt * sizeof(u32));
-        c->iovf.ensure(nt);
-        const bool lds_seams = !(c->debug & CC_DEBUG_GLOBAL_STITCH);
-        auto clear_seams = [&] {
-            HIP_OK(hipMemsetAsync(c->big.p, lds_seams ? 0 : 1, nb, s));
-            HIP_OK(hipMemsetAsync(c->iovf.p, lds_seams ? 0 : 1, nt, s));
-            HIP_OK(hipMemsetAsync(c->ipc.p, 0, nt * sizeof(u32), s));
-        };
         auto seams = [&](hipStream_t q, int64_t t0, int64_t t1) {
             launch_on(c, q, "k_seams", [&] {
                 k_seams<0><<<(unsigned)((t1 - t0 + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, q>>>(
@@ -266,7 +264,6 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
                     c->ipc.as<u32>(), c->iovf.as<u8>(), t0, t1, nullptr);
             });
         };
-        clear_seams();
         // The front runs in chunks of whole tile z-layers.  The seams of a chunk read only its
         // faces and those of the layers below, so k_seams of chunk i runs on the side stream
         // while k_spec of chunk i + 1 streams the input (k_seams is latency-bound, k_spec
@@ -336,12 +333,11 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             k_block_uf<<<(unsigned)nb, SB_THREADS, 0, s>>>(g, COUNT, c->pairsl.as<u64>(), c->pc.as<u32>(), P, KR, big);
         });
     }
-    launch(c, "k_stitch_intra", [&] { k_stitch<false><<<(unsigned)((nt + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(g, FACES, P, KR, big, nullptr); });
+    const unsigned stitch_grid = (unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, 2048);
+    launch(c, "k_stitch_intra", [&] { k_stitch<false><<<stitch_grid, SP_WAVES * 64, 0, s>>>(g, FACES, P, KR, big, nullptr); });
 
     // block-local roots: per-tile counts -> exclusive scan -> one host read of the total (the one
     // mid-run host sync; it sizes the radix sort)
-    c->rc.ensure((nt + 1) * sizeof(u32));
-    c->roff.ensure((nt + 1) * sizeof(u32));
     u32* RC = c->rc.as<u32>();
     u32* ROFF = c->roff.as<u32>();
     launch(c, "k_count_roots", [&] { k_count_roots<<<grid1d(nt, WAVES), NTHREADS, 0, s>>>(g, COUNT, P, RC); });
@@ -349,7 +345,6 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         size_t tmp_bytes = 0;
         HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, RC, ROFF, (int)nt + 1, s));
         c->cub_tmp.ensure(tmp_bytes);
-        HIP_OK(hipMemsetAsync(RC + nt, 0, sizeof(u32), s));
         launch(c, "scan_roots", [&] {
             HIP_OK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, RC, ROFF, (int)nt + 1, s));
         });
@@ -372,7 +367,6 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     u64* values = c->values.as<u64>();
     u64* offsets = c->offsets.as<u64>();
     u64* scalars = c->scalars.as<u64>();
-    HIP_OK(hipMemsetAsync(seg_start, 0, 2 * nb * sizeof(u32), s));
     if (nr > 0) {
         launch(c, "k_collect_roots", [&] { k_collect_roots<<<grid1d(nt, WAVES), NTHREADS, 0, s>>>(g, COUNT, P, KR, ROFF, keys, vals); });
         int end_bit = KEY_BITS;
@@ -446,7 +440,8 @@ static void phase_rid(cc_ctx* c, uint64_t base) {
             k_inter_union<<<grid, SP_WAVES * 64, 0, s>>>(g, c->ipairs.as<u64>(), c->ipc.as<u32>(), c->P.as<u32>(), c->KR.as<u64>());
         });
         // tiles whose block-face pairs overflowed their list (and every tile under CC_DEBUG_GLOBAL_STITCH)
-        launch(c, "k_stitch_inter", [&] { k_stitch<true><<<grid, SP_WAVES * 64, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), c->big.as<u8>(), c->iovf.as<u8>()); });
+        const unsigned stitch_grid = (unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, 2048);
+        launch(c, "k_stitch_inter", [&] { k_stitch<true><<<stitch_grid, SP_WAVES * 64, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), c->big.as<u8>(), c->iovf.as<u8>()); });
     }
     st.n_map = 0;
     st.stage = 2;
