@@ -205,6 +205,36 @@ __device__ __forceinline__ void gunion(u32* P, const u64* K, u32 a, u32 b) {
 #define CC_FOR(i, n) \
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)(n); i += (int64_t)gridDim.x * blockDim.x)
 
+// the roots of a and b, both walks advancing together (their loads in flight at once; path
+// halving as gfind)
+__device__ __forceinline__ void gfind2(u32* P, u32& a, u32& b) {
+    while (true) {
+        const u32 pa = gload(P + a), pb = gload(P + b);
+        const bool da = pa == a, db = pb == b;
+        if (da && db) return;
+        const u32 ga = da ? a : gload(P + pa), gb = db ? b : gload(P + pb);
+        if (!da) {
+            if (ga != pa) gstore(P + a, ga);
+            a = ga;
+        }
+        if (!db) {
+            if (gb != pb) gstore(P + b, gb);
+            b = gb;
+        }
+    }
+}
+
+// gunion for two nodes whose roots were just found (usually still roots: one round of loads)
+__device__ __forceinline__ void gunion_roots(u32* P, const u64* K, u32 a, u32 b) {
+    while (true) {
+        gfind2(P, a, b);
+        if (a == b) return;
+        const u64 ka = K[a], kb = K[b];
+        if (ka < kb) { const u32 t = a; a = b; b = t; }
+        if (atomicCAS(P + a, a, b) == a) return;
+    }
+}
+
 // ---- block-wide exclusive scan (NTHREADS threads) ----
 __device__ __forceinline__ u32 block_excl_scan(u32 v, u32* scratch, u32* total) {
     const int tid = cc_tid(), lane = tid & 63, wave = tid >> 6;

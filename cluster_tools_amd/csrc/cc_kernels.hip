@@ -1761,19 +1761,41 @@ __global__ __launch_bounds__(256) void k_block_face_flags(Geom g, const face_t* 
     }
 }
 
-// Block-face unions from the k_seams lists, one wave per tile: node pairs -> current roots,
+// Block-face unions from the k_seams lists.  A wave takes 64 consecutive tiles and walks their
+// lists as one flat sequence, one pair per lane (a wave per tile left most lanes idle and paid
+// a dependent-load chain per tile); node pairs -> current roots (both finds together),
 // duplicate root pairs dropped per wave, union keyed by rid (the smaller rid becomes the root).
-__global__ __launch_bounds__(SP_WAVES * 64) void k_inter_union(Geom g, const u64* __restrict__ IPAIRS,
-                                                               const u32* __restrict__ IPC, u32* P,
-                                                               const u64* __restrict__ K) {
+__global__ __launch_bounds__(256) void k_inter_union(Geom g, const u64* __restrict__ IPAIRS,
+                                                     const u32* __restrict__ IPC, u32* P,
+                                                     const u64* __restrict__ K) {
     const int lane = threadIdx.x & 63;
-    const int64_t t = (int64_t)blockIdx.x * SP_WAVES + (threadIdx.x >> 6);
-    if (t >= g.n_tiles) return;
-    const u32 n = IPC[t];
-    for (u32 i = lane; i < n; i += 64) {
-        const u64 pr = IPAIRS[t * TPI + i];
-        const u32 ra = gfind(P, (u32)(pr >> 32)), rb = gfind(P, (u32)pr);
-        if (ra != rb && wave_first(((u64)ra << 32) | rb)) gunion(P, K, ra, rb);
+    const int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+    if (t0 >= g.n_tiles) return;
+    const int64_t tl = t0 + lane;
+    const u32 cnt = tl < g.n_tiles ? IPC[tl] : 0u;
+    u32 incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const u32 y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const u32 total = __shfl(incl, 63, 64), excl = incl - cnt;
+    for (u32 j = 0; j < total; j += 64) {
+        const u32 q = j + lane;
+        // owner tile of flat pair q: the last lane whose exclusive offset is <= q
+        int lo = 0;
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1) {
+            const u32 e = (u32)__shfl((int)excl, lo + st, 64);
+            if (e <= q) lo += st;
+        }
+        const u32 eo = (u32)__shfl((int)excl, lo, 64);
+        if (q < total) {
+            const u64 pr = IPAIRS[(t0 + lo) * TPI + (q - eo)];
+            u32 ra = (u32)(pr >> 32), rb = (u32)pr;
+            gfind2(P, ra, rb);
+            if (ra != rb && wave_first(((u64)ra << 32) | rb)) gunion_roots(P, K, ra, rb);
+        }
     }
 }
 

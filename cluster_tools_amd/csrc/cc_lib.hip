@@ -435,9 +435,8 @@ static void phase_rid(cc_ctx* c, uint64_t base) {
         }
     }
     if (!st.local_only && !st.identity_lut) {
-        const unsigned grid = (unsigned)((nt + SP_WAVES - 1) / SP_WAVES);
         launch(c, "k_inter_union", [&] {
-            k_inter_union<<<grid, SP_WAVES * 64, 0, s>>>(g, c->ipairs.as<u64>(), c->ipc.as<u32>(), c->P.as<u32>(), c->KR.as<u64>());
+            k_inter_union<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(g, c->ipairs.as<u64>(), c->ipc.as<u32>(), c->P.as<u32>(), c->KR.as<u64>());
         });
         // tiles whose block-face pairs overflowed their list (and every tile under CC_DEBUG_GLOBAL_STITCH)
         const unsigned stitch_grid = (unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, 2048);
