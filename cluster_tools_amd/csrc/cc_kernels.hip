@@ -1877,9 +1877,14 @@ __device__ __forceinline__ int flat_tile(const u32* off, int n, u32 i) {
 
 // The block's tiles are visited as flat index ranges (nodes, pairs) so that every global load of
 // a phase is in flight at once; the per-tile loops this replaces waited on one tile at a time.
+// RL / RCB (nullable): the block's roots in first-voxel order -- skimage's label order inside the
+// block (block_components.py:179) -- as node ids in RL[b * SB_LCAP + rank], their count in RCB[b]
+// (replaces the global count / collect / radix sort of every root when no block needed the
+// global fallback)
 __global__ __launch_bounds__(SB_THREADS) void k_block_uf(Geom g, const u32* __restrict__ COUNT,
                                                          const u64* __restrict__ PAIRS, const u32* __restrict__ PC,
-                                                         u32* P, const u64* __restrict__ KEY, u8* big) {
+                                                         u32* P, const u64* __restrict__ KEY, u8* big, u32* RL,
+                                                         u32* RCB) {
     __shared__ u32 noff[SB_MAXT + 1];      // nodes of the block's tiles, exclusive scan
     __shared__ u32 poff[SB_MAXT + 1];      // intra pairs of the block's tiles, exclusive scan
     __shared__ u32 lpar[SB_LCAP];
@@ -1949,6 +1954,98 @@ __global__ __launch_bounds__(SB_THREADS) void k_block_uf(Geom g, const u32* __re
             P[(u64)tile_of(lt) * g.cap + (i - noff[lt])] = (u32)((u64)tile_of(lo) * g.cap + (r - noff[lo]));
         }
     }
+    if (!RL) return;
+    // roots sorted by first voxel: (key << 13 | local index) packed, compacted into lkey (the keys
+    // of the roots are taken into registers first), bitonic sort in LDS
+    static_assert(SB_LCAP <= (1 << 13) && KEY_BITS + 13 <= 64, "packed root keys");
+    __shared__ u32 nroot;
+    constexpr int PER = SB_LCAP / SB_THREADS;
+    u64 mine[PER];
+    if (tid == 0) nroot = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const u32 i = tid + j * SB_THREADS;
+        mine[j] = (i < N && lpar[i] == i) ? (lkey[i] << 13) | i : ~0ull;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+        if (mine[j] != ~0ull) lkey[atomicAdd(&nroot, 1u)] = mine[j];
+    __syncthreads();
+    const u32 R = nroot;
+    u32 R2 = 1;
+    while (R2 < R) R2 <<= 1;
+    for (u32 i = R + tid; i < R2; i += SB_THREADS) lkey[i] = ~0ull;
+    __syncthreads();
+    for (u32 k = 2; k <= R2; k <<= 1)
+        for (u32 j = k >> 1; j > 0; j >>= 1) {
+            for (u32 i = tid; i < R2; i += SB_THREADS) {
+                const u32 l = i ^ j;
+                if (l > i) {
+                    const u64 a = lkey[i], c = lkey[l];
+                    if ((a > c) == ((i & k) == 0)) { lkey[i] = c; lkey[l] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    for (u32 r = tid; r < R; r += SB_THREADS) {
+        const u32 i = (u32)(lkey[r] & 0x1FFFu);
+        const int lt = flat_tile(noff, ntb, i);
+        RL[(u64)b * SB_LCAP + r] = (u32)((u64)tile_of(lt) * g.cap + (i - noff[lt]));
+    }
+    if (tid == 0) RCB[b] = R;
+}
+
+// Per-block root counts -> block values (n + 1, or 0 for an empty block: block_components.py:175-182),
+// their exclusive scan (merge_offsets.py:115-120) and that of the root counts; scalars[0] = sum of
+// the values, scalars[2] = number of roots.  One workgroup, chunks of SB_THREADS blocks.
+__global__ __launch_bounds__(SB_THREADS) void k_block_scan(int64_t nb, const u32* __restrict__ RCB, u32* ROFFB,
+                                                           u64* values, u64* offsets, u64* scalars) {
+    __shared__ u64 wsum[2][SB_THREADS / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    u64 carry_r = 0, carry_v = 0;
+    for (int64_t b0 = 0; b0 < nb; b0 += SB_THREADS) {
+        const int64_t b = b0 + tid;
+        const u64 r = b < nb ? RCB[b] : 0ull, v = r ? r + 1 : 0ull;
+        u64 xr = r, xv = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const u64 yr = __shfl_up(xr, o, 64), yv = __shfl_up(xv, o, 64);
+            if (lane >= o) { xr += yr; xv += yv; }
+        }
+        if (lane == 63) { wsum[0][wave] = xr; wsum[1][wave] = xv; }
+        __syncthreads();
+        u64 br = 0, bv = 0, tr = 0, tv = 0;
+#pragma unroll
+        for (int w = 0; w < SB_THREADS / 64; ++w) {
+            if (w < wave) { br += wsum[0][w]; bv += wsum[1][w]; }
+            tr += wsum[0][w]; tv += wsum[1][w];
+        }
+        if (b < nb) {
+            ROFFB[b] = (u32)(carry_r + br + xr - r);
+            values[b] = v;
+            offsets[b] = carry_v + bv + xv - v;
+        }
+        carry_r += tr; carry_v += tv;
+        __syncthreads();
+    }
+    if (tid == 0) { scalars[0] = carry_v; scalars[2] = carry_r; }
+}
+
+// the sorted per-block root lists as the (key, node) arrays of the generic path: keys2 = block <<
+// KEY_BITS | first voxel, vals2 = node, segment [seg_start, seg_end) of each block
+__global__ __launch_bounds__(256) void k_emit_roots(const u32* __restrict__ RL, const u32* __restrict__ RCB,
+                                                    const u32* __restrict__ ROFFB, const u64* __restrict__ KEY,
+                                                    u64* keys2, u32* vals2, u32* seg_start, u32* seg_end) {
+    const int64_t b = blockIdx.x;
+    const u32 R = RCB[b], off = ROFFB[b];
+    for (u32 r = threadIdx.x; r < R; r += 256) {
+        const u32 node = RL[(u64)b * SB_LCAP + r];
+        keys2[off + r] = ((u64)b << KEY_BITS) | KEY[node];
+        vals2[off + r] = node;
+    }
+    if (threadIdx.x == 0) { seg_start[b] = off; seg_end[b] = off + R; }
 }
 
 constexpr int WAVES = NTHREADS / 64;
@@ -2053,12 +2150,9 @@ __global__ void k_lut(int64_t n, const u32* vals, u32* P, const u64* KR, u64 bas
     if (r == node && rep == KR[r]) atomicAdd((unsigned long long*)&scalars[1], 1ull);   // components owned here
 }
 
-// final label of every node.  FIN may alias KR when !LOCAL: a root's entry KR[root] = rid is
-// overwritten with apply_map(rid) while other waves may still read it.  That is safe because
-// apply_map is idempotent -- V[i] is the smallest id of its seam set, and that id is in U with
-// V = itself -- so a reader computes apply_map(rid) or apply_map(apply_map(rid)), the same value
-// (tests/test_gpu_sharded.py checks the sharded labels against the oracle).  LOCAL (stage-level
-// block_components) writes the block-local skimage label rid - offset into a separate FIN.
+// final label of every node into FIN (a separate buffer).  LOCAL (stage-level block_components)
+// writes the block-local skimage label rid - offset; the fused path does not run this kernel --
+// k_pass2<true> resolves each tile component's label itself, reading KR without writing it.
 template <bool LOCAL>
 __global__ __launch_bounds__(NTHREADS) void k_finalize(Geom g, const u32* COUNT, u32* P, const u64* KR,
                                                        const u64* offsets, const u64* U, const u64* V,
@@ -2229,8 +2323,13 @@ __device__ __forceinline__ void store2(u64* __restrict__ out, int64_t idx, u64 v
     }
 }
 
+// UF (the fused path, in place of a k_finalize pass over all nodes): the final label of tile
+// component k is apply_map(KR[root of its node]); the finds are issued before the tile CCL so
+// their dependent loads overlap it.  !UF: FIN holds the label of every node (k_finalize<true>).
+template <bool UF>
 __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restrict__ BITS, const u32* COUNT,
-                                                    const u64* __restrict__ FIN, u64* __restrict__ out) {
+                                                    const u64* __restrict__ FIN, u32* P, const u64* U, const u64* V,
+                                                    int64_t m, u64* __restrict__ out) {
     __shared__ u64 rows[NROWS];             // split bit rows (see tile_ccl)
     __shared__ TileCCL T;
     __shared__ u64 lab[LABCAP];
@@ -2254,11 +2353,23 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
         }
         return;
     }
+    const u32 base = (u32)(t * g.cap);
+    auto label = [&](u32 node) -> u64 { return UF ? apply_map(FIN[gfind(P, node)], U, V, m) : FIN[node]; };
+    constexpr int LPT = LABCAP / NTHREADS;
+    u64 lv[LPT];
+#pragma unroll
+    for (int j = 0; j < LPT; ++j) {
+        const u32 k = tid + j * NTHREADS;
+        lv[j] = k < R ? label(base + k) : 0ull;
+    }
     for (int i = tid; i < NROWS; i += NTHREADS) rows[i] = BITS[t * NROWS + i];
     __syncthreads();
     tile_ccl(rows, T, (u32*)lab);
-    const u32 base = (u32)(t * g.cap);
-    for (u32 k = tid; k < R && k < LABCAP; k += NTHREADS) lab[k] = FIN[base + k];
+#pragma unroll
+    for (int j = 0; j < LPT; ++j) {
+        const u32 k = tid + j * NTHREADS;
+        if (k < R) lab[k] = lv[j];
+    }
     __syncthreads();
     for (int c = tid; c < NC; c += NTHREADS) {
         const int cz = c / (CY * CX), cy = (c / CX) % CY, cx = c % CX;
@@ -2270,7 +2381,7 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
         if (m) {
             const u32 k = cube_k(T, c);
             if (k < LABCAP) v = lab[k];
-            else v = __builtin_nontemporal_load(FIN + base + k);
+            else v = UF ? label(base + k) : __builtin_nontemporal_load(FIN + base + k);
         }
         const bool two = 2 * cx + 1 < ti.lx;
 #pragma unroll
@@ -2329,7 +2440,6 @@ template __global__ void k_fix<true>(Geom, const u32*, const BlockParam*, const 
 template __global__ void k_seams<0>(Geom, const face_t*, u64*, u32*, u8*, u64*, u32*, u8*, int64_t, int64_t, const u32*);
 template __global__ void k_stitch<false>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_stitch<true>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);
-template __global__ void k_finalize<false>(Geom, const u32*, u32*, const u64*, const u64*, const u64*, const u64*, int64_t, u64*);
 template __global__ void k_finalize<true>(Geom, const u32*, u32*, const u64*, const u64*, const u64*, const u64*, int64_t, u64*);
 template __global__ void k_plane_labels<false>(Geom, const face_t*, u32*, const u64*, u64*, u64);
 template __global__ void k_plane_labels<true>(Geom, const face_t*, u32*, const u64*, u64*, u64);

@@ -53,7 +53,7 @@ struct cc_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t side = nullptr;      // k_seams of finished front chunks, concurrent with the next chunk
     // workspace
-    DevBuf tiles, bstat, bparam, bits, faces, count, rc, roff, P, KR, FIN, keys, keys2, vals, vals2, seg,
+    DevBuf tiles, bstat, bparam, bits, faces, count, rc, roff, rl, rcb, P, KR, FIN, keys, keys2, vals, vals2, seg,
         values, offsets, lut, cub_tmp, scalars, scalars2, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2,
         flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf, spec, mark, bflag,
         ev_main, ev_z, ev_seg, ev_gt, ev_flag, ev_part,   // evaluation (cc_eval.hip)
@@ -328,16 +328,56 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         }
     }
     u8* big = c->big.as<u8>();
-    if (!(c->debug & CC_DEBUG_GLOBAL_STITCH)) {
+    u32* seg_start = c->seg.as<u32>();
+    u32* seg_end = seg_start + nb;
+    u64* values = c->values.as<u64>();
+    u64* offsets = c->offsets.as<u64>();
+    u64* scalars = c->scalars.as<u64>();
+    auto ensure_roots = [&](int64_t nr) {
+        c->keys.ensure(std::max<int64_t>(1, nr) * sizeof(u64));
+        c->keys2.ensure(std::max<int64_t>(1, nr) * sizeof(u64));
+        c->vals.ensure(std::max<int64_t>(1, nr) * sizeof(u32));
+        c->vals2.ensure(std::max<int64_t>(1, nr) * sizeof(u32));
+    };
+    const bool block_uf = !(c->debug & CC_DEBUG_GLOBAL_STITCH);
+    // k_block_uf also ranks each block's roots in first-voxel order (RL / RCB); that ranking is
+    // complete unless some block took the global fallback (big[nb])
+    c->rl.ensure((size_t)nb * SB_LCAP * sizeof(u32));
+    c->rcb.ensure(2 * nb * sizeof(u32));
+    u32* RL = c->rl.as<u32>();
+    u32* RCB = c->rcb.as<u32>();
+    u32* ROFFB = RCB + nb;
+    if (block_uf) {
         launch(c, "k_block_uf", [&] {
-            k_block_uf<<<(unsigned)nb, SB_THREADS, 0, s>>>(g, COUNT, c->pairsl.as<u64>(), c->pc.as<u32>(), P, KR, big);
+            k_block_uf<<<(unsigned)nb, SB_THREADS, 0, s>>>(g, COUNT, c->pairsl.as<u64>(), c->pc.as<u32>(), P, KR, big, RL, RCB);
         });
     }
     const unsigned stitch_grid = (unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, 2048);
     launch(c, "k_stitch_intra", [&] { k_stitch<false><<<stitch_grid, SP_WAVES * 64, 0, s>>>(g, FACES, P, KR, big, nullptr); });
 
-    // block-local roots: per-tile counts -> exclusive scan -> one host read of the total (the one
-    // mid-run host sync; it sizes the radix sort)
+    // one mid-run host read: whether any block took the fallback, and the number of roots (it
+    // sizes the root arrays / LUT)
+    u8 any_big = 1;
+    u64 nr_blocks = 0;
+    if (block_uf) {
+        launch(c, "k_block_scan", [&] { k_block_scan<<<1, SB_THREADS, 0, s>>>(nb, RCB, ROFFB, values, offsets, scalars); });
+        HIP_OK(hipMemcpyAsync(&nr_blocks, scalars + 2, sizeof(u64), hipMemcpyDeviceToHost, s));
+        HIP_OK(hipMemcpyAsync(&any_big, big + nb, 1, hipMemcpyDeviceToHost, s));
+        sync(c);
+    }
+    if (!any_big) {
+        const int64_t nr = (int64_t)nr_blocks;
+        st.nr = nr;
+        ensure_roots(nr);
+        launch(c, "k_emit_roots", [&] {
+            k_emit_roots<<<(unsigned)nb, 256, 0, s>>>(RL, RCB, ROFFB, KR, c->keys2.as<u64>(), c->vals2.as<u32>(), seg_start, seg_end);
+        });
+        st.stage = 1;
+        return;
+    }
+
+    // generic path (some block was stitched in global memory): block-local roots of every tile
+    // -> per-tile counts -> exclusive scan -> host read of the total (sizes the radix sort)
     u32* RC = c->rc.as<u32>();
     u32* ROFF = c->roff.as<u32>();
     launch(c, "k_count_roots", [&] { k_count_roots<<<grid1d(nt, WAVES), NTHREADS, 0, s>>>(g, COUNT, P, RC); });
@@ -354,19 +394,12 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     sync(c);
     const int64_t nr = n_roots_h;
     st.nr = nr;
-    c->keys.ensure(std::max<int64_t>(1, nr) * sizeof(u64));
-    c->keys2.ensure(std::max<int64_t>(1, nr) * sizeof(u64));
-    c->vals.ensure(std::max<int64_t>(1, nr) * sizeof(u32));
-    c->vals2.ensure(std::max<int64_t>(1, nr) * sizeof(u32));
+    ensure_roots(nr);
     u64* keys = c->keys.as<u64>();
     u64* keys2 = c->keys2.as<u64>();
     u32* vals = c->vals.as<u32>();
     u32* vals2 = c->vals2.as<u32>();
-    u32* seg_start = c->seg.as<u32>();
-    u32* seg_end = seg_start + nb;
-    u64* values = c->values.as<u64>();
-    u64* offsets = c->offsets.as<u64>();
-    u64* scalars = c->scalars.as<u64>();
+    HIP_OK(hipMemsetAsync(seg_start, 0, 2 * nb * sizeof(u32), s));
     if (nr > 0) {
         launch(c, "k_collect_roots", [&] { k_collect_roots<<<grid1d(nt, WAVES), NTHREADS, 0, s>>>(g, COUNT, P, KR, ROFF, keys, vals); });
         int end_bit = KEY_BITS;
@@ -557,10 +590,13 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
         launch(c, "k_lut_init", [&] { k_lut_init<<<grid1d(lut_cap), 256, 0, s>>>(lut_cap, scalars, base, lut); });
         if (nr > 0)
             launch(c, "k_lut", [&] { k_lut<<<grid1d(nr), 256, 0, s>>>(nr, c->vals2.as<u32>(), P, KR, base, U, V, m, lut, scalars); });
-        launch(c, "k_finalize", [&] { k_finalize<false><<<grid1d(nt, WAVES), NTHREADS, 0, s>>>(g, COUNT, P, KR, offsets, U, V, m, KR); });
         c->lut_valid = true;
     }
-    launch(c, "k_pass2", [&] { k_pass2<<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, FIN, out); });
+    // the fused path resolves each tile component's final label inside k_pass2 (no k_finalize)
+    launch(c, "k_pass2", [&] {
+        if (st.local_only) k_pass2<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, FIN, nullptr, nullptr, nullptr, 0, out);
+        else k_pass2<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, KR, P, U, V, m, out);
+    });
 
     u64 sc[4] = {0, 0, 0, 0};
     HIP_OK(hipMemcpyAsync(sc, scalars, 4 * sizeof(u64), hipMemcpyDeviceToHost, s));
@@ -639,7 +675,7 @@ void cc_destroy(cc_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     if (c->side) (void)hipStreamSynchronize(c->side);
-    DevBuf* bufs[] = {&c->tiles, &c->bstat, &c->bparam, &c->bits, &c->faces, &c->count, &c->rc, &c->roff, &c->P, &c->KR,
+    DevBuf* bufs[] = {&c->tiles, &c->bstat, &c->bparam, &c->bits, &c->faces, &c->count, &c->rc, &c->roff, &c->rl, &c->rcb, &c->P, &c->KR,
                       &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
                       &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
