@@ -106,7 +106,9 @@ __device__ __forceinline__ TileInfo tile_info(const Geom& g, int64_t t) {
 }
 
 // IEEE-754 total order for non-NaN floats as unsigned ints (-0 < +0).
-__device__ __host__ __forceinline__ u32 f2ord(u32 u) { return (u & 0x80000000u) ? ~u : (u | 0x80000000u); }
+// (written as one xor with a sign-derived mask: v_ashrrev + v_bitop3 on gfx950, where the select
+// form took four VALU ops per voxel)
+__device__ __host__ __forceinline__ u32 f2ord(u32 u) { return u ^ ((u32)((int32_t)u >> 31) | 0x80000000u); }
 __device__ __host__ __forceinline__ u32 ord2f(u32 o) { return (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o; }
 
 // The reference's per-voxel predicate with block statistics (block_components.py:161,166-173).

@@ -735,6 +735,9 @@ __device__ __forceinline__ TileInfo uniform_ti(TileInfo ti) {
 // bounds miss the exact ones by about the extremes' sampling error, so a denser sample leaves
 // fewer tiles with a voxel in between; 1/512 left 8 % of the C3 tiles to k_fix)
 constexpr int SAMPLE_DZ = 4, SAMPLE_DY = 16;
+#ifndef CC_F4_SERIAL
+#define CC_F4_SERIAL 1
+#endif
 
 __device__ __forceinline__ void block_extent(const Geom& g, int64_t b, int e0[3], int el[3]) {
     const int bi[3] = {(int)(b / ((int64_t)g.nb[2] * g.nb[1])), (int)((b / g.nb[2]) % g.nb[1]), (int)(b % g.nb[2])};
@@ -891,17 +894,41 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
     const int tid = cc_tid(), lane = tid & 63, wave = wave_id();
     const u32 lo = p.lo, hi = p.hi;
-    u32 mn = 0xFFFFFFFFu, mx = 0u, A = 0u, B = 0xFFFFFFFFu, C = 0u, D = 0xFFFFFFFFu;
-    // one voxel: statistics, nearest values around the guessed bounds, foreground predicate
+    // Statistics: ordered min / max of every voxel, and the nearest values around the guessed
+    // bounds as the min / max of the wrapped distances k1 = o - lo and k2 = hi - o (mod 2^32) over
+    // the used voxels: o - lo puts every voxel at or above lo below every voxel under it, so
+    // min k1 gives the smallest value >= lo and max k1 the largest value < lo (hi - o likewise);
+    // no per-voxel select on the side of the bound (TB is derived once per tile below).
+    u32 mn = 0xFFFFFFFFu, mx = 0u, K1N = 0xFFFFFFFFu, K1X = 0u, K2N = 0xFFFFFFFFu, K2X = 0u;
+    auto fgp = [&](u32 o) -> bool { return SIDES == 1 ? o >= lo : SIDES == 2 ? o <= hi : (o >= lo && o <= hi); };
+    // one voxel (partial tiles)
     auto voxel = [&](float x, u32 mk) -> bool {
         const u32 o = f2ord(__float_as_uint(x));
         mn = min(mn, o);
         mx = max(mx, o);
-        const bool ge = o >= lo, le = o <= hi;
         const bool use = !HAS_MASK || mk != 0;
-        if (SIDES & 1) { A = max(A, use && !ge ? o : 0u); B = min(B, use && ge ? o : 0xFFFFFFFFu); }
-        if (SIDES & 2) { C = max(C, use && le ? o : 0u); D = min(D, use && !le ? o : 0xFFFFFFFFu); }
-        return use && (SIDES == 1 ? ge : SIDES == 2 ? le : ge && le);
+        if (SIDES & 1) { const u32 k = o - lo; K1N = min(K1N, use ? k : ~0u); K1X = max(K1X, use ? k : 0u); }
+        if (SIDES & 2) { const u32 k = hi - o; K2N = min(K2N, use ? k : ~0u); K2X = max(K2X, use ? k : 0u); }
+        return use && fgp(o);
+    };
+    // four voxels of one float4 (full tiles): the same, min / max folded three operands at a time
+    auto quad = [&](float4 v, uchar4 mk, bool fg[4]) {
+        const u32 o0 = f2ord(__float_as_uint(v.x)), o1 = f2ord(__float_as_uint(v.y));
+        const u32 o2 = f2ord(__float_as_uint(v.z)), o3 = f2ord(__float_as_uint(v.w));
+        mn = min(min(min(min(mn, o0), o1), o2), o3);
+        mx = max(max(max(max(mx, o0), o1), o2), o3);
+        const bool u0 = !HAS_MASK || mk.x, u1 = !HAS_MASK || mk.y, u2 = !HAS_MASK || mk.z, u3 = !HAS_MASK || mk.w;
+        if (SIDES & 1) {
+            const u32 k0 = o0 - lo, k1 = o1 - lo, k2 = o2 - lo, k3 = o3 - lo;
+            K1N = min(min(min(min(K1N, u0 ? k0 : ~0u), u1 ? k1 : ~0u), u2 ? k2 : ~0u), u3 ? k3 : ~0u);
+            K1X = max(max(max(max(K1X, u0 ? k0 : 0u), u1 ? k1 : 0u), u2 ? k2 : 0u), u3 ? k3 : 0u);
+        }
+        if (SIDES & 2) {
+            const u32 k0 = hi - o0, k1 = hi - o1, k2 = hi - o2, k3 = hi - o3;
+            K2N = min(min(min(min(K2N, u0 ? k0 : ~0u), u1 ? k1 : ~0u), u2 ? k2 : ~0u), u3 ? k3 : ~0u);
+            K2X = max(max(max(max(K2X, u0 ? k0 : 0u), u1 ? k1 : 0u), u2 ? k2 : 0u), u3 ? k3 : 0u);
+        }
+        fg[0] = u0 && fgp(o0); fg[1] = u1 && fgp(o1); fg[2] = u2 && fgp(o2); fg[3] = u3 && fgp(o3);
     };
     const bool f4 = ti.lz == TZ && ti.ly == TY && ti.lx == TX && ((ti.x0 | (int)(g.X & 3)) & 3) == 0;
     if (f4) {
@@ -920,17 +947,24 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         for (int z0 = 0; z0 < TZ; z0 += RZ4) {
             float4 v[RZ4];
             uchar4 mk[RZ4];
-#pragma unroll
-            for (int a = 0; a < RZ4; ++a) {
+            auto ld = [&](int a) {
                 v[a] = *reinterpret_cast<const float4*>(pz + (z0 + a) * sz);
                 if (HAS_MASK) mk[a] = *reinterpret_cast<const uchar4*>(mz + (z0 + a) * sz);
-            }
+            };
+            if (!CC_F4_SERIAL)
+#pragma unroll
+                for (int a = 0; a < RZ4; ++a) ld(a);
 #pragma unroll
             for (int a = 0; a < RZ4; ++a) {
-                const u64 b0 = __ballot(voxel(v[a].x, HAS_MASK ? (u32)mk[a].x : 1u));
-                const u64 b1 = __ballot(voxel(v[a].y, HAS_MASK ? (u32)mk[a].y : 1u));
-                const u64 b2 = __ballot(voxel(v[a].z, HAS_MASK ? (u32)mk[a].z : 1u));
-                const u64 b3 = __ballot(voxel(v[a].w, HAS_MASK ? (u32)mk[a].w : 1u));
+                if (CC_F4_SERIAL) {
+                    // each load issued right before its use, one in flight per wave (an empty asm
+                    // with a memory clobber keeps the next load below the previous processing)
+                    asm volatile("" ::: "memory");
+                    ld(a);
+                }
+                bool fg[4];
+                quad(v[a], HAS_MASK ? mk[a] : uchar4{}, fg);
+                const u64 b0 = __ballot(fg[0]), b1 = __ballot(fg[1]), b2 = __ballot(fg[2]), b3 = __ballot(fg[3]);
                 CC_WRITELANE2(R[0], R[1], (u32)b0, (u32)(b0 >> 32), z0 + a);
                 CC_WRITELANE2(R[2], R[3], (u32)b1, (u32)(b1 >> 32), z0 + a);
                 CC_WRITELANE2(R[4], R[5], (u32)b2, (u32)(b2 >> 32), z0 + a);
@@ -965,21 +999,33 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     for (int o = 32; o > 0; o >>= 1) {
         mn = min(mn, (u32)__shfl_xor(mn, o, 64));
         mx = max(mx, (u32)__shfl_xor(mx, o, 64));
-        if (SIDES & 1) { A = max(A, (u32)__shfl_xor(A, o, 64)); B = min(B, (u32)__shfl_xor(B, o, 64)); }
-        if (SIDES & 2) { C = max(C, (u32)__shfl_xor(C, o, 64)); D = min(D, (u32)__shfl_xor(D, o, 64)); }
+        if (SIDES & 1) { K1N = min(K1N, (u32)__shfl_xor(K1N, o, 64)); K1X = max(K1X, (u32)__shfl_xor(K1X, o, 64)); }
+        if (SIDES & 2) { K2N = min(K2N, (u32)__shfl_xor(K2N, o, 64)); K2X = max(K2X, (u32)__shfl_xor(K2X, o, 64)); }
     }
     if (lane == 0) {
-        red[0][wave] = mn; red[1][wave] = mx; red[2][wave] = A; red[3][wave] = B; red[4][wave] = C; red[5][wave] = D;
+        red[0][wave] = mn; red[1][wave] = mx; red[2][wave] = K1N; red[3][wave] = K1X; red[4][wave] = K2N;
+        red[5][wave] = K2X;
     }
     __syncthreads();
     if (tid == 0) {
         for (int w = 1; w < NTHREADS / 64; ++w) {
             mn = min(mn, red[0][w]); mx = max(mx, red[1][w]);
-            A = max(A, red[2][w]); B = min(B, red[3][w]); C = max(C, red[4][w]); D = min(D, red[5][w]);
+            K1N = min(K1N, red[2][w]); K1X = max(K1X, red[3][w]); K2N = min(K2N, red[4][w]); K2X = max(K2X, red[5][w]);
         }
         atomicMin(sa.smin + ti.block, mn);
         atomicMax(sa.smax + ti.block, mx);
         if (mx > 0xFF800000u || mn < 0x007FFFFFu) atomicOr(sa.sflag + ti.block, 1u);    // NaN
+        // TB from the wrapped distances: A = max used o < lo, B = min used o >= lo, C = max used
+        // o <= hi, D = min used o > hi (0 / ~0 when there is none)
+        u32 A = 0u, B = 0xFFFFFFFFu, C = 0u, D = 0xFFFFFFFFu;
+        if (SIDES & 1) {
+            if ((u64)K1N + lo < (1ull << 32)) B = K1N + lo;
+            if ((u64)K1X + lo >= (1ull << 32)) A = K1X + lo;
+        }
+        if (SIDES & 2) {
+            if (K2N <= hi) C = hi - K2N;
+            if (K2X > hi) D = hi - K2X;
+        }
         u32* tb = sa.TB + 4 * t;
         tb[0] = A; tb[1] = B; tb[2] = C; tb[3] = D;
     }
