@@ -1462,7 +1462,11 @@ __device__ __forceinline__ void seam_rows3(const face_t* S, const int mode[3], i
             u64 C = A & sh(B, dx);
             if (dx) C &= ~(sh(A, dx) | B);
             if (dr) C &= ~(Ad | sh(B0, dx));
-            for (u64 m = C & ~(C << 1); m; m &= m - 1) {
+            u64 m0 = C & ~(C << 1);
+            // a (0, 0) run starting where the row before also had a (0, 0) contact repeats that
+            // contact's pair (rows r - 1 and r are adjacent on both sides): only the topmost emits
+            if (!dr && !dx) m0 &= ~(Am & Bm);
+            for (u64 m = m0; m; m &= m - 1) {
                 const int x = __builtin_ctzll(m);
                 const u32 ka = FA[(r >> 1) * stride + (x >> 1)] & FK_MASK;
                 const u32 kb = FB[(rb >> 1) * stride + ((x + dx) >> 1)] & FK_MASK;
