@@ -23,6 +23,10 @@ __device__ __forceinline__ u64 rl_slot(const u64* keys, u64 mask, u64 key) {
 }
 
 constexpr int RL_Q = 8;      // loads per lane per wave iteration (RL_Q * VW voxels in flight)
+#ifndef CC_RL_QA
+#define CC_RL_QA 8
+#endif
+constexpr int RL_QA = CC_RL_QA;   // the same for k_rl_apply
 constexpr int RL_WG = 512;   // threads per workgroup
 typedef unsigned long long rl_u64x2 __attribute__((ext_vector_type(2)));
 constexpr int RL_LDS_BITS = 11;
@@ -67,11 +71,11 @@ struct RlVec {
 // run-head mask of a lane's RL_Q x VW ids (bit q VW + j): the id differs from its left neighbour
 // (same lane or the lane below; lane 0's first id always), ids 2^64 - 1 past the end excluded;
 // e_or |= EV_ERR_GT for a reserved id inside the range
-template <int VW>
+template <int VW, int Q = RL_Q>
 __device__ __forceinline__ u32 rl_heads(const RlVec<VW>* x, int64_t base, int64_t end, int lane, u32& e_or) {
     u32 hm = 0;
 #pragma unroll
-    for (int q = 0; q < RL_Q; ++q) {
+    for (int q = 0; q < Q; ++q) {
         const int64_t i = base + (q * 64 + lane) * VW;
         const u64 prev = (u64)__shfl_up((unsigned long long)x[q].v[VW - 1], 1);
 #pragma unroll
@@ -85,11 +89,11 @@ __device__ __forceinline__ u32 rl_heads(const RlVec<VW>* x, int64_t base, int64_
     return hm;
 }
 
-template <int VW>
+template <int VW, int Q = RL_Q>
 __device__ __forceinline__ u64 rl_pick(const RlVec<VW>* x, int b) {
     u64 k = 0;
 #pragma unroll
-    for (int q = 0; q < RL_Q; ++q)
+    for (int q = 0; q < Q; ++q)
 #pragma unroll
         for (int j = 0; j < VW; ++j) if (q * VW + j == b) k = x[q].v[j];
     return k;
@@ -214,14 +218,14 @@ __global__ __launch_bounds__(RL_WG) void k_rl_apply(const u64* lab, int64_t n, i
     };
     const int lane = threadIdx.x & 63;
     const int64_t beg = (int64_t)blockIdx.x * per_wg, end = min(n, beg + per_wg);
-    for (int64_t base = beg + (int64_t)(threadIdx.x & ~63) * RL_Q * VW; base < end; base += (int64_t)RL_WG * RL_Q * VW) {
-        RlVec<VW> x[RL_Q];
+    for (int64_t base = beg + (int64_t)(threadIdx.x & ~63) * RL_QA * VW; base < end; base += (int64_t)RL_WG * RL_QA * VW) {
+        RlVec<VW> x[RL_QA];
 #pragma unroll
-        for (int q = 0; q < RL_Q; ++q) x[q].load(lab, base + (q * 64 + lane) * VW, end);
+        for (int q = 0; q < RL_QA; ++q) x[q].load(lab, base + (q * 64 + lane) * VW, end);
         u32 e_or = 0;
-        const u32 hm = rl_heads<VW>(x, base, end, lane, e_or);
+        const u32 hm = rl_heads<VW, RL_QA>(x, base, end, lane, e_or);
 #pragma unroll
-        for (int q = 0; q < RL_Q; ++q) {
+        for (int q = 0; q < RL_QA; ++q) {
             const int64_t i = base + (q * 64 + lane) * VW;
             const u32 hq = (hm >> (q * VW)) & ((1u << VW) - 1);
             // one lookup site per group of 64 lanes
