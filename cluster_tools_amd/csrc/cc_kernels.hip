@@ -2364,6 +2364,9 @@ constexpr int LABCAP = 2048;          // component labels cached in LDS
 
 // store the two voxels (x, x+1) of one cube row segment; 16-B store when aligned
 // (plain stores: non-temporal ones measured 0.3 ms slower over the 34 GB of C3)
+// (HIP's ulonglong2 is only 8-B aligned, so this compiles to two dwordx2 stores per lane at 16-B
+// stride; a 16-B aligned vector type giving one dwordx4 per lane measured slower: k_pass2 5.85 vs
+// 5.50 ms at C3, same box)
 __device__ __forceinline__ void store2(u64* __restrict__ out, int64_t idx, u64 v0, u64 v1, bool two, bool vec) {
     if (two && vec) {
         *reinterpret_cast<ulonglong2*>(out + idx) = make_ulonglong2(v0, v1);
