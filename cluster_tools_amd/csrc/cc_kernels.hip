@@ -2049,9 +2049,10 @@ __global__ __launch_bounds__(SB_THREADS) void k_block_uf(Geom g, const u32* __re
 
 // Per-block root counts -> block values (n + 1, or 0 for an empty block: block_components.py:175-182),
 // their exclusive scan (merge_offsets.py:115-120) and that of the root counts; scalars[0] = sum of
-// the values, scalars[2] = number of roots.  One workgroup, chunks of SB_THREADS blocks.
+// the values, scalars[2] = number of roots, scalars[3] = whether any block took the global
+// fallback (big[nb]) -- the host reads [2..3] in one copy.  One workgroup, chunks of SB_THREADS blocks.
 __global__ __launch_bounds__(SB_THREADS) void k_block_scan(int64_t nb, const u32* __restrict__ RCB, u32* ROFFB,
-                                                           u64* values, u64* offsets, u64* scalars) {
+                                                           u64* values, u64* offsets, const u8* big, u64* scalars) {
     __shared__ u64 wsum[2][SB_THREADS / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     u64 carry_r = 0, carry_v = 0;
@@ -2080,7 +2081,7 @@ __global__ __launch_bounds__(SB_THREADS) void k_block_scan(int64_t nb, const u32
         carry_r += tr; carry_v += tv;
         __syncthreads();
     }
-    if (tid == 0) { scalars[0] = carry_v; scalars[2] = carry_r; }
+    if (tid == 0) { scalars[0] = carry_v; scalars[2] = carry_r; scalars[3] = big[nb] ? 1ull : 0ull; }
 }
 
 // the sorted per-block root lists as the (key, node) arrays of the generic path: keys2 = block <<

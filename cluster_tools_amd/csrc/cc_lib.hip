@@ -42,6 +42,28 @@ struct DevBuf {
     }
 };
 
+// pinned host memory for the pipeline's small read-backs: a copy into pageable memory went
+// through the runtime's staging path (25-80 us of idle GPU per read in the C3 trace)
+struct HostPin {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void* ensure(size_t n) {
+        if (n > bytes) {
+            if (p) HIP_OK(hipHostFree(p));
+            p = nullptr;
+            const size_t nb = std::max<size_t>(n, 64 << 10);
+            HIP_OK(hipHostMalloc(&p, nb, hipHostMallocDefault));
+            bytes = nb;
+        }
+        return p;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
 struct ProfEntry {
     int64_t count = 0;
     double ms = 0;
@@ -66,6 +88,7 @@ struct cc_ctx {
     uint64_t n_labels = 0;
     std::vector<uint64_t> h_values, h_offsets;
     std::vector<int32_t> h_tab;
+    HostPin pin;             // small read-backs (see HostPin)
     bool lut_valid = false;
     // profiling
     int prof = 0;          // 0 off, 1 every launch, 2 the volume-sized kernels only (cc_set_profiling)
@@ -139,6 +162,28 @@ static void sync(cc_ctx* c) {
     if (c->prof) resolve_profile(c);
 }
 
+// read-backs through the pinned buffer: enqueue (device src, bytes) pieces at increasing offsets,
+// one synchronisation, then copy out on the host.  Nothing else may use c->pin meanwhile.
+struct Readback {
+    cc_ctx* c;
+    size_t off = 0;
+    std::vector<std::pair<void*, std::pair<size_t, size_t>>> outs;   // (host dst, (offset, bytes))
+    Readback(cc_ctx* c_, size_t total) : c(c_) { c->pin.ensure(total); }
+    void add(void* dst, const void* src, size_t bytes) {
+        off = (off + 15) & ~size_t(15);
+        if (bytes) HIP_OK(hipMemcpyAsync((char*)c->pin.p + off, src, bytes, hipMemcpyDeviceToHost, c->stream));
+        outs.push_back({dst, {off, bytes}});
+        off += bytes;
+    }
+    // resolve = false: the side stream may still run timed kernels (the k_fix count is read
+    // while k_seams runs), so the stream is synchronised without resolving the profile events
+    void wait(bool resolve = true) {
+        if (resolve) sync(c);
+        else HIP_OK(hipStreamSynchronize(c->stream));
+        for (auto& o : outs) if (o.second.second) std::memcpy(o.first, (char*)c->pin.p + o.second.first, o.second.second);
+    }
+};
+
 // 1-D grid; element kernels index one element per thread, so n must stay below 2^32 threads
 // (volume-sized kernels use CC_FOR with the grid capped by grid_stride()).
 static inline unsigned grid1d(int64_t n, int bs = 256) {
@@ -148,10 +193,16 @@ static inline unsigned grid1d(int64_t n, int bs = 256) {
 static inline unsigned grid_stride(int64_t n, int bs = 256) { return (unsigned)std::min<int64_t>(1 << 20, std::max<int64_t>(1, (n + bs - 1) / bs)); }
 
 static void upload_geom(cc_ctx* c, HostGeom& hg) {
-    c->h_tab = hg.tab;     // kept alive in the ctx until the stream has consumed it
-    c->tiles.ensure(c->h_tab.size() * sizeof(int32_t));
-    HIP_OK(hipMemcpyAsync(c->tiles.p, c->h_tab.data(), c->h_tab.size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                          c->stream));
+    // the tables of the last upload are still on the device when the geometry repeats (the
+    // common case: one volume shape per context); otherwise upload (h_tab stays alive in the ctx
+    // until the stream has consumed it)
+    const size_t bytes = hg.tab.size() * sizeof(int32_t);
+    const size_t cap_before = c->tiles.bytes;      // ensure() only reallocates to a larger size
+    c->tiles.ensure(bytes);
+    if (!(c->tiles.bytes == cap_before && c->h_tab == hg.tab)) {
+        c->h_tab = hg.tab;
+        HIP_OK(hipMemcpyAsync(c->tiles.p, c->h_tab.data(), bytes, hipMemcpyHostToDevice, c->stream));
+    }
     bind_geom_tables(hg, c->tiles.as<int32_t>());
 }
 
@@ -302,8 +353,11 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         u32* list = flag + nt;
         u8* fchg = (u8*)(list + nt + 1);
         u32 nfix = 0;
-        HIP_OK(hipMemcpyAsync(&nfix, FIX, sizeof(u32), hipMemcpyDeviceToHost, s));
-        HIP_OK(hipStreamSynchronize(s));
+        {
+            Readback rb(c, 64);
+            rb.add(&nfix, FIX, sizeof(u32));
+            rb.wait(false);
+        }
         st.n_fix = nfix;
         if (lds_seams) stream_wait(c, c->side, s);
         if (nfix) {
@@ -360,10 +414,13 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     u8 any_big = 1;
     u64 nr_blocks = 0;
     if (block_uf) {
-        launch(c, "k_block_scan", [&] { k_block_scan<<<1, SB_THREADS, 0, s>>>(nb, RCB, ROFFB, values, offsets, scalars); });
-        HIP_OK(hipMemcpyAsync(&nr_blocks, scalars + 2, sizeof(u64), hipMemcpyDeviceToHost, s));
-        HIP_OK(hipMemcpyAsync(&any_big, big + nb, 1, hipMemcpyDeviceToHost, s));
-        sync(c);
+        launch(c, "k_block_scan", [&] { k_block_scan<<<1, SB_THREADS, 0, s>>>(nb, RCB, ROFFB, values, offsets, big, scalars); });
+        u64 sc23[2] = {0, 1};
+        Readback rb(c, 64);
+        rb.add(sc23, scalars + 2, 2 * sizeof(u64));       // roots, "any block big" (k_block_scan)
+        rb.wait();
+        nr_blocks = sc23[0];
+        any_big = sc23[1] ? 1 : 0;
     }
     if (!any_big) {
         const int64_t nr = (int64_t)nr_blocks;
@@ -390,8 +447,11 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         });
     }
     u32 n_roots_h = 0;
-    HIP_OK(hipMemcpyAsync(&n_roots_h, ROFF + nt, sizeof(u32), hipMemcpyDeviceToHost, s));
-    sync(c);
+    {
+        Readback rb(c, 64);
+        rb.add(&n_roots_h, ROFF + nt, sizeof(u32));
+        rb.wait();
+    }
     const int64_t nr = n_roots_h;
     st.nr = nr;
     ensure_roots(nr);
@@ -427,8 +487,9 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
 
 static uint64_t read_sum_v(cc_ctx* c) {
     u64 v = 0;
-    HIP_OK(hipMemcpyAsync(&v, c->scalars.p, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-    sync(c);
+    Readback rb(c, 64);
+    rb.add(&v, c->scalars.p, sizeof(u64));
+    rb.wait();
     state(c).sum_v = v;
     return v;
 }
@@ -599,12 +660,15 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
     });
 
     u64 sc[4] = {0, 0, 0, 0};
-    HIP_OK(hipMemcpyAsync(sc, scalars, 4 * sizeof(u64), hipMemcpyDeviceToHost, s));
     c->h_values.resize(nb);
     c->h_offsets.resize(nb);
-    HIP_OK(hipMemcpyAsync(c->h_values.data(), c->values.p, nb * sizeof(u64), hipMemcpyDeviceToHost, s));
-    HIP_OK(hipMemcpyAsync(c->h_offsets.data(), offsets, nb * sizeof(u64), hipMemcpyDeviceToHost, s));
-    sync(c);
+    {
+        Readback rb(c, 4 * sizeof(u64) + 2 * nb * sizeof(u64) + 64);
+        rb.add(sc, scalars, 4 * sizeof(u64));
+        rb.add(c->h_values.data(), c->values.p, nb * sizeof(u64));
+        rb.add(c->h_offsets.data(), offsets, nb * sizeof(u64));
+        rb.wait();
+    }
     st.sum_v = sc[0];
     st.stage = 3;
     c->n_blocks = nb;
@@ -683,6 +747,7 @@ void cc_destroy(cc_ctx* c) {
                       &c->ev_main, &c->ev_z, &c->ev_seg, &c->ev_gt, &c->ev_flag, &c->ev_part, &c->rl_wg,
                       &c->gs1, &c->gs2, &c->gs_tab};
     for (DevBuf* b : bufs) b->release();
+    c->pin.release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
