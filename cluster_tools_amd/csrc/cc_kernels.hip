@@ -1050,6 +1050,22 @@ __global__ void k_verify(Geom g, const BlockParam* guess, const BlockParam* bp, 
     }
 }
 
+// k_block_params and k_verify in one launch: every tile derives its block's exact parameters from
+// the statistics (a few dozen float ops), the block's first tile stores them for k_fix
+__global__ void k_params_verify(Geom g, const BlockParam* guess, const u32* smin, const u32* smax, const u32* sflag,
+                                float thr, int mode, BlockParam* bp, const u32* TB, u32* FIX) {
+    CC_FOR(t, g.n_tiles) {
+        const TileInfo ti = tile_info(g, t);
+        const int64_t b = ti.block;
+        const BlockParam T = block_param(smin[b], smax[b], sflag[b], thr, mode);
+        const bool first = (ti.iz == 0 || g.tblk[0][ti.iz - 1] != g.tblk[0][ti.iz]) &&
+                           (ti.iy == 0 || g.tblk[1][ti.iy - 1] != g.tblk[1][ti.iy]) &&
+                           (ti.ix == 0 || g.tblk[2][ti.ix - 1] != g.tblk[2][ti.ix]);
+        if (first) bp[b] = T;
+        if (!spec_valid(guess[b], T, TB + 4 * t, mode)) FIX[1 + atomicAdd(FIX, 1u)] = (u32)t;
+    }
+}
+
 // pass 1 with the exact parameters for the listed tiles, one workgroup per tile (the host reads
 // the count first: a fixed grid walking the list hoisted the tile set-up out of the loop and
 // spilled; a grid over all tiles paid ~2 us of dependent loads per returning workgroup)
@@ -2085,9 +2101,11 @@ __global__ __launch_bounds__(SB_THREADS) void k_block_scan(int64_t nb, const u32
 }
 
 // the sorted per-block root lists as the (key, node) arrays of the generic path: keys2 = block <<
-// KEY_BITS | first voxel, vals2 = node, segment [seg_start, seg_end) of each block
+// KEY_BITS | first voxel, vals2 = node, segment [seg_start, seg_end) of each block; offsets
+// (nullable): each root's key becomes its reference id offsets[b] + rank + 1 (each root is read
+// and written by its own thread only)
 __global__ __launch_bounds__(256) void k_emit_roots(const u32* __restrict__ RL, const u32* __restrict__ RCB,
-                                                    const u32* __restrict__ ROFFB, const u64* __restrict__ KEY,
+                                                    const u32* __restrict__ ROFFB, u64* KEY, const u64* offsets,
                                                     u64* keys2, u32* vals2, u32* seg_start, u32* seg_end) {
     const int64_t b = blockIdx.x;
     const u32 R = RCB[b], off = ROFFB[b];
@@ -2095,6 +2113,7 @@ __global__ __launch_bounds__(256) void k_emit_roots(const u32* __restrict__ RL, 
         const u32 node = RL[(u64)b * SB_LCAP + r];
         keys2[off + r] = ((u64)b << KEY_BITS) | KEY[node];
         vals2[off + r] = node;
+        if (offsets) KEY[node] = offsets[b] + r + 1;      // its reference id (k_assign_rid with base 0)
     }
     if (threadIdx.x == 0) { seg_start[b] = off; seg_end[b] = off + R; }
 }
@@ -2188,6 +2207,32 @@ __device__ __forceinline__ u64 apply_map(u64 v, const u64* U, const u64* V, int6
 __global__ void k_lut_init(u64 cap, const u64* scalars, u64 base, u64* lut) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < cap && i <= scalars[0]) lut[i] = base + i;
+}
+
+// k_lut_init and k_lut in one launch, one thread per id of this volume (slab): id = base + i is
+// the rid of rank r = id - offsets[b] - 1 of the last block b whose range starts at or below it
+// (empty blocks share the next block's offset); a root's id maps to its component's
+// representative, every other id (label 0 of a block, the slack id) to itself
+__global__ void k_lut_all(u64 cap, int64_t nb, u64 base, const u64* __restrict__ offsets, const u64* __restrict__ values,
+                          const u32* __restrict__ seg_start, const u32* __restrict__ vals, u32* P, const u64* KR,
+                          const u64* U, const u64* V, int64_t m, u64* lut, u64* scalars) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap || i > scalars[0]) return;
+    const u64 id = base + i;
+    int64_t lo = 0, hi = nb - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (offsets[mid] <= id) lo = mid; else hi = mid - 1;
+    }
+    const u64 off = offsets[lo], v = values[lo];
+    u64 rep = id;
+    if (off < id && id - off < v) {                       // rank id - off - 1 in [0, v - 1)
+        const u32 node = vals[seg_start[lo] + (u32)(id - off - 1)];
+        const u32 r = gfind(P, node);
+        rep = apply_map(KR[r], U, V, m);
+        if (r == node && rep == KR[r]) atomicAdd((unsigned long long*)&scalars[1], 1ull);   // components owned here
+    }
+    lut[i] = rep;
 }
 
 __global__ void k_lut(int64_t n, const u32* vals, u32* P, const u64* KR, u64 base, const u64* U, const u64* V,

@@ -228,6 +228,7 @@ struct RunState {
     uint64_t n_fix = 0;        // tiles relabelled by k_fix
     bool identity_lut = false; // the empty-job emulation dropped every block-face merge
     int stage = 0;             // 1 local done, 2 rid done, 3 final done
+    bool rid0 = false;         // k_emit_roots already wrote the roots' ids for base 0
 };
 
 static RunState& state(cc_ctx* c) {
@@ -344,10 +345,9 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
                 seams(c->side, t0, t1);
             }
         }
-        launch(c, "k_block_params", [&] {
-            k_block_params<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, smin, smax, sflag, thr, mode, bp);
+        launch(c, "k_params_verify", [&] {
+            k_params_verify<<<grid_stride(nt), 256, 0, s>>>(g, guess, smin, smax, sflag, thr, mode, bp, TB, FIX);
         });
-        launch(c, "k_verify", [&] { k_verify<<<grid_stride(nt), 256, 0, s>>>(g, guess, bp, TB, mode, FIX); });
         c->mark.ensure((size_t)(2 * nt + 1) * sizeof(u32) + nt);
         u32* flag = c->mark.as<u32>();
         u32* list = flag + nt;
@@ -427,8 +427,10 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         st.nr = nr;
         ensure_roots(nr);
         launch(c, "k_emit_roots", [&] {
-            k_emit_roots<<<(unsigned)nb, 256, 0, s>>>(RL, RCB, ROFFB, KR, c->keys2.as<u64>(), c->vals2.as<u32>(), seg_start, seg_end);
+            k_emit_roots<<<(unsigned)nb, 256, 0, s>>>(RL, RCB, ROFFB, KR, offsets, c->keys2.as<u64>(), c->vals2.as<u32>(),
+                                                      seg_start, seg_end);
         });
+        st.rid0 = true;
         st.stage = 1;
         return;
     }
@@ -504,7 +506,7 @@ static void phase_rid(cc_ctx* c, uint64_t base) {
     st.base = base;
     u64* offsets = c->offsets.as<u64>();
     if (base) launch(c, "k_add_base", [&] { k_add_base<<<grid1d(nb), 256, 0, s>>>(nb, offsets, base); });
-    if (nr > 0)
+    if (nr > 0 && !(st.rid0 && base == 0))
         launch(c, "k_assign_rid", [&] {
             k_assign_rid<<<grid1d(nr), 256, 0, s>>>(nr, c->keys2.as<u64>(), c->vals2.as<u32>(), c->seg.as<u32>(),
                                                     offsets, c->KR.as<u64>());
@@ -648,9 +650,10 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
         c->lut.ensure(lut_cap * sizeof(u64));
         u64* lut = c->lut.as<u64>();
         const u64 base = st.base;
-        launch(c, "k_lut_init", [&] { k_lut_init<<<grid1d(lut_cap), 256, 0, s>>>(lut_cap, scalars, base, lut); });
-        if (nr > 0)
-            launch(c, "k_lut", [&] { k_lut<<<grid1d(nr), 256, 0, s>>>(nr, c->vals2.as<u32>(), P, KR, base, U, V, m, lut, scalars); });
+        launch(c, "k_lut_all", [&] {
+            k_lut_all<<<grid1d(lut_cap), 256, 0, s>>>(lut_cap, nb, base, offsets, c->values.as<u64>(), c->seg.as<u32>(),
+                                                      c->vals2.as<u32>(), P, KR, U, V, m, lut, scalars);
+        });
         c->lut_valid = true;
     }
     // the fused path resolves each tile component's final label inside k_pass2 (no k_finalize)
