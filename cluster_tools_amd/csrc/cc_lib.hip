@@ -578,8 +578,9 @@ static int64_t dedup_pairs(cc_ctx* c, u64* pa, u64* pb, u64* qa, u64* qb, int64_
     HIP_OK(hipcub::DeviceSelect::Flagged(c->cub_tmp.p, tb, pa, flags, qa, nsel, (int)n, s));
     HIP_OK(hipcub::DeviceSelect::Flagged(c->cub_tmp.p, tb, pb, flags, qb, nsel, (int)n, s));
     int nu = 0;
-    HIP_OK(hipMemcpyAsync(&nu, nsel, sizeof(int), hipMemcpyDeviceToHost, s));
-    sync(c);
+    Readback rb(c, 64);
+    rb.add(&nu, nsel, sizeof(int));
+    rb.wait();
     return nu;
 }
 
@@ -606,8 +607,11 @@ static void phase_map(cc_ctx* c, const u64* pairs, int64_t n) {
     c->cub_tmp.ensure(tb);
     HIP_OK(hipcub::DeviceSelect::Unique(c->cub_tmp.p, tb, ids2, ids, nsel, (int)(2 * n), s));
     int m = 0;
-    HIP_OK(hipMemcpyAsync(&m, nsel, sizeof(int), hipMemcpyDeviceToHost, s));
-    sync(c);
+    {
+        Readback rb(c, 64);
+        rb.add(&m, nsel, sizeof(int));
+        rb.wait();
+    }
     // U = ids[0:m]; index pairs; union-find (smallest index = smallest id) -> V
     c->map_vals.ensure(std::max<int64_t>(1, m) * sizeof(u64));
     u64* ip = ids2;    // 2n indices

@@ -210,8 +210,11 @@ static int64_t seam_pairs_impl(cc_ctx* c, UP upper, const uint64_t* lower, int64
                                                                                   (u64)capn);
     });
     unsigned long long n_raw = 0;
-    HIP_OK(hipMemcpyAsync(&n_raw, cnt, sizeof(n_raw), hipMemcpyDeviceToHost, s));
-    sync(c);
+    {
+        Readback rb(c, 64);
+        rb.add(&n_raw, cnt, sizeof(n_raw));
+        rb.wait();
+    }
     int64_t nu = 0;
     launch(c, "seam_dedup", [&] { nu = dedup_pairs(c, pa, pb, qa, qb, (int64_t)n_raw); });
     if (pairs && cap > 0 && nu > 0) {
