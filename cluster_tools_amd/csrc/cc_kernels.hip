@@ -249,14 +249,19 @@ __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T, u32* list =
     }
     __syncthreads();
     if (STOP == 3) return 0;
-    // 4. compact index k of every root, in run-id order
+    // 4. compact index k of every root, in run-id order; a root also records its cube layer cz in
+    // bits 12-14 (run ids < 4096): the component's first voxel lies in that layer (the root is
+    // its first run in cube order, so no run of it has a smaller cz), so phase 5 only offers
+    // first voxels from runs of that layer
+    static_assert(NRUN <= (1 << 12) && CZ <= 8, "root | cz << 12 | k << 16");
     u32 total = 0;
     {
         const u32 base = block_excl_scan(n, T.scratch, &total);
         u32 k = base;
+        const u32 czb = (u32)(qrow / CY) << 12;
         for (u32 m = Bq; m; m &= m - 1) {
             const u32 r = r0 + (u32)__popc(Brow & ((1u << __builtin_ctz(m)) - 1));
-            if (par[r] == r) par[r] = r | (k++ << 16);
+            if (par[r] == r) par[r] = r | czb | (k++ << 16);
         }
         if (firstv)
             for (u32 i = tid; i < total; i += NTHREADS) firstv[i] = NONE;
@@ -274,10 +279,11 @@ __device__ __forceinline__ u32 tile_ccl(const u64* rows, TileCCL& T, u32* list =
     for (u32 m = Bq; m; m &= m - 1) {
         const int c0 = __builtin_ctz(m);
         const u32 r = r0 + (u32)__popc(Brow & ((1u << c0) - 1));
-        const u32 root = par[r] & 0xFFFFu;
-        const u32 pk = par[root] & 0xFFFF0000u;
+        const u32 root = par[r] & 0xFFFu;
+        const u32 pr = par[root];
+        const u32 pk = pr & 0xFFFF0000u;
         if (root != r) par[r] = root | pk;
-        if (firstv) {
+        if (firstv && ((pr >> 12) & 7u) == (u32)cz) {
             const int c1 = c0 + __builtin_ctz(~(E >> c0));                    // end cube
             const u32 M = mask_le(c1) & ~((1u << c0) - 1);
             u32 idx = NONE;
