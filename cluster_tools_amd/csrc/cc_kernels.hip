@@ -1551,7 +1551,6 @@ template <class EM>
 __device__ __forceinline__ void seam_edges_rows(const Geom& g, const face_t* S, const face_t* E, int64_t t,
                                                 const TileInfo& ti, int lane, EM&& emit) {
     const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2;
-    const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
     const bool zok = ti.iz > 0 && g.tblk[0][ti.iz] == g.tblk[0][ti.iz - 1];
     auto yok = [&](int s) { const int j = ti.iy + s; return j >= 0 && j < g.nt[1] && g.tblk[1][j] == g.tblk[1][ti.iy]; };
     auto xok = [&](int s) { const int j = ti.ix + s; return j >= 0 && j < g.nt[2] && g.tblk[2][j] == g.tblk[2][ti.ix]; };
@@ -2429,11 +2428,14 @@ __device__ __forceinline__ void store2(u64* __restrict__ out, int64_t idx, u64 v
 }
 
 // UF (the fused path, in place of a k_finalize pass over all nodes): the final label of tile
-// component k is apply_map(KR[root of its node]); the finds are issued before the tile CCL so
+// component k is apply_map(KR[root of its node]) (see below); the finds are issued before the tile CCL so
 // their dependent loads overlap it.  !UF: FIN holds the label of every node (k_finalize<true>).
+// With a seam map (m > 0, z-slab shards) the representative comes from the LUT k_lut_all built
+// (lut[rid - base] = apply_map(rid) for every root id of this slab): one load instead of a binary
+// search over the m mapped ids per component.
 template <bool UF>
 __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restrict__ BITS, const u32* COUNT,
-                                                    const u64* __restrict__ FIN, u32* P, const u64* U, const u64* V,
+                                                    const u64* __restrict__ FIN, u32* P, const u64* lut, u64 id_base,
                                                     int64_t m, u64* __restrict__ out) {
     __shared__ u64 rows[NROWS];             // split bit rows (see tile_ccl)
     __shared__ TileCCL T;
@@ -2459,7 +2461,11 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
         return;
     }
     const u32 base = (u32)(t * g.cap);
-    auto label = [&](u32 node) -> u64 { return UF ? apply_map(FIN[gfind(P, node)], U, V, m) : FIN[node]; };
+    auto label = [&](u32 node) -> u64 {
+        if (!UF) return FIN[node];
+        const u64 v = FIN[gfind(P, node)];
+        return m ? lut[v - id_base] : v;
+    };
     constexpr int LPT = LABCAP / NTHREADS;
     u64 lv[LPT];
 #pragma unroll

@@ -662,8 +662,8 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
     }
     // the fused path resolves each tile component's final label inside k_pass2 (no k_finalize)
     launch(c, "k_pass2", [&] {
-        if (st.local_only) k_pass2<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, FIN, nullptr, nullptr, nullptr, 0, out);
-        else k_pass2<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, KR, P, U, V, m, out);
+        if (st.local_only) k_pass2<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, FIN, nullptr, nullptr, 0, 0, out);
+        else k_pass2<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, KR, P, c->lut.as<u64>(), st.base, m, out);
     });
 
     u64 sc[4] = {0, 0, 0, 0};
