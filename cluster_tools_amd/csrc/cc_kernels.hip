@@ -2436,11 +2436,18 @@ __device__ __forceinline__ void store2(u64* __restrict__ out, int64_t idx, u64 v
 template <bool UF>
 __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restrict__ BITS, const u32* COUNT,
                                                     const u64* __restrict__ FIN, u32* P, const u64* lut, u64 id_base,
-                                                    int64_t m, u64* __restrict__ out) {
+                                                    int64_t m, u64* __restrict__ out, int order) {
     __shared__ u64 rows[NROWS];             // split bit rows (see tile_ccl)
     __shared__ TileCCL T;
     __shared__ u64 lab[LABCAP];
-    const int64_t t = blockIdx.x;
+    // tile order: 0 linear (x fastest), 1 z fastest (the host picks 1 for rows of >= 4096 voxels:
+    // writing the 4096-wide C5 slabs in x-fastest order took 6.09-6.14 ms, z-fastest 5.36 ms;
+    // C3's 2048-wide volume is the other way round, 5.60 vs 5.84 ms)
+    int64_t t = blockIdx.x;
+    if (order == 1) {
+        const int64_t n0 = g.nt[0];
+        t = (t % n0) * ((int64_t)g.nt[1] * g.nt[2]) + t / n0;
+    }
     const TileInfo ti = tile_info(g, t);
     const int tid = threadIdx.x;
     const u32 R = COUNT[t];

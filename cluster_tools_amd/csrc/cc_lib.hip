@@ -662,8 +662,12 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
     }
     // the fused path resolves each tile component's final label inside k_pass2 (no k_finalize)
     launch(c, "k_pass2", [&] {
-        if (st.local_only) k_pass2<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, FIN, nullptr, nullptr, 0, 0, out);
-        else k_pass2<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, KR, P, c->lut.as<u64>(), st.base, m, out);
+        // tile order of the write pass (see k_pass2): z fastest for rows of >= 4096 voxels
+        // (CC_PASS2_ORDER = 0 / 1 forces one, A/B only)
+        int order = g.X >= 4096 ? 1 : 0;
+        if (const char* e = std::getenv("CC_PASS2_ORDER"); e && *e) order = std::atoi(e) ? 1 : 0;
+        if (st.local_only) k_pass2<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, FIN, nullptr, nullptr, 0, 0, out, order);
+        else k_pass2<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, KR, P, c->lut.as<u64>(), st.base, m, out, order);
     });
 
     u64 sc[4] = {0, 0, 0, 0};
