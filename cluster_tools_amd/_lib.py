@@ -25,7 +25,7 @@ EXPORTS = (
     'cc_seam_pairs', 'cc_shard_finish', 'cc_set_debug', 'cc_threshold', 'cc_shard_top_plane32',
     'cc_seam_pairs32', 'cc_shard_top_cubes32', 'cc_seam_pairs_cubes32',
     'cc_evaluate', 'cc_get_overlaps', 'cc_relabel_consecutive', 'cc_set_option', 'cc_channel_mean',
-    'cc_gaussian_smooth_blocks', 'cc_gaussian_taps',
+    'cc_gaussian_smooth_blocks', 'cc_gaussian_taps', 'cc_result_size',
 )
 # CC_DTYPE_* of include/cc_mi355x.h (cc_channel_mean)
 DTYPES = {'float32': 0, 'float64': 1, 'uint8': 2, 'int8': 3, 'uint16': 4, 'int16': 5, 'uint32': 6,
@@ -114,6 +114,7 @@ def load():
         'cc_channel_mean': (I, [P, P, I, P, P, i64, P]),
         'cc_gaussian_smooth_blocks': (I, [P, P, P, P, ctypes.c_double, P]),
         'cc_gaussian_taps': (I, [ctypes.c_double, P, I]),
+        'cc_result_size': (i64, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

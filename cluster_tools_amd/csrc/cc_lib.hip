@@ -728,6 +728,8 @@ const char* cc_version(void) { return "cc_mi355x 0.2 gfx950 src=" CC_SRC_HASH; }
 
 const char* cc_last_error(void) { return g_err.c_str(); }
 
+int64_t cc_result_size(void) { return (int64_t)sizeof(cc_result); }
+
 int cc_create(int device, cc_ctx** out) {
     CC_TRY({
         CC_REQUIRE(out != nullptr, "out is NULL");

@@ -190,15 +190,22 @@ static bool decode_chunk(const std::string& p, const Spec& s, std::vector<uint8_
     if (!read_file(p, file)) return false;
     if (file.size() < 4) throw std::runtime_error("truncated chunk header " + p);
     const uint16_t mode = be16(file.data()), nd = be16(file.data() + 2);
+    if (mode > 1) throw std::runtime_error("unsupported chunk mode " + std::to_string(mode) + " " + p);
     if (nd != s.ndim) throw std::runtime_error("chunk ndim mismatch " + p);
     size_t off = 4 + 4 * (size_t)nd + (mode == 1 ? 4 : 0);
     if (file.size() < off) throw std::runtime_error("truncated chunk header " + p);
+    // the header is untrusted: every dim bounded by the dataset's chunk size (so the product
+    // cannot overflow), and a varlength (mode 1) element count must equal that product -- the
+    // caller indexes the decoded array with these dims
     int64_t n = 1;
     for (int a = 0; a < nd; ++a) {
-        cd[nd - 1 - a] = be32(file.data() + 4 + 4 * a);     // header dims fastest first
-        n *= cd[nd - 1 - a];
+        const int64_t d = be32(file.data() + 4 + 4 * a);     // header dims fastest first
+        if (d > s.chunks[nd - 1 - a]) throw std::runtime_error("chunk dims exceed the dataset's chunk size " + p);
+        cd[nd - 1 - a] = d;
+        n *= d;
     }
-    if (mode == 1) n = be32(file.data() + 4 + 4 * nd);
+    if (mode == 1 && (int64_t)be32(file.data() + 4 + 4 * nd) != n)
+        throw std::runtime_error("varlength chunk element count differs from its dims " + p);
     const size_t bytes = (size_t)n * s.esize;
     std::vector<uint8_t> raw;
     const uint8_t* payload = file.data() + off;
@@ -246,7 +253,10 @@ static void encode_chunk(const std::string& p, const Spec& s, const uint8_t* arr
     }
     const size_t k = p.find_last_of('/');
     mkdirs(p.substr(0, k));
-    const std::string tmp = p + ".tmp" + std::to_string((unsigned long long)std::hash<std::thread::id>()(std::this_thread::get_id()));
+    // unique per process AND thread: thread ids repeat across processes (ranks of the sharded
+    // job, concurrent local jobs writing one dataset)
+    const std::string tmp = p + ".tmp" + std::to_string((long long)::getpid()) + "_" +
+                            std::to_string((unsigned long long)std::hash<std::thread::id>()(std::this_thread::get_id()));
     FILE* f = std::fopen(tmp.c_str(), "wb");
     if (!f) throw std::runtime_error("open " + tmp + ": " + std::strerror(errno));
     const size_t w = std::fwrite(out.data(), 1, out.size(), f);
@@ -324,6 +334,9 @@ static void write_region(const std::string& ds, const Spec& s, const uint8_t* in
             exists = decode_chunk(p, s, file, arr, od);
             bool same = exists;
             for (int a = 0; a < s.ndim && same; ++a) same = od[a] == cd[a];
+            // an edge chunk may be stored full size (dims >= the truncated box), never smaller
+            for (int a = 0; a < s.ndim && exists; ++a)
+                if (od[a] < cd[a]) throw std::runtime_error("chunk smaller than its box " + p);
             if (!same) {     // absent, or stored full size at an edge: rebuild in the truncated shape
                 std::vector<uint8_t> t((size_t)n * s.esize, 0);
                 if (exists) {

@@ -316,7 +316,14 @@ def block_components(job_id, config_path):
     nb = vu.Blocking([0, 0, 0], list(shape), block_shape).numberOfBlocks
 
     if fused:
-        if int(config.get('gpus', 1)) > 1:
+        sharded = int(config.get('gpus', 1)) > 1
+        if sharded and int(config.get('quirk_jobs', 0)) > 0:
+            # the empty-job emulation (merge_assignments.py:115-123) needs every block's face-pair
+            # flag in one place: it runs on the single-volume fused path only
+            fu.log('reference_empty_job_quirk is set: running on one GPU instead of %i z-slab ranks'
+                   % int(config['gpus']))
+            sharded = False
+        if sharded:
             values, lut, res, timing = _fused_sharded(config_path, config, shape, nb)
         else:
             values, lut, res, timing = _fused_single(config, shape, nb)

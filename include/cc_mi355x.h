@@ -50,6 +50,10 @@ typedef struct {
                                merge, the LUT is the identity (merge_assignments.py:115-123) */
 } cc_result;
 
+/* sizeof(cc_result) as built: a binding checks its struct against it before passing one
+ * (ctypes: assert ctypes.sizeof(_Res) == cc_result_size()).  No GPU needed. */
+int64_t     cc_result_size(void);
+
 /* --- context ----------------------------------------------------------- */
 int         cc_create(int device, cc_ctx** out);
 void        cc_destroy(cc_ctx* ctx);

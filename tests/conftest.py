@@ -16,6 +16,25 @@ def pytest_configure(config):
     config.addinivalue_line('markers', 'slow: large-volume checks')
 
 
+def integration_blocks():
+    """The ```python blocks of INTEGRATION.md, in order (the reference-side bindings a maintainer
+    would add; the tests execute them as written)."""
+    import re
+    txt = open(os.path.join(ROOT, 'INTEGRATION.md')).read()
+    return re.findall(r'```python\n(.*?)```', txt, flags=re.S)
+
+
+def exec_integration_binding():
+    """Execute INTEGRATION.md section B's binding block as written, with CC_MI355X_LIB naming the
+    in-tree library; returns its namespace (label_volume, _Res, _L, ...)."""
+    from cluster_tools_amd import _lib
+    os.environ['CC_MI355X_LIB'] = _lib.LIB_PATH
+    block = [b for b in integration_blocks() if 'cc_mi355x.py' in b][0]
+    ns = {'__name__': 'cc_mi355x_binding'}
+    exec(compile(block, 'INTEGRATION.md#B', 'exec'), ns)
+    return ns
+
+
 def golden_index():
     with open(os.path.join(GOLDEN, 'index.json')) as f:
         return json.load(f)

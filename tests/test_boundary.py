@@ -86,3 +86,28 @@ def test_binary_provenance():
     """The library in the tree was built from the tree's sources (cc_version's src= hash)."""
     from cluster_tools_amd import _lib, build
     assert _lib.check_provenance() == build.source_hash()
+
+
+def test_integration_binding_struct_matches_library():
+    """INTEGRATION.md's reference-side binding (run as written) declares struct cc_result with
+    the library's size and field order (the documented _Res had 6 of 7 fields)."""
+    import ctypes
+    from conftest import exec_integration_binding
+    from cluster_tools_amd import _lib
+    ns = exec_integration_binding()           # its own assert compares with cc_result_size()
+    L = _lib.load()
+    assert ctypes.sizeof(ns['_Res']) == L.cc_result_size() == ctypes.sizeof(_lib.CCResult)
+    assert [f for f, _ in ns['_Res']._fields_] == [f for f, _ in _lib.CCResult._fields_]
+    hdr = open(os.path.join(ROOT, 'include', 'cc_mi355x.h')).read()
+    body = hdr[hdr.index('typedef struct {'):hdr.index('} cc_result;')]
+    fields = re.findall(r'(?:u?int64_t)\s+(\w+);', re.sub(r'/\*.*?\*/', '', body, flags=re.S))
+    assert fields == [f for f, _ in _lib.CCResult._fields_]
+
+
+def test_integration_blocks_compile():
+    """Every python block of INTEGRATION.md is valid python."""
+    from conftest import integration_blocks
+    blocks = integration_blocks()
+    assert len(blocks) >= 4
+    for i, b in enumerate(blocks):
+        compile(b, 'INTEGRATION.md#%d' % i, 'exec')

@@ -301,3 +301,31 @@ def test_c3_continuous_vs_oracle(ctx, mode):
     and exact bounds; the result must still be bit-exact."""
     res = _full_size_vs_oracle(ctx, (1024, 2048, 2048), (64, 512, 512), mode, dither=True)
     assert res['n_relabelled_tiles'] < 131072 // 4
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize('mode', ['greater'])
+def test_c5_slab_vs_oracle(ctx, mode):
+    """BASELINE config 5's per-rank slab: (256, 4096, 4096), block (64, 512, 512) -- 4096-voxel rows
+    (32 KB apart), the geometry on which the host picks k_pass2's z-fastest tile order (X >= 4096)
+    -- bit-exact against the C oracle (same voxel count as C3)."""
+    _full_size_vs_oracle(ctx, (256, 4096, 4096), (64, 512, 512), mode)
+
+
+PASS2_ORDER_CASES = [
+    ((96, 320, 448), (32, 128, 128), 'greater'),
+    ((96, 320, 448), (32, 128, 128), 'less'),
+    ((70, 130, 300), (35, 65, 150), 'less'),       # odd blocks: partial tiles at every block end
+]
+
+
+@pytest.mark.parametrize('order', ['0', '1'])
+@pytest.mark.parametrize('shape,bs,mode', PASS2_ORDER_CASES)
+def test_pass2_tile_order_vs_oracle(ctx, monkeypatch, shape, bs, mode, order):
+    """Both k_pass2 tile orders (x fastest / z fastest; CC_PASS2_ORDER, read on every call) on the
+    fused path give the oracle's labels (order 1 was only reached by X >= 4096)."""
+    monkeypatch.setenv('CC_PASS2_ORDER', order)
+    inp = O.boundary_map(shape, origin=(5, 9, 2))
+    _check_against_oracle(ctx, inp, bs, 0.5, mode)
+    inp = O.boundary_map(shape, origin=(5, 9, 2), dither=True)
+    _check_against_oracle(ctx, inp, bs, 0.41, mode)

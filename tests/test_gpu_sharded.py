@@ -98,3 +98,57 @@ def test_sharded_c4_scale_vs_oracle(mode, masked, form):
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.parametrize('order', ['0', '1'])
+@pytest.mark.parametrize('mode', ['greater', 'less'])
+def test_sharded_pass2_tile_order(monkeypatch, mode, order):
+    """Both k_pass2 tile orders on the seam-map (z-slab) path against the oracle."""
+    import torch
+    from cluster_tools_amd import _lib
+    from cluster_tools_amd.distributed import label_slabs_single_process, assemble_lut
+    monkeypatch.setenv('CC_PASS2_ORDER', order)
+    shape, bs = (96, 320, 448), (32, 128, 128)
+    x = O.boundary_map(shape, origin=(1, 4, 7))
+    ctxs = [_lib.Context(0) for _ in range(3)]
+    try:
+        lab, res, sums, luts = label_slabs_single_process(ctxs, torch.from_numpy(x).cuda(), bs, 0.5, mode)
+        ref = O.label_volume(x, bs, 0.5, mode, n_threads=8)
+        np.testing.assert_array_equal(lab.cpu().numpy().view(np.uint64), ref['labels'])
+        np.testing.assert_array_equal(assemble_lut(luts, sums), ref['lut'])
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize('mode', ['greater', 'less'])
+def test_sharded_c5_geometry_vs_oracle(mode):
+    """C5's seam geometry on one GPU: (256, 4096, 4096) as 2 z-slabs of (128, 4096, 4096), block
+    (64, 512, 512), the 4096 x 4096 seam crossing as cubes32 planes (what the ranks send over xGMI),
+    the z-fastest k_pass2 order (X >= 4096) -- raw labels and the assembled LUT bit-exact against
+    the C oracle on the whole volume (reference face semantics: block_faces.py:87-113)."""
+    import os
+    import torch
+    from cluster_tools_amd import _lib
+    from cluster_tools_amd.distributed import label_slabs_single_process, assemble_lut
+    shape, bs = (256, 4096, 4096), (64, 512, 512)
+    ctxs = [_lib.Context(0) for _ in range(2)]
+    try:
+        x = ctxs[0].generate_boundary_map(shape)
+        torch.cuda.synchronize()
+        b, res, sums, luts = label_slabs_single_process(ctxs, x, bs, 0.5, mode, form='cubes32')
+        inp = x.cpu().numpy()
+        del x
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        r = O.label_volume(inp, bs, 0.5, mode, n_threads=threads)
+        del inp
+        assert sum(sums) + 1 == r['n_labels']
+        np.testing.assert_array_equal(assemble_lut(luts, sums), r['lut'])
+        ref = torch.from_numpy(r.pop('labels').view(np.int64)).cuda()
+        assert bool(torch.equal(b, ref))
+        del ref, b
+        torch.cuda.empty_cache()
+    finally:
+        for c in ctxs:
+            c.close()

@@ -117,8 +117,9 @@ def _write_task_config(cfg, name, values):
         json.dump(values, f)
 
 
+@pytest.mark.parametrize('gpus', [1, 2])
 @pytest.mark.parametrize('name', ['bmap_quirk', 'bmap_greater', 'bmap_less'])
-def test_workflow_empty_job_emulation(tmp_path, name):
+def test_workflow_empty_job_emulation(tmp_path, name, gpus):
     """merge_assignments config 'reference_empty_job_quirk' with the golden run's face-job count as
     max_jobs: the fused job reproduces the reference's output (identity LUT for bmap_quirk)."""
     from cluster_tools_amd import n5
@@ -130,6 +131,12 @@ def test_workflow_empty_job_emulation(tmp_path, name):
     c = MergeAssignmentsLocal.default_task_config()
     c['reference_empty_job_quirk'] = True
     _write_task_config(cfg, 'merge_assignments', c)
+    if gpus > 1:
+        # the z-slab path cannot emulate the quirk; the job must not silently drop it
+        from cluster_tools_amd.thresholded_components.block_components import BlockComponentsLocal
+        bc = BlockComponentsLocal.default_task_config()
+        bc.update({'gpus': gpus, 'dist_backend': 'gloo'})
+        _write_task_config(cfg, 'block_components', bc)
     t = ThresholdedComponentsWorkflow(tmp_folder=str(tmp_path / 'tmp'), config_dir=cfg, target='local',
                                       max_jobs=meta['n_jobs_block_faces'], input_path=data,
                                       input_key='volumes/boundaries', output_path=data, output_key='data',
@@ -213,3 +220,43 @@ def test_workflow_c1(tmp_path, mode):
     for k in ('n5_read_s', 'h2d_s', 'device_s', 'd2h_s', 'n5_write_s'):
         assert timing[k] > 0
     print('C1 %s timing: %s' % (mode, timing))
+
+
+def test_integration_binding_runs_as_documented():
+    """INTEGRATION.md section B executed as written (the ctypes binding a maintainer would add to
+    the reference): label_volume on a golden volume against the oracle and the reference's
+    artefacts, then the Threshold and evaluation snippets in the same namespace."""
+    import ctypes
+    import torch
+    from conftest import exec_integration_binding, integration_blocks, golden_index
+    ns = exec_integration_binding()
+    name = 'bmap_mask'
+    meta, d = golden_index()[name], load_golden(name)
+    out, values, lut, max_id = ns['label_volume'](d['input'], meta['block_shape'], float(d['threshold']),
+                                                   meta['mode'], mask=d['mask'])
+    r = O.label_volume(d['input'], meta['block_shape'], float(d['threshold']), meta['mode'], d['mask'])
+    np.testing.assert_array_equal(out, r['labels'])
+    np.testing.assert_array_equal(values, d['block_values'])
+    np.testing.assert_array_equal(lut, r['lut'])
+    assert max_id == int(d['max_id'])
+    # the Threshold / evaluation blocks extend the same module namespace
+    for b in integration_blocks():
+        if 'def threshold_volume' in b or 'def measures_on_device' in b:
+            exec(compile(b, 'INTEGRATION.md', 'exec'), ns)
+    L = ns['_L']
+    ctx = ctypes.c_void_p()
+    assert L.cc_create(0, ctypes.byref(ctx)) == 0
+    try:
+        x = torch.from_numpy(d['input']).cuda()
+        got = torch.empty(x.shape, dtype=torch.uint8, device='cuda')
+        torch.cuda.synchronize()
+        ns['threshold_volume'](ctx, x.data_ptr(), x.shape, meta['block_shape'], float(d['threshold']),
+                               meta['mode'], got.data_ptr())
+        want = O.threshold_volume(d['input'], meta['block_shape'], float(d['threshold']), meta['mode'])
+        np.testing.assert_array_equal(got.cpu().numpy(), want)
+        seg = torch.from_numpy(out.view(np.int64)).cuda()
+        torch.cuda.synchronize()
+        m = ns['measures_on_device'](ctx, seg.data_ptr(), seg.data_ptr(), seg.shape, meta['block_shape'])
+        assert abs(m['rand-index'] - 1.0) < 1e-12 and abs(m['vi-split']) < 1e-12 and abs(m['vi-merge']) < 1e-12
+    finally:
+        L.cc_destroy(ctx)

@@ -143,3 +143,60 @@ def test_corrupt_chunk_raises(tmp_path):
     open(path, 'wb').write(buf[:-9])
     with pytest.raises(RuntimeError):
         n5.open_file(p, 'r')['seg'][:]
+
+
+def _raw_chunk(path, mode, dims_fastest_first, payload, count=None):
+    """A chunk file with an arbitrary (possibly lying) header, raw payload."""
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    head = struct.pack('>HH', mode, len(dims_fastest_first)) + struct.pack('>' + 'I' * len(dims_fastest_first),
+                                                                          *dims_fastest_first)
+    if mode == 1:
+        head += struct.pack('>I', count)
+    with open(path, 'wb') as f:
+        f.write(head + payload)
+
+
+def test_malformed_chunk_headers_raise(tmp_path):
+    """Chunk headers are untrusted input: unknown modes, dims beyond the dataset's
+    chunk size, a varlength count that differs from the dims, and a chunk smaller than its box
+    must raise -- never index past the decoded array -- for reads and for the read-merge-rewrite
+    of a partial write."""
+    import pytest
+    p = str(tmp_path / 'm.n5')
+    with n5.open_file(p) as f:
+        ds = f.create_dataset('v', shape=(8, 8, 8), dtype='uint32', chunks=(4, 4, 4), compression='raw')
+    chunk = os.path.join(p, 'v', '0', '0', '0')
+    full = np.arange(64, dtype='>u4').tobytes()
+    cases = [
+        (2, (4, 4, 4), full, None),                    # object mode: not a numeric chunk
+        (0, (4, 4, 0x10000), full, None),              # dims beyond the chunk size
+        (0, (0xFFFFFFFF, 0xFFFFFFFF, 4), full, None),  # product would overflow
+        (1, (4, 4, 4), full[:16], 4),                  # varlength count != prod(dims)
+        (0, (4, 2, 4), full[:128], None),              # smaller than its (4, 4, 4) box
+    ]
+    for mode, dims, payload, count in cases:
+        _raw_chunk(chunk, mode, dims, payload, count)
+        with pytest.raises(RuntimeError):
+            ds[0:4, 0:4, 0:4]
+        with pytest.raises(RuntimeError):             # partial write: read-merge-rewrite
+            ds[1:3, 1:3, 1:3] = np.ones((2, 2, 2), dtype='uint32')
+    # a well-formed varlength chunk still reads
+    _raw_chunk(chunk, 1, (4, 4, 4), full, 64)
+    np.testing.assert_array_equal(ds[0:4, 0:4, 0:4].ravel(), np.arange(64, dtype='uint32'))
+
+
+def test_temp_names_differ_across_processes(tmp_path):
+    """Two processes writing the same chunk use distinct temp files (pid in the name)."""
+    import subprocess
+    import sys
+    p = str(tmp_path / 'r.n5')
+    with n5.open_file(p) as f:
+        f.create_dataset('seg', shape=(64, 64, 64), dtype='uint64', chunks=(64, 64, 64), compression='gzip')
+    code = ('import sys, numpy as np; sys.path.insert(0, %r); from cluster_tools_amd import n5\n'
+            'ds = n5.open_file(%r)["seg"]\n'
+            'for i in range(20): ds[:] = np.full((64, 64, 64), int(sys.argv[1]), dtype=np.uint64)\n'
+            % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), p))
+    procs = [subprocess.Popen([sys.executable, '-c', code, str(k)]) for k in (3, 5)]
+    assert all(q.wait(timeout=120) == 0 for q in procs)
+    v = n5.open_file(p, 'r')['seg'][:]
+    assert len(np.unique(v)) == 1 and int(v[0, 0, 0]) in (3, 5)
