@@ -488,3 +488,48 @@ int64_t oracle_n_blocks(const int64_t* shape, const int64_t* block_shape) {
     grid_init(&g, shape, block_shape);
     return g.n_blocks;
 }
+
+/* ------------------------------------------------------------------------- */
+/* canonical relabel (the parity contract, BASELINE north_star): first        */
+/* occurrence in C order -> 1, 2, ...; 0 stays 0.  Same result as oracle.py's */
+/* numpy canon(), in one pass with an open-addressing hash (large volumes).   */
+/* Returns the number of distinct non-zero ids, or -1 if it exceeds 2^32-2.    */
+/* ------------------------------------------------------------------------- */
+int64_t oracle_canon_u64(const uint64_t* in, int64_t n, uint32_t* out) {
+    int64_t cap = 1 << 16;
+    uint64_t* key = (uint64_t*)calloc((size_t)cap, sizeof(uint64_t));
+    uint32_t* val = (uint32_t*)malloc((size_t)cap * sizeof(uint32_t));
+    if (!key || !val) { free(key); free(val); return -1; }
+    int64_t used = 0;
+    uint64_t prev = 0;
+    uint32_t prev_v = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const uint64_t v = in[i];
+        if (v == 0) { out[i] = 0; continue; }
+        if (v == prev && prev_v) { out[i] = prev_v; continue; }   /* runs are the common case */
+        if (2 * (used + 1) > cap) {                                /* grow x2, rehash */
+            int64_t nc = 2 * cap;
+            uint64_t* nk = (uint64_t*)calloc((size_t)nc, sizeof(uint64_t));
+            uint32_t* nv = (uint32_t*)malloc((size_t)nc * sizeof(uint32_t));
+            if (!nk || !nv) { free(nk); free(nv); free(key); free(val); return -1; }
+            for (int64_t j = 0; j < cap; ++j)
+                if (key[j]) {
+                    uint64_t h = splitmix64(key[j]) & (uint64_t)(nc - 1);
+                    while (nk[h]) h = (h + 1) & (uint64_t)(nc - 1);
+                    nk[h] = key[j]; nv[h] = val[j];
+                }
+            free(key); free(val);
+            key = nk; val = nv; cap = nc;
+        }
+        uint64_t h = splitmix64(v) & (uint64_t)(cap - 1);
+        while (key[h] && key[h] != v) h = (h + 1) & (uint64_t)(cap - 1);
+        if (!key[h]) {
+            if (used >= 0xFFFFFFFELL) { free(key); free(val); return -1; }
+            key[h] = v; val[h] = (uint32_t)(++used);
+        }
+        out[i] = prev_v = val[h];
+        prev = v;
+    }
+    free(key); free(val);
+    return used;
+}

@@ -86,10 +86,12 @@ def n_blocks_of(shape, block_shape):
     return int(np.prod([-(-s // b) for s, b in zip(shape, block_shape)]))
 
 
-def run_reference(inp, block_shape, threshold, mode, mask=None, n_jobs_bc=2, n_jobs_bf=1, channel=None, extra=None):
+def run_reference(inp, block_shape, threshold, mode, mask=None, n_jobs_bc=2, n_jobs_bf=1, channel=None, extra=None,
+                  compression='gzip'):
     """Run the five reference stages in a scratch folder; return artefacts.  channel (int or
     list): inp is 4-D (C, Z, Y, X) and block_components averages those channels
-    (block_components.py:150-159)."""
+    (block_components.py:150-159).  compression None: an uncompressed scratch output (large
+    cases; the storage codec does not enter the arithmetic)."""
     tmp = tempfile.mkdtemp(prefix='golden_')
     try:
         in_path = os.path.join(tmp, 'in.h5')
@@ -102,7 +104,7 @@ def run_reference(inp, block_shape, threshold, mode, mask=None, n_jobs_bc=2, n_j
         # output dataset as BlockComponentsBase.run_impl creates it (block_components.py:99-106)
         chunks = tuple(max(1, min(bs // 2, sh)) for bs, sh in zip(block_shape, shape))
         with h5py.File(out_path, 'w') as f:
-            f.require_dataset('seg', shape=shape, dtype='uint64', compression='gzip', chunks=chunks)
+            f.require_dataset('seg', shape=shape, dtype='uint64', compression=compression, chunks=chunks)
         nb = n_blocks_of(shape, block_shape)
         block_list = list(range(nb))
 
