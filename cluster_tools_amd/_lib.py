@@ -31,7 +31,8 @@ EXPORTS = (
 DTYPES = {'float32': 0, 'float64': 1, 'uint8': 2, 'int8': 3, 'uint16': 4, 'int16': 5, 'uint32': 6,
           'int32': 7, 'uint64': 8, 'int64': 9}
 # every symbol include/cc_n5.h declares (libcc_n5.so: host-only N5 codec)
-N5_LIB_PATH = os.path.join(_HERE, 'lib', 'libcc_n5.so')
+# override: the sanitizer build (tools/asan.sh) only
+N5_LIB_PATH = os.environ.get('CC_N5_LIB_PATH') or os.path.join(_HERE, 'lib', 'libcc_n5.so')
 N5_EXPORTS = ('cc_n5_version', 'cc_n5_last_error', 'cc_n5_read', 'cc_n5_write')
 
 

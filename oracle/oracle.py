@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, 'libcc_oracle.so')
+# override: the sanitizer build (tools/asan.sh) only
+_LIB_PATH = os.environ.get('CC_ORACLE_LIB') or os.path.join(_HERE, 'libcc_oracle.so')
 _lib = None
 
 MODES = {'greater': 0, 'less': 1, 'equal': 2}
