@@ -25,7 +25,7 @@ EXPORTS = (
     'cc_seam_pairs', 'cc_shard_finish', 'cc_set_debug', 'cc_threshold', 'cc_shard_top_plane32',
     'cc_seam_pairs32', 'cc_shard_top_cubes32', 'cc_seam_pairs_cubes32',
     'cc_evaluate', 'cc_get_overlaps', 'cc_relabel_consecutive', 'cc_set_option', 'cc_channel_mean',
-    'cc_gaussian_smooth_blocks', 'cc_gaussian_taps', 'cc_result_size',
+    'cc_gaussian_smooth_blocks', 'cc_gaussian_taps', 'cc_result_size', 'cc_resize_mask_nearest',
 )
 # CC_DTYPE_* of include/cc_mi355x.h (cc_channel_mean)
 DTYPES = {'float32': 0, 'float64': 1, 'uint8': 2, 'int8': 3, 'uint16': 4, 'int16': 5, 'uint32': 6,
@@ -116,6 +116,7 @@ def load():
         'cc_gaussian_smooth_blocks': (I, [P, P, P, P, ctypes.c_double, P]),
         'cc_gaussian_taps': (I, [ctypes.c_double, P, I]),
         'cc_result_size': (i64, []),
+        'cc_resize_mask_nearest': (I, [P, P, P, P, i64, i64, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -300,8 +301,30 @@ class Context:
         if out is None:
             out = torch.empty(shape[1:], dtype=torch.float32, device=dev)
         assert out.dtype == torch.float32 and tuple(out.shape) == tuple(shape[1:]) and out.is_contiguous()
-        _check(load().cc_channel_mean(self._h, _ptr(buf), DTYPES[dt], _ptr(_i64(shape)), _ptr(chans),
+        shape_a = _i64(shape)                         # alive across the call
+        _check(load().cc_channel_mean(self._h, _ptr(buf), DTYPES[dt], _ptr(shape_a), _ptr(chans),
                                       len(chans), _ptr(out)))
+        return out
+
+    def resize_mask(self, mask, shape, z0=0, nz=None):
+        """A mask of another shape than the volume (volume_utils.py:174-184, elf ResizedVolume
+        order 0): rows z0 .. z0 + nz of it resized to `shape` by nearest neighbour on the device
+        (cc_resize_mask_nearest), as a uint8 CUDA tensor of (nz, Y, X).  `mask` is a numpy array
+        or a CUDA uint8 tensor of any (mZ, mY, mX)."""
+        import torch
+        shape = tuple(int(s) for s in shape)
+        nz = shape[0] - z0 if nz is None else int(nz)
+        dev = torch.device('cuda', self.device)
+        if not hasattr(mask, 'data_ptr'):
+            m = np.ascontiguousarray(mask)
+            if m.dtype != np.uint8:
+                m = (m != 0).astype(np.uint8)
+            mask = torch.from_numpy(m).to(dev)
+        assert mask.is_cuda and mask.dtype == torch.uint8 and mask.dim() == 3 and mask.is_contiguous()
+        out = torch.empty((nz,) + shape[1:], dtype=torch.uint8, device=mask.device)
+        torch.cuda.current_stream(mask.device).synchronize()
+        ms, vs = _i64(mask.shape), _i64(shape)        # alive across the call
+        _check(load().cc_resize_mask_nearest(self._h, _ptr(mask), _ptr(ms), _ptr(vs), int(z0), int(nz), _ptr(out)))
         return out
 
     def gaussian_smooth_blocks(self, inp, block_shape, sigma, out=None):

@@ -15,6 +15,7 @@
 #include "cc_kernels.hip"
 #include "cc_stage_kernels.hip"
 #include "cc_generate.hip"
+#include "cc_mask.hip"
 
 using namespace cc;
 
@@ -80,7 +81,8 @@ struct cc_ctx {
         flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf, spec, mark, bflag,
         ev_main, ev_z, ev_seg, ev_gt, ev_flag, ev_part,   // evaluation (cc_eval.hip)
         rl_wg,                                            // relabel: per-workgroup id lists
-        gs1, gs2, gs_tab;                                 // Gaussian prefilter temporaries (cc_prefilter.hip)
+        gs1, gs2, gs_tab,                                 // Gaussian prefilter temporaries (cc_prefilter.hip)
+        mask_xmap;                                        // resized masks (cc_mask.hip)
     int64_t ev_cap = 0;      // entries per evaluation hash table of the last cc_evaluate
     int64_t rl_cap = 0;      // id-set slots of the last cc_relabel_consecutive
     // last run
@@ -758,7 +760,7 @@ void cc_destroy(cc_ctx* c) {
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
                       &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec, &c->mark, &c->bflag,
                       &c->ev_main, &c->ev_z, &c->ev_seg, &c->ev_gt, &c->ev_flag, &c->ev_part, &c->rl_wg,
-                      &c->gs1, &c->gs2, &c->gs_tab};
+                      &c->gs1, &c->gs2, &c->gs_tab, &c->mask_xmap};
     for (DevBuf* b : bufs) b->release();
     c->pin.release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
@@ -881,6 +883,30 @@ int cc_threshold(cc_ctx* c, const float* in, const int64_t shape[3], const int64
         launch(c, "k_threshold", [&] { k_threshold<<<(unsigned)nt, NTHREADS, 0, s>>>(g, bp, in, thr, md, out); });
         sync(c);
         st.stage = 0;
+    })
+}
+
+int cc_resize_mask_nearest(cc_ctx* c, const uint8_t* mask, const int64_t mshape[3], const int64_t shape[3],
+                           int64_t z0, int64_t nz, uint8_t* out) {
+    CC_TRY({
+        CC_REQUIRE(c && mask && mshape && shape && out, "NULL argument");
+        for (int a = 0; a < 3; ++a) CC_REQUIRE(mshape[a] > 0 && shape[a] > 0, "empty mask or volume");
+        CC_REQUIRE(z0 >= 0 && nz >= 0 && z0 + nz <= shape[0], "z range outside the volume");
+        CC_REQUIRE(shape[1] * shape[2] < (1LL << 40) && (2 * shape[2] + 1) * mshape[2] < (1LL << 62) &&
+                       (2 * shape[1] + 1) * mshape[1] < (1LL << 62) && (2 * shape[0] + 1) * mshape[0] < (1LL << 62),
+                   "mask / volume extents too large");
+        CC_REQUIRE(nz * shape[1] < (1LL << 31), "too many rows for one launch");
+        HIP_OK(hipSetDevice(c->device));
+        if (nz == 0) return 0;
+        hipStream_t s = c->stream;
+        c->mask_xmap.ensure(shape[2] * sizeof(int32_t));
+        launch(c, "k_mask_xmap", [&] { k_mask_xmap<<<grid_stride(shape[2]), 256, 0, s>>>(shape[2], mshape[2], c->mask_xmap.as<int32_t>()); });
+        const dim3 grid((unsigned)((shape[2] + 1023) / 1024), (unsigned)(nz * shape[1]));
+        launch(c, "k_mask_resize", [&] {
+            k_mask_resize<<<grid, 256, 0, s>>>(mask, mshape[0], mshape[1], mshape[2], shape[0], shape[1], shape[2], z0,
+                                               c->mask_xmap.as<int32_t>(), out);
+        });
+        sync(c);
     })
 }
 

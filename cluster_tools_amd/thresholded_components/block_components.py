@@ -126,6 +126,28 @@ def _read(path, key, box=None, dtype=None):
     return a if dtype is None else a.astype(dtype, copy=False)
 
 
+def read_mask(config, shape, box=None):
+    """The job's mask on the host: (uint8 array, resized).  A full-resolution mask is read over
+    `box`; a mask of another shape (vu.ResizedMask) is read whole and resized on the device by
+    device_mask (cc_resize_mask_nearest).  (None, False) without a mask."""
+    if not config.get('mask_path', ''):
+        return None, False
+    m = vu.load_mask(config['mask_path'], config['mask_key'], shape)
+    resized = isinstance(m, vu.ResizedMask)
+    a = _read(config['mask_path'], config['mask_key'], None if resized else box)
+    return (a != 0).astype(np.uint8), resized
+
+
+def device_mask(ctx, mask, resized, shape, dev, z0=0, nz=None):
+    """uint8 CUDA mask of the (slab of the) volume from read_mask's result."""
+    import torch
+    if mask is None:
+        return None
+    if resized:
+        return ctx.resize_mask(mask, shape, z0, nz)
+    return torch.from_numpy(mask).to(dev)
+
+
 def channel_list(channel):
     """The reference's `channel` (int or list of ints, block_components.py:152) as a list; a
     JSON / luigi round trip may hand it over as a string."""
@@ -204,10 +226,7 @@ def _fused_single(config, shape, nb):
     timing = {'voxels': int(np.prod(shape)), 'gpus': 1}
     t = time.perf_counter()
     inp, chans = read_input(config)
-    mask = None
-    if config.get('mask_path', ''):
-        vu.load_mask(config['mask_path'], config['mask_key'], shape)
-        mask = (_read(config['mask_path'], config['mask_key']) != 0).astype(np.uint8)
+    mask, resized = read_mask(config, shape)
     timing['n5_read_s'] = time.perf_counter() - t
     device = int(os.environ.get('CC_DEVICE', '0'))
     dev = torch.device('cuda', device)
@@ -220,7 +239,7 @@ def _fused_single(config, shape, nb):
             x = torch.from_numpy(inp).to(dev)
         else:
             x = torch.from_numpy(inp.reshape(-1).view(np.uint8)).to(dev)
-        m = None if mask is None else torch.from_numpy(mask).to(dev)
+        m = device_mask(ctx, mask, resized, shape, dev)
         torch.cuda.synchronize(dev)
         timing['h2d_s'] = time.perf_counter() - t
         stack_shape, stack_dtype = inp.shape, inp.dtype
@@ -332,13 +351,10 @@ def block_components(job_id, config_path):
         import torch
         from cluster_tools_amd import _lib
         inp, chans = read_input(config)
-        mask = None
-        if config.get('mask_path', ''):
-            vu.load_mask(config['mask_path'], config['mask_key'], shape)
-            mask = (_read(config['mask_path'], config['mask_key']) != 0).astype(np.uint8)
+        mask, resized = read_mask(config, shape)
         with _lib.Context(int(os.environ.get('CC_DEVICE', '0'))) as ctx:
             x = to_device(ctx, inp, chans, ctx.torch_device(), config)
-            m = None if mask is None else torch.from_numpy(mask).to(x.device)
+            m = device_mask(ctx, mask, resized, shape, x.device)
             lab_dev, values = ctx.block_components(x, block_shape, threshold, mode, m)
             labels = lab_dev.cpu().numpy().view(np.uint64)
         _write_output(config, labels, [(0, s) for s in shape])

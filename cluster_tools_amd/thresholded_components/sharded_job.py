@@ -51,20 +51,17 @@ def main(config_path, out_dir):
 
     t = time.perf_counter()
     inp, chans = bc.read_input(config, box)
-    mask = None
-    if config.get('mask_path', ''):
-        vu.load_mask(config['mask_path'], config['mask_key'], shape)
-        mask = (bc._read(config['mask_path'], config['mask_key'], box) != 0).astype(np.uint8)
+    mask, resized = bc.read_mask(config, shape, box)
     timing['n5_read_s'] = time.perf_counter() - t
+    ctx = _lib.Context(gpu)
     t = time.perf_counter()
     x = torch.from_numpy(inp if chans is None else inp.reshape(-1).view(np.uint8)).to(dev)
-    m = None if mask is None else torch.from_numpy(mask).to(dev)
+    m = bc.device_mask(ctx, mask, resized, shape, dev, z0, zs)
     torch.cuda.synchronize(dev)
     timing['h2d_s'] = time.perf_counter() - t
     stack_shape, stack_dtype = inp.shape, inp.dtype
     del inp, mask
 
-    ctx = _lib.Context(gpu)
     if chans is not None or float(config.get('sigma_prefilter', 0) or 0) > 0:
         # input preparation (channel mean, sigma_prefilter: block-local, so slab-local)
         ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)

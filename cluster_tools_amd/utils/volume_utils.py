@@ -72,10 +72,23 @@ def block_to_bb(block):
     return tuple(slice(beg, end) for beg, end in zip(block.begin, block.end))
 
 
+class ResizedMask:
+    """A mask whose shape differs from the volume's (volume_utils.py:178-183: elf
+    ResizedVolume(mask, shape, order=0)).  The labelling jobs read `volume` whole and resize it
+    nearest-neighbour on the device (cc_resize_mask_nearest) -- see DESIGN.md for the rounding
+    (parity with elf unpinned: elf is absent)."""
+
+    def __init__(self, volume, shape):
+        if len(volume.shape) != len(shape):
+            raise ValueError('mask of %i dimensions for a %i-d volume' % (len(volume.shape), len(shape)))
+        self.volume = volume
+        self.shape = tuple(shape)
+        self.mask_shape = tuple(volume.shape)
+
+
 def load_mask(mask_path, mask_key, shape):
-    """volume_utils.py:174-184 for a full-resolution mask (resized masks are rejected)."""
+    """volume_utils.py:174-184: the mask dataset at full resolution, else a ResizedMask."""
     ds = file_reader(mask_path, 'r')[mask_key]
     if tuple(ds.shape) != tuple(shape):
-        raise NotImplementedError('mask shape %s != volume shape %s (ResizedVolume not supported)'
-                                  % (ds.shape, shape))
+        return ResizedMask(ds, shape)
     return ds

@@ -144,6 +144,15 @@ int cc_gaussian_smooth_blocks(cc_ctx* ctx, const float* in_dev, const int64_t sh
                               const int64_t block_shape[3], double sigma, float* out_dev);
 int cc_gaussian_taps(double sigma, float* taps, int cap);
 
+/* Masks of another shape than the volume (block_components.py:274-275 -> volume_utils.py:174-184:
+ * elf ResizedVolume(mask, shape, order=0)): out_dev = rows z0 .. z0 + nz of the mask resized to
+ * shape by nearest neighbour, src(c) = floor((c + 0.5) * m / S) per axis (skimage resize(order=0)
+ * of the whole mask), as uint8 0 / 1; mask_dev is the (mZ, mY, mX) uint8 mask, out_dev nz*Y*X
+ * bytes.  The result is the mask argument of the labelling entry points.  elf is absent: the
+ * reference resizes each block's crop, whose rounding this does not restate (parity unpinned). */
+int cc_resize_mask_nearest(cc_ctx* ctx, const uint8_t* mask_dev, const int64_t mshape[3], const int64_t shape[3],
+                           int64_t z0, int64_t nz, uint8_t* out_dev);
+
 /* merge_offsets (merge_offsets.py:104-120): exclusive scan of values; writes offsets
  * and empty flags; returns n_labels through *n_labels. Host arrays. */
 int cc_merge_offsets(const uint64_t* values_host, int64_t n_blocks, uint64_t* offsets_host,

@@ -115,6 +115,19 @@ def canon(labels):
     return out.reshape(np.shape(labels))
 
 
+def resize_mask_nearest(mask, shape):
+    """A mask of another shape resized to `shape` by pixel-centre nearest neighbour, the rule
+    cc_resize_mask_nearest implements for elf ResizedVolume(order=0) (volume_utils.py:174-184):
+    src(c) = floor((c + 0.5) * m / S) per axis, result uint8 0 / 1.  (elf is absent: this restates
+    the product's documented rule, parity with elf unpinned.)"""
+    mask = np.asarray(mask)
+    idx = []
+    for m, S in zip(mask.shape, shape):
+        c = np.arange(S, dtype=np.int64)
+        idx.append(np.minimum(((2 * c + 1) * m) // (2 * S), m - 1))
+    return (mask[np.ix_(*idx)] != 0).astype(np.uint8)
+
+
 def canon_fast(labels):
     """canon() for large uint64 volumes (cc_oracle.c oracle_canon_u64: one pass, hash map)."""
     a = np.ascontiguousarray(labels)

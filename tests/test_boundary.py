@@ -111,3 +111,23 @@ def test_integration_blocks_compile():
     assert len(blocks) >= 4
     for i, b in enumerate(blocks):
         compile(b, 'INTEGRATION.md#%d' % i, 'exec')
+
+
+def test_resized_mask_rule_and_loader(tmp_path):
+    """Masks of another shape (volume_utils.py:174-184): load_mask returns a ResizedMask instead of
+    raising, and the oracle's nearest-neighbour rule on a hand example (2x upsampling repeats,
+    2x downsampling takes the odd centres)."""
+    from cluster_tools_amd import n5
+    from cluster_tools_amd.utils import volume_utils as vu
+    from oracle import oracle as O
+    m = np.arange(8, dtype=np.uint8).reshape(2, 2, 2) % 3
+    up = O.resize_mask_nearest(m, (4, 4, 4))
+    np.testing.assert_array_equal(up, (m.repeat(2, 0).repeat(2, 1).repeat(2, 2) != 0).astype(np.uint8))
+    big = np.random.default_rng(0).integers(0, 2, (6, 8, 10)).astype(np.uint8)
+    np.testing.assert_array_equal(O.resize_mask_nearest(big, (3, 4, 5)), big[1::2, 1::2, 1::2])
+    p = str(tmp_path / 'm.n5')
+    with n5.open_file(p) as f:
+        f.create_dataset('mask', data=big, chunks=(3, 4, 5), compression='gzip')
+    r = vu.load_mask(p, 'mask', (12, 16, 20))
+    assert isinstance(r, vu.ResizedMask) and r.mask_shape == (6, 8, 10) and r.shape == (12, 16, 20)
+    assert not isinstance(vu.load_mask(p, 'mask', (6, 8, 10)), vu.ResizedMask)

@@ -329,3 +329,18 @@ def test_pass2_tile_order_vs_oracle(ctx, monkeypatch, shape, bs, mode, order):
     _check_against_oracle(ctx, inp, bs, 0.5, mode)
     inp = O.boundary_map(shape, origin=(5, 9, 2), dither=True)
     _check_against_oracle(ctx, inp, bs, 0.41, mode)
+
+
+@pytest.mark.parametrize('mshape,shape', [((20, 36, 44), (40, 72, 88)), ((40, 72, 88), (40, 72, 88)),
+                                          ((13, 50, 17), (40, 72, 88)), ((80, 30, 200), (40, 72, 89))])
+def test_resized_mask_device_vs_oracle(ctx, mshape, shape):
+    """cc_resize_mask_nearest (elf ResizedVolume(order=0) stand-in, volume_utils.py:174-184) against
+    the oracle's rule, whole volume and z-slabs; then the labelling with it (parity with elf
+    itself unpinned: elf is absent)."""
+    rng = np.random.default_rng(sum(mshape))
+    m = (rng.random(mshape) < 0.6).astype(np.uint8) * 3
+    want = O.resize_mask_nearest(m, shape)
+    np.testing.assert_array_equal(ctx.resize_mask(m, shape).cpu().numpy(), want)
+    np.testing.assert_array_equal(ctx.resize_mask(m, shape, z0=7, nz=16).cpu().numpy(), want[7:23])
+    inp = O.boundary_map(shape, origin=(2, 3, 4))
+    _check_against_oracle(ctx, inp, (16, 32, 32), 0.5, 'less', want)

@@ -260,3 +260,32 @@ def test_integration_binding_runs_as_documented():
         assert abs(m['rand-index'] - 1.0) < 1e-12 and abs(m['vi-split']) < 1e-12 and abs(m['vi-merge']) < 1e-12
     finally:
         L.cc_destroy(ctx)
+
+
+@pytest.mark.parametrize('gpus', [1, 2])
+def test_workflow_resized_mask(tmp_path, gpus):
+    """A mask dataset at half resolution (block_components.py:274-275 -> ResizedVolume order 0):
+    the workflow output equals the oracle labelling with the mask resized by the documented
+    nearest-neighbour rule (parity with elf unpinned), on one GPU and over two z-slab ranks."""
+    from cluster_tools_amd import n5
+    from cluster_tools_amd.thresholded_components import ThresholdedComponentsWorkflow
+    from cluster_tools_amd.thresholded_components.block_components import BlockComponentsLocal
+    name, bs = 'bmap_greater', (16, 32, 32)
+    d, data, cfg = _setup(tmp_path, name, bs)
+    shape = d['input'].shape
+    low = (np.random.default_rng(4).random(tuple(-(-s // 2) for s in shape)) < 0.7).astype(np.uint8)
+    with n5.open_file(data) as f:
+        f.create_dataset('volumes/mask_s1', data=low, chunks=(8, 16, 16), compression='gzip')
+    if gpus > 1:
+        c = BlockComponentsLocal.default_task_config()
+        c.update({'gpus': gpus, 'dist_backend': 'gloo'})
+        _write_task_config(cfg, 'block_components', c)
+    t = ThresholdedComponentsWorkflow(tmp_folder=str(tmp_path / 'tmp'), config_dir=cfg, target='local', max_jobs=4,
+                                      input_path=data, input_key='volumes/boundaries', output_path=data,
+                                      output_key='data', assignment_key='assignments', threshold=0.5,
+                                      threshold_mode='greater', mask_path=data, mask_key='volumes/mask_s1')
+    assert _build([t], tmp_path / 'tmp')
+    ref = O.label_volume(d['input'], bs, 0.5, 'greater', O.resize_mask_nearest(low, shape))
+    with n5.open_file(data, 'r') as f:
+        np.testing.assert_array_equal(f['data'][:], ref['labels'])
+        np.testing.assert_array_equal(f['assignments'][:], ref['lut'])
