@@ -2339,8 +2339,10 @@ __global__ __launch_bounds__(SEAM_PAIR_THREADS) void k_seam_pairs(int64_t n, int
                                                                   const u64* lower, u64* pa, u64* pb,
                                                                   unsigned long long* counter, u64 cap) {
     // workgroup-aggregated append: one global atomic per 1024 voxels (one per wave still
-    // serialised ~1.8 ms on the single counter)
+    // serialised ~1.8 ms on the single counter); counter[1] = the largest id emitted (atomicMax
+    // per workgroup: it sizes the packed key of dedup_pairs)
     __shared__ u32 wcnt[SEAM_PAIR_THREADS / 64];
+    __shared__ unsigned long long wmax[SEAM_PAIR_THREADS / 64];
     __shared__ unsigned long long gbase;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool emit = false;
@@ -2355,12 +2357,20 @@ __global__ __launch_bounds__(SEAM_PAIR_THREADS) void k_seam_pairs(int64_t n, int
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const u64 m = __ballot(emit);
-    if (lane == 0) wcnt[wave] = (u32)__popcll(m);
+    u64 mx = emit ? (a > b ? a : b) : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { const u64 t = __shfl_xor(mx, o, 64); mx = t > mx ? t : mx; }
+    if (lane == 0) { wcnt[wave] = (u32)__popcll(m); wmax[wave] = mx; }
     __syncthreads();
     if (threadIdx.x == 0) {
         u32 tot = 0;
-        for (int w = 0; w < SEAM_PAIR_THREADS / 64; ++w) { const u32 c = wcnt[w]; wcnt[w] = tot; tot += c; }
+        unsigned long long gm = 0;
+        for (int w = 0; w < SEAM_PAIR_THREADS / 64; ++w) {
+            const u32 c = wcnt[w]; wcnt[w] = tot; tot += c;
+            gm = wmax[w] > gm ? wmax[w] : gm;
+        }
         gbase = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
+        if (tot) atomicMax(counter + 1, gm);
     }
     __syncthreads();
     if (emit) {

@@ -558,27 +558,47 @@ static void phase_planes(cc_ctx* c, uint64_t* bottom, uint64_t* top) {
 }
 
 // sort (a, b) pairs lexicographically and drop duplicates; pa/pb are inputs (clobbered),
-// results in qa/qb; returns the number of unique pairs (host sync)
-static int64_t dedup_pairs(cc_ctx* c, u64* pa, u64* pb, u64* qa, u64* qb, int64_t n) {
+// results in qa/qb; returns the number of unique pairs (host sync).  max_id: an upper bound of
+// every id (~0 = unknown).  Ids below 2^32 are packed into one key a << nb | b (nb = bit width of
+// max_id): one radix sort over 2 nb bits and one unique, instead of two 64-bit sorts and a flag pass.
+static int64_t dedup_pairs(cc_ctx* c, u64* pa, u64* pb, u64* qa, u64* qb, int64_t n, uint64_t max_id = ~0ull) {
     hipStream_t s = c->stream;
     if (n == 0) return 0;
-    size_t tb = 0;
-    HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, pb, qb, pa, qa, (int)n, 0, 64, s));
-    c->cub_tmp.ensure(tb);
-    HIP_OK(hipcub::DeviceRadixSort::SortPairs(c->cub_tmp.p, tb, pb, qb, pa, qa, (int)n, 0, 64, s));
-    HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, qa, pa, qb, pb, (int)n, 0, 64, s));
-    c->cub_tmp.ensure(tb);
-    HIP_OK(hipcub::DeviceRadixSort::SortPairs(c->cub_tmp.p, tb, qa, pa, qb, pb, (int)n, 0, 64, s));
-    c->flags.ensure(n + 16);
-    u8* flags = c->flags.as<u8>();
-    k_unique_flags<<<grid1d(n), 256, 0, s>>>(n, pa, pb, flags);
-    HIP_OK(hipGetLastError());
+    CC_REQUIRE(n < (1LL << 31), "too many pairs for one sort");
     c->scalars2.ensure(16);
     int* nsel = (int*)c->scalars2.p;
-    HIP_OK(hipcub::DeviceSelect::Flagged(nullptr, tb, pa, flags, qa, nsel, (int)n, s));
-    c->cub_tmp.ensure(tb);
-    HIP_OK(hipcub::DeviceSelect::Flagged(c->cub_tmp.p, tb, pa, flags, qa, nsel, (int)n, s));
-    HIP_OK(hipcub::DeviceSelect::Flagged(c->cub_tmp.p, tb, pb, flags, qb, nsel, (int)n, s));
+    size_t tb = 0;
+    if (max_id < (1ull << 32)) {
+        int nbits = 1;
+        while (nbits < 32 && (max_id >> nbits)) ++nbits;
+        u64* k0 = qa;            // qa / qb are free until the unpack
+        u64* k1 = qb;
+        k_pack_pairs<<<grid1d(n), 256, 0, s>>>(n, pa, pb, nbits, k0);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, k0, k1, (int)n, 0, 2 * nbits, s));
+        c->cub_tmp.ensure(tb);
+        HIP_OK(hipcub::DeviceRadixSort::SortKeys(c->cub_tmp.p, tb, k0, k1, (int)n, 0, 2 * nbits, s));
+        HIP_OK(hipcub::DeviceSelect::Unique(nullptr, tb, k1, pa, nsel, (int)n, s));
+        c->cub_tmp.ensure(tb);
+        HIP_OK(hipcub::DeviceSelect::Unique(c->cub_tmp.p, tb, k1, pa, nsel, (int)n, s));
+        k_unpack_pairs<<<grid1d(n), 256, 0, s>>>(nsel, pa, nbits, qa, qb);
+        HIP_OK(hipGetLastError());
+    } else {
+        HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, pb, qb, pa, qa, (int)n, 0, 64, s));
+        c->cub_tmp.ensure(tb);
+        HIP_OK(hipcub::DeviceRadixSort::SortPairs(c->cub_tmp.p, tb, pb, qb, pa, qa, (int)n, 0, 64, s));
+        HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, qa, pa, qb, pb, (int)n, 0, 64, s));
+        c->cub_tmp.ensure(tb);
+        HIP_OK(hipcub::DeviceRadixSort::SortPairs(c->cub_tmp.p, tb, qa, pa, qb, pb, (int)n, 0, 64, s));
+        c->flags.ensure(n + 16);
+        u8* flags = c->flags.as<u8>();
+        k_unique_flags<<<grid1d(n), 256, 0, s>>>(n, pa, pb, flags);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipcub::DeviceSelect::Flagged(nullptr, tb, pa, flags, qa, nsel, (int)n, s));
+        c->cub_tmp.ensure(tb);
+        HIP_OK(hipcub::DeviceSelect::Flagged(c->cub_tmp.p, tb, pa, flags, qa, nsel, (int)n, s));
+        HIP_OK(hipcub::DeviceSelect::Flagged(c->cub_tmp.p, tb, pb, flags, qb, nsel, (int)n, s));
+    }
     int nu = 0;
     Readback rb(c, 64);
     rb.add(&nu, nsel, sizeof(int));

@@ -22,39 +22,47 @@ int64_t cc_block_faces(cc_ctx* c, const uint64_t* labels, const int64_t shape[3]
         const int64_t capn = std::max<int64_t>(1, n_face);
         c->pairs.ensure(2 * capn * sizeof(u64));
         c->pairs2.ensure(2 * capn * sizeof(u64));
-        c->counter.ensure(sizeof(unsigned long long));
+        c->counter.ensure(2 * sizeof(unsigned long long));
         c->scalars.ensure(4 * sizeof(u64));
         u64* pa = c->pairs.as<u64>();
         u64* pb = pa + capn;
         u64* qa = c->pairs2.as<u64>();
         u64* qb = qa + capn;
         unsigned long long* cnt = (unsigned long long*)c->counter.p;
-        HIP_OK(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), s));
         u8* bflag = nullptr;
         if (block_has_pairs_host) {
             c->bflag.ensure(n_blocks);
             bflag = c->bflag.as<u8>();
             HIP_OK(hipMemsetAsync(bflag, 0, n_blocks, s));
         }
+        unsigned long long* maxid = cnt + 1;
+        HIP_OK(hipMemsetAsync(cnt, 0, 2 * sizeof(unsigned long long), s));
         for (int a = 0; a < 3; ++a) {
+            FaceGeom G;
+            for (int d = 0; d < 3; ++d) { G.S[d] = shape[d]; G.B[d] = block_shape[d]; G.nb[d] = nb[d]; }
+            G.axis = a;
+            G.fdim = a == 2 ? 1 : 2;
+            G.rdim = a == 0 ? 1 : 0;
+            G.nrow = shape[G.rdim];
+            G.nchunk = (shape[G.fdim] + FACE_PAIR_THREADS - 1) / FACE_PAIR_THREADS;
             const int64_t nplanes = (shape[a] - 1) / block_shape[a];
-            const int64_t work = nplanes * (shape[0] * shape[1] * shape[2] / shape[a]);
-            if (work == 0) continue;
+            const int64_t ngrid = nplanes * G.nrow * G.nchunk;
+            if (ngrid == 0) continue;
+            CC_REQUIRE(ngrid < (1LL << 31), "face-pair grid too large");
             launch(c, "k_face_pairs", [&] {
-                k_face_pairs<<<grid1d(work), 256, 0, s>>>(a, shape[0], shape[1], shape[2], block_shape[0],
-                                                          block_shape[1], block_shape[2], nb[0], nb[1], nb[2],
-                                                          labels, c->offsets.as<u64>(), pa, pb, cnt, (u64)capn,
-                                                          bflag);
+                k_face_pairs<<<(unsigned)ngrid, FACE_PAIR_THREADS, 0, s>>>(G, labels, c->offsets.as<u64>(), pa, pb, cnt,
+                                                                          (u64)capn, maxid, bflag);
             });
         }
-        unsigned long long n_raw = 0;
-        HIP_OK(hipMemcpyAsync(&n_raw, cnt, sizeof(n_raw), hipMemcpyDeviceToHost, s));
+        unsigned long long rb2[2] = {0, 0};
+        HIP_OK(hipMemcpyAsync(rb2, cnt, sizeof(rb2), hipMemcpyDeviceToHost, s));
         if (bflag) HIP_OK(hipMemcpyAsync(block_has_pairs_host, bflag, n_blocks, hipMemcpyDeviceToHost, s));
         sync(c);
-        const int64_t n = (int64_t)n_raw;
+        const int64_t n = (int64_t)rb2[0];
         if (n == 0) return 0;
+        CC_REQUIRE(n <= capn, "face pair buffer overflow");
         // lexicographic sort + unique (block_faces.py:112,132,172 np.unique(axis=0))
-        const int64_t nu = dedup_pairs(c, pa, pb, qa, qb, n);
+        const int64_t nu = dedup_pairs(c, pa, pb, qa, qb, n, (uint64_t)rb2[1]);
         if (pairs_host && cap > 0) {
             const int64_t m = std::min<int64_t>(cap, nu);
             std::vector<u64> ha(m), hb(m);
@@ -117,11 +125,16 @@ int cc_write(cc_ctx* c, uint64_t* labels, const int64_t shape[3], const int64_t 
         HIP_OK(hipMemcpyAsync(c->offsets.p, offsets_host, n_blocks * sizeof(u64), hipMemcpyHostToDevice, s));
         HIP_OK(hipMemcpyAsync(c->lut.p, lut_host, n_labels * sizeof(u64), hipMemcpyHostToDevice, s));
         HIP_OK(hipMemsetAsync(c->counter.p, 0, sizeof(u32), s));
-        launch(c, "k_write_offsets", [&] {
-            k_write_offsets<<<grid_stride(n), 256, 0, s>>>(shape[0], shape[1], shape[2], block_shape[0], block_shape[1],
-                                                      block_shape[2], nb[1], nb[2], labels, c->offsets.as<u64>(),
-                                                      c->lut.as<u64>(), n_labels, c->counter.as<u32>());
-        });
+        const int64_t nchunk = (shape[2] + WRITE_CHUNK - 1) / WRITE_CHUNK;
+        const int64_t ngrid = shape[0] * shape[1] * nchunk;
+        CC_REQUIRE(ngrid < (1LL << 31) && shape[2] < (1LL << 32), "volume too large for the write grid");
+        if (ngrid > 0)
+            launch(c, "k_write_offsets", [&] {
+                k_write_offsets<<<(unsigned)ngrid, WRITE_THREADS, 0, s>>>(shape[1], shape[2], block_shape[0], block_shape[1],
+                                                                         (u32)block_shape[2], nb[1], nb[2], nchunk, labels,
+                                                                         c->offsets.as<u64>(), c->lut.as<u64>(), n_labels,
+                                                                         c->counter.as<u32>());
+            });
         u32 herr = 0;
         HIP_OK(hipMemcpyAsync(&herr, c->counter.p, sizeof(u32), hipMemcpyDeviceToHost, s));
         sync(c);
@@ -196,27 +209,29 @@ static int64_t seam_pairs_impl(cc_ctx* c, UP upper, const uint64_t* lower, int64
     const int64_t capn = std::max<int64_t>(1, n);
     c->pairs.ensure(2 * capn * sizeof(u64));
     c->pairs2.ensure(2 * capn * sizeof(u64));
-    c->counter.ensure(sizeof(unsigned long long));
+    c->counter.ensure(2 * sizeof(unsigned long long));
     u64* pa = c->pairs.as<u64>();
     u64* pb = pa + capn;
     u64* qa = c->pairs2.as<u64>();
     u64* qb = qa + capn;
     unsigned long long* cnt = (unsigned long long*)c->counter.p;
-    HIP_OK(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), s));
+    HIP_OK(hipMemsetAsync(cnt, 0, 2 * sizeof(unsigned long long), s));
     // plane width for the 'pair above' filter (any value is correct; the slab's X is exact)
     const int64_t X = (c->run && state(c).hg.g.Y * state(c).hg.g.X == n) ? state(c).hg.g.X : n;
     launch(c, "k_seam_pairs", [&] {
         k_seam_pairs<UP><<<grid1d(n, SEAM_PAIR_THREADS), SEAM_PAIR_THREADS, 0, s>>>(n, X, upper, lower, pa, pb, cnt,
                                                                                   (u64)capn);
     });
-    unsigned long long n_raw = 0;
+    unsigned long long rb2[2] = {0, 0};          // raw pair count, largest id
     {
         Readback rb(c, 64);
-        rb.add(&n_raw, cnt, sizeof(n_raw));
+        rb.add(rb2, cnt, sizeof(rb2));
         rb.wait();
     }
+    const unsigned long long n_raw = rb2[0];
+    CC_REQUIRE(n_raw <= (unsigned long long)capn, "seam pair buffer overflow");
     int64_t nu = 0;
-    launch(c, "seam_dedup", [&] { nu = dedup_pairs(c, pa, pb, qa, qb, (int64_t)n_raw); });
+    launch(c, "seam_dedup", [&] { nu = dedup_pairs(c, pa, pb, qa, qb, (int64_t)n_raw, (uint64_t)rb2[1]); });
     if (pairs && cap > 0 && nu > 0) {
         const int64_t m = std::min<int64_t>(cap, nu);
         launch(c, "k_interleave", [&] { k_interleave<<<grid1d(m), 256, 0, s>>>(m, qa, qb, pairs); });
