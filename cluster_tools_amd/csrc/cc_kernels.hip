@@ -2530,12 +2530,9 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
 // per tile; the block parameters come from k_block_stats + k_block_params (the same exact
 // foreground interval the labelling path uses).  float4 loads / uchar4 stores on full tiles.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(NTHREADS) void k_threshold(Geom g, const BlockParam* __restrict__ bp,
-                                                        const float* __restrict__ in, float thr, int mode,
-                                                        u8* __restrict__ out) {
-    const int64_t t = blockIdx.x;
-    const TileInfo ti = tile_info(g, t);
-    const BlockParam p = uniform_bp(bp[ti.block]);
+// threshold of one tile with block parameters p (uint8 0 / 1)
+__device__ __forceinline__ void threshold_tile(const Geom& g, const TileInfo& ti, const BlockParam& p,
+                                               const float* __restrict__ in, float thr, int mode, u8* __restrict__ out) {
     const int tid = threadIdx.x;
     const int n = ti.lz * ti.ly;
     auto at = [&](int row, int x) { return ((int64_t)(ti.z0 + row / ti.ly) * g.Y + ti.y0 + row % ti.ly) * g.X + ti.x0 + x; };
@@ -2553,6 +2550,105 @@ __global__ __launch_bounds__(NTHREADS) void k_threshold(Geom g, const BlockParam
             const int64_t o = at(i / ti.lx, i % ti.lx);
             out[o] = voxel_pred(p, in[o], thr, mode);
         }
+    }
+}
+
+__global__ __launch_bounds__(NTHREADS) void k_threshold(Geom g, const BlockParam* __restrict__ bp,
+                                                        const float* __restrict__ in, float thr, int mode,
+                                                        u8* __restrict__ out) {
+    const int64_t t = blockIdx.x;
+    const TileInfo ti = tile_info(g, t);
+    threshold_tile(g, ti, uniform_bp(bp[ti.block]), in, thr, mode, out);
+}
+
+// Speculative Threshold task: ONE read of the input.  Like k_spec (the labelling front), every
+// tile is thresholded with its block's guessed interval (k_sample + k_guess) while the exact block
+// statistics and the tile's TB (nearest values around the guessed bounds) accumulate; then
+// k_params_verify lists the tiles whose guessed bits are not exact and k_thr_fix rewrites only
+// those from the input.  Blocks without a guess are read for statistics only here (their tiles
+// are always listed).  SIDES as k_spec.
+template <int SIDES>
+__global__ __launch_bounds__(NTHREADS) void k_thr_spec(Geom g, SpecArgs sa, const float* __restrict__ in,
+                                                       u8* __restrict__ out) {
+    __shared__ u32 red[6][NTHREADS / 64];
+    const int64_t t = sa.t0 + blockIdx.x;
+    const TileInfo ti = tile_info(g, t);
+    const BlockParam p = uniform_bp(sa.guess[ti.block]);
+    if (p.kind != BP_INTERVAL) {
+        stats_tile(g, ti, in, sa.smin, sa.smax, sa.sflag, red);
+        return;
+    }
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const u32 lo = p.lo, hi = p.hi;
+    u32 mn = 0xFFFFFFFFu, mx = 0u, K1N = 0xFFFFFFFFu, K1X = 0u, K2N = 0xFFFFFFFFu, K2X = 0u;
+    auto voxel = [&](float x) -> u8 {
+        const u32 o = f2ord(__float_as_uint(x));
+        mn = min(mn, o);
+        mx = max(mx, o);
+        if (SIDES & 1) { const u32 k = o - lo; K1N = min(K1N, k); K1X = max(K1X, k); }
+        if (SIDES & 2) { const u32 k = hi - o; K2N = min(K2N, k); K2X = max(K2X, k); }
+        return SIDES == 1 ? o >= lo : SIDES == 2 ? o <= hi : (o >= lo && o <= hi);
+    };
+    const int n = ti.lz * ti.ly;
+    auto at = [&](int row, int x) { return ((int64_t)(ti.z0 + row / ti.ly) * g.Y + ti.y0 + row % ti.ly) * g.X + ti.x0 + x; };
+    if (ti.lx == TX && ((g.X | ti.x0) & 3) == 0) {
+        for (int i = tid; i < n * (TX / 4); i += NTHREADS) {
+            const int64_t o = at(i / (TX / 4), 4 * (i % (TX / 4)));
+            const float4 v = *reinterpret_cast<const float4*>(in + o);
+            uchar4 r;
+            r.x = voxel(v.x); r.y = voxel(v.y); r.z = voxel(v.z); r.w = voxel(v.w);
+            *reinterpret_cast<uchar4*>(out + o) = r;
+        }
+    } else {
+        for (int i = tid; i < n * ti.lx; i += NTHREADS) {
+            const int64_t o = at(i / ti.lx, i % ti.lx);
+            out[o] = voxel(in[o]);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (u32)__shfl_xor(mn, o, 64));
+        mx = max(mx, (u32)__shfl_xor(mx, o, 64));
+        if (SIDES & 1) { K1N = min(K1N, (u32)__shfl_xor(K1N, o, 64)); K1X = max(K1X, (u32)__shfl_xor(K1X, o, 64)); }
+        if (SIDES & 2) { K2N = min(K2N, (u32)__shfl_xor(K2N, o, 64)); K2X = max(K2X, (u32)__shfl_xor(K2X, o, 64)); }
+    }
+    if (lane == 0) {
+        red[0][wave] = mn; red[1][wave] = mx; red[2][wave] = K1N; red[3][wave] = K1X; red[4][wave] = K2N;
+        red[5][wave] = K2X;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < NTHREADS / 64; ++w) {
+            mn = min(mn, red[0][w]); mx = max(mx, red[1][w]);
+            K1N = min(K1N, red[2][w]); K1X = max(K1X, red[3][w]); K2N = min(K2N, red[4][w]); K2X = max(K2X, red[5][w]);
+        }
+        atomicMin(sa.smin + ti.block, mn);
+        atomicMax(sa.smax + ti.block, mx);
+        if (mx > 0xFF800000u || mn < 0x007FFFFFu) atomicOr(sa.sflag + ti.block, 1u);    // NaN
+        u32 A = 0u, B = 0xFFFFFFFFu, C = 0u, D = 0xFFFFFFFFu;      // as k_spec
+        if (SIDES & 1) {
+            if ((u64)K1N + lo < (1ull << 32)) B = K1N + lo;
+            if ((u64)K1X + lo >= (1ull << 32)) A = K1X + lo;
+        }
+        if (SIDES & 2) {
+            if (K2N <= hi) C = hi - K2N;
+            if (K2X > hi) D = hi - K2X;
+        }
+        u32* tb = sa.TB + 4 * t;
+        tb[0] = A; tb[1] = B; tb[2] = C; tb[3] = D;
+    }
+}
+
+// the tiles k_params_verify listed (FIX[0] of them, ids in FIX[1..]) thresholded again with their
+// block's exact parameters; a fixed grid walks the list (usually empty: the grid returns at once)
+__global__ __launch_bounds__(NTHREADS) void k_thr_fix(Geom g, const u32* FIX, const BlockParam* __restrict__ bp,
+                                                      const float* __restrict__ in, float thr, int mode,
+                                                      u8* __restrict__ out) {
+    const u32 n = __builtin_amdgcn_readfirstlane(FIX[0]);
+    for (u32 i = blockIdx.x; i < n; i += gridDim.x) {
+        const int64_t t = __builtin_amdgcn_readfirstlane(FIX[1 + i]);
+        const TileInfo ti = uniform_ti(tile_info(g, t));
+        threshold_tile(g, ti, uniform_bp(bp[ti.block]), in, thr, mode, out);
     }
 }
 

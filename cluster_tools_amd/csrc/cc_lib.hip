@@ -3,6 +3,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -23,6 +25,10 @@ static thread_local std::string g_err;
 
 #include "cc_host.hpp"
 
+// host time spent in device allocations (instrumentation of the cold, first-call cost: reported by
+// cc_get_profile as the pseudo-kernel "host_alloc" -- count = hipMalloc calls, ms = their time)
+static std::atomic<int64_t> g_alloc_count{0}, g_alloc_ns{0};
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -30,11 +36,14 @@ struct DevBuf {
     T* as() const { return (T*)p; }
     void ensure(size_t need) {
         if (need <= bytes && p) return;
+        const auto t0 = std::chrono::steady_clock::now();
         if (p) HIP_OK(hipFree(p));
         p = nullptr;
         size_t nb = std::max<size_t>(need + need / 8, 256);
         HIP_OK(hipMalloc(&p, nb));
         bytes = nb;
+        g_alloc_count += 1;
+        g_alloc_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     }
     void release() {
         if (p) (void)hipFree(p);
@@ -893,14 +902,48 @@ int cc_threshold(cc_ctx* c, const float* in, const int64_t shape[3], const int64
         u32* smax = smin + nb;
         u32* sflag = smax + nb;
         BlockParam* bp = c->bparam.as<BlockParam>();
+        BlockParam* guess = bp + nb;
         const float thr = (float)threshold;          // numpy: python float -> float32
-        HIP_OK(hipMemsetAsync(smin, 0xFF, nb * sizeof(u32), s));
-        HIP_OK(hipMemsetAsync(smax, 0x00, 2 * nb * sizeof(u32), s));
-        launch(c, "k_block_stats", [&] { k_block_stats<<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, smin, smax, sflag); });
-        launch(c, "k_block_params", [&] {
-            k_block_params<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, smin, smax, sflag, thr, md, bp);
-        });
-        launch(c, "k_threshold", [&] { k_threshold<<<(unsigned)nt, NTHREADS, 0, s>>>(g, bp, in, thr, md, out); });
+        if (const char* e = std::getenv("CC_THRESHOLD_TWO_PASS"); e && std::string(e) == "1") {
+            // A/B only: statistics pass, then the threshold pass (two reads of the input)
+            HIP_OK(hipMemsetAsync(smin, 0xFF, nb * sizeof(u32), s));
+            HIP_OK(hipMemsetAsync(smax, 0x00, 2 * nb * sizeof(u32), s));
+            launch(c, "k_block_stats", [&] { k_block_stats<<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, smin, smax, sflag); });
+            launch(c, "k_block_params", [&] {
+                k_block_params<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, smin, smax, sflag, thr, md, bp);
+            });
+            launch(c, "k_threshold", [&] { k_threshold<<<(unsigned)nt, NTHREADS, 0, s>>>(g, bp, in, thr, md, out); });
+        } else {
+            // one read: sample -> guessed interval -> threshold + exact statistics + TB per tile ->
+            // exact parameters, list of tiles whose guessed output is not exact -> rewrite those
+            c->spec.ensure((4 * nt + 4 * SAMPLE_PARTS * nb + nt + 1) * sizeof(u32));
+            u32* TB = c->spec.as<u32>();
+            u32* SPART = TB + 4 * nt;
+            u32* FIX = SPART + 4 * SAMPLE_PARTS * nb;
+            HIP_OK(hipMemsetAsync(smin, 0xFF, nb * sizeof(u32), s));
+            HIP_OK(hipMemsetAsync(smax, 0x00, 2 * nb * sizeof(u32), s));
+            HIP_OK(hipMemsetAsync(FIX, 0, sizeof(u32), s));
+            launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART); });
+            launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, md, guess); });
+            if (const char* e = std::getenv("CC_SPEC"); e && std::string(e) == "0")     // test hook: no guesses
+                HIP_OK(hipMemsetAsync(guess, 0, nb * sizeof(BlockParam), s));
+            SpecArgs sa;
+            sa.guess = guess;
+            sa.smin = smin; sa.smax = smax; sa.sflag = sflag;
+            sa.TB = TB;
+            sa.t0 = 0;
+            launch(c, "k_thr_spec", [&] {
+                if (md == MODE_GREATER) k_thr_spec<1><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, out);
+                else if (md == MODE_LESS) k_thr_spec<2><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, out);
+                else k_thr_spec<3><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, out);
+            });
+            launch(c, "k_params_verify", [&] {
+                k_params_verify<<<grid_stride(nt), 256, 0, s>>>(g, guess, smin, smax, sflag, thr, md, bp, TB, FIX);
+            });
+            launch(c, "k_thr_fix", [&] {
+                k_thr_fix<<<(unsigned)std::min<int64_t>(nt, 2048), NTHREADS, 0, s>>>(g, FIX, bp, in, thr, md, out);
+            });
+        }
         sync(c);
         st.stage = 0;
     })
@@ -975,6 +1018,8 @@ int cc_reset_profile(cc_ctx* c) {
     CC_TRY({
         CC_REQUIRE(c, "ctx is NULL");
         c->prof_acc.clear();
+        g_alloc_count = 0;
+        g_alloc_ns = 0;
     })
 }
 
@@ -982,7 +1027,9 @@ int cc_get_profile(cc_ctx* c, char* names, int names_cap, int64_t* counts, doubl
     if (!c) { g_err = "ctx is NULL"; return -1; }
     std::string joined;
     int i = 0;
-    for (auto& kv : c->prof_acc) {
+    std::map<std::string, ProfEntry> acc = c->prof_acc;
+    if (g_alloc_count) acc["host_alloc"] = ProfEntry{g_alloc_count.load(), g_alloc_ns.load() * 1e-6};
+    for (auto& kv : acc) {
         if (i >= cap) break;
         if (!joined.empty()) joined += ",";
         joined += kv.first;

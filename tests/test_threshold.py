@@ -79,3 +79,25 @@ def test_threshold_task_n5(tmp_path):
         assert tuple(ds.chunks) == tuple(max(1, min(b // 2, s)) for b, s in zip(bs, x.shape))
         np.testing.assert_array_equal(ds[:], exp)
     assert (tmp_path / 'tmp' / 'threshold.log').exists()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('variant', ['spec', 'no_guess', 'two_pass'])
+@pytest.mark.parametrize('mode,thr', [('greater', 0.5), ('less', 0.37), ('equal', 0.5)])
+def test_gpu_speculative_threshold_corrected(ctx, monkeypatch, variant, mode, thr):
+    """The one-read Threshold (k_thr_spec: guessed interval, exact statistics + TB, k_thr_fix of
+    the listed tiles) on inputs whose guess misses: continuous (dithered) data and block extremes
+    off the sampled rows; against the oracle, and the no-guess / two-pass variants."""
+    import torch
+    if variant == 'no_guess':
+        monkeypatch.setenv('CC_SPEC', '0')
+    elif variant == 'two_pass':
+        monkeypatch.setenv('CC_THRESHOLD_TWO_PASS', '1')
+    rng = np.random.default_rng(3)
+    q = (rng.integers(0, 17, (64, 128, 192)) / np.float32(16)).astype(np.float32)
+    q[1, 1, 5] = -1.0                      # outliers off the sampled rows (z = 8 mod 16, y = 16 mod 32)
+    q[33, 70, 100] = 3.0
+    for x, bs in [(O.boundary_map((96, 200, 256), origin=(5, 3, 1), dither=True), (32, 100, 128)),
+                  (q, (32, 64, 96)), (q, (64, 128, 192))]:
+        got = ctx.threshold(torch.from_numpy(x).cuda(), bs, thr, mode).cpu().numpy()
+        np.testing.assert_array_equal(got, O.threshold_volume(x, bs, thr, mode))
