@@ -473,12 +473,17 @@ class Context:
         bs = _i64(block_shape)
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         flags = np.zeros(len(offsets), dtype=np.uint8) if with_block_flags else None
+        # one call when the pairs fit the first buffer (the count comes back either way; a larger
+        # count is fetched by a second call with the exact capacity)
+        cap = 1 << 20
+        pairs = np.empty((cap, 2), dtype=np.uint64)
         n = _check(load().cc_block_faces(self._h, _ptr(labels_dev), _ptr(shape), _ptr(bs), _ptr(offsets),
-                                         None, 0, _ptr(flags)))
-        pairs = np.empty((n, 2), dtype=np.uint64)
-        if n:
+                                         _ptr(pairs), cap, _ptr(flags)))
+        if n > cap:
+            pairs = np.empty((n, 2), dtype=np.uint64)
             _check(load().cc_block_faces(self._h, _ptr(labels_dev), _ptr(shape), _ptr(bs), _ptr(offsets),
                                          _ptr(pairs), n, None))
+        pairs = pairs[:n].copy() if n < cap else pairs
         return (pairs, flags) if with_block_flags else pairs
 
     def merge_assignments(self, pairs, n_labels):

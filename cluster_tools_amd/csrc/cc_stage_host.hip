@@ -43,15 +43,15 @@ int64_t cc_block_faces(cc_ctx* c, const uint64_t* labels, const int64_t shape[3]
             G.axis = a;
             G.fdim = a == 2 ? 1 : 2;
             G.rdim = a == 0 ? 1 : 0;
-            G.nrow = shape[G.rdim];
-            G.nchunk = (shape[G.fdim] + FACE_PAIR_THREADS - 1) / FACE_PAIR_THREADS;
             const int64_t nplanes = (shape[a] - 1) / block_shape[a];
-            const int64_t ngrid = nplanes * G.nrow * G.nchunk;
-            if (ngrid == 0) continue;
-            CC_REQUIRE(ngrid < (1LL << 31), "face-pair grid too large");
+            const int64_t nchunk = (shape[G.fdim] + FP_CHUNK - 1) / FP_CHUNK;
+            if (nplanes == 0) continue;
+            CC_REQUIRE(shape[G.rdim] < 65536 && nplanes < 65536 && nchunk < (1LL << 31) && shape[G.fdim] < (1LL << 32),
+                       "face-pair grid out of range (rows < 65536)");
+            const dim3 grid((unsigned)nchunk, (unsigned)shape[G.rdim], (unsigned)nplanes);
             launch(c, "k_face_pairs", [&] {
-                k_face_pairs<<<(unsigned)ngrid, FACE_PAIR_THREADS, 0, s>>>(G, labels, c->offsets.as<u64>(), pa, pb, cnt,
-                                                                          (u64)capn, maxid, bflag);
+                k_face_pairs<<<grid, FACE_PAIR_THREADS, 0, s>>>(G, labels, c->offsets.as<u64>(), pa, pb, cnt, (u64)capn,
+                                                                maxid, bflag);
             });
         }
         unsigned long long rb2[2] = {0, 0};
@@ -126,14 +126,12 @@ int cc_write(cc_ctx* c, uint64_t* labels, const int64_t shape[3], const int64_t 
         HIP_OK(hipMemcpyAsync(c->lut.p, lut_host, n_labels * sizeof(u64), hipMemcpyHostToDevice, s));
         HIP_OK(hipMemsetAsync(c->counter.p, 0, sizeof(u32), s));
         const int64_t nchunk = (shape[2] + WRITE_CHUNK - 1) / WRITE_CHUNK;
-        const int64_t ngrid = shape[0] * shape[1] * nchunk;
-        CC_REQUIRE(ngrid < (1LL << 31) && shape[2] < (1LL << 32), "volume too large for the write grid");
-        if (ngrid > 0)
+        CC_REQUIRE(shape[0] < 65536 && shape[1] < 65536 && shape[2] < (1LL << 32), "volume too large for the write grid");
+        if (n > 0)
             launch(c, "k_write_offsets", [&] {
-                k_write_offsets<<<(unsigned)ngrid, WRITE_THREADS, 0, s>>>(shape[1], shape[2], block_shape[0], block_shape[1],
-                                                                         (u32)block_shape[2], nb[1], nb[2], nchunk, labels,
-                                                                         c->offsets.as<u64>(), c->lut.as<u64>(), n_labels,
-                                                                         c->counter.as<u32>());
+                k_write_offsets<<<dim3((unsigned)nchunk, (unsigned)shape[1], (unsigned)shape[0]), WRITE_THREADS, 0, s>>>(
+                    shape[1], shape[2], block_shape[0], block_shape[1], (u32)block_shape[2], nb[1], nb[2], labels,
+                    c->offsets.as<u64>(), c->lut.as<u64>(), n_labels, c->counter.as<u32>());
             });
         u32 herr = 0;
         HIP_OK(hipMemcpyAsync(&herr, c->counter.p, sizeof(u32), hipMemcpyDeviceToHost, s));

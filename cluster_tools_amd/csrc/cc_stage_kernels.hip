@@ -8,81 +8,109 @@ namespace cc {
 
 // Face pairs of one axis (volume_utils.py:187-215, halo 1; block_faces.py:87-113): voxel p on the
 // last plane of its block along `axis` pairs with p + e_axis in the next block when both labels
-// are non-zero.  Grid: one workgroup per (face plane k, row r, chunk of 1024 along the row's
-// contiguous dimension f); the row walks f = x (z / y faces: coalesced uint64 loads) or f = y
-// (x faces).  A pair equal to that of the voxel before it along f or the one in the previous
-// row is not emitted (the dedup that follows sees every distinct pair at least once: its first
-// voxel in index order always emits), and appends are aggregated per workgroup: one global
-// atomic per 1024 voxels instead of one per pair.  maxid (atomicMax per workgroup) sizes the
-// packed sort of dedup_pairs.  No 64-bit division: the coordinates come from the grid, block
-// indices from 32-bit divisions.
-constexpr int FACE_PAIR_THREADS = 1024;
+// are non-zero.  Grid (chunk, row r, face plane k): a face plane is walked in rows along its
+// fast dimension f (x for z / y faces: coalesced, one 16-B load per two voxels; y for x faces:
+// strided by nature), FP_PER voxels per thread.  A pair equal to that of the voxel before it
+// along f or of the voxel in the previous row is not emitted (the dedup that follows sees every
+// distinct pair at least once: its first voxel in index order always emits), appends are
+// aggregated per workgroup (one global atomic per workgroup that has pairs), and maxid
+// (atomicMax) sizes the packed sort of dedup_pairs.  No 64-bit division: coordinates from the
+// grid, the block index along f from one 32-bit division per thread.
+constexpr int FACE_PAIR_THREADS = 256, FP_PER = 4, FP_CHUNK = FACE_PAIR_THREADS * FP_PER;
 
 struct FaceGeom {
     int64_t S[3], B[3], nb[3];
     int axis, fdim, rdim;          // face normal, the plane's fast (row) and slow (row index) dimensions
-    int64_t nrow;                  // rows per face plane = S[rdim]
-    int64_t nchunk;                // chunks of FACE_PAIR_THREADS along fdim
 };
-
-__device__ __forceinline__ int64_t fg_index(const FaceGeom& G, const int64_t p[3]) {
-    return (p[0] * G.S[1] + p[1]) * G.S[2] + p[2];
-}
-__device__ __forceinline__ int64_t fg_block(const FaceGeom& G, const int64_t p[3]) {
-    return (((int64_t)((u32)p[0] / (u32)G.B[0])) * G.nb[1] + (int64_t)((u32)p[1] / (u32)G.B[1])) * G.nb[2] +
-           (int64_t)((u32)p[2] / (u32)G.B[2]);
-}
 
 __global__ __launch_bounds__(FACE_PAIR_THREADS) void k_face_pairs(FaceGeom G, const u64* __restrict__ L,
                                                                   const u64* __restrict__ off, u64* pa, u64* pb,
                                                                   unsigned long long* counter, u64 cap,
                                                                   unsigned long long* maxid, u8* bflag) {
     __shared__ u32 wcnt[FACE_PAIR_THREADS / 64];
+    __shared__ unsigned long long wmax[FACE_PAIR_THREADS / 64];
     __shared__ unsigned long long gbase;
-    const int64_t w = blockIdx.x;
-    const int64_t chunk = w % G.nchunk, row = (w / G.nchunk) % G.nrow, k = w / (G.nchunk * G.nrow);
     const int ax = G.axis, fd = G.fdim, rd = G.rdim;
-    int64_t p[3];
-    p[ax] = (k + 1) * G.B[ax] - 1;
-    p[rd] = row;
-    p[fd] = chunk * FACE_PAIR_THREADS + threadIdx.x;
-    const int64_t stride = ax == 0 ? G.S[1] * G.S[2] : ax == 1 ? G.S[2] : 1;
-    bool emit = false;
-    u64 a = 0, b = 0;
-    if (p[fd] < G.S[fd]) {
-        const int64_t i = fg_index(G, p);
-        const u64 la = L[i], lb = L[i + stride];
-        if (la && lb) {
-            int64_t q[3] = {p[0], p[1], p[2]};
-            q[ax] += 1;
-            const int64_t ba = fg_block(G, p), bb = fg_block(G, q);
-            a = la + off[ba];
-            b = lb + off[bb];
-            emit = true;
-            if (bflag) bflag[ba] = 1;      // block ba's face job has a pair (block_faces.py:116-137)
-            // the same pair at the voxel before (f - 1) or in the previous row (r - 1): drop
-            for (int d = 0; d < 2 && emit; ++d) {
-                const int dim = d == 0 ? fd : rd;
-                if (p[dim] == 0) continue;
-                int64_t pn[3] = {p[0], p[1], p[2]};
-                pn[dim] -= 1;
-                const int64_t in = fg_index(G, pn);
-                const u64 na = L[in], nbv = L[in + stride];
-                if (na && nbv) {
-                    int64_t qn[3] = {pn[0], pn[1], pn[2]};
-                    qn[ax] += 1;
-                    if (na + off[fg_block(G, pn)] == a && nbv + off[fg_block(G, qn)] == b) emit = false;
-                }
+    const int64_t row = blockIdx.y, k = blockIdx.z;
+    const int64_t f0 = ((int64_t)blockIdx.x * FACE_PAIR_THREADS + threadIdx.x) * FP_PER;
+    const int64_t Sf = G.S[fd];
+    // strides of the three roles in the C-order volume
+    const int64_t st[3] = {G.S[1] * G.S[2], G.S[2], 1};
+    const int64_t pax = (k + 1) * G.B[ax] - 1;                 // last plane of block row k along ax
+    const int64_t base = pax * st[ax] + row * st[rd];          // voxel (pax, row, f = 0)
+    const int64_t sf = st[fd], sa = st[ax], sr = st[rd];
+    // block indices: along ax k / k + 1, along rd row / B, along f per voxel
+    const int64_t bi_r = row / G.B[rd];
+    int64_t mul[3];                                            // block-index strides per dimension
+    mul[0] = G.nb[1] * G.nb[2]; mul[1] = G.nb[2]; mul[2] = 1;
+    const int64_t ba_fix = k * mul[ax] + bi_r * mul[rd], bb_fix = (k + 1) * mul[ax] + bi_r * mul[rd];
+    u64 la[FP_PER], lb[FP_PER];
+    bool in[FP_PER];
+#pragma unroll
+    for (int j = 0; j < FP_PER; ++j) {
+        in[j] = f0 + j < Sf;
+        la[j] = in[j] ? L[base + (f0 + j) * sf] : 0ull;
+        lb[j] = in[j] ? L[base + (f0 + j) * sf + sa] : 0ull;
+    }
+    // the voxel before this thread's first one (f0 - 1) and the previous row's, for the dedup
+    const bool hp = f0 > 0 && f0 - 1 < Sf, hr = row > 0;
+    const u64 pla = hp ? L[base + (f0 - 1) * sf] : 0ull, plb = hp ? L[base + (f0 - 1) * sf + sa] : 0ull;
+    const u32 Bf = (u32)G.B[fd];
+    const u32 bf0 = (u32)f0 / Bf;                              // block index along f of voxel f0
+    const u32 fe = (bf0 + 1) * Bf;                             // first f of the next block
+    const u64 prow_bi = (u64)((row - 1) / G.B[rd]);            // block row of the previous row
+    bool emit[FP_PER];
+    u64 a[FP_PER], b[FP_PER];
+    u64 mx = 0;
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < FP_PER; ++j) {
+        const int64_t f = f0 + j;
+        // FP_PER consecutive voxels cross at most one block face when B_f >= FP_PER
+        const u32 bfj = Bf >= (u32)FP_PER ? bf0 + ((u64)f >= fe ? 1u : 0u) : (u32)f / Bf;
+        emit[j] = in[j] && la[j] && lb[j];
+        a[j] = emit[j] ? la[j] + off[ba_fix + bfj * mul[fd]] : 0ull;
+        b[j] = emit[j] ? lb[j] + off[bb_fix + bfj * mul[fd]] : 0ull;
+        if (emit[j]) {
+            // previous voxel along f: in registers, or the loaded f0 - 1
+            u64 qa = 0, qb = 0;
+            if (j > 0) { qa = a[j - 1]; qb = b[j - 1]; }
+            else if (hp && pla && plb) {
+                const u32 bfp = (u32)(f0 - 1) / Bf;
+                qa = pla + off[ba_fix + bfp * mul[fd]];
+                qb = plb + off[bb_fix + bfp * mul[fd]];
+            }
+            if (qa == a[j] && qb == b[j]) emit[j] = false;
+        }
+        if (emit[j] && hr) {
+            // previous row (same f): its block row may differ
+            const int64_t ip = base - sr + f * sf;
+            const u64 ra = L[ip], rb = L[ip + sa];
+            if (ra && rb) {
+                const int64_t fa = k * mul[ax] + (int64_t)prow_bi * mul[rd] + bfj * mul[fd];
+                const int64_t fb = (k + 1) * mul[ax] + (int64_t)prow_bi * mul[rd] + bfj * mul[fd];
+                if (ra + off[fa] == a[j] && rb + off[fb] == b[j]) emit[j] = false;
             }
         }
+        if (emit[j]) {
+            any = true;
+            mx = a[j] > mx ? a[j] : mx;
+            mx = b[j] > mx ? b[j] : mx;
+            if (bflag) bflag[ba_fix + bfj * mul[fd]] = 1;      // block_faces.py:116-137 job flag
+        }
     }
+    u32 cnt = 0;
+#pragma unroll
+    for (int j = 0; j < FP_PER; ++j) cnt += emit[j] ? 1u : 0u;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const u64 m = __ballot(emit);
-    u64 mx = emit ? (a > b ? a : b) : 0ull;
+    // wave-exclusive scan of the per-thread counts
+    u32 x = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) { const u32 y = __shfl_up(x, o, 64); if (lane >= o) x += y; }
+    const u32 wtot = __shfl(x, 63, 64);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) { const u64 t = __shfl_xor(mx, o, 64); mx = t > mx ? t : mx; }
-    __shared__ unsigned long long wmax[FACE_PAIR_THREADS / 64];
-    if (lane == 0) { wcnt[wave] = (u32)__popcll(m); wmax[wave] = mx; }
+    if (lane == 0) { wcnt[wave] = wtot; wmax[wave] = mx; }
     __syncthreads();
     if (threadIdx.x == 0) {
         u32 tot = 0;
@@ -95,10 +123,14 @@ __global__ __launch_bounds__(FACE_PAIR_THREADS) void k_face_pairs(FaceGeom G, co
         if (tot) atomicMax(maxid, gm);
     }
     __syncthreads();
-    if (emit) {
-        const unsigned long long pos = gbase + wcnt[wave] + __popcll(m & ((1ull << lane) - 1));
-        if (pos < cap) { pa[pos] = a; pb[pos] = b; }
-    }
+    (void)any;
+    unsigned long long pos = gbase + wcnt[wave] + (x - cnt);
+#pragma unroll
+    for (int j = 0; j < FP_PER; ++j)
+        if (emit[j]) {
+            if (pos < cap) { pa[pos] = a[j]; pb[pos] = b[j]; }
+            ++pos;
+        }
 }
 
 __global__ void k_interleave(int64_t n, const u64* a, const u64* b, u64* out) {
@@ -165,22 +197,20 @@ __global__ void k_resolve64(u64 n, u64* P) {
 }
 
 // write.py:185-202 -- per non-empty block seg[seg != 0] += off[block]; seg = lut[seg], in place.
-// One workgroup per (row (z, y), chunk of 512 voxels): the row's block-row index comes from the
-// grid, the x block from a 32-bit division; each lane moves two voxels with one 16-B load and (if
-// either is non-zero) one 16-B store -- background pairs are not rewritten (they stay 0).
-constexpr int WRITE_THREADS = 256, WRITE_CHUNK = 2 * WRITE_THREADS;
+// Grid (chunk of WRITE_CHUNK voxels, y, z): the row's block-row offsets from the grid, the x block
+// from one 32-bit division per 16-B pair; each lane issues its WRITE_PER 16-B loads first (memory
+// parallelism), then the offset / LUT gathers, then the stores -- background pairs are not
+// rewritten (they stay 0).
+constexpr int WRITE_THREADS = 256, WRITE_PER = 4, WRITE_CHUNK = 2 * WRITE_THREADS * WRITE_PER;
 
 __global__ __launch_bounds__(WRITE_THREADS) void k_write_offsets(int64_t Y, int64_t X, int64_t bz, int64_t by,
-                                                                 u32 bx, int64_t nby, int64_t nbx, int64_t nchunk,
+                                                                 u32 bx, int64_t nby, int64_t nbx,
                                                                  u64* __restrict__ L, const u64* __restrict__ off,
                                                                  const u64* __restrict__ lut, u64 n_labels, u32* err) {
-    const int64_t w = blockIdx.x;
-    const int64_t row = w / nchunk, chunk = w % nchunk;
-    const int64_t z = row / Y, y = row % Y;
+    const int64_t z = blockIdx.z, y = blockIdx.y;
     const u64* offr = off + ((z / bz) * nby + y / by) * nbx;
-    u64* Lr = L + row * X;
-    const int64_t x = chunk * WRITE_CHUNK + 2 * (int64_t)threadIdx.x;
-    if (x >= X) return;
+    u64* Lr = L + (z * Y + y) * X;
+    const int64_t x0 = (int64_t)blockIdx.x * WRITE_CHUNK + 2 * (int64_t)threadIdx.x;
     bool bad = false;
     auto map = [&](u64 v, int64_t xx) -> u64 {
         if (!v) return 0ull;
@@ -189,17 +219,33 @@ __global__ __launch_bounds__(WRITE_THREADS) void k_write_offsets(int64_t Y, int6
         return lut[id];
     };
     if ((X & 1) == 0) {
-        ulonglong2 v = *reinterpret_cast<const ulonglong2*>(Lr + x);
-        if (v.x | v.y) {
-            v.x = map(v.x, x);
-            v.y = map(v.y, x + 1);
-            *reinterpret_cast<ulonglong2*>(Lr + x) = v;
+        ulonglong2 v[WRITE_PER];
+#pragma unroll
+        for (int j = 0; j < WRITE_PER; ++j) {
+            const int64_t x = x0 + j * 2 * WRITE_THREADS;
+            v[j] = x < X ? *reinterpret_cast<const ulonglong2*>(Lr + x) : make_ulonglong2(0ull, 0ull);
+        }
+#pragma unroll
+        for (int j = 0; j < WRITE_PER; ++j) {
+            const int64_t x = x0 + j * 2 * WRITE_THREADS;
+            if (v[j].x | v[j].y) {
+                v[j].x = map(v[j].x, x);
+                v[j].y = map(v[j].y, x + 1);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < WRITE_PER; ++j) {
+            const int64_t x = x0 + j * 2 * WRITE_THREADS;
+            if (x < X && (v[j].x | v[j].y)) *reinterpret_cast<ulonglong2*>(Lr + x) = v[j];
         }
     } else {
-        for (int k = 0; k < 2 && x + k < X; ++k) {
-            const u64 v = Lr[x + k];
-            if (v) Lr[x + k] = map(v, x + k);
-        }
+        for (int j = 0; j < WRITE_PER; ++j)
+            for (int q = 0; q < 2; ++q) {
+                const int64_t x = x0 + j * 2 * WRITE_THREADS + q;
+                if (x >= X) continue;
+                const u64 v = Lr[x];
+                if (v) Lr[x] = map(v, x);
+            }
     }
     if (bad) atomicOr(err, 1u);
 }

@@ -53,7 +53,7 @@ def _library_provenance():
     """On a GPU box, refuse to test a libcc_mi355x.so built from other sources than this tree's
     (cc_version() carries the source hash build.py embedded)."""
     import torch
-    if torch.cuda.is_available():
+    if torch.cuda.is_available() and not os.environ.get('CC_LIB_PATH'):   # CC_LIB_PATH: A/B builds only
         from cluster_tools_amd import _lib
         _lib.check_provenance()
     yield
