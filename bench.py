@@ -195,6 +195,10 @@ def main():
     value = nvox_all * args.steps / dt / 1e9
     b_alg = B_ALG + (1.0 if masked else 0.0)
     # dominant kernel of this rank, timed by HIP events on the stream it runs on
+    # host_* entries are the library's host-side accounting (allocations, stream synchronisations)
+    host = {k: v for k, v in breakdown.items() if k.startswith('host_')}
+    prof = {k: v for k, v in prof.items() if not k.startswith('host_')}
+    breakdown = {k: v for k, v in breakdown.items() if not k.startswith('host_')}
     kern = {k: v for k, v in prof.items() if v['count']}
     dom = max(kern, key=lambda k: kern[k]['total_ms'])
     avg_ms = kern[dom]['total_ms'] / kern[dom]['count']
@@ -234,6 +238,8 @@ def main():
                          'frac': round(e2e_gbs / HBM_PEAK_GBS, 4)},
         'kernels_ms_per_step': {k: round(v['total_ms'] / args.steps, 4) for k, v in
                                 sorted(breakdown.items(), key=lambda kv: -kv[1]['total_ms']) if v['count']},
+        'host_per_step': {k: {'count': v['count'] / args.steps, 'ms': round(v['total_ms'] / args.steps, 4)}
+                          for k, v in host.items()},
         'result': res,
         'lib': {'version': _lib.version(), 'src': lib_src},
     }

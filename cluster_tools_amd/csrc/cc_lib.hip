@@ -28,6 +28,8 @@ static thread_local std::string g_err;
 // host time spent in device allocations (instrumentation of the cold, first-call cost: reported by
 // cc_get_profile as the pseudo-kernel "host_alloc" -- count = hipMalloc calls, ms = their time)
 static std::atomic<int64_t> g_alloc_count{0}, g_alloc_ns{0};
+// host synchronisations of the library's streams (reported as "host_sync": count, host ms waited)
+static std::atomic<int64_t> g_sync_count{0}, g_sync_ns{0};
 
 struct DevBuf {
     void* p = nullptr;
@@ -168,8 +170,15 @@ static void resolve_profile(cc_ctx* c) {
     c->pending.clear();
 }
 
+static void stream_sync(hipStream_t st) {
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_OK(hipStreamSynchronize(st));
+    g_sync_count += 1;
+    g_sync_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+}
+
 static void sync(cc_ctx* c) {
-    HIP_OK(hipStreamSynchronize(c->stream));
+    stream_sync(c->stream);
     if (c->prof) resolve_profile(c);
 }
 
@@ -190,7 +199,7 @@ struct Readback {
     // while k_seams runs), so the stream is synchronised without resolving the profile events
     void wait(bool resolve = true) {
         if (resolve) sync(c);
-        else HIP_OK(hipStreamSynchronize(c->stream));
+        else stream_sync(c->stream);
         for (auto& o : outs) if (o.second.second) std::memcpy(o.first, (char*)c->pin.p + o.second.first, o.second.second);
     }
 };
@@ -1020,6 +1029,8 @@ int cc_reset_profile(cc_ctx* c) {
         c->prof_acc.clear();
         g_alloc_count = 0;
         g_alloc_ns = 0;
+        g_sync_count = 0;
+        g_sync_ns = 0;
     })
 }
 
@@ -1029,6 +1040,7 @@ int cc_get_profile(cc_ctx* c, char* names, int names_cap, int64_t* counts, doubl
     int i = 0;
     std::map<std::string, ProfEntry> acc = c->prof_acc;
     if (g_alloc_count) acc["host_alloc"] = ProfEntry{g_alloc_count.load(), g_alloc_ns.load() * 1e-6};
+    if (g_sync_count) acc["host_sync"] = ProfEntry{g_sync_count.load(), g_sync_ns.load() * 1e-6};
     for (auto& kv : acc) {
         if (i >= cap) break;
         if (!joined.empty()) joined += ",";

@@ -45,13 +45,13 @@ def main():
         ctx.label_volume(x, bs, 0.5, 'greater', out=out)
         torch.cuda.synchronize()
         warm.append(time.perf_counter() - t0)
-    kern_ms = sum(v['total_ms'] for k, v in cold_prof.items() if k != 'host_alloc')
+    kern_ms = sum(v['total_ms'] for k, v in cold_prof.items() if not k.startswith('host_'))
     print(json.dumps({
         'workload': 'C1 geometry %s block %s (one-shot drop-in job)' % (shape, bs),
         'ctx_create_ms': round(t_create * 1e3, 3), 'cold_call_ms': round(cold * 1e3, 3),
         'warm_call_ms': round(min(warm) * 1e3, 3), 'warm_calls_ms': [round(w * 1e3, 3) for w in warm],
         'cold_kernel_event_ms': round(kern_ms, 3),
-        'cold_host_alloc': cold_prof.get('host_alloc'),
+        'cold_host_alloc': cold_prof.get('host_alloc'), 'cold_host_sync': cold_prof.get('host_sync'),
         'cold_breakdown_ms': {k: round(v['total_ms'], 3) for k, v in
                               sorted(cold_prof.items(), key=lambda kv: -kv[1]['total_ms'])},
         'n_labels': res['n_labels'], 'process_s_to_first_call': round(time.perf_counter() - t_imp, 2)}))
