@@ -249,6 +249,7 @@ struct RunState {
     bool identity_lut = false; // the empty-job emulation dropped every block-face merge
     int stage = 0;             // 1 local done, 2 rid done, 3 final done
     bool rid0 = false;         // k_emit_roots already wrote the roots' ids for base 0
+    bool sum_known = false;    // sum_v already read back (phase_local's fast path)
 };
 
 static RunState& state(cc_ctx* c) {
@@ -435,12 +436,16 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     u64 nr_blocks = 0;
     if (block_uf) {
         launch(c, "k_block_scan", [&] { k_block_scan<<<1, SB_THREADS, 0, s>>>(nb, RCB, ROFFB, values, offsets, big, scalars); });
-        u64 sc23[2] = {0, 1};
+        u64 sc[4] = {0, 0, 0, 1};
         Readback rb(c, 64);
-        rb.add(sc23, scalars + 2, 2 * sizeof(u64));       // roots, "any block big" (k_block_scan)
+        rb.add(sc, scalars, 4 * sizeof(u64));             // sum of values, -, roots, "any block big" (k_block_scan)
         rb.wait();
-        nr_blocks = sc23[0];
-        any_big = sc23[1] ? 1 : 0;
+        nr_blocks = sc[2];
+        any_big = sc[3] ? 1 : 0;
+        if (!any_big) {                                   // the slab's sum of block values (cc_shard_begin)
+            st.sum_v = sc[0];
+            st.sum_known = true;
+        }
     }
     if (!any_big) {
         const int64_t nr = (int64_t)nr_blocks;
@@ -508,6 +513,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
 }
 
 static uint64_t read_sum_v(cc_ctx* c) {
+    if (state(c).sum_known) return state(c).sum_v;        // read back with the root count
     u64 v = 0;
     Readback rb(c, 64);
     rb.add(&v, c->scalars.p, sizeof(u64));

@@ -191,8 +191,7 @@ int cc_shard_planes(cc_ctx* c, uint64_t* bottom, uint64_t* top) {
     CC_TRY({
         CC_REQUIRE(c, "NULL ctx");
         HIP_OK(hipSetDevice(c->device));
-        phase_planes(c, bottom, top);
-        sync(c);
+        phase_planes(c, bottom, top);      // enqueued on the ctx's stream (callers order by stream)
     })
 }
 

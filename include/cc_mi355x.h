@@ -186,7 +186,8 @@ int cc_write(cc_ctx* ctx, uint64_t* labels_dev, const int64_t shape[3],
  *                    block values (merge_offsets.py:115-120 restricted to the slab)
  *   [allgather of the sums -> id_base = sum over the slabs below]
  *   cc_shard_assign  global ids (offsets + id_base) and the slab's 6-connected block-face unions
- *   cc_shard_planes  bottom / top voxel planes as component ids (Y*X uint64 each, NULL = skip)
+ *   cc_shard_planes  bottom / top voxel planes as component ids (Y*X uint64 each, NULL = skip);
+ *                    enqueued on the ctx's stream, returns without waiting (order by stream)
  *   [send top plane to rank r+1; rank r+1 forms the seam pairs with cc_seam_pairs;
  *    allgather of all seam pairs]
  *   cc_shard_finish  replicated union-find over all seam pairs, LUT, final labels.
