@@ -1,4 +1,5 @@
-"""Timing of the device Threshold task (cc_threshold: k_block_stats + k_block_params + k_threshold,
+"""Timing of the device Threshold task (cc_threshold: by default k_sample/k_guess -> k_thr_spec -> k_params_verify
+-> k_thr_fix of the listed tiles; CC_THRESHOLD_TWO_PASS=1 selects k_block_stats + k_block_params + k_threshold,
 reference thresholded_components/threshold.py) on C3.  Prints one JSON line: Gvox/s and the
 roofline of the two volume kernels at their algorithmic bytes (k_block_stats 4 B/voxel read,
 k_threshold 4 B read + 1 B uint8 write)."""
@@ -32,11 +33,13 @@ def main():
     k = {n: v['total_ms'] / steps for n, v in prof.items()}
     n = x.numel()
     roof = {}
-    for name, b in (('k_block_stats', 4.0), ('k_threshold', 5.0)):
+    for name, b in (('k_block_stats', 4.0), ('k_threshold', 5.0), ('k_thr_spec', 5.0)):
         if name in k:
             ach = n * b / (k[name] * 1e-3) / 1e9
             roof[name] = {'achieved_gbs': round(ach, 1), 'frac': round(ach / 8000.0, 4), 'alg_bytes_per_voxel': b}
     print(json.dumps({'metric': 'Gvoxels/sec Threshold task (normalize + threshold -> uint8)',
+                      'variant': 'two_pass' if os.environ.get('CC_THRESHOLD_TWO_PASS') == '1' else 'speculative',
+                      'e2e_frac_at_5B': round(n * 5.0 / dt / 1e9 / 8000.0, 4),
                       'value': round(n / dt / 1e9, 3), 'unit': 'Gvox/s', 'ms_per_step': round(dt * 1e3, 3),
                       'roofline': roof,
                       'kernels_ms_per_step': {a: round(v, 4) for a, v in sorted(k.items(), key=lambda kv: -kv[1])}}))
