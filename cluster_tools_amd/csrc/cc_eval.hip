@@ -243,7 +243,7 @@ struct EvSums {
 };
 
 static EvSums ev_table_sums(cc_ctx* c, const u64* keys, const u64* cnts, int64_t cap, u64* pu, double* pf) {
-    hipStream_t s = c->stream;
+    hipStream_t s = cstream(c);
     launch(c, "k_ev_reduce", [&] { k_ev_reduce<<<EV_REDUCE_WG, 256, 0, s>>>(keys, cnts, (u64)cap, pu, pf); });
     std::vector<u64> hu(2 * EV_REDUCE_WG);
     std::vector<double> hf(2 * EV_REDUCE_WG);
@@ -267,7 +267,7 @@ int cc_evaluate(cc_ctx* c, const uint64_t* seg, const uint64_t* gt, const int64_
     CC_TRY({
         CC_REQUIRE(c && seg && gt && shape && block_shape && out, "bad arguments");
         HIP_OK(hipSetDevice(c->device));
-        hipStream_t s = c->stream;
+        hipStream_t s = cstream(c);
         int64_t nb[3];
         for (int a = 0; a < 3; ++a) {
             CC_REQUIRE(shape[a] >= 1 && block_shape[a] >= 1, "shape and block_shape must be >= 1");
@@ -357,8 +357,8 @@ int64_t cc_get_overlaps(cc_ctx* c, uint64_t* seg_ids, uint64_t* gt_ids, uint64_t
         HIP_OK(hipSetDevice(c->device));
         const int64_t tc = c->ev_cap;
         std::vector<u64> h(2 * tc);
-        HIP_OK(hipMemcpyAsync(h.data(), c->ev_main.p, 2 * tc * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipStreamSynchronize(c->stream));
+        HIP_OK(hipMemcpyAsync(h.data(), c->ev_main.p, 2 * tc * sizeof(u64), hipMemcpyDeviceToHost, cstream(c)));
+        HIP_OK(hipStreamSynchronize(cstream(c)));
         int64_t k = 0;
         for (int64_t e = 0; e < tc; ++e) {
             if (h[e] == EV_EMPTY) continue;

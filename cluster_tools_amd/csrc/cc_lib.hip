@@ -1,6 +1,6 @@
 // cc_lib.hip -- host orchestration and the C ABI (include/cc_mi355x.h).
-// One translation unit: kernels (cc_kernels.hip, cc_stage_kernels.hip, cc_generate.hip) + hipcub.
-#include <hipcub/hipcub.hpp>
+// One translation unit: kernels (cc_kernels.hip, cc_stage_kernels.hip, cc_generate.hip) and the
+// library's own scan / sort / select (cc_prims.hip; no hipcub: see there why).
 
 #include <algorithm>
 #include <atomic>
@@ -53,6 +53,8 @@ struct DevBuf {
         bytes = 0;
     }
 };
+
+#include "cc_prims.hip"
 
 // pinned host memory for the pipeline's small read-backs: a copy into pageable memory went
 // through the runtime's staging path (25-80 us of idle GPU per read in the C3 trace)
@@ -114,6 +116,21 @@ struct cc_ctx {
     void* run = nullptr;     // RunState of the current labelling run
 };
 
+// the context's stream: the caller's (cc_set_stream), else its own, created on first use -- a
+// queue's creation costs milliseconds, and a job that hands over its stream never needs one
+static hipStream_t cstream(cc_ctx* c) {
+    if (!c->stream) {
+        if (!c->own_stream) HIP_OK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+        c->stream = c->own_stream;
+    }
+    return c->stream;
+}
+// the side stream (k_seams of finished front chunks), created on first use
+static hipStream_t side_stream(cc_ctx* c) {
+    if (!c->side) HIP_OK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    return c->side;
+}
+
 // ------------------------------------------------------------------------------------------
 // helpers
 // ------------------------------------------------------------------------------------------
@@ -146,7 +163,7 @@ static void launch_on(cc_ctx* c, hipStream_t s, const char* name, F&& f) {
 }
 
 template <class F>
-static void launch(cc_ctx* c, const char* name, F&& f) { launch_on(c, c->stream, name, static_cast<F&&>(f)); }
+static void launch(cc_ctx* c, const char* name, F&& f) { launch_on(c, cstream(c), name, static_cast<F&&>(f)); }
 
 // stream `waiter` waits for the work enqueued so far on `from`
 static void stream_wait(cc_ctx* c, hipStream_t from, hipStream_t waiter) {
@@ -178,7 +195,7 @@ static void stream_sync(hipStream_t st) {
 }
 
 static void sync(cc_ctx* c) {
-    stream_sync(c->stream);
+    stream_sync(cstream(c));
     if (c->prof) resolve_profile(c);
 }
 
@@ -191,7 +208,7 @@ struct Readback {
     Readback(cc_ctx* c_, size_t total) : c(c_) { c->pin.ensure(total); }
     void add(void* dst, const void* src, size_t bytes) {
         off = (off + 15) & ~size_t(15);
-        if (bytes) HIP_OK(hipMemcpyAsync((char*)c->pin.p + off, src, bytes, hipMemcpyDeviceToHost, c->stream));
+        if (bytes) HIP_OK(hipMemcpyAsync((char*)c->pin.p + off, src, bytes, hipMemcpyDeviceToHost, cstream(c)));
         outs.push_back({dst, {off, bytes}});
         off += bytes;
     }
@@ -199,7 +216,7 @@ struct Readback {
     // while k_seams runs), so the stream is synchronised without resolving the profile events
     void wait(bool resolve = true) {
         if (resolve) sync(c);
-        else stream_sync(c->stream);
+        else stream_sync(cstream(c));
         for (auto& o : outs) if (o.second.second) std::memcpy(o.first, (char*)c->pin.p + o.second.first, o.second.second);
     }
 };
@@ -221,7 +238,7 @@ static void upload_geom(cc_ctx* c, HostGeom& hg) {
     c->tiles.ensure(bytes);
     if (!(c->tiles.bytes == cap_before && c->h_tab == hg.tab)) {
         c->h_tab = hg.tab;
-        HIP_OK(hipMemcpyAsync(c->tiles.p, c->h_tab.data(), bytes, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(hipMemcpyAsync(c->tiles.p, c->h_tab.data(), bytes, hipMemcpyHostToDevice, cstream(c)));
     }
     bind_geom_tables(hg, c->tiles.as<int32_t>());
 }
@@ -272,7 +289,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     st.local_only = local_only;
     const int64_t nt = g.n_tiles, nb = g.n_blocks;
     const uint64_t nodes = (uint64_t)nt * g.cap;
-    hipStream_t s = c->stream;
+    hipStream_t s = cstream(c);
 
     c->bstat.ensure(nb * 3 * sizeof(u32));
     c->bparam.ensure(2 * nb * sizeof(BlockParam));     // exact parameters, then the guesses (k_sample)
@@ -343,7 +360,9 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         // bandwidth-bound).  Tiles k_fix relabels later get their seams recomputed below.
         const int64_t layer = (int64_t)g.nt[1] * g.nt[2];
         const int64_t n_chunks = lds_seams ? std::min<int64_t>(g.nt[0], c->front_chunks) : 1;
-        if (lds_seams) stream_wait(c, s, c->side);
+        // one chunk (the default): the seams follow on the same stream, no side stream needed
+        const hipStream_t ss = n_chunks > 1 ? side_stream(c) : s;
+        if (lds_seams && ss != s) stream_wait(c, s, ss);
         for (int64_t ci = 0; ci < n_chunks; ++ci) {
             const int64_t t0 = g.nt[0] * ci / n_chunks * layer, t1 = g.nt[0] * (ci + 1) / n_chunks * layer;
             sa.t0 = t0;
@@ -362,8 +381,8 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
 #undef CC_SPEC_LAUNCH
             });
             if (lds_seams) {
-                stream_wait(c, s, c->side);
-                seams(c->side, t0, t1);
+                if (ss != s) stream_wait(c, s, ss);
+                seams(ss, t0, t1);
             }
         }
         launch(c, "k_params_verify", [&] {
@@ -380,7 +399,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             rb.wait(false);
         }
         st.n_fix = nfix;
-        if (lds_seams) stream_wait(c, c->side, s);
+        if (lds_seams && ss != s) stream_wait(c, ss, s);
         if (nfix) {
             HIP_OK(hipMemsetAsync(fchg, 0, nt, s));
             launch(c, "k_fix", [&] {
@@ -465,14 +484,8 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     u32* RC = c->rc.as<u32>();
     u32* ROFF = c->roff.as<u32>();
     launch(c, "k_count_roots", [&] { k_count_roots<<<grid1d(nt, WAVES), NTHREADS, 0, s>>>(g, COUNT, P, RC); });
-    {
-        size_t tmp_bytes = 0;
-        HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, RC, ROFF, (int)nt + 1, s));
-        c->cub_tmp.ensure(tmp_bytes);
-        launch(c, "scan_roots", [&] {
-            HIP_OK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, RC, ROFF, (int)nt + 1, s));
-        });
-    }
+    c->cub_tmp.ensure(prims::scan_tmp_bytes<u32>(nt + 1));
+    launch(c, "scan_roots", [&] { prims::scan_excl<u32>(RC, ROFF, nt + 1, (char*)c->cub_tmp.p, s); });
     u32 n_roots_h = 0;
     {
         Readback rb(c, 64);
@@ -491,23 +504,12 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         launch(c, "k_collect_roots", [&] { k_collect_roots<<<grid1d(nt, WAVES), NTHREADS, 0, s>>>(g, COUNT, P, KR, ROFF, keys, vals); });
         int end_bit = KEY_BITS;
         while ((1LL << (end_bit - KEY_BITS)) < nb) ++end_bit;
-        size_t tmp_bytes = 0;
-        HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys2, vals, vals2, (int)nr, 0, end_bit, s));
-        c->cub_tmp.ensure(tmp_bytes);
-        launch(c, "radix_sort", [&] {
-            HIP_OK(hipcub::DeviceRadixSort::SortPairs(c->cub_tmp.p, tmp_bytes, keys, keys2, vals, vals2, (int)nr, 0, end_bit, s));
-        });
+        launch(c, "radix_sort", [&] { prims::sort_pairs<u64, u32>(keys, keys2, vals, vals2, nr, 0, end_bit, c->cub_tmp, s); });
         launch(c, "k_segments", [&] { k_segments<<<grid1d(nr), 256, 0, s>>>(nr, keys2, seg_start, seg_end); });
     }
     launch(c, "k_values", [&] { k_values<<<grid1d(nb), 256, 0, s>>>(nb, seg_start, seg_end, values); });
-    {
-        size_t tmp_bytes = 0;
-        HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, values, offsets, (int)nb, s));
-        c->cub_tmp.ensure(tmp_bytes);
-        launch(c, "scan_offsets", [&] {
-            HIP_OK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, values, offsets, (int)nb, s));
-        });
-    }
+    c->cub_tmp.ensure(prims::scan_tmp_bytes<u64>(nb));
+    launch(c, "scan_offsets", [&] { prims::scan_excl<u64>(values, offsets, nb, (char*)c->cub_tmp.p, s); });
     launch(c, "k_nlabels", [&] { k_nlabels<<<1, 1, 0, s>>>(nb, values, offsets, scalars); });
     st.stage = 1;
 }
@@ -527,7 +529,7 @@ static void phase_rid(cc_ctx* c, uint64_t base) {
     RunState& st = state(c);
     CC_REQUIRE(st.stage == 1, "phase order: call begin first");
     Geom& g = st.hg.g;
-    hipStream_t s = c->stream;
+    hipStream_t s = cstream(c);
     const int64_t nb = g.n_blocks, nr = st.nr, nt = g.n_tiles;
     st.base = base;
     u64* offsets = c->offsets.as<u64>();
@@ -573,7 +575,7 @@ static void phase_planes(cc_ctx* c, uint64_t* bottom, uint64_t* top) {
     RunState& st = state(c);
     CC_REQUIRE(st.stage == 2 && !st.local_only, "phase order: call assign first");
     Geom& g = st.hg.g;
-    hipStream_t s = c->stream;
+    hipStream_t s = cstream(c);
     const unsigned nlayer = (unsigned)((int64_t)g.nt[1] * g.nt[2]);
     if (bottom)
         launch(c, "k_plane_labels", [&] { k_plane_labels<false><<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), bottom); });
@@ -586,12 +588,11 @@ static void phase_planes(cc_ctx* c, uint64_t* bottom, uint64_t* top) {
 // every id (~0 = unknown).  Ids below 2^32 are packed into one key a << nb | b (nb = bit width of
 // max_id): one radix sort over 2 nb bits and one unique, instead of two 64-bit sorts and a flag pass.
 static int64_t dedup_pairs(cc_ctx* c, u64* pa, u64* pb, u64* qa, u64* qb, int64_t n, uint64_t max_id = ~0ull) {
-    hipStream_t s = c->stream;
+    hipStream_t s = cstream(c);
     if (n == 0) return 0;
     CC_REQUIRE(n < (1LL << 31), "too many pairs for one sort");
     c->scalars2.ensure(16);
     int* nsel = (int*)c->scalars2.p;
-    size_t tb = 0;
     if (max_id < (1ull << 32)) {
         int nbits = 1;
         while (nbits < 32 && (max_id >> nbits)) ++nbits;
@@ -599,29 +600,19 @@ static int64_t dedup_pairs(cc_ctx* c, u64* pa, u64* pb, u64* qa, u64* qb, int64_
         u64* k1 = qb;
         k_pack_pairs<<<grid1d(n), 256, 0, s>>>(n, pa, pb, nbits, k0);
         HIP_OK(hipGetLastError());
-        HIP_OK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, k0, k1, (int)n, 0, 2 * nbits, s));
-        c->cub_tmp.ensure(tb);
-        HIP_OK(hipcub::DeviceRadixSort::SortKeys(c->cub_tmp.p, tb, k0, k1, (int)n, 0, 2 * nbits, s));
-        HIP_OK(hipcub::DeviceSelect::Unique(nullptr, tb, k1, pa, nsel, (int)n, s));
-        c->cub_tmp.ensure(tb);
-        HIP_OK(hipcub::DeviceSelect::Unique(c->cub_tmp.p, tb, k1, pa, nsel, (int)n, s));
+        prims::sort_keys<u64>(k0, k1, n, 0, 2 * nbits, c->cub_tmp, s);
+        prims::select_unique<u64>(k1, pa, nsel, n, c->cub_tmp, s);
         k_unpack_pairs<<<grid1d(n), 256, 0, s>>>(nsel, pa, nbits, qa, qb);
         HIP_OK(hipGetLastError());
     } else {
-        HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, pb, qb, pa, qa, (int)n, 0, 64, s));
-        c->cub_tmp.ensure(tb);
-        HIP_OK(hipcub::DeviceRadixSort::SortPairs(c->cub_tmp.p, tb, pb, qb, pa, qa, (int)n, 0, 64, s));
-        HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, qa, pa, qb, pb, (int)n, 0, 64, s));
-        c->cub_tmp.ensure(tb);
-        HIP_OK(hipcub::DeviceRadixSort::SortPairs(c->cub_tmp.p, tb, qa, pa, qb, pb, (int)n, 0, 64, s));
+        prims::sort_pairs<u64, u64>(pb, qb, pa, qa, n, 0, 64, c->cub_tmp, s);
+        prims::sort_pairs<u64, u64>(qa, pa, qb, pb, n, 0, 64, c->cub_tmp, s);
         c->flags.ensure(n + 16);
         u8* flags = c->flags.as<u8>();
         k_unique_flags<<<grid1d(n), 256, 0, s>>>(n, pa, pb, flags);
         HIP_OK(hipGetLastError());
-        HIP_OK(hipcub::DeviceSelect::Flagged(nullptr, tb, pa, flags, qa, nsel, (int)n, s));
-        c->cub_tmp.ensure(tb);
-        HIP_OK(hipcub::DeviceSelect::Flagged(c->cub_tmp.p, tb, pa, flags, qa, nsel, (int)n, s));
-        HIP_OK(hipcub::DeviceSelect::Flagged(c->cub_tmp.p, tb, pb, flags, qb, nsel, (int)n, s));
+        prims::select_flagged<u64>(pa, flags, qa, nsel, n, c->cub_tmp, s);
+        prims::select_flagged<u64>(pb, flags, qb, nsel, n, c->cub_tmp, s);
     }
     int nu = 0;
     Readback rb(c, 64);
@@ -634,7 +625,7 @@ static int64_t dedup_pairs(cc_ctx* c, u64* pa, u64* pb, u64* qa, u64* qb, int64_
 static void phase_map(cc_ctx* c, const u64* pairs, int64_t n) {
     RunState& st = state(c);
     CC_REQUIRE(st.stage == 2, "phase order");
-    hipStream_t s = c->stream;
+    hipStream_t s = cstream(c);
     st.n_map = 0;
     if (n <= 0) return;
     // distinct ids
@@ -643,15 +634,10 @@ static void phase_map(cc_ctx* c, const u64* pairs, int64_t n) {
     u64* ids = c->map_ids.as<u64>();
     u64* ids2 = c->map_ids2.as<u64>();
     HIP_OK(hipMemcpyAsync(ids, pairs, 2 * n * sizeof(u64), hipMemcpyDeviceToDevice, s));
-    size_t tb = 0;
-    HIP_OK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, ids, ids2, (int)(2 * n), 0, 64, s));
-    c->cub_tmp.ensure(tb);
-    HIP_OK(hipcub::DeviceRadixSort::SortKeys(c->cub_tmp.p, tb, ids, ids2, (int)(2 * n), 0, 64, s));
+    prims::sort_keys<u64>(ids, ids2, 2 * n, 0, 64, c->cub_tmp, s);
     c->scalars2.ensure(16);
     int* nsel = (int*)c->scalars2.p;
-    HIP_OK(hipcub::DeviceSelect::Unique(nullptr, tb, ids2, ids, nsel, (int)(2 * n), s));
-    c->cub_tmp.ensure(tb);
-    HIP_OK(hipcub::DeviceSelect::Unique(c->cub_tmp.p, tb, ids2, ids, nsel, (int)(2 * n), s));
+    prims::select_unique<u64>(ids2, ids, nsel, 2 * n, c->cub_tmp, s);
     int m = 0;
     {
         Readback rb(c, 64);
@@ -678,7 +664,7 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
     RunState& st = state(c);
     CC_REQUIRE(st.stage == 2, "phase order: call assign first");
     Geom& g = st.hg.g;
-    hipStream_t s = c->stream;
+    hipStream_t s = cstream(c);
     const int64_t nt = g.n_tiles, nb = g.n_blocks, nr = st.nr;
     const uint64_t nodes = (uint64_t)nt * g.cap;
     u32* P = c->P.as<u32>();
@@ -785,9 +771,6 @@ int cc_create(int device, cc_ctx** out) {
         HIP_OK(hipSetDevice(device));
         cc_ctx* c = new cc_ctx();
         c->device = device;
-        HIP_OK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
-        HIP_OK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-        c->stream = c->own_stream;
         if (const char* e = std::getenv("CC_FRONT_CHUNKS")) c->front_chunks = std::max(1, atoi(e));
         *out = c;
     })
@@ -796,7 +779,7 @@ int cc_create(int device, cc_ctx** out) {
 void cc_destroy(cc_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->side) (void)hipStreamSynchronize(c->side);
     DevBuf* bufs[] = {&c->tiles, &c->bstat, &c->bparam, &c->bits, &c->faces, &c->count, &c->rc, &c->roff, &c->rl, &c->rcb, &c->P, &c->KR,
                       &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
@@ -841,16 +824,16 @@ int cc_label_volume_host(cc_ctx* c, const float* in, const uint8_t* mask, const 
         const int64_t n = shape[0] * shape[1] * shape[2];
         c->in_tmp.ensure(n * sizeof(float));
         c->out_tmp.ensure(n * sizeof(u64));
-        HIP_OK(hipMemcpyAsync(c->in_tmp.p, in, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        HIP_OK(hipMemcpyAsync(c->in_tmp.p, in, n * sizeof(float), hipMemcpyHostToDevice, cstream(c)));
         const uint8_t* dmask = nullptr;
         if (mask) {
             c->mask_tmp.ensure(n);
-            HIP_OK(hipMemcpyAsync(c->mask_tmp.p, mask, n, hipMemcpyHostToDevice, c->stream));
+            HIP_OK(hipMemcpyAsync(c->mask_tmp.p, mask, n, hipMemcpyHostToDevice, cstream(c)));
             dmask = c->mask_tmp.as<uint8_t>();
         }
         run_pipeline(c, c->in_tmp.as<float>(), dmask, shape, block_shape, threshold, to_mode(mode),
                      c->out_tmp.as<uint64_t>(), false, res);
-        HIP_OK(hipMemcpyAsync(labels, c->out_tmp.p, n * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipMemcpyAsync(labels, c->out_tmp.p, n * sizeof(u64), hipMemcpyDeviceToHost, cstream(c)));
         sync(c);
     })
 }
@@ -875,7 +858,7 @@ int64_t cc_get_lut(cc_ctx* c, uint64_t* out, int64_t cap) {
     if (cap < (int64_t)c->n_labels) { g_err = "cap too small"; return -1; }
     try {
         HIP_OK(hipSetDevice(c->device));
-        HIP_OK(hipMemcpyAsync(out, c->lut.p, c->n_labels * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipMemcpyAsync(out, c->lut.p, c->n_labels * sizeof(u64), hipMemcpyDeviceToHost, cstream(c)));
         sync(c);
     } catch (const CCError& e) {
         g_err = e.msg;
@@ -910,7 +893,7 @@ int cc_threshold(cc_ctx* c, const float* in, const int64_t shape[3], const int64
         upload_geom(c, st.hg);
         Geom& g = st.hg.g;
         const int64_t nt = g.n_tiles, nb = g.n_blocks;
-        hipStream_t s = c->stream;
+        hipStream_t s = cstream(c);
         c->bstat.ensure(nb * 3 * sizeof(u32));
         c->bparam.ensure(2 * nb * sizeof(BlockParam));
         u32* smin = c->bstat.as<u32>();
@@ -976,7 +959,7 @@ int cc_resize_mask_nearest(cc_ctx* c, const uint8_t* mask, const int64_t mshape[
         CC_REQUIRE(nz * shape[1] < (1LL << 31), "too many rows for one launch");
         HIP_OK(hipSetDevice(c->device));
         if (nz == 0) return 0;
-        hipStream_t s = c->stream;
+        hipStream_t s = cstream(c);
         c->mask_xmap.ensure(shape[2] * sizeof(int32_t));
         launch(c, "k_mask_xmap", [&] { k_mask_xmap<<<grid_stride(shape[2]), 256, 0, s>>>(shape[2], mshape[2], c->mask_xmap.as<int32_t>()); });
         const dim3 grid((unsigned)((shape[2] + 1023) / 1024), (unsigned)(nz * shape[1]));

@@ -63,7 +63,7 @@ static void launch_channel_mean(cc_ctx* c, const void* in, int64_t n, const Chan
                      (n % V == 0);
     const int64_t work = vec ? n / V : n;
     const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (work + 255) / 256), 256 * 16);
-    hipStream_t s = c->stream;
+    hipStream_t s = cstream(c);
     launch(c, "k_channel_mean", [&] {
         if (vec) k_channel_mean<T, V><<<grid, 256, 0, s>>>((const T*)in, n, cl, out);
         else k_channel_mean<T, 1><<<grid, 256, 0, s>>>((const T*)in, n, cl, out);
@@ -307,7 +307,7 @@ int cc_gaussian_smooth_blocks(cc_ctx* c, const float* in, const int64_t shape[3]
         }
         HIP_OK(hipSetDevice(c->device));
         const int64_t Z = shape[0], Y = shape[1], X = shape[2], n = Z * Y * X;
-        hipStream_t s = c->stream;
+        hipStream_t s = cstream(c);
         // block statistics (ordered min / max, NaN flag) -> normalize parameters
         RunState& st = state(c);
         st = RunState();

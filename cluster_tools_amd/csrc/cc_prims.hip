@@ -1,0 +1,345 @@
+// cc_prims.hip -- the library's own device primitives: exclusive scan, LSD radix sort (keys or
+// key/value pairs, any bit range), select-unique and select-flagged.
+//
+// Why not hipcub / rocprim: their dispatch instantiates every tuning configuration of every
+// algorithm used (944 of the code object's 1041 kernels, 1.3 MB of kernel metadata), and the HIP
+// runtime loads the whole code object on the library's first launch: 25-27 ms that every
+// one-shot drop-in job (one process, one call) paid before its first kernel ran
+// (profiles/r03_c1_cold.json, r03_cold_probe.json).  Every sort here is small (root lists of
+// the fallback path, seam pairs, the distinct ids of relabel): a few hundred thousand keys, far
+// from where onesweep tuning matters.
+//
+// Layout: 256-thread workgroups (4 waves of 64).  Radix sort: 8-bit digits, per pass
+//   k_rs_hist    per-workgroup digit histograms of a 2048-key tile, digit-major [d][wg]
+//   scan         exclusive scan of the 256 x nwg histogram (= each tile's first slot per digit)
+//   k_rs_scatter the tile in 8 rounds of 256 keys in index order; a key's rank among equal
+//                digits of its wave from 8 ballots, the waves' counts prefixed per digit in LDS
+//                (stable: rounds, waves and lanes are visited in index order)
+// Scan: tiles of 4096 (16 per thread): per-tile sums -> one-workgroup scan of the sums ->
+// each tile rescanned with its carry.
+namespace cc {
+namespace prims {
+
+constexpr int PT = 256;                 // threads per workgroup
+constexpr int PW = PT / 64;             // waves
+constexpr int SC_ITEMS = 16;
+constexpr int SC_TILE = PT * SC_ITEMS;  // scan tile
+constexpr int RS_ITEMS = 8;
+constexpr int RS_TILE = PT * RS_ITEMS;  // radix-sort tile
+constexpr int RADIX = 256;
+static_assert(PT == RADIX, "k_rs_scatter maps one thread to each digit");
+
+struct NoVal {};
+
+template <class T>
+__device__ __forceinline__ T shfl_up_t(T x, int o) {
+    if constexpr (sizeof(T) == 8) {
+        const u32 lo = (u32)__shfl_up((int)(u32)x, o, 64), hi = (u32)__shfl_up((int)(u32)((u64)x >> 32), o, 64);
+        return (T)(((u64)hi << 32) | lo);
+    } else {
+        return (T)__shfl_up((int)x, o, 64);
+    }
+}
+
+// exclusive scan of one value per thread over the workgroup; *total = the sum
+template <class T>
+__device__ __forceinline__ T wg_excl_scan(T v, T* sh, T* total) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    T x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const T y = shfl_up_t(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wave] = x;
+    __syncthreads();
+    T base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < PW; ++w) {
+        const T s = sh[w];
+        if (w < wave) base += s;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+// per-tile sums
+template <class T>
+__global__ __launch_bounds__(PT) void k_scan_reduce(const T* __restrict__ in, int64_t n, T* part) {
+    __shared__ T sh[PW];
+    const int64_t base = (int64_t)blockIdx.x * SC_TILE;
+    T s = 0;
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {
+        const int64_t i = base + j * PT + threadIdx.x;
+        if (i < n) s += in[i];
+    }
+    T tot;
+    wg_excl_scan(s, sh, &tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+// exclusive scan of a tile, starting from carry (part[wg], or 0); in == out allowed
+template <class T>
+__device__ __forceinline__ T scan_tile(const T* in, T* out, int64_t base, int64_t n, T carry, T* tile, T* sh) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {
+        const int64_t i = base + j * PT + tid;
+        tile[j * PT + tid] = i < n ? in[i] : (T)0;
+    }
+    __syncthreads();
+    T v[SC_ITEMS], s = 0;
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) { v[j] = tile[tid * SC_ITEMS + j]; s += v[j]; }
+    T tot;
+    T run = carry + wg_excl_scan(s, sh, &tot);
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) { tile[tid * SC_ITEMS + j] = run; run += v[j]; }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {
+        const int64_t i = base + j * PT + tid;
+        if (i < n) out[i] = tile[j * PT + tid];
+    }
+    __syncthreads();
+    return carry + tot;
+}
+
+template <class T>
+__global__ __launch_bounds__(PT) void k_scan_down(const T* in, T* out, int64_t n, const T* __restrict__ part) {
+    __shared__ T tile[SC_TILE];
+    __shared__ T sh[PW];
+    scan_tile(in, out, (int64_t)blockIdx.x * SC_TILE, n, part ? part[blockIdx.x] : (T)0, tile, sh);
+}
+
+// one workgroup: exclusive scan of part[0, m) in place (the tile sums)
+template <class T>
+__global__ __launch_bounds__(PT) void k_scan_single(T* part, int64_t m) {
+    __shared__ T tile[SC_TILE];
+    __shared__ T sh[PW];
+    T carry = 0;
+    for (int64_t b = 0; b < m; b += SC_TILE) carry = scan_tile(part, part, b, m, carry, tile, sh);
+}
+
+template <class K>
+__global__ __launch_bounds__(PT) void k_rs_hist(const K* __restrict__ kin, int64_t n, int shift, u32 mask, int64_t nwg,
+                                                u32* hist) {
+    __shared__ u32 h[RADIX];
+    const int tid = threadIdx.x;
+    h[tid] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * RS_TILE;
+#pragma unroll
+    for (int j = 0; j < RS_ITEMS; ++j) {
+        const int64_t i = base + j * PT + tid;
+        if (i < n) atomicAdd(&h[(u32)(kin[i] >> shift) & mask], 1u);
+    }
+    __syncthreads();
+    hist[(int64_t)tid * nwg + blockIdx.x] = h[tid];
+}
+
+template <class K, class V>
+__global__ __launch_bounds__(PT) void k_rs_scatter(const K* __restrict__ kin, K* __restrict__ kout,
+                                                   const V* __restrict__ vin, V* __restrict__ vout, int64_t n,
+                                                   int shift, u32 mask, int64_t nwg, const u32* __restrict__ hoff) {
+    constexpr bool HASV = !std::is_same<V, NoVal>::value;
+    __shared__ u32 run[RADIX];
+    __shared__ u32 wc[PW][RADIX];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    run[tid] = hoff[(int64_t)tid * nwg + blockIdx.x];
+    const int64_t base = (int64_t)blockIdx.x * RS_TILE;
+    const u64 lt = (1ull << lane) - 1;
+    for (int j = 0; j < RS_ITEMS; ++j) {
+        const int64_t i = base + j * PT + tid;
+        const bool valid = i < n;
+        const K k = valid ? kin[i] : (K)0;
+        V v{};
+        if constexpr (HASV) { if (valid) v = vin[i]; }
+        const u32 d = (u32)(k >> shift) & mask;
+        u64 peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const u64 bb = __ballot((d >> b) & 1u);
+            peers &= ((d >> b) & 1u) ? bb : ~bb;
+        }
+#pragma unroll
+        for (int q = 0; q < PW; ++q) wc[q][tid] = 0;
+        __syncthreads();
+        const u32 rank = (u32)__popcll(peers & lt);
+        if (valid && rank == 0) wc[w][d] = (u32)__popcll(peers);
+        __syncthreads();
+        {
+            u32 r = run[tid];
+#pragma unroll
+            for (int q = 0; q < PW; ++q) { const u32 c = wc[q][tid]; wc[q][tid] = r; r += c; }
+            run[tid] = r;
+        }
+        __syncthreads();
+        if (valid) {
+            const u32 pos = wc[w][d] + rank;
+            kout[pos] = k;
+            if constexpr (HASV) vout[pos] = v;
+        }
+        __syncthreads();
+    }
+}
+
+template <class T>
+__global__ void k_flag_unique(const T* __restrict__ in, int64_t n, u32* f) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) f[i] = (i == 0 || in[i] != in[i - 1]) ? 1u : 0u;
+}
+__global__ void k_flag_u8(const u8* __restrict__ fl, int64_t n, u32* f) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) f[i] = fl[i] ? 1u : 0u;
+}
+// keep element i when its flag is set (UNIQUE: flag recomputed from the sorted input); pos =
+// exclusive scan of the flags; nsel = the number kept
+template <class T, bool UNIQUE>
+__global__ void k_compact(const T* __restrict__ in, const u8* __restrict__ fl, const u32* __restrict__ pos, int64_t n,
+                          T* __restrict__ out, int* nsel) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const bool keep = UNIQUE ? (i == 0 || in[i] != in[i - 1]) : fl[i] != 0;
+    if (keep) out[pos[i]] = in[i];
+    if (i == n - 1) *nsel = (int)(pos[i] + (keep ? 1u : 0u));
+}
+
+// ---- host side: temporaries carved from one caller buffer (the context's cub_tmp) ----------
+struct Carve {
+    char* p;
+    size_t off = 0;
+    template <class T>
+    T* take(int64_t n) {
+        off = (off + 255) & ~(size_t)255;
+        T* r = (T*)(p ? p + off : nullptr);
+        off += (size_t)std::max<int64_t>(n, 1) * sizeof(T);
+        return r;
+    }
+};
+
+inline unsigned nblk(int64_t n, int64_t per) { return (unsigned)std::max<int64_t>(1, (n + per - 1) / per); }
+
+template <class T>
+size_t scan_tmp_bytes(int64_t n) {
+    Carve cv{nullptr};
+    if (n > SC_TILE) cv.take<T>((n + SC_TILE - 1) / SC_TILE);
+    return cv.off + 256;
+}
+
+// exclusive prefix sum of in[0, n) into out (in == out allowed)
+template <class T>
+void scan_excl(const T* in, T* out, int64_t n, char* tmp, hipStream_t s) {
+    if (n <= 0) return;
+    if (n <= SC_TILE) {
+        k_scan_down<T><<<1, PT, 0, s>>>(in, out, n, nullptr);
+    } else {
+        Carve cv{tmp};
+        const int64_t m = (n + SC_TILE - 1) / SC_TILE;
+        T* part = cv.take<T>(m);
+        k_scan_reduce<T><<<(unsigned)m, PT, 0, s>>>(in, n, part);
+        k_scan_single<T><<<1, PT, 0, s>>>(part, m);
+        k_scan_down<T><<<(unsigned)m, PT, 0, s>>>(in, out, n, part);
+    }
+    HIP_OK(hipGetLastError());
+}
+
+template <class K, class V>
+size_t sort_tmp_bytes(int64_t n) {
+    Carve cv{nullptr};
+    const int64_t nwg = (n + RS_TILE - 1) / RS_TILE;
+    cv.take<K>(n);
+    if constexpr (!std::is_same<V, NoVal>::value) cv.take<V>(n);
+    cv.take<u32>(RADIX * nwg);
+    const size_t a = cv.off;
+    return a + scan_tmp_bytes<u32>(RADIX * nwg) + 256;
+}
+
+// stable LSD radix sort of keys bits [b0, b1) (values follow); kin / vin are left untouched
+template <class K, class V>
+void sort_pairs(const K* kin, K* kout, const V* vin, V* vout, int64_t n, int b0, int b1, DevBuf& tmpbuf, hipStream_t s) {
+    constexpr bool HASV = !std::is_same<V, NoVal>::value;
+    if (n <= 0) return;
+    CC_REQUIRE(n < (1LL << 31), "too many keys for one sort");
+    tmpbuf.ensure(sort_tmp_bytes<K, V>(n));
+    Carve cv{(char*)tmpbuf.p};
+    const int64_t nwg = (n + RS_TILE - 1) / RS_TILE;
+    K* kalt = cv.take<K>(n);
+    V* valt = HASV ? cv.take<V>(n) : nullptr;
+    u32* hist = cv.take<u32>(RADIX * nwg);
+    char* stmp = (char*)tmpbuf.p + ((cv.off + 255) & ~(size_t)255);
+    const int passes = b1 > b0 ? (b1 - b0 + 7) / 8 : 0;
+    if (passes == 0) {
+        HIP_OK(hipMemcpyAsync(kout, kin, n * sizeof(K), hipMemcpyDeviceToDevice, s));
+        if constexpr (HASV) HIP_OK(hipMemcpyAsync(vout, vin, n * sizeof(V), hipMemcpyDeviceToDevice, s));
+        return;
+    }
+    const K* ks = kin;
+    const V* vs = vin;
+    for (int p = 0; p < passes; ++p) {
+        K* kd = ((passes - 1 - p) % 2 == 0) ? kout : kalt;
+        V* vd = ((passes - 1 - p) % 2 == 0) ? vout : valt;
+        const int shift = b0 + 8 * p;
+        const int bits = std::min(8, b1 - shift);
+        const u32 mask = (1u << bits) - 1;
+        k_rs_hist<K><<<(unsigned)nwg, PT, 0, s>>>(ks, n, shift, mask, nwg, hist);
+        HIP_OK(hipGetLastError());
+        scan_excl<u32>(hist, hist, RADIX * nwg, stmp, s);
+        k_rs_scatter<K, V><<<(unsigned)nwg, PT, 0, s>>>(ks, kd, vs, vd, n, shift, mask, nwg, hist);
+        HIP_OK(hipGetLastError());
+        ks = kd;
+        vs = vd;
+    }
+}
+
+template <class K>
+void sort_keys(const K* kin, K* kout, int64_t n, int b0, int b1, DevBuf& tmp, hipStream_t s) {
+    sort_pairs<K, NoVal>(kin, kout, nullptr, nullptr, n, b0, b1, tmp, s);
+}
+
+// out = the first element of every run of equal elements of the sorted in[0, n); *nsel (device) = count
+template <class T>
+void select_unique(const T* in, T* out, int* nsel, int64_t n, DevBuf& tmpbuf, hipStream_t s) {
+    if (n <= 0) { HIP_OK(hipMemsetAsync(nsel, 0, sizeof(int), s)); return; }
+    Carve cv{nullptr};
+    cv.take<u32>(n);
+    tmpbuf.ensure(cv.off + scan_tmp_bytes<u32>(n) + 256);
+    Carve c2{(char*)tmpbuf.p};
+    u32* pos = c2.take<u32>(n);
+    char* stmp = (char*)tmpbuf.p + ((c2.off + 255) & ~(size_t)255);
+    k_flag_unique<T><<<nblk(n, 256), 256, 0, s>>>(in, n, pos);
+    HIP_OK(hipGetLastError());
+    scan_excl<u32>(pos, pos, n, stmp, s);
+    k_compact<T, true><<<nblk(n, 256), 256, 0, s>>>(in, nullptr, pos, n, out, nsel);
+    HIP_OK(hipGetLastError());
+}
+
+// out = in[i] for every i with flags[i] != 0, in order; *nsel (device) = count
+template <class T>
+void select_flagged(const T* in, const u8* flags, T* out, int* nsel, int64_t n, DevBuf& tmpbuf, hipStream_t s) {
+    if (n <= 0) { HIP_OK(hipMemsetAsync(nsel, 0, sizeof(int), s)); return; }
+    Carve cv{nullptr};
+    cv.take<u32>(n);
+    tmpbuf.ensure(cv.off + scan_tmp_bytes<u32>(n) + 256);
+    Carve c2{(char*)tmpbuf.p};
+    u32* pos = c2.take<u32>(n);
+    char* stmp = (char*)tmpbuf.p + ((c2.off + 255) & ~(size_t)255);
+    k_flag_u8<<<nblk(n, 256), 256, 0, s>>>(flags, n, pos);
+    HIP_OK(hipGetLastError());
+    scan_excl<u32>(pos, pos, n, stmp, s);
+    k_compact<T, false><<<nblk(n, 256), 256, 0, s>>>(in, flags, pos, n, out, nsel);
+    HIP_OK(hipGetLastError());
+}
+
+// exclusive scan with the temporaries in tmpbuf
+template <class T>
+void scan_excl(const T* in, T* out, int64_t n, DevBuf& tmpbuf, hipStream_t s) {
+    tmpbuf.ensure(scan_tmp_bytes<T>(n));
+    scan_excl<T>(in, out, n, (char*)tmpbuf.p, s);
+}
+
+}  // namespace prims
+}  // namespace cc

@@ -272,7 +272,7 @@ int cc_relabel_consecutive(cc_ctx* c, const uint64_t* labels, uint64_t* out, int
     CC_TRY({
         CC_REQUIRE(c && labels && out && n >= 0 && n_unique && start_label, "bad arguments");
         HIP_OK(hipSetDevice(c->device));
-        hipStream_t s = c->stream;
+        hipStream_t s = cstream(c);
         *n_unique = 0;
         *start_label = 1;
         if (n == 0) return 0;
@@ -312,12 +312,7 @@ int cc_relabel_consecutive(cc_ctx* c, const uint64_t* labels, uint64_t* out, int
                 continue;
             }
             const int64_t nu = h[1];
-            size_t tmp = 0;
-            HIP_OK(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, comp, sorted, (int)nu, 0, 64, s));
-            c->cub_tmp.ensure(tmp);
-            launch(c, "radix_sort", [&] {
-                HIP_OK(hipcub::DeviceRadixSort::SortKeys(c->cub_tmp.p, tmp, comp, sorted, (int)nu, 0, 64, s));
-            });
+            launch(c, "radix_sort", [&] { prims::sort_keys<u64>(comp, sorted, nu, 0, 64, c->cub_tmp, s); });
             u64 first = 1;
             HIP_OK(hipMemcpyAsync(&first, sorted, sizeof(u64), hipMemcpyDeviceToHost, s));
             sync(c);

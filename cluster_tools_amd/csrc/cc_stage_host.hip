@@ -8,7 +8,7 @@ int64_t cc_block_faces(cc_ctx* c, const uint64_t* labels, const int64_t shape[3]
     try {
         CC_REQUIRE(c && labels && shape && block_shape && offsets_host, "NULL argument");
         HIP_OK(hipSetDevice(c->device));
-        hipStream_t s = c->stream;
+        hipStream_t s = cstream(c);
         int64_t nb[3], n_face = 0;
         for (int a = 0; a < 3; ++a) {
             CC_REQUIRE(shape[a] >= 1 && block_shape[a] >= 1, "bad shape / block_shape");
@@ -84,7 +84,7 @@ int cc_merge_assignments(cc_ctx* c, const uint64_t* pairs_host, int64_t n_pairs,
         CC_REQUIRE(c && lut_host && n_labels >= 1 && n_pairs >= 0, "bad arguments");
         CC_REQUIRE(n_pairs == 0 || pairs_host, "pairs is NULL");
         HIP_OK(hipSetDevice(c->device));
-        hipStream_t s = c->stream;
+        hipStream_t s = cstream(c);
         c->lut.ensure(n_labels * sizeof(u64));
         c->pairs.ensure(std::max<int64_t>(1, 2 * n_pairs) * sizeof(u64));
         c->counter.ensure(sizeof(u32));
@@ -114,7 +114,7 @@ int cc_write(cc_ctx* c, uint64_t* labels, const int64_t shape[3], const int64_t 
     CC_TRY({
         CC_REQUIRE(c && labels && shape && block_shape && offsets_host && lut_host && n_labels >= 1, "bad arguments");
         HIP_OK(hipSetDevice(c->device));
-        hipStream_t s = c->stream;
+        hipStream_t s = cstream(c);
         int64_t nb[3];
         for (int a = 0; a < 3; ++a) nb[a] = (shape[a] + block_shape[a] - 1) / block_shape[a];
         const int64_t n_blocks = nb[0] * nb[1] * nb[2];
@@ -152,7 +152,7 @@ int cc_generate_boundary_map(cc_ctx* c, float* out, const int64_t shape[3], cons
         CC_REQUIRE(shape[1] * nxb < (1LL << 24) && shape[0] < 65536, "volume too large for the generator grid");
         const dim3 grid((unsigned)(shape[1] * nxb), (unsigned)shape[0]);
         launch(c, "k_generate", [&] {
-            k_generate<<<grid, 256, 0, c->stream>>>(out, shape[0], shape[1], shape[2], o[0], o[1], o[2], seed, dither);
+            k_generate<<<grid, 256, 0, cstream(c)>>>(out, shape[0], shape[1], shape[2], o[0], o[1], o[2], seed, dither);
         });
         sync(c);
     })
@@ -202,7 +202,7 @@ static int64_t seam_pairs_impl(cc_ctx* c, UP upper, const uint64_t* lower, int64
                                int64_t cap) {
     CC_REQUIRE(c && upper.p && lower && n >= 0, "bad arguments");
     HIP_OK(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
+    hipStream_t s = cstream(c);
     const int64_t capn = std::max<int64_t>(1, n);
     c->pairs.ensure(2 * capn * sizeof(u64));
     c->pairs2.ensure(2 * capn * sizeof(u64));
@@ -281,7 +281,7 @@ int cc_shard_top_cubes32(cc_ctx* c, uint32_t* cubes) {
         Geom& g = st.hg.g;
         for (int a = 1; a < 3; ++a)   // tile origins = block origins + multiples of TY / TX
             CC_REQUIRE(g.nb[a] == 1 || st.bs[a] % 2 == 0, "cube form needs even tile origins (even block_shape[1:])");
-        hipStream_t s = c->stream;
+        hipStream_t s = cstream(c);
         const unsigned nlayer = (unsigned)((int64_t)g.nt[1] * g.nt[2]);
         launch(c, "k_top_cubes", [&] {
             k_top_cubes<<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), cubes,
@@ -298,7 +298,7 @@ int cc_shard_top_plane32(cc_ctx* c, uint32_t* top32) {
         CC_REQUIRE(st.stage == 2, "phase order: call cc_shard_assign first");
         CC_REQUIRE(st.sum_v < 0xFFFFFFFEull, "slab id range does not fit the 32-bit plane form");
         Geom& g = st.hg.g;
-        hipStream_t s = c->stream;
+        hipStream_t s = cstream(c);
         const unsigned nlayer = (unsigned)((int64_t)g.nt[1] * g.nt[2]);
         launch(c, "k_plane_labels", [&] {
             k_plane_labels<true, u32><<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(),

@@ -1,0 +1,58 @@
+"""Cold-start probe: in a fresh process with torch's queue already warm,
+time (1) the first launch from a one-kernel library (tools/cold_probe.hip -> tools/libcold_probe.so)
+and (2) ctx creation + the first and second cc_label_volume on a small volume.  The difference
+between the two first launches is the cost of loading libcc_mi355x.so's code object.
+Prints one JSON line."""
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from cluster_tools_amd import _lib
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    a = torch.zeros(16, dtype=torch.int32, device=dev)
+    a.add_(1)
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream(dev).cuda_stream
+    r = {}
+    t0 = time.perf_counter()
+    P = ctypes.CDLL(os.path.join(ROOT, 'tools', 'libcold_probe.so'))
+    P.probe_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    r['probe_dlopen_ms'] = (time.perf_counter() - t0) * 1e3
+    for k in ('probe_first_ms', 'probe_second_ms'):
+        t0 = time.perf_counter()
+        assert P.probe_launch(st, a.data_ptr()) == 0
+        torch.cuda.synchronize()
+        r[k] = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
+    _lib.load()
+    r['lib_dlopen_ms'] = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
+    ctx = _lib.Context(0)
+    ctx.set_stream(st)
+    torch.cuda.synchronize()
+    r['ctx_create_ms'] = (time.perf_counter() - t0) * 1e3
+    shape, bs = (64, 128, 128), (32, 64, 64)
+    x = torch.rand(shape, dtype=torch.float32, device=dev)
+    out = torch.empty(shape, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    for k in ('label_first_ms', 'label_second_ms', 'label_third_ms'):
+        t0 = time.perf_counter()
+        ctx.label_volume(x, bs, 0.5, 'greater', out=out)
+        torch.cuda.synchronize()
+        r[k] = (time.perf_counter() - t0) * 1e3
+    ctx.close()
+    r['env'] = {k: os.environ[k] for k in os.environ if k.startswith(('HIP_', 'AMD_', 'CC_'))}
+    print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}))
+
+
+if __name__ == '__main__':
+    main()
