@@ -86,7 +86,6 @@ struct ProfEntry {
 struct cc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t own_stream = nullptr;
     hipStream_t side = nullptr;      // k_seams of finished front chunks, concurrent with the next chunk
     // workspace
     DevBuf tiles, bstat, bparam, bits, faces, count, rc, roff, rl, rcb, P, KR, FIN, keys, keys2, vals, vals2, seg,
@@ -116,15 +115,10 @@ struct cc_ctx {
     void* run = nullptr;     // RunState of the current labelling run
 };
 
-// the context's stream: the caller's (cc_set_stream), else its own, created on first use -- a
-// queue's creation costs milliseconds, and a job that hands over its stream never needs one
-static hipStream_t cstream(cc_ctx* c) {
-    if (!c->stream) {
-        if (!c->own_stream) HIP_OK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
-        c->stream = c->own_stream;
-    }
-    return c->stream;
-}
+// the context's stream: the caller's (cc_set_stream), else the null stream -- which is torch's
+// default stream too.  No stream of its own: creating one costs a hardware queue (10 ms in the
+// C1 cold-call trace, profiles/r03_c1_trace_*), paid by every one-shot job.
+static hipStream_t cstream(cc_ctx* c) { return c->stream; }
 // the side stream (k_seams of finished front chunks), created on first use
 static hipStream_t side_stream(cc_ctx* c) {
     if (!c->side) HIP_OK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
@@ -779,7 +773,7 @@ int cc_create(int device, cc_ctx** out) {
 void cc_destroy(cc_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->stream);
     if (c->side) (void)hipStreamSynchronize(c->side);
     DevBuf* bufs[] = {&c->tiles, &c->bstat, &c->bparam, &c->bits, &c->faces, &c->count, &c->rc, &c->roff, &c->rl, &c->rcb, &c->P, &c->KR,
                       &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
@@ -792,7 +786,6 @@ void cc_destroy(cc_ctx* c) {
     c->pin.release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
-    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     if (c->side) (void)hipStreamDestroy(c->side);
     delete (RunState*)c->run;
     delete c;
@@ -801,7 +794,7 @@ void cc_destroy(cc_ctx* c) {
 int cc_set_stream(cc_ctx* c, void* stream) {
     CC_TRY({
         CC_REQUIRE(c, "ctx is NULL");
-        c->stream = stream ? (hipStream_t)stream : c->own_stream;
+        c->stream = (hipStream_t)stream;
     })
 }
 

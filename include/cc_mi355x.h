@@ -58,7 +58,8 @@ int64_t     cc_result_size(void);
 int         cc_create(int device, cc_ctx** out);
 void        cc_destroy(cc_ctx* ctx);
 const char* cc_last_error(void);
-/* use an existing hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL -> ctx's own */
+/* use an existing hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL (the default)
+ * -> the null stream */
 int         cc_set_stream(cc_ctx* ctx, void* hip_stream);
 /* library version string, e.g. "cc_mi355x 0.2 gfx950 src=0123456789abcdef": src = SHA-256 prefix of
  * the sources (csrc/ files, this header) the library was built from (binary provenance, build.py) */
