@@ -12,6 +12,9 @@ Workloads (--workload):
   c5 (default at N > 1)  weak scaling: each rank owns a (256, 4096, 4096) slab of a
        (256 N, 4096, 4096) volume -- at N = 8 this is C5, (2048, 4096, 4096)
   c2   (512, 512, 512), block (128, 128, 128)
+  c1   (125, 1250, 1250), block (50, 512, 512): BASELINE config 1's geometry; the line also carries
+       `cold_start`: a fresh process (a child of this one, input handed over as a .npy file) timing
+       its FIRST cc_label_volume -- what every one-shot target='local' job pays -- and the warm calls
   --dither: continuous input (the map plus a sub-2^-8 dither).  N > 1 runs one process per GPU;
   seams are stitched over RCCL (cluster_tools_amd/distributed.py).
 Rank 0 prints one JSON line.
@@ -37,6 +40,7 @@ WORKLOADS = {
     'c4': {'shape': (1024, 2048, 2048), 'block': (64, 512, 512), 'scaling': 'strong', 'mask': True},
     'c5': {'per_rank': (256, 4096, 4096), 'block': (64, 512, 512), 'scaling': 'weak'},
     'c2': {'shape': (512, 512, 512), 'block': (128, 128, 128), 'scaling': 'strong'},
+    'c1': {'shape': (125, 1250, 1250), 'block': (50, 512, 512), 'scaling': 'strong'},
 }
 
 
@@ -55,23 +59,25 @@ def parse():
     p.add_argument('--shape', default=None, help='override Z,Y,X (per-rank slab for N > 1)')
     p.add_argument('--workload', default=None, choices=sorted(WORKLOADS),
                    help='c3 (default at N=1), c4 (C3 + mask, strong-scaled z-slabs), c5 (default at N>1: '
-                        '(256N,4096,4096), weak), c2 (512^3, block 128^3)')
+                        '(256N,4096,4096), weak), c2 (512^3, block 128^3), c1 (125x1250x1250, block '
+                        '50x512x512, + cold_start)')
     p.add_argument('--block-shape', default=None)
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-sample-z', type=int, default=1024)
+    p.add_argument('--cold-child', default=None, help=argparse.SUPPRESS)   # internal: see cold_start()
     p.add_argument('--traffic-json', default=None,
                    help='tools/prof_summary.py output (rocprofv3 FETCH_SIZE / WRITE_SIZE passes) to fill '
                         'roofline.traffic; default profiles/traffic_<workload tag>.json when present')
     return p.parse_args()
 
 
-def cpu_baseline(args, block_shape, shape_yx):
+def cpu_baseline(args, block_shape, shape_yx, nz):
     """Oracle C restatement of the reference target='local' path on host cores, on a bounded
     sample: the first `cpu_sample_z` planes of the same synthetic volume."""
     from oracle import oracle as O
     threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or len(os.sched_getaffinity(0))
     threads = max(1, min(threads, 64))
-    shape = (args.cpu_sample_z,) + tuple(shape_yx)
+    shape = (min(args.cpu_sample_z, nz),) + tuple(shape_yx)
     x = O.boundary_map(shape, n_threads=threads, dither=args.dither)
     t0 = time.perf_counter()
     r = O.label_volume(x, block_shape, args.threshold, args.mode, n_threads=threads, want_lut=False)
@@ -84,8 +90,60 @@ def cpu_baseline(args, block_shape, shape_yx):
                       % (threads, list(shape), list(block_shape), dt)}
 
 
+def cold_child(args):
+    """Runs in a fresh process (cold_start): the input is read from a .npy file and uploaded,
+    then the FIRST library call is timed -- context creation, code-object load on the first
+    launch, workspace allocation, the kernels -- followed by warm calls.  Prints one JSON line."""
+    import numpy as np
+    import torch
+    from cluster_tools_amd import _lib
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    x = torch.from_numpy(np.load(args.cold_child)).to(dev)
+    out = torch.empty(x.shape, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    block_shape = tuple(int(v) for v in args.block_shape.split(','))
+    t0 = time.perf_counter()
+    ctx = _lib.Context(0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    ctx.label_volume(x, block_shape, args.threshold, args.mode, out=out)
+    torch.cuda.synchronize()
+    cold = time.perf_counter() - t0
+    warm = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        ctx.label_volume(x, block_shape, args.threshold, args.mode, out=out)
+        torch.cuda.synchronize()
+        warm.append(time.perf_counter() - t0)
+    ctx.close()
+    print(json.dumps({'cold_ms': round(cold * 1e3, 3), 'warm_ms': round(min(warm) * 1e3, 3)}), flush=True)
+
+
+def cold_start(args, x, block_shape):
+    """First-call cost of a one-shot job: `x` (the device input) goes to a .npy file, a child
+    process (subprocess, not exec) runs cold_child on it."""
+    import subprocess
+    import tempfile
+    import numpy as np
+    with tempfile.TemporaryDirectory(prefix='cc_cold_') as d:
+        path = os.path.join(d, 'x.npy')
+        np.save(path, x.cpu().numpy())
+        cmd = [sys.executable, os.path.abspath(__file__), '--cold-child', path, '--block-shape',
+               ','.join(map(str, block_shape)), '--threshold', str(args.threshold), '--mode', args.mode]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        raise RuntimeError('cold-start child failed (%d): %s' % (r.returncode, r.stderr[-2000:]))
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    res['how'] = ('fresh process: torch up and the input in HBM, then timed: cc_create + the first '
+                  'cc_label_volume (code-object load, workspace allocation, kernels) to completion; '
+                  'warm_ms = the best of the next 5 calls')
+    return res
+
+
 def main():
     args = parse()
+    if args.cold_child:
+        return cold_child(args)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -243,10 +301,12 @@ def main():
         'result': res,
         'lib': {'version': _lib.version(), 'src': lib_src},
     }
+    if wl == 'c1' and world == 1:
+        line['cold_start'] = cold_start(args, x, block_shape)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         del x, out
         torch.cuda.empty_cache()
-        line['cpu_baseline'] = cpu_baseline(args, block_shape, slab[1:])
+        line['cpu_baseline'] = cpu_baseline(args, block_shape, slab[1:], slab[0])
     elif rank == 0:
         line['cpu_baseline'] = None
     if rank == 0:

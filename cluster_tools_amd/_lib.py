@@ -410,10 +410,12 @@ class Context:
         o = np.lexsort((b, a))
         return a[o], b[o], c[o]
 
-    def relabel_consecutive(self, labels, out=None):
+    def relabel_consecutive(self, labels, out=None, cap_hint=1 << 20):
         """RelabelWorkflow (relabel_workflow.py:10-60, find_labeling.py:84-120) on device:
         returns (relabelled tensor, assignments (n, 2) uint64 [old id, new id]).  `labels` is a
-        uint64 (torch int64 / uint64) CUDA tensor; out may be `labels` (in place)."""
+        uint64 (torch int64 / uint64) CUDA tensor; out may be `labels` (in place).  cap_hint: the
+        expected number of distinct ids (sizes the host table and the device id set; a larger
+        count costs a second call)."""
         import torch
         assert hasattr(labels, 'data_ptr') and labels.is_cuda and labels.element_size() == 8
         assert labels.is_contiguous() and labels.dtype in (torch.int64, torch.uint64)
@@ -423,7 +425,7 @@ class Context:
         torch.cuda.current_stream(labels.device).synchronize()
         L = load()
         nu, st = np.zeros(1, dtype=np.uint64), np.zeros(1, dtype=np.uint64)
-        cap = 1 << 20
+        cap = max(1, int(cap_hint))
         while True:
             # a table larger than cap is reported (n_unique) before out is touched, so in-place
             # calls are safe: the second call has the exact size

@@ -29,7 +29,8 @@ constexpr u64 EV_EMPTY = ~0ull;
 constexpr u64 EV_ZTAG = 1ull << 63;
 constexpr int EV_LDS = 2048;       // LDS hash entries per workgroup
 constexpr int EV_LDS_PROBES = 32;
-constexpr int EV_PROBES = 4096;    // global probe limit before reporting the table as full
+constexpr int EV_PROBES = 1024;    // global probe limit before reporting the table as full (a full
+                                   // table costs every further insert this many probes before the rerun)
 constexpr int EV_Q = 8;            // loads of 64 voxels per wave item
 constexpr int EV_ROW = 64 * EV_Q;  // voxels of one row per wave item
 constexpr u32 EV_ERR_SEG = 1, EV_ERR_GT = 2, EV_ERR_FULL = 4;
@@ -286,7 +287,9 @@ int cc_evaluate(cc_ctx* c, const uint64_t* seg, const uint64_t* gt, const int64_
         c->ev_flag.ensure(n_blocks * sizeof(u32) + 16);
         c->ev_part.ensure(4 * EV_REDUCE_WG * sizeof(u64));
         c->counter.ensure(sizeof(u32));
-        int64_t cap = std::max<int64_t>(c->ev_cap, 1 << 16);
+        // 2^20 slots (16 MB per table) to start: C3-sized partitions hold ~150 k pairs, and a table
+        // that fills up costs a slow pass plus a rerun (the 80 ms first call of round 2)
+        int64_t cap = std::max<int64_t>(c->ev_cap, 1 << 20);
         for (;;) {
             c->ev_main.ensure(2 * cap * sizeof(u64));
             c->ev_z.ensure(2 * cap * sizeof(u64));

@@ -2611,15 +2611,15 @@ __global__ __launch_bounds__(NTHREADS) void k_threshold(Geom g, const BlockParam
 // k_params_verify lists the tiles whose guessed bits are not exact and k_thr_fix rewrites only
 // those from the input.  Blocks without a guess are read for statistics only here (their tiles
 // are always listed).  SIDES as k_spec.
+// one tile (any shape): the generic path of k_thr_spec
 template <int SIDES>
-__global__ __launch_bounds__(NTHREADS) void k_thr_spec(Geom g, SpecArgs sa, const float* __restrict__ in,
-                                                       u8* __restrict__ out) {
-    __shared__ u32 red[6][NTHREADS / 64];
-    const int64_t t = sa.t0 + blockIdx.x;
+__device__ __forceinline__ void thr_spec_tile(const Geom& g, const SpecArgs& sa, int64_t t, const float* __restrict__ in,
+                                              u8* __restrict__ out, u32 (*red)[NTHREADS / 64]) {
     const TileInfo ti = tile_info(g, t);
     const BlockParam p = uniform_bp(sa.guess[ti.block]);
     if (p.kind != BP_INTERVAL) {
         stats_tile(g, ti, in, sa.smin, sa.smax, sa.sflag, red);
+        __syncthreads();       // red is reused by the next tile of the workgroup
         return;
     }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2680,6 +2680,113 @@ __global__ __launch_bounds__(NTHREADS) void k_thr_spec(Geom g, SpecArgs sa, cons
         }
         u32* tb = sa.TB + 4 * t;
         tb[0] = A; tb[1] = B; tb[2] = C; tb[3] = D;
+    }
+    __syncthreads();           // red is reused by the next tile of the workgroup
+}
+
+// TB of one tile from its reduced wrapped-distance statistics (as k_spec)
+template <int SIDES>
+__device__ __forceinline__ void thr_tile_tb(u32* tb, u32 lo, u32 hi, u32 K1N, u32 K1X, u32 K2N, u32 K2X) {
+    u32 A = 0u, B = 0xFFFFFFFFu, C = 0u, D = 0xFFFFFFFFu;
+    if (SIDES & 1) {
+        if ((u64)K1N + lo < (1ull << 32)) B = K1N + lo;
+        if ((u64)K1X + lo >= (1ull << 32)) A = K1X + lo;
+    }
+    if (SIDES & 2) {
+        if (K2N <= hi) C = hi - K2N;
+        if (K2X > hi) D = hi - K2X;
+    }
+    tb[0] = A; tb[1] = B; tb[2] = C; tb[3] = D;
+}
+
+// k_thr_spec: four x-adjacent tiles per workgroup.  The uint8 output rows of one tile are 64 B --
+// half a 128-B line, the other half written by another workgroup at another time, which is what
+// held the one-tile kernel at 2.5 TB/s of stores (profiles/r03_thr_spec.json).  When the four
+// tiles are full, in one block and 16-B aligned, the workgroup treats them as one 16 x 32 x 256
+// slab: a lane owns 16 consecutive voxels of a row (four float4 loads, ONE 16-B store), 16 lanes a
+// 256-voxel row, a wave 4 rows of a plane, the 8 waves the 32 rows, 16 planes; statistics per lane,
+// reduced per tile (a lane's voxels lie in tile (lane % 16) / 4).  Otherwise the tiles go one at a
+// time through thr_spec_tile.
+template <int SIDES>
+__global__ __launch_bounds__(NTHREADS) void k_thr_spec(Geom g, SpecArgs sa, const float* __restrict__ in,
+                                                       u8* __restrict__ out) {
+    __shared__ u32 red[6][NTHREADS / 64];
+    __shared__ u32 red4[6][4][NTHREADS / 64];
+    const int64_t t0 = sa.t0 + 4 * (int64_t)blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    bool fast = t0 + 3 < g.n_tiles && (g.X & 15) == 0;
+    TileInfo ti = tile_info(g, t0);
+    if (fast) {
+        const TileInfo tl = tile_info(g, t0 + 3);
+        fast = (ti.ix & 3) == 0 && tl.iz == ti.iz && tl.iy == ti.iy && tl.block == ti.block && ti.lz == TZ &&
+               ti.ly == TY && ti.lx == TX && tl.lx == TX && (ti.x0 & 15) == 0 &&
+               sa.guess[ti.block].kind == BP_INTERVAL;
+    }
+    if (!fast) {
+        for (int k = 0; k < 4 && t0 + k < g.n_tiles; ++k) thr_spec_tile<SIDES>(g, sa, t0 + k, in, out, red);
+        return;
+    }
+    const BlockParam p = uniform_bp(sa.guess[ti.block]);
+    const u32 lo = p.lo, hi = p.hi;
+    u32 mn = 0xFFFFFFFFu, mx = 0u, K1N = 0xFFFFFFFFu, K1X = 0u, K2N = 0xFFFFFFFFu, K2X = 0u;
+    auto fgp = [&](u32 o) -> u32 { return SIDES == 1 ? o >= lo : SIDES == 2 ? o <= hi : (o >= lo && o <= hi); };
+    auto quad = [&](float4 v) -> u32 {
+        const u32 o0 = f2ord(__float_as_uint(v.x)), o1 = f2ord(__float_as_uint(v.y));
+        const u32 o2 = f2ord(__float_as_uint(v.z)), o3 = f2ord(__float_as_uint(v.w));
+        mn = min(min(min(min(mn, o0), o1), o2), o3);
+        mx = max(max(max(max(mx, o0), o1), o2), o3);
+        if (SIDES & 1) {
+            const u32 k0 = o0 - lo, k1 = o1 - lo, k2 = o2 - lo, k3 = o3 - lo;
+            K1N = min(min(min(min(K1N, k0), k1), k2), k3);
+            K1X = max(max(max(max(K1X, k0), k1), k2), k3);
+        }
+        if (SIDES & 2) {
+            const u32 k0 = hi - o0, k1 = hi - o1, k2 = hi - o2, k3 = hi - o3;
+            K2N = min(min(min(min(K2N, k0), k1), k2), k3);
+            K2X = max(max(max(max(K2X, k0), k1), k2), k3);
+        }
+        return fgp(o0) | (fgp(o1) << 8) | (fgp(o2) << 16) | (fgp(o3) << 24);
+    };
+    const int64_t sz = g.Y * g.X;
+    const int64_t o0 = ((int64_t)ti.z0 * g.Y + ti.y0 + 4 * wave + (lane >> 4)) * g.X + ti.x0 + 16 * (lane & 15);
+    const float* pin = in + o0;
+    u8* pout = out + o0;
+#pragma unroll 2
+    for (int z = 0; z < TZ; ++z) {
+        const float4* q = reinterpret_cast<const float4*>(pin + z * sz);
+        const float4 v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3];
+        uint4 r;
+        r.x = quad(v0); r.y = quad(v1); r.z = quad(v2); r.w = quad(v3);
+        *reinterpret_cast<uint4*>(pout + z * sz) = r;
+    }
+    // reduce over the lanes of one tile: xor 1, 2 (the 4 lanes of a tile row), 16, 32 (the rows)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        if (o == 4 || o == 8) continue;
+        mn = min(mn, (u32)__shfl_xor(mn, o, 64));
+        mx = max(mx, (u32)__shfl_xor(mx, o, 64));
+        if (SIDES & 1) { K1N = min(K1N, (u32)__shfl_xor(K1N, o, 64)); K1X = max(K1X, (u32)__shfl_xor(K1X, o, 64)); }
+        if (SIDES & 2) { K2N = min(K2N, (u32)__shfl_xor(K2N, o, 64)); K2X = max(K2X, (u32)__shfl_xor(K2X, o, 64)); }
+    }
+    if (lane < 16 && (lane & 3) == 0) {
+        const int k = lane >> 2;
+        red4[0][k][wave] = mn; red4[1][k][wave] = mx; red4[2][k][wave] = K1N; red4[3][k][wave] = K1X;
+        red4[4][k][wave] = K2N; red4[5][k][wave] = K2X;
+    }
+    __syncthreads();
+    if (tid < 4) {
+        const int k = tid;
+        mn = red4[0][k][0]; mx = red4[1][k][0]; K1N = red4[2][k][0]; K1X = red4[3][k][0]; K2N = red4[4][k][0];
+        K2X = red4[5][k][0];
+        for (int w = 1; w < NTHREADS / 64; ++w) {
+            mn = min(mn, red4[0][k][w]); mx = max(mx, red4[1][k][w]);
+            K1N = min(K1N, red4[2][k][w]); K1X = max(K1X, red4[3][k][w]);
+            K2N = min(K2N, red4[4][k][w]); K2X = max(K2X, red4[5][k][w]);
+        }
+        atomicMin(sa.smin + ti.block, mn);
+        atomicMax(sa.smax + ti.block, mx);
+        if (mx > 0xFF800000u || mn < 0x007FFFFFu) atomicOr(sa.sflag + ti.block, 1u);    // NaN
+        thr_tile_tb<SIDES>(sa.TB + 4 * (t0 + k), lo, hi, K1N, K1X, K2N, K2X);
     }
 }
 

@@ -924,9 +924,10 @@ int cc_threshold(cc_ctx* c, const float* in, const int64_t shape[3], const int64
             sa.TB = TB;
             sa.t0 = 0;
             launch(c, "k_thr_spec", [&] {
-                if (md == MODE_GREATER) k_thr_spec<1><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, out);
-                else if (md == MODE_LESS) k_thr_spec<2><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, out);
-                else k_thr_spec<3><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, out);
+                const unsigned ng = (unsigned)((nt + 3) / 4);       // four x-adjacent tiles per workgroup
+                if (md == MODE_GREATER) k_thr_spec<1><<<ng, NTHREADS, 0, s>>>(g, sa, in, out);
+                else if (md == MODE_LESS) k_thr_spec<2><<<ng, NTHREADS, 0, s>>>(g, sa, in, out);
+                else k_thr_spec<3><<<ng, NTHREADS, 0, s>>>(g, sa, in, out);
             });
             launch(c, "k_params_verify", [&] {
                 k_params_verify<<<grid_stride(nt), 256, 0, s>>>(g, guess, smin, smax, sflag, thr, md, bp, TB, FIX);

@@ -286,7 +286,15 @@ int cc_relabel_consecutive(cc_ctx* c, const uint64_t* labels, uint64_t* out, int
         u64* WGL = c->rl_wg.as<u64>();
         u32* WGN = reinterpret_cast<u32*>(WGL + (size_t)ugrid * EV_LDS);
         c->counter.ensure(2 * sizeof(u32));
-        int64_t cap = std::max<int64_t>(c->rl_cap, 1 << 16);   // grown tables are kept for the next call
+        // id-set slots: at least twice the caller's table capacity (its expected number of distinct
+        // ids, bounded by n), so the set is sized right on the first pass -- a set that fills up
+        // makes every further insert walk EV_PROBES slots before the pass is rerun larger (the
+        // 666 ms first call of round 2); grown sets are kept for the next call
+        int64_t cap = std::max<int64_t>(c->rl_cap, 1 << 16);
+        if (uniques_host && cap_host > 0) {
+            const int64_t want = 2 * std::min<int64_t>(std::min<int64_t>(cap_host, n), 1LL << 27);
+            while (cap < want) cap *= 2;
+        }
         for (;;) {
             c->ev_seg.ensure(2 * cap * sizeof(u64));     // keys | new ids
             u64* keys = c->ev_seg.as<u64>();

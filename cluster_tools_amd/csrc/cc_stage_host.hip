@@ -46,9 +46,10 @@ int64_t cc_block_faces(cc_ctx* c, const uint64_t* labels, const int64_t shape[3]
             const int64_t nplanes = (shape[a] - 1) / block_shape[a];
             const int64_t nchunk = (shape[G.fdim] + FP_CHUNK - 1) / FP_CHUNK;
             if (nplanes == 0) continue;
-            CC_REQUIRE(shape[G.rdim] < 65536 && nplanes < 65536 && nchunk < (1LL << 31) && shape[G.fdim] < (1LL << 32),
-                       "face-pair grid out of range (rows < 65536)");
-            const dim3 grid((unsigned)nchunk, (unsigned)shape[G.rdim], (unsigned)nplanes);
+            const int64_t nrowg = (shape[G.rdim] + FP_ROWS - 1) / FP_ROWS;
+            CC_REQUIRE(nrowg < 65536 && nplanes < 65536 && nchunk < (1LL << 31) && shape[G.fdim] < (1LL << 32),
+                       "face-pair grid out of range");
+            const dim3 grid((unsigned)nchunk, (unsigned)nrowg, (unsigned)nplanes);
             launch(c, "k_face_pairs", [&] {
                 k_face_pairs<<<grid, FACE_PAIR_THREADS, 0, s>>>(G, labels, c->offsets.as<u64>(), pa, pb, cnt, (u64)capn,
                                                                 maxid, bflag);

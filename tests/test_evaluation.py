@@ -132,10 +132,10 @@ def test_gpu_evaluate_sparse_64bit_ids(ctx, ignore):
 
 @pytest.mark.gpu
 def test_gpu_evaluate_table_growth(ctx):
-    """~400k distinct pairs: more than the first table (2^16 entries) holds."""
+    """~1M distinct pairs: more than the first table (2^20 entries, kept at most half full) holds."""
     import torch
     rng = np.random.default_rng(7)
-    shape = (32, 128, 128)
+    shape = (64, 128, 128)
     seg = rng.integers(1, 1 << 20, size=shape).astype(np.uint64)
     gt = rng.integers(1, 1 << 20, size=shape).astype(np.uint64)
     want, ov = E.measures(seg, gt, (32, 64, 64), ignore_label=0)

@@ -101,6 +101,27 @@ SYNTH = [
 ]
 
 
+@pytest.mark.parametrize('shape,bs,mode', SYNTH[:6])
+def test_stage_path_vs_oracle(ctx, shape, bs, mode):
+    """The stage entry points chained (block_components -> merge_offsets -> block_faces ->
+    merge_assignments -> write; fused=False) on synthetic volumes larger than the goldens: face
+    rows over several row groups of k_face_pairs, block rows changing inside a group, odd X (the
+    8-B load path) and even X (16-B loads): final labels bit-exact against the oracle's."""
+    import torch
+    from cluster_tools_amd import _lib
+    inp = O.boundary_map(shape, origin=(7, 3, 1))
+    r = O.label_volume(inp, bs, 0.5, mode, None, n_threads=8)
+    local, values = ctx.block_components(torch.from_numpy(inp).cuda(), bs, 0.5, mode)
+    np.testing.assert_array_equal(values, r['values'])
+    offsets, _, n_labels = _lib.merge_offsets(values)
+    assert n_labels == r['n_labels']
+    pairs = ctx.block_faces(local, bs, offsets)
+    lut = ctx.merge_assignments(pairs, n_labels)
+    np.testing.assert_array_equal(lut, r['lut'])
+    ctx.write(local, bs, offsets, lut)
+    np.testing.assert_array_equal(local.cpu().numpy().view(np.uint64), r['labels'])
+
+
 @pytest.mark.parametrize('n_jobs', [1, 4, 27, 1000])
 def test_empty_job_emulation_vs_oracle(ctx, n_jobs):
     """CC_OPT_EMPTY_JOB_QUIRK against the oracle's emulation for several max_jobs: the LUT is the

@@ -25,7 +25,7 @@ def test_gpu_relabel_matches_oracle(ctx, case):
     elif case == 'no_zero_sparse':
         lab = rng.integers(1, 1 << 62, size=(7, 33, 65), dtype=np.int64).astype(np.uint64)
         lab[:, :, :30] = lab[0, 0, 0]
-    elif case == 'many_ids':       # > the first table (2^16 slots)
+    elif case == 'many_ids':       # > the first id set (2^16 slots, with the small cap_hint below)
         lab = rng.integers(0, 1 << 40, size=(16, 128, 128), dtype=np.int64).astype(np.uint64)
     elif case == 'runs_big':       # several workgroup ranges, runs crossing lanes and ranges
         lab = np.repeat(rng.integers(0, 3000, size=(40, 64, 32)), 37, axis=2).astype(np.uint64)
@@ -40,7 +40,9 @@ def test_gpu_relabel_matches_oracle(ctx, case):
         buf[1:] = d.reshape(-1)
         d = buf[1:].view(d.shape)
         assert d.data_ptr() % 16 == 8
-    out, table = ctx.relabel_consecutive(d)
+    # many_ids: a small capacity hint, so the device id set (2^16 slots) grows and the host table
+    # is too small for the first call (the second call has the exact size)
+    out, table = ctx.relabel_consecutive(d, cap_hint=1024 if case == 'many_ids' else 1 << 20)
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), want)
     np.testing.assert_array_equal(table, wa)
     out2, table2 = ctx.relabel_consecutive(d, out=d)     # in place

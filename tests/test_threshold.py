@@ -44,7 +44,10 @@ def test_gpu_matches_reference(ctx, name):
 @pytest.mark.gpu
 @pytest.mark.parametrize('shape,bs,mode', [((96, 200, 256), (64, 100, 128), 'greater'),
                                            ((70, 130, 203), (32, 64, 50), 'less'),
-                                           ((64, 128, 128), (64, 128, 128), 'equal')])
+                                           ((64, 128, 128), (64, 128, 128), 'equal'),
+                                           # four full tiles of one block per workgroup (16-B stores)
+                                           ((48, 96, 512), (32, 64, 256), 'greater'),
+                                           ((48, 96, 768), (48, 96, 384), 'less')])
 def test_gpu_matches_oracle_larger(ctx, shape, bs, mode):
     """Full and ragged tiles (float4 and scalar paths), unaligned X, one-block volumes."""
     import torch
@@ -97,7 +100,11 @@ def test_gpu_speculative_threshold_corrected(ctx, monkeypatch, variant, mode, th
     q = (rng.integers(0, 17, (64, 128, 192)) / np.float32(16)).astype(np.float32)
     q[1, 1, 5] = -1.0                      # outliers off the sampled rows (z = 8 mod 16, y = 16 mod 32)
     q[33, 70, 100] = 3.0
+    q2 = (rng.integers(0, 17, (64, 128, 512)) / np.float32(16)).astype(np.float32)
+    q2[2, 3, 300] = -1.0                   # outliers off the sampled rows, in four-tile workgroups
+    q2[40, 99, 17] = 3.0
     for x, bs in [(O.boundary_map((96, 200, 256), origin=(5, 3, 1), dither=True), (32, 100, 128)),
-                  (q, (32, 64, 96)), (q, (64, 128, 192))]:
+                  (O.boundary_map((64, 128, 512), origin=(5, 3, 1), dither=True), (32, 64, 256)),
+                  (q, (32, 64, 96)), (q, (64, 128, 192)), (q2, (32, 128, 256))]:
         got = ctx.threshold(torch.from_numpy(x).cuda(), bs, thr, mode).cpu().numpy()
         np.testing.assert_array_equal(got, O.threshold_volume(x, bs, thr, mode))

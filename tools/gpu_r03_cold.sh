@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU box: the cold-start probes (tools/cold_probe.py, tools/bench_c1_cold.py) into gpurun_out/cold_TAG/
+# GPU box: the cold-start probes (tools/cold_probe.py, bench.py --workload c1) into gpurun_out/cold_TAG/
 # Usage: gpurun -- tools/gpu_r03_cold.sh TAG
 set -e -o pipefail
 TAG=$1
@@ -9,4 +9,4 @@ O=gpurun_out/cold_$TAG
 mkdir -p $O
 timeout -k 10 120 python -u tools/cold_probe.py > $O/probe.json; cat $O/probe.json
 timeout -k 10 120 python -u tools/cold_probe.py > $O/probe2.json; cat $O/probe2.json
-timeout -k 10 200 python -u tools/bench_c1_cold.py > $O/c1_cold.json; cat $O/c1_cold.json
+timeout -k 10 200 python -u bench.py --workload c1 > $O/c1_cold.json; cat $O/c1_cold.json

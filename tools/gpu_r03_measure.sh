@@ -12,7 +12,7 @@ mkdir -p $O
 timeout -k 10 300 python -u tools/bench_stage.py greater > $O/stage_greater.json; cat $O/stage_greater.json
 timeout -k 10 300 python -u tools/bench_threshold.py > $O/thr_spec.json; cat $O/thr_spec.json
 CC_THRESHOLD_TWO_PASS=1 timeout -k 10 300 python -u tools/bench_threshold.py > $O/thr_two.json; cat $O/thr_two.json
-timeout -k 10 300 python -u tools/bench_c1_cold.py > $O/c1_cold.json; cat $O/c1_cold.json
+timeout -k 10 300 python -u bench.py --workload c1 --no-cpu-baseline > $O/c1_cold.json; cat $O/c1_cold.json
 timeout -k 10 300 python -u tools/bench_sharded_slabs.py 8 c4 5 > $O/slabs8_c4.json; cat $O/slabs8_c4.json
 timeout -k 10 300 python -u tools/bench_sharded_slabs.py 8 c3 5 > $O/slabs8_c3.json; cat $O/slabs8_c3.json
 "$ROOT/tools/profile_cmd.sh" stage_$TAG tools/bench_stage.py greater
