@@ -759,6 +759,9 @@ constexpr int SAMPLE_DZ = 4, SAMPLE_DY = 16;
 #ifndef CC_F4_PREFETCH
 #define CC_F4_PREFETCH 0
 #endif
+#ifndef CC_NN_WALK
+#define CC_NN_WALK 1        // k_spec's raw-bit walk for non-negative blocks (0: ordered walk only, A/B)
+#endif
 #ifndef CC_WL_BATCH
 #define CC_WL_BATCH 0
 #endif
@@ -872,7 +875,9 @@ __global__ void k_guess(int64_t nb, const u32* part, float thr, int mode, BlockP
     const bool nan = mx > 0xFF800000u || mn < 0x007FFFFFu;
     // On continuous data the sampled extremes are not the block's, so the guessed bound misses
     // the exact one by a little: only tiles holding a voxel between the two are relabelled.
-    guess[b] = widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
+    BlockParam gp = widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
+    gp.pad = (!nan && mn >= 0x80000000u) ? BP_NONNEG : 0u;     // smallest sampled value >= +0
+    guess[b] = gp;
 }
 
 // One launch for the front's initial state (it replaced nine memsets of ~4 us each): ordered
@@ -935,27 +940,43 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         if (SIDES & 2) { const u32 k = hi - o; K2N = min(K2N, use ? k : ~0u); K2X = max(K2X, use ? k : 0u); }
         return use && fgp(o);
     };
-    // four voxels of one float4 (full tiles): the same, min / max folded three operands at a time
-    auto quad = [&](float4 v, uchar4 mk, bool fg[4]) {
-        const u32 o0 = f2ord(__float_as_uint(v.x)), o1 = f2ord(__float_as_uint(v.y));
-        const u32 o2 = f2ord(__float_as_uint(v.z)), o3 = f2ord(__float_as_uint(v.w));
+    // four voxels of one float4 (full tiles): the same, min / max folded three operands at a time.
+    // NN (the block's guess says non-negative, BP_NONNEG): on the raw bits -- for raw < 2^31,
+    // ord = raw + 2^31, so o - lo = raw - (lo - 2^31), hi - o = (hi - 2^31) - raw, min / max are
+    // those of the raw bits (+ 2^31 afterwards) and the foreground test compares raw with the
+    // shifted bound: no per-voxel f2ord, a quarter of the walk's VALU.  A value with the sign bit
+    // set breaks this; the wave sees it in its raw max and walks its rows again on ord values.
+    const u32 lof = lo >= 0x80000000u ? lo - 0x80000000u : 0u;              // o >= lo <=> raw >= lof
+    const bool hiok = hi >= 0x80000000u;                                    // o <= hi <=> hiok && raw <= hif
+    const u32 hif = hi - 0x80000000u;
+    auto quad = [&](auto NNC, float4 v, uchar4 mk, bool fg[4]) {
+        constexpr bool NN = decltype(NNC)::value;
+        const u32 o0 = NN ? __float_as_uint(v.x) : f2ord(__float_as_uint(v.x));
+        const u32 o1 = NN ? __float_as_uint(v.y) : f2ord(__float_as_uint(v.y));
+        const u32 o2 = NN ? __float_as_uint(v.z) : f2ord(__float_as_uint(v.z));
+        const u32 o3 = NN ? __float_as_uint(v.w) : f2ord(__float_as_uint(v.w));
         mn = min(min(min(min(mn, o0), o1), o2), o3);
         mx = max(max(max(max(mx, o0), o1), o2), o3);
         const bool u0 = !HAS_MASK || mk.x, u1 = !HAS_MASK || mk.y, u2 = !HAS_MASK || mk.z, u3 = !HAS_MASK || mk.w;
+        const u32 l1 = NN ? lo - 0x80000000u : lo, h2 = NN ? hi - 0x80000000u : hi;
         if (SIDES & 1) {
-            const u32 k0 = o0 - lo, k1 = o1 - lo, k2 = o2 - lo, k3 = o3 - lo;
+            const u32 k0 = o0 - l1, k1 = o1 - l1, k2 = o2 - l1, k3 = o3 - l1;
             K1N = min(min(min(min(K1N, u0 ? k0 : ~0u), u1 ? k1 : ~0u), u2 ? k2 : ~0u), u3 ? k3 : ~0u);
             K1X = max(max(max(max(K1X, u0 ? k0 : 0u), u1 ? k1 : 0u), u2 ? k2 : 0u), u3 ? k3 : 0u);
         }
         if (SIDES & 2) {
-            const u32 k0 = hi - o0, k1 = hi - o1, k2 = hi - o2, k3 = hi - o3;
+            const u32 k0 = h2 - o0, k1 = h2 - o1, k2 = h2 - o2, k3 = h2 - o3;
             K2N = min(min(min(min(K2N, u0 ? k0 : ~0u), u1 ? k1 : ~0u), u2 ? k2 : ~0u), u3 ? k3 : ~0u);
             K2X = max(max(max(max(K2X, u0 ? k0 : 0u), u1 ? k1 : 0u), u2 ? k2 : 0u), u3 ? k3 : 0u);
         }
-        fg[0] = u0 && fgp(o0); fg[1] = u1 && fgp(o1); fg[2] = u2 && fgp(o2); fg[3] = u3 && fgp(o3);
+        auto fgq = [&](u32 o) -> bool {
+            if (!NN) return fgp(o);
+            return SIDES == 1 ? o >= lof : SIDES == 2 ? (hiok && o <= hif) : (o >= lof && hiok && o <= hif);
+        };
+        fg[0] = u0 && fgq(o0); fg[1] = u1 && fgq(o1); fg[2] = u2 && fgq(o2); fg[3] = u3 && fgq(o3);
     };
     const bool f4 = ti.lz == TZ && ti.ly == TY && ti.lx == TX && ((ti.x0 | (int)(g.X & 3)) & 3) == 0;
-    if (f4) {
+    auto f4walk = [&](auto NNC) {
         // Full, 16-B aligned tile: float4 per lane (4 rows of 64 voxels per load instruction, a
         // quarter of the load instructions of the lane = x walk).  Wave w owns rows y = 4w .. 4w+3
         // of every plane; lane l holds x = 4 (l % 16) .. + 3 of row 4w + l / 16.  The four
@@ -969,7 +990,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         u32 R[8] = {0, 0, 0, 0, 0, 0, 0, 0};      // lane z: ballots (lo, hi) of values 0..3 of plane z
         auto plane_bits = [&](int z, float4 v, uchar4 mk) {
             bool fg[4];
-            quad(v, mk, fg);
+            quad(NNC, v, mk, fg);
             const u64 b0 = __ballot(fg[0]), b1 = __ballot(fg[1]), b2 = __ballot(fg[2]), b3 = __ballot(fg[3]);
 #if CC_WL_BATCH
             CC_WRITELANE8(R, b0, b1, b2, b3, z);
@@ -1032,6 +1053,26 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         // split form: even voxels x = 4i (j = 0), 4i + 2 (j = 2) -> bits 2i, 2i + 1 of the low half
         const u32 even = spread2(seg[0]) | (spread2(seg[2]) << 1), odd = spread2(seg[1]) | (spread2(seg[3]) << 1);
         L.rows[zz * TY + 4 * wave + qq] = ((u64)odd << 32) | even;
+    };
+    if (f4) {
+        // (not for the 'equal' variants nor the masked 'less' one: with two walks their register
+        // budget spills)
+        constexpr bool NN_OK = CC_NN_WALK && SIDES != 3 && !(HAS_MASK && SIDES == 2);
+        bool ordwalk = !NN_OK || !(p.pad & BP_NONNEG);
+        if constexpr (NN_OK) if (!ordwalk) {
+            f4walk(std::true_type{});
+            u32 wmx = mx;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) wmx = max(wmx, (u32)__shfl_xor(wmx, o, 64));
+            ordwalk = __builtin_amdgcn_readfirstlane(wmx) >= 0x80000000u;
+            if (ordwalk) {                    // a value below +0 in this wave's rows: walk them on ord values
+                mn = 0xFFFFFFFFu; mx = 0u; K1N = 0xFFFFFFFFu; K1X = 0u; K2N = 0xFFFFFFFFu; K2X = 0u;
+            } else {
+                mn += 0x80000000u;            // raw -> ord (raw < 2^31)
+                mx += 0x80000000u;
+            }
+        }
+        if (ordwalk) f4walk(std::false_type{});
     } else {
         for (int i = tid; i < NROWS; i += NTHREADS) L.rows[i] = 0;
         __syncthreads();
@@ -2352,75 +2393,176 @@ __global__ __launch_bounds__(NTHREADS) void k_plane_labels(Geom g, const face_t*
 // voxel of every distinct pair in index order always emits, so the sort + unique that follows
 // sees every pair at least once but only ~ the pair regions' corners (the unfiltered plane gave
 // millions of single-counter atomics, 3.2 ms for a 4096^2 seam).  Appends are wave-aggregated.
-constexpr int SEAM_PAIR_THREADS = 1024;
+// k_seam_pairs: 256 threads, 8 consecutive plane voxels per thread per round, 4 rounds per
+// workgroup (8192 voxels); appends collect in an LDS buffer and leave with one global atomic per
+// workgroup -- the one-voxel-per-thread kernel took one atomic per 1024 voxels, serialised on the
+// counter at ~24 ns each (0.10 ms of the 0.104 ms of a 2048^2 seam, profiles/r03_slabs8_c3.json)
+constexpr int SEAM_PAIR_THREADS = 256, SPV = 8, SP_ROUNDS = 4, SP_BUF = 2 * SEAM_PAIR_THREADS * SPV;
+constexpr int64_t SP_WG_VOXELS = (int64_t)SEAM_PAIR_THREADS * SPV * SP_ROUNDS;
 // Readers of the upper plane for k_seam_pairs: raw(i) is compared between neighbours (0 =
 // background), id(raw) is the global id.
 struct UpperIds {                  // uint64 ids (single-process schedule, stage tests)
     const u64* p;
-    __device__ __forceinline__ u64 raw(int64_t i) const { return p[i]; }
+    __device__ __forceinline__ u64 raw(int64_t i, u32, u32) const { return p[i]; }
     __device__ __forceinline__ u64 id(u64 r) const { return r; }
+    __device__ __forceinline__ int64_t width(int64_t X) const { return X; }
 };
 struct UpperIds32 {                // uint32 id - base + 1 per voxel
     const u32* p;
     u64 base;
-    __device__ __forceinline__ u64 raw(int64_t i) const { return p[i]; }
+    __device__ __forceinline__ u64 raw(int64_t i, u32, u32) const { return p[i]; }
     __device__ __forceinline__ u64 id(u64 r) const { return r - 1 + base; }
+    __device__ __forceinline__ int64_t width(int64_t X) const { return X; }
 };
 struct UpperCubes32 {              // per 2x2 cube: (id - base + 1) << 4 | 4 voxel bits (y&1)*2 + (x&1)
     const u32* p;
     u64 base;
     u32 X, CXg;
-    __device__ __forceinline__ u64 raw(int64_t i) const {
-        const u32 ii = (u32)i, y = ii / X, x = ii - y * X;
+    __device__ __forceinline__ u64 raw(int64_t, u32 y, u32 x) const {
         const u32 c = p[(y >> 1) * CXg + (x >> 1)];
         return ((c >> ((y & 1) * 2 + (x & 1))) & 1u) ? (u64)(c >> 4) : 0ull;
     }
     __device__ __forceinline__ u64 id(u64 r) const { return r - 1 + base; }
+    __device__ __forceinline__ int64_t width(int64_t) const { return X; }     // (y, x) need the cube grid's X
 };
+
+// Facing voxel pairs of a seam (plane voxel i: upper id, lower id), both non-zero.  A pair equal to
+// that of voxel i - 1 or i - X is not emitted (the first voxel of every distinct pair in index
+// order always is).  counter[0] = pairs appended, counter[1] = the largest id emitted (it sizes the
+// packed key of dedup_pairs).
+// htab (optional): a device hash set of emitted pairs (key a << 32 | b, empty = ~0, hmask + 1 slots):
+// a pair already in it is dropped, so only distinct pairs are appended -- a 2048^2 membrane seam
+// emits ~47 k pairs after the i - 1 / i - X filters but holds ~150 distinct ones.  The slot is read
+// before the CAS (the popular pairs' slots are read from L2 instead of serialising atomics on
+// them).  Pairs with an id >= 2^32, or whose probe sequence is full, are appended anyway and
+// counter[2] is flagged (the host then dedups by sorting).
+constexpr int SEAM_HASH_PROBES = 64;
+__device__ __forceinline__ int seam_hash_insert(u64* htab, u32 hmask, u64 key) {     // 1 new, 0 dup, -1 full
+    u32 h = (u32)((key * 0x9E3779B97F4A7C15ull) >> 40) & hmask;
+    for (int p = 0; p < SEAM_HASH_PROBES; ++p) {
+        u64 cur = __builtin_nontemporal_load(htab + h);
+        if (cur == key) return 0;
+        if (cur == ~0ull) {
+            cur = atomicCAS((unsigned long long*)(htab + h), ~0ull, (unsigned long long)key);
+            if (cur == ~0ull) return 1;
+            if (cur == key) return 0;
+        }
+        h = (h + 1) & hmask;
+    }
+    return -1;
+}
 
 template <class UP>
 __global__ __launch_bounds__(SEAM_PAIR_THREADS) void k_seam_pairs(int64_t n, int64_t X, UP upper,
-                                                                  const u64* lower, u64* pa, u64* pb,
-                                                                  unsigned long long* counter, u64 cap) {
-    // workgroup-aggregated append: one global atomic per 1024 voxels (one per wave still
-    // serialised ~1.8 ms on the single counter); counter[1] = the largest id emitted (atomicMax
-    // per workgroup: it sizes the packed key of dedup_pairs)
+                                                                  const u64* __restrict__ lower, u64* pa, u64* pb,
+                                                                  unsigned long long* counter, u64 cap, u64* htab,
+                                                                  u32 hmask) {
     __shared__ u32 wcnt[SEAM_PAIR_THREADS / 64];
     __shared__ unsigned long long wmax[SEAM_PAIR_THREADS / 64];
     __shared__ unsigned long long gbase;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool emit = false;
-    u64 a = 0, b = 0;
-    if (i < n) {
-        const u64 u = upper.raw(i);
-        b = lower[i];
-        emit = u && b;
-        if (emit && i > 0 && upper.raw(i - 1) == u && lower[i - 1] == b) emit = false;
-        if (emit && i >= X && upper.raw(i - X) == u && lower[i - X] == b) emit = false;
-        a = upper.id(u);
-    }
+    __shared__ u64 bufa[SP_BUF], bufb[SP_BUF];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const u64 m = __ballot(emit);
-    u64 mx = emit ? (a > b ? a : b) : 0ull;
+    const bool vec = ((uintptr_t)lower & 15) == 0;
+    X = upper.width(X);                                        // plane row width of the (y, x) walk
+    const u32 Xu = (u32)X;
+    u64 mx = 0;
+    u32 nbuf = 0;
+    auto flush = [&]() {
+        if (threadIdx.x == 0) gbase = nbuf ? atomicAdd(counter, (unsigned long long)nbuf) : 0ull;
+        __syncthreads();
+        const unsigned long long b0 = gbase;
+        for (u32 q = threadIdx.x; q < nbuf; q += SEAM_PAIR_THREADS)
+            if (b0 + q < cap) { pa[b0 + q] = bufa[q]; pb[b0 + q] = bufb[q]; }
+        __syncthreads();
+        nbuf = 0;
+    };
+    for (int r = 0; r < SP_ROUNDS; ++r) {
+        const int64_t i0 = (int64_t)blockIdx.x * SP_WG_VOXELS + ((int64_t)r * SEAM_PAIR_THREADS + threadIdx.x) * SPV;
+        u64 lo[SPV], up[SPV];
+        if (vec && i0 + SPV <= n) {
+#pragma unroll
+            for (int j = 0; j < SPV; j += 2) {
+                const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(lower + i0 + j);
+                lo[j] = v.x; lo[j + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < SPV; ++j) lo[j] = i0 + j < n ? lower[i0 + j] : 0ull;
+        }
+        // (y, x) of i0, then stepped (one 32-bit division per thread and round; planes < 2^32 voxels)
+        u32 y = (u32)((u64)i0 / Xu), x = (u32)(i0 - (int64_t)y * X);
+        u32 yy = y, xx = x;
+#pragma unroll
+        for (int j = 0; j < SPV; ++j) {
+            up[j] = (i0 + j < n) ? upper.raw(i0 + j, yy, xx) : 0ull;
+            if (++xx == Xu) { xx = 0; ++yy; }
+        }
+        // voxel i0 - 1: lane - 1's last one; the first lane of a wave loads it
+        u64 pu = __shfl_up(up[SPV - 1], 1, 64), pl = __shfl_up(lo[SPV - 1], 1, 64);
+        if (lane == 0) {
+            pu = pl = 0;
+            if (i0 > 0 && i0 - 1 < n) {
+                const u32 py = x ? y : y - 1, px = x ? x - 1 : Xu - 1;
+                pu = upper.raw(i0 - 1, py, px);
+                pl = lower[i0 - 1];
+            }
+        }
+        bool emit[SPV];
+        u32 cnt = 0;
+        yy = y; xx = x;
+#pragma unroll
+        for (int j = 0; j < SPV; ++j) {
+            const int64_t i = i0 + j;
+            const u64 u = up[j], b = lo[j];
+            const u64 qu = j ? up[j - 1] : pu, ql = j ? lo[j - 1] : pl;
+            bool e = i < n && u && b && !(qu == u && ql == b);
+            if (e && i >= X && upper.raw(i - X, yy - 1, xx) == u && lower[i - X] == b) e = false;
+            if (e && htab) {
+                const u64 a = upper.id(u);
+                if ((a | b) >> 32) {
+                    atomicOr(counter + 2, 1ull);
+                } else {
+                    const int r = seam_hash_insert(htab, hmask, (a << 32) | b);
+                    if (r < 0) atomicOr(counter + 2, 2ull);
+                    e = r != 0;
+                }
+            }
+            emit[j] = e;
+            if (e) {
+                const u64 a = upper.id(u);
+                mx = a > mx ? a : mx;
+                mx = b > mx ? b : mx;
+                ++cnt;
+            }
+            if (++xx == Xu) { xx = 0; ++yy; }
+        }
+        u32 xs = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) { const u32 t = __shfl_up(xs, o, 64); if (lane >= o) xs += t; }
+        if (lane == 63) wcnt[wave] = xs;
+        __syncthreads();
+        u32 wb = 0, tot = 0;
+#pragma unroll
+        for (int v = 0; v < SEAM_PAIR_THREADS / 64; ++v) { const u32 c = wcnt[v]; wb += v < wave ? c : 0u; tot += c; }
+        __syncthreads();
+        if (nbuf + tot > (u32)SP_BUF) flush();
+        u32 pos = nbuf + wb + xs - cnt;
+#pragma unroll
+        for (int j = 0; j < SPV; ++j)
+            if (emit[j]) { bufa[pos] = upper.id(up[j]); bufb[pos] = lo[j]; ++pos; }
+        nbuf += tot;
+    }
+    __syncthreads();
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) { const u64 t = __shfl_xor(mx, o, 64); mx = t > mx ? t : mx; }
-    if (lane == 0) { wcnt[wave] = (u32)__popcll(m); wmax[wave] = mx; }
+    if (lane == 0) wmax[wave] = mx;
     __syncthreads();
     if (threadIdx.x == 0) {
-        u32 tot = 0;
         unsigned long long gm = 0;
-        for (int w = 0; w < SEAM_PAIR_THREADS / 64; ++w) {
-            const u32 c = wcnt[w]; wcnt[w] = tot; tot += c;
-            gm = wmax[w] > gm ? wmax[w] : gm;
-        }
-        gbase = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
-        if (tot) atomicMax(counter + 1, gm);
+        for (int v = 0; v < SEAM_PAIR_THREADS / 64; ++v) gm = wmax[v] > gm ? wmax[v] : gm;
+        if (gm) atomicMax(counter + 1, gm);
     }
-    __syncthreads();
-    if (emit) {
-        const unsigned long long pos = gbase + wcnt[wave] + __popcll(m & ((1ull << lane) - 1));
-        if (pos < cap) { pa[pos] = a; pb[pos] = b; }
-    }
+    if (nbuf) flush();
 }
 
 // The top voxel plane as one u32 per 2x2 cube of the global cube grid (ceil(Y/2) x ceil(X/2);
@@ -2441,6 +2583,27 @@ __global__ __launch_bounds__(NTHREADS) void k_top_cubes(Geom g, const face_t* __
         u32 w = 0;
         if (a) w = ((u32)(KR[gfind(P, base + (a & FK_MASK))] - sub + 1) << 4) | (a >> FK_BITS);
         cubes[(int64_t)(ti.y0 / 2 + cy) * CXg + ti.x0 / 2 + cx] = w;
+    }
+}
+
+// copy of the seam-pair ids with their largest value (atomicMax per workgroup into *mx): sizes the
+// radix sort of phase_map (ids of a C3 run fit 12 bits: 2 passes instead of 8)
+__global__ __launch_bounds__(256) void k_copy_max64(int64_t n, const u64* __restrict__ in, u64* out,
+                                                    unsigned long long* mx) {
+    __shared__ unsigned long long wm[4];
+    u64 m = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const u64 v = in[i];
+        out[i] = v;
+        m = v > m ? v : m;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { const u64 t = __shfl_xor(m, o, 64); m = t > m ? t : m; }
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; ++w) m = wm[w] > m ? wm[w] : m;
+        if (m) atomicMax(mx, (unsigned long long)m);
     }
 }
 

@@ -94,7 +94,8 @@ struct cc_ctx {
         ev_main, ev_z, ev_seg, ev_gt, ev_flag, ev_part,   // evaluation (cc_eval.hip)
         rl_wg,                                            // relabel: per-workgroup id lists
         gs1, gs2, gs_tab,                                 // Gaussian prefilter temporaries (cc_prefilter.hip)
-        mask_xmap;                                        // resized masks (cc_mask.hip)
+        mask_xmap,                                        // resized masks (cc_mask.hip)
+        seam_hash;                                        // seam pair hash set (k_seam_pairs)
     int64_t ev_cap = 0;      // entries per evaluation hash table of the last cc_evaluate
     int64_t rl_cap = 0;      // id-set slots of the last cc_relabel_consecutive
     // last run
@@ -587,7 +588,13 @@ static int64_t dedup_pairs(cc_ctx* c, u64* pa, u64* pb, u64* qa, u64* qb, int64_
     CC_REQUIRE(n < (1LL << 31), "too many pairs for one sort");
     c->scalars2.ensure(16);
     int* nsel = (int*)c->scalars2.p;
-    if (max_id < (1ull << 32)) {
+    if (max_id < (1ull << 32) && n <= prims::SU_MAX) {
+        // a few thousand pairs: one workgroup packs, sorts, dedups and unpacks them in LDS
+        int nbits = 1;
+        while (nbits < 32 && (max_id >> nbits)) ++nbits;
+        prims::k_pairs_sort_unique_small<<<1, prims::SU_T, 0, s>>>(pa, pb, (int)n, nbits, nullptr, 0, qa, qb, nsel);
+        HIP_OK(hipGetLastError());
+    } else if (max_id < (1ull << 32)) {
         int nbits = 1;
         while (nbits < 32 && (max_id >> nbits)) ++nbits;
         u64* k0 = qa;            // qa / qb are free until the unpack
@@ -627,17 +634,34 @@ static void phase_map(cc_ctx* c, const u64* pairs, int64_t n) {
     c->map_ids2.ensure(2 * n * sizeof(u64));
     u64* ids = c->map_ids.as<u64>();
     u64* ids2 = c->map_ids2.as<u64>();
-    HIP_OK(hipMemcpyAsync(ids, pairs, 2 * n * sizeof(u64), hipMemcpyDeviceToDevice, s));
-    prims::sort_keys<u64>(ids, ids2, 2 * n, 0, 64, c->cub_tmp, s);
     c->scalars2.ensure(16);
     int* nsel = (int*)c->scalars2.p;
-    prims::select_unique<u64>(ids2, ids, nsel, 2 * n, c->cub_tmp, s);
     int m = 0;
+    u64 id_max = 0;
+    if (2 * n <= prims::SU_MAX) {
+        // a few thousand ids: one workgroup sorts and dedups them in LDS
+        launch(c, "seam_sort_small", [&] { prims::k_sort_unique_small<<<1, prims::SU_T, 0, s>>>(pairs, (int)(2 * n), ids, nsel); });
+    } else {
+        unsigned long long* dmax = (unsigned long long*)c->scalars2.p + 1;
+        HIP_OK(hipMemsetAsync(dmax, 0, sizeof(u64), s));
+        launch(c, "k_copy_max64", [&] { k_copy_max64<<<grid_stride(2 * n), 256, 0, s>>>(2 * n, pairs, ids, dmax); });
+        {
+            Readback rb(c, 64);
+            rb.add(&id_max, dmax, sizeof(u64));
+            rb.wait();
+        }
+        int nbits = 1;
+        while (nbits < 64 && (id_max >> nbits)) ++nbits;
+        launch(c, "seam_sort", [&] { prims::sort_keys<u64>(ids, ids2, 2 * n, 0, nbits, c->cub_tmp, s); });
+        launch(c, "seam_unique", [&] { prims::select_unique<u64>(ids2, ids, nsel, 2 * n, c->cub_tmp, s); });
+    }
     {
         Readback rb(c, 64);
         rb.add(&m, nsel, sizeof(int));
         rb.wait();
     }
+    if (std::getenv("CC_DEBUG_SIZES"))       // dev hook: sizes of the seam schedule
+        std::fprintf(stderr, "[cc] phase_map pairs %lld ids %d max_id %llu\n", (long long)n, m, (unsigned long long)id_max);
     // U = ids[0:m]; index pairs; union-find (smallest index = smallest id) -> V
     c->map_vals.ensure(std::max<int64_t>(1, m) * sizeof(u64));
     u64* ip = ids2;    // 2n indices
@@ -781,7 +805,7 @@ void cc_destroy(cc_ctx* c) {
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
                       &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec, &c->mark, &c->bflag,
                       &c->ev_main, &c->ev_z, &c->ev_seg, &c->ev_gt, &c->ev_flag, &c->ev_part, &c->rl_wg,
-                      &c->gs1, &c->gs2, &c->gs_tab, &c->mask_xmap};
+                      &c->gs1, &c->gs2, &c->gs_tab, &c->mask_xmap, &c->seam_hash};
     for (DevBuf* b : bufs) b->release();
     c->pin.release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }

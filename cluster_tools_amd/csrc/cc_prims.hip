@@ -115,14 +115,16 @@ __global__ __launch_bounds__(PT) void k_scan_down(const T* in, T* out, int64_t n
     scan_tile(in, out, (int64_t)blockIdx.x * SC_TILE, n, part ? part[blockIdx.x] : (T)0, tile, sh);
 }
 
-// one workgroup: exclusive scan of part[0, m) in place (the tile sums)
+// one workgroup: exclusive scan of in[0, m) into out (the tile sums, in place; or a whole short
+// array: one launch instead of three)
 template <class T>
-__global__ __launch_bounds__(PT) void k_scan_single(T* part, int64_t m) {
+__global__ __launch_bounds__(PT) void k_scan_single(const T* in, T* out, int64_t m) {
     __shared__ T tile[SC_TILE];
     __shared__ T sh[PW];
     T carry = 0;
-    for (int64_t b = 0; b < m; b += SC_TILE) carry = scan_tile(part, part, b, m, carry, tile, sh);
+    for (int64_t b = 0; b < m; b += SC_TILE) carry = scan_tile(in, out, b, m, carry, tile, sh);
 }
+constexpr int64_t SC_SINGLE_MAX = 2 * SC_TILE;      // arrays up to this length: one workgroup
 
 template <class K>
 __global__ __launch_bounds__(PT) void k_rs_hist(const K* __restrict__ kin, int64_t n, int shift, u32 mask, int64_t nwg,
@@ -208,6 +210,142 @@ __global__ void k_compact(const T* __restrict__ in, const u8* __restrict__ fl, c
     if (i == n - 1) *nsel = (int)(pos[i] + (keep ? 1u : 0u));
 }
 
+// ---- one-workgroup sort + unique of up to SU_MAX u64 keys in LDS ----------------------------
+// The seam schedule sorts a few hundred to a few thousand keys per slab (unique seam pairs, the
+// distinct ids of all seams); the multi-kernel sort is launch-bound there (3 kernels per 8-bit
+// pass), so one 1024-thread workgroup does it all in LDS: the key bound (largest key) -> passes,
+// per pass a digit histogram (LDS atomics), its scan, and the stable scatter in rounds of 1024
+// keys (ranks among equal digits from 8 ballots per wave, wave counts prefixed per digit), then
+// the unique keys compacted in order.
+constexpr int SU_T = 1024, SU_W = SU_T / 64, SU_MAX = 8192;
+struct SortSmallLDS {
+    u64 a[SU_MAX], b[SU_MAX];
+    u32 wc[SU_W][RADIX];
+    u32 run[RADIX];
+    u64 red[SU_W];
+    u32 sh[SU_W];
+};
+
+// sorts L.a[0, n) (result in *res, which is L.a or L.b), returns nothing; keys < 2^bits
+__device__ __forceinline__ u64* su_sort(SortSmallLDS& L, int n, int bits) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u64 lt = (1ull << lane) - 1;
+    u64* src = L.a;
+    u64* dst = L.b;
+    for (int shift = 0; shift < bits; shift += 8) {
+        const u32 mask = (1u << min(8, bits - shift)) - 1;
+        if (tid < RADIX) L.run[tid] = 0;
+        __syncthreads();
+        for (int i = tid; i < n; i += SU_T) atomicAdd(&L.run[(u32)(src[i] >> shift) & mask], 1u);
+        __syncthreads();
+        if (w == 0) {                              // exclusive scan of the 256 digit counts
+            u32 v[4], sum = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { v[j] = L.run[4 * lane + j]; sum += v[j]; }
+            u32 x = sum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) { const u32 y = __shfl_up(x, o, 64); if (lane >= o) x += y; }
+            u32 r = x - sum;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { L.run[4 * lane + j] = r; r += v[j]; }
+        }
+        __syncthreads();
+        for (int r0 = 0; r0 < n; r0 += SU_T) {
+            const int i = r0 + tid;
+            const bool valid = i < n;
+            const u64 k = valid ? src[i] : 0ull;
+            const u32 d = (u32)(k >> shift) & mask;
+            u64 peers = __ballot(valid);
+#pragma unroll
+            for (int bb = 0; bb < 8; ++bb) {
+                const u64 q = __ballot((d >> bb) & 1u);
+                peers &= ((d >> bb) & 1u) ? q : ~q;
+            }
+            for (int j = tid; j < SU_W * RADIX; j += SU_T) (&L.wc[0][0])[j] = 0;
+            __syncthreads();
+            const u32 rank = (u32)__popcll(peers & lt);
+            if (valid && rank == 0) L.wc[w][d] = (u32)__popcll(peers);
+            __syncthreads();
+            if (tid < RADIX) {
+                u32 r = L.run[tid];
+                for (int q = 0; q < SU_W; ++q) { const u32 c = L.wc[q][tid]; L.wc[q][tid] = r; r += c; }
+                L.run[tid] = r;
+            }
+            __syncthreads();
+            if (valid) dst[L.wc[w][d] + rank] = k;
+            __syncthreads();
+        }
+        u64* t = src; src = dst; dst = t;
+    }
+    return src;
+}
+
+// largest of L.a[0, n) over the workgroup
+__device__ __forceinline__ u64 su_max(SortSmallLDS& L, int n) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    u64 m = 0;
+    for (int i = tid; i < n; i += SU_T) m = L.a[i] > m ? L.a[i] : m;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { const u64 t = __shfl_xor(m, o, 64); m = t > m ? t : m; }
+    if (lane == 0) L.red[w] = m;
+    __syncthreads();
+    m = 0;
+    for (int q = 0; q < SU_W; ++q) m = L.red[q] > m ? L.red[q] : m;
+    __syncthreads();
+    return m;
+}
+
+// unique keys of the sorted k[0, n) in order: emit(position, key); returns the count
+template <class EMIT>
+__device__ __forceinline__ int su_unique(SortSmallLDS& L, const u64* k, int n, EMIT&& emit) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int carry = 0;
+    for (int r0 = 0; r0 < n; r0 += SU_T) {
+        const int i = r0 + tid;
+        const u32 f = (i < n && (i == 0 || k[i] != k[i - 1])) ? 1u : 0u;
+        const u64 bal = __ballot(f);
+        if (lane == 0) L.sh[w] = (u32)__popcll(bal);
+        __syncthreads();
+        u32 before = 0, tot = 0;
+        for (int q = 0; q < SU_W; ++q) { const u32 c = L.sh[q]; before += q < w ? c : 0u; tot += c; }
+        if (f) emit(carry + (int)(before + (u32)__popcll(bal & ((1ull << lane) - 1))), k[i]);
+        carry += (int)tot;
+        __syncthreads();
+    }
+    return carry;
+}
+
+// sorted distinct values of in[0, n) (n <= SU_MAX) -> out, *nsel = their count
+__global__ __launch_bounds__(SU_T) void k_sort_unique_small(const u64* __restrict__ in, int n, u64* out, int* nsel) {
+    __shared__ SortSmallLDS L;
+    for (int i = threadIdx.x; i < n; i += SU_T) L.a[i] = in[i];
+    __syncthreads();
+    const u64 mx = su_max(L, n);
+    int bits = 0;
+    while (bits < 64 && (mx >> bits)) ++bits;
+    const u64* k = su_sort(L, n, bits);
+    const int m = su_unique(L, k, n, [&](int pos, u64 v) { out[pos] = v; });
+    if (threadIdx.x == 0) *nsel = m;
+}
+
+// sorted distinct (a, b) pairs of pa / pb [0, n) (n <= SU_MAX, every id < 2^nb) -> pairs
+// ([m][2], at most cap written; qa / qb, if given, get them too), *nsel = m
+__global__ __launch_bounds__(SU_T) void k_pairs_sort_unique_small(const u64* __restrict__ pa, const u64* __restrict__ pb,
+                                                                  int n, int nb, u64* pairs, int64_t cap, u64* qa,
+                                                                  u64* qb, int* nsel) {
+    __shared__ SortSmallLDS L;
+    for (int i = threadIdx.x; i < n; i += SU_T) L.a[i] = (pa[i] << nb) | pb[i];
+    __syncthreads();
+    const u64* k = su_sort(L, n, 2 * nb);
+    const u64 lo = (1ull << nb) - 1;
+    const int m = su_unique(L, k, n, [&](int pos, u64 v) {
+        const u64 a = v >> nb, b = v & lo;
+        if (pairs && pos < cap) { pairs[2 * pos] = a; pairs[2 * pos + 1] = b; }
+        if (qa) { qa[pos] = a; qb[pos] = b; }
+    });
+    if (threadIdx.x == 0) *nsel = m;
+}
+
 // ---- host side: temporaries carved from one caller buffer (the context's cub_tmp) ----------
 struct Carve {
     char* p;
@@ -226,7 +364,7 @@ inline unsigned nblk(int64_t n, int64_t per) { return (unsigned)std::max<int64_t
 template <class T>
 size_t scan_tmp_bytes(int64_t n) {
     Carve cv{nullptr};
-    if (n > SC_TILE) cv.take<T>((n + SC_TILE - 1) / SC_TILE);
+    if (n > SC_SINGLE_MAX) cv.take<T>((n + SC_TILE - 1) / SC_TILE);
     return cv.off + 256;
 }
 
@@ -234,14 +372,14 @@ size_t scan_tmp_bytes(int64_t n) {
 template <class T>
 void scan_excl(const T* in, T* out, int64_t n, char* tmp, hipStream_t s) {
     if (n <= 0) return;
-    if (n <= SC_TILE) {
-        k_scan_down<T><<<1, PT, 0, s>>>(in, out, n, nullptr);
+    if (n <= SC_SINGLE_MAX) {
+        k_scan_single<T><<<1, PT, 0, s>>>(in, out, n);
     } else {
         Carve cv{tmp};
         const int64_t m = (n + SC_TILE - 1) / SC_TILE;
         T* part = cv.take<T>(m);
         k_scan_reduce<T><<<(unsigned)m, PT, 0, s>>>(in, n, part);
-        k_scan_single<T><<<1, PT, 0, s>>>(part, m);
+        k_scan_single<T><<<1, PT, 0, s>>>(part, part, m);
         k_scan_down<T><<<(unsigned)m, PT, 0, s>>>(in, out, n, part);
     }
     HIP_OK(hipGetLastError());

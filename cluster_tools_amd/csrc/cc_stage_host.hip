@@ -212,15 +212,21 @@ static int64_t seam_pairs_impl(cc_ctx* c, UP upper, const uint64_t* lower, int64
     u64* pb = pa + capn;
     u64* qa = c->pairs2.as<u64>();
     u64* qb = qa + capn;
+    c->counter.ensure(4 * sizeof(unsigned long long));
     unsigned long long* cnt = (unsigned long long*)c->counter.p;
-    HIP_OK(hipMemsetAsync(cnt, 0, 2 * sizeof(unsigned long long), s));
+    // the pair hash set (see k_seam_pairs): 2^16 slots
+    constexpr int64_t HS = 1 << 16;
+    c->seam_hash.ensure(HS * sizeof(u64));
+    u64* htab = c->seam_hash.as<u64>();
+    HIP_OK(hipMemsetAsync(cnt, 0, 3 * sizeof(unsigned long long), s));
+    HIP_OK(hipMemsetAsync(htab, 0xFF, HS * sizeof(u64), s));
     // plane width for the 'pair above' filter (any value is correct; the slab's X is exact)
     const int64_t X = (c->run && state(c).hg.g.Y * state(c).hg.g.X == n) ? state(c).hg.g.X : n;
     launch(c, "k_seam_pairs", [&] {
-        k_seam_pairs<UP><<<grid1d(n, SEAM_PAIR_THREADS), SEAM_PAIR_THREADS, 0, s>>>(n, X, upper, lower, pa, pb, cnt,
-                                                                                  (u64)capn);
+        k_seam_pairs<UP><<<(unsigned)((n + SP_WG_VOXELS - 1) / SP_WG_VOXELS), SEAM_PAIR_THREADS, 0, s>>>(
+            n, X, upper, lower, pa, pb, cnt, (u64)capn, htab, (u32)(HS - 1));
     });
-    unsigned long long rb2[2] = {0, 0};          // raw pair count, largest id
+    unsigned long long rb2[3] = {0, 0, 0};       // pairs appended, largest id, flags
     {
         Readback rb(c, 64);
         rb.add(rb2, cnt, sizeof(rb2));
@@ -229,7 +235,26 @@ static int64_t seam_pairs_impl(cc_ctx* c, UP upper, const uint64_t* lower, int64
     const unsigned long long n_raw = rb2[0];
     CC_REQUIRE(n_raw <= (unsigned long long)capn, "seam pair buffer overflow");
     int64_t nu = 0;
+    if (rb2[2] == 0 && n_raw <= (unsigned long long)prims::SU_MAX) {
+        // the appended pairs are distinct: one workgroup sorts them into the caller's buffer
+        nu = (int64_t)n_raw;
+        int nb = 1;
+        while (nb < 32 && (rb2[1] >> nb)) ++nb;
+        c->scalars2.ensure(16);
+        if (nu > 0)
+            launch(c, "seam_sort_small", [&] {
+                prims::k_pairs_sort_unique_small<<<1, prims::SU_T, 0, s>>>(pa, pb, (int)nu, nb, pairs, cap, nullptr, nullptr,
+                                                                          (int*)c->scalars2.p);
+            });
+        if (std::getenv("CC_DEBUG_SIZES"))       // dev hook: sizes of the seam schedule
+            std::fprintf(stderr, "[cc] seam_pairs plane %lld unique %lld max_id %llu (hash set)\n", (long long)n,
+                         (long long)nu, (unsigned long long)rb2[1]);
+        return nu;
+    }
     launch(c, "seam_dedup", [&] { nu = dedup_pairs(c, pa, pb, qa, qb, (int64_t)n_raw, (uint64_t)rb2[1]); });
+    if (std::getenv("CC_DEBUG_SIZES"))       // dev hook: sizes of the seam schedule
+        std::fprintf(stderr, "[cc] seam_pairs plane %lld raw %llu unique %lld max_id %llu\n", (long long)n,
+                     n_raw, (long long)nu, (unsigned long long)rb2[1]);
     if (pairs && cap > 0 && nu > 0) {
         const int64_t m = std::min<int64_t>(cap, nu);
         launch(c, "k_interleave", [&] { k_interleave<<<grid1d(m), 256, 0, s>>>(m, qa, qb, pairs); });

@@ -188,6 +188,24 @@ def test_speculated_interval_corrected(ctx, mode, thr, outlier):
     _check_against_oracle(ctx, inp, (32, 64, 96), thr, mode, mask)
 
 
+@pytest.mark.parametrize('mode', ['greater', 'less'])
+@pytest.mark.parametrize('value', [-0.0, -1e-30, -0.25])
+def test_nonneg_walk_fallback(ctx, mode, value):
+    """k_spec's raw-bit walk (blocks whose sample is non-negative, BP_NONNEG): a value with the
+    sign bit set (-0, a negative denormal, a negative number) off the sampled rows sends its wave
+    back to the ordered walk; statistics, bits and labels must stay exact (with and without a
+    mask, the masked 'greater' variant has the raw walk too)."""
+    rng = np.random.default_rng(11)
+    inp = (rng.integers(0, 17, (64, 128, 192)) / np.float32(16)).astype(np.float32)
+    inp[1, 1, 5] = value                  # off the sampled rows (z = 8 mod 16, y = 16 mod 32)
+    inp[40, 77, 130] = value
+    inp[63, 127, 191] = value             # last voxel of the last (full) tile
+    for bs in [(32, 64, 96), (64, 128, 192)]:
+        _check_against_oracle(ctx, inp, bs, 0.5, mode)
+    mask = (rng.random(inp.shape) < 0.9).astype(np.uint8)
+    _check_against_oracle(ctx, inp, (32, 64, 96), 0.5, mode, mask)
+
+
 def test_mask_vs_oracle(ctx):
     from oracle.synth import ellipsoid_mask
     shape = (64, 160, 192)
