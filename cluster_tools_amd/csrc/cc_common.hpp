@@ -41,14 +41,12 @@ constexpr int KEY_BITS = 36;               // packed sort key: block << 36 | fir
 
 enum { MODE_GREATER = 0, MODE_LESS = 1, MODE_EQUAL = 2 };
 enum { BP_EMPTY = 0, BP_INTERVAL = 1, BP_EXACT = 2 };
-// BlockParam.pad flags of a guessed interval (k_guess)
-constexpr u32 BP_NONNEG = 1;   // the block's sample held no value below +0 (k_spec's raw-bit walk)
 
 struct BlockParam {      // per reference block, from its min/max (volume_utils.py:98-105)
     float mn, m;         // min and max(x - min) (NaN where numpy's would be NaN)
     u32 lo, hi;          // foreground <=> lo <= ord(x) <= hi   (kind == BP_INTERVAL)
     u32 kind;
-    u32 pad;             // guesses: BP_NONNEG; 0 otherwise
+    u32 pad;
 };
 
 // block parameters read from global memory come back in VGPRs (the compiler cannot prove the
@@ -61,7 +59,7 @@ __device__ __forceinline__ BlockParam uniform_bp(const BlockParam& q) {
     p.lo = __builtin_amdgcn_readfirstlane(q.lo);
     p.hi = __builtin_amdgcn_readfirstlane(q.hi);
     p.kind = __builtin_amdgcn_readfirstlane(q.kind);
-    p.pad = __builtin_amdgcn_readfirstlane(q.pad);
+    p.pad = 0;
     return p;
 }
 

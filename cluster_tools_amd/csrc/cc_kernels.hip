@@ -759,9 +759,6 @@ constexpr int SAMPLE_DZ = 4, SAMPLE_DY = 16;
 #ifndef CC_F4_PREFETCH
 #define CC_F4_PREFETCH 0
 #endif
-#ifndef CC_NN_WALK
-#define CC_NN_WALK 1        // k_spec's raw-bit walk for non-negative blocks (0: ordered walk only, A/B)
-#endif
 #ifndef CC_WL_BATCH
 #define CC_WL_BATCH 0
 #endif
@@ -875,9 +872,7 @@ __global__ void k_guess(int64_t nb, const u32* part, float thr, int mode, BlockP
     const bool nan = mx > 0xFF800000u || mn < 0x007FFFFFu;
     // On continuous data the sampled extremes are not the block's, so the guessed bound misses
     // the exact one by a little: only tiles holding a voxel between the two are relabelled.
-    BlockParam gp = widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
-    gp.pad = (!nan && mn >= 0x80000000u) ? BP_NONNEG : 0u;     // smallest sampled value >= +0
-    guess[b] = gp;
+    guess[b] = widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
 }
 
 // One launch for the front's initial state (it replaced nine memsets of ~4 us each): ordered
@@ -940,43 +935,27 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         if (SIDES & 2) { const u32 k = hi - o; K2N = min(K2N, use ? k : ~0u); K2X = max(K2X, use ? k : 0u); }
         return use && fgp(o);
     };
-    // four voxels of one float4 (full tiles): the same, min / max folded three operands at a time.
-    // NN (the block's guess says non-negative, BP_NONNEG): on the raw bits -- for raw < 2^31,
-    // ord = raw + 2^31, so o - lo = raw - (lo - 2^31), hi - o = (hi - 2^31) - raw, min / max are
-    // those of the raw bits (+ 2^31 afterwards) and the foreground test compares raw with the
-    // shifted bound: no per-voxel f2ord, a quarter of the walk's VALU.  A value with the sign bit
-    // set breaks this; the wave sees it in its raw max and walks its rows again on ord values.
-    const u32 lof = lo >= 0x80000000u ? lo - 0x80000000u : 0u;              // o >= lo <=> raw >= lof
-    const bool hiok = hi >= 0x80000000u;                                    // o <= hi <=> hiok && raw <= hif
-    const u32 hif = hi - 0x80000000u;
-    auto quad = [&](auto NNC, float4 v, uchar4 mk, bool fg[4]) {
-        constexpr bool NN = decltype(NNC)::value;
-        const u32 o0 = NN ? __float_as_uint(v.x) : f2ord(__float_as_uint(v.x));
-        const u32 o1 = NN ? __float_as_uint(v.y) : f2ord(__float_as_uint(v.y));
-        const u32 o2 = NN ? __float_as_uint(v.z) : f2ord(__float_as_uint(v.z));
-        const u32 o3 = NN ? __float_as_uint(v.w) : f2ord(__float_as_uint(v.w));
+    // four voxels of one float4 (full tiles): the same, min / max folded three operands at a time
+    auto quad = [&](float4 v, uchar4 mk, bool fg[4]) {
+        const u32 o0 = f2ord(__float_as_uint(v.x)), o1 = f2ord(__float_as_uint(v.y));
+        const u32 o2 = f2ord(__float_as_uint(v.z)), o3 = f2ord(__float_as_uint(v.w));
         mn = min(min(min(min(mn, o0), o1), o2), o3);
         mx = max(max(max(max(mx, o0), o1), o2), o3);
         const bool u0 = !HAS_MASK || mk.x, u1 = !HAS_MASK || mk.y, u2 = !HAS_MASK || mk.z, u3 = !HAS_MASK || mk.w;
-        const u32 l1 = NN ? lo - 0x80000000u : lo, h2 = NN ? hi - 0x80000000u : hi;
         if (SIDES & 1) {
-            const u32 k0 = o0 - l1, k1 = o1 - l1, k2 = o2 - l1, k3 = o3 - l1;
+            const u32 k0 = o0 - lo, k1 = o1 - lo, k2 = o2 - lo, k3 = o3 - lo;
             K1N = min(min(min(min(K1N, u0 ? k0 : ~0u), u1 ? k1 : ~0u), u2 ? k2 : ~0u), u3 ? k3 : ~0u);
             K1X = max(max(max(max(K1X, u0 ? k0 : 0u), u1 ? k1 : 0u), u2 ? k2 : 0u), u3 ? k3 : 0u);
         }
         if (SIDES & 2) {
-            const u32 k0 = h2 - o0, k1 = h2 - o1, k2 = h2 - o2, k3 = h2 - o3;
+            const u32 k0 = hi - o0, k1 = hi - o1, k2 = hi - o2, k3 = hi - o3;
             K2N = min(min(min(min(K2N, u0 ? k0 : ~0u), u1 ? k1 : ~0u), u2 ? k2 : ~0u), u3 ? k3 : ~0u);
             K2X = max(max(max(max(K2X, u0 ? k0 : 0u), u1 ? k1 : 0u), u2 ? k2 : 0u), u3 ? k3 : 0u);
         }
-        auto fgq = [&](u32 o) -> bool {
-            if (!NN) return fgp(o);
-            return SIDES == 1 ? o >= lof : SIDES == 2 ? (hiok && o <= hif) : (o >= lof && hiok && o <= hif);
-        };
-        fg[0] = u0 && fgq(o0); fg[1] = u1 && fgq(o1); fg[2] = u2 && fgq(o2); fg[3] = u3 && fgq(o3);
+        fg[0] = u0 && fgp(o0); fg[1] = u1 && fgp(o1); fg[2] = u2 && fgp(o2); fg[3] = u3 && fgp(o3);
     };
     const bool f4 = ti.lz == TZ && ti.ly == TY && ti.lx == TX && ((ti.x0 | (int)(g.X & 3)) & 3) == 0;
-    auto f4walk = [&](auto NNC) {
+    if (f4) {
         // Full, 16-B aligned tile: float4 per lane (4 rows of 64 voxels per load instruction, a
         // quarter of the load instructions of the lane = x walk).  Wave w owns rows y = 4w .. 4w+3
         // of every plane; lane l holds x = 4 (l % 16) .. + 3 of row 4w + l / 16.  The four
@@ -990,7 +969,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         u32 R[8] = {0, 0, 0, 0, 0, 0, 0, 0};      // lane z: ballots (lo, hi) of values 0..3 of plane z
         auto plane_bits = [&](int z, float4 v, uchar4 mk) {
             bool fg[4];
-            quad(NNC, v, mk, fg);
+            quad(v, mk, fg);
             const u64 b0 = __ballot(fg[0]), b1 = __ballot(fg[1]), b2 = __ballot(fg[2]), b3 = __ballot(fg[3]);
 #if CC_WL_BATCH
             CC_WRITELANE8(R, b0, b1, b2, b3, z);
@@ -1053,26 +1032,6 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         // split form: even voxels x = 4i (j = 0), 4i + 2 (j = 2) -> bits 2i, 2i + 1 of the low half
         const u32 even = spread2(seg[0]) | (spread2(seg[2]) << 1), odd = spread2(seg[1]) | (spread2(seg[3]) << 1);
         L.rows[zz * TY + 4 * wave + qq] = ((u64)odd << 32) | even;
-    };
-    if (f4) {
-        // (not for the 'equal' variants nor the masked 'less' one: with two walks their register
-        // budget spills)
-        constexpr bool NN_OK = CC_NN_WALK && SIDES != 3 && !(HAS_MASK && SIDES == 2);
-        bool ordwalk = !NN_OK || !(p.pad & BP_NONNEG);
-        if constexpr (NN_OK) if (!ordwalk) {
-            f4walk(std::true_type{});
-            u32 wmx = mx;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) wmx = max(wmx, (u32)__shfl_xor(wmx, o, 64));
-            ordwalk = __builtin_amdgcn_readfirstlane(wmx) >= 0x80000000u;
-            if (ordwalk) {                    // a value below +0 in this wave's rows: walk them on ord values
-                mn = 0xFFFFFFFFu; mx = 0u; K1N = 0xFFFFFFFFu; K1X = 0u; K2N = 0xFFFFFFFFu; K2X = 0u;
-            } else {
-                mn += 0x80000000u;            // raw -> ord (raw < 2^31)
-                mx += 0x80000000u;
-            }
-        }
-        if (ordwalk) f4walk(std::false_type{});
     } else {
         for (int i = tid; i < NROWS; i += NTHREADS) L.rows[i] = 0;
         __syncthreads();

@@ -190,11 +190,10 @@ def test_speculated_interval_corrected(ctx, mode, thr, outlier):
 
 @pytest.mark.parametrize('mode', ['greater', 'less'])
 @pytest.mark.parametrize('value', [-0.0, -1e-30, -0.25])
-def test_nonneg_walk_fallback(ctx, mode, value):
-    """k_spec's raw-bit walk (blocks whose sample is non-negative, BP_NONNEG): a value with the
-    sign bit set (-0, a negative denormal, a negative number) off the sampled rows sends its wave
-    back to the ordered walk; statistics, bits and labels must stay exact (with and without a
-    mask, the masked 'greater' variant has the raw walk too)."""
+def test_sign_bit_values_off_sample(ctx, mode, value):
+    """Values with the sign bit set (-0, a negative denormal, a negative number) off the sampled
+    rows of otherwise non-negative data: the guessed interval and the block statistics must come
+    out exact (statistics in the IEEE total order, -0 < +0), with and without a mask."""
     rng = np.random.default_rng(11)
     inp = (rng.integers(0, 17, (64, 128, 192)) / np.float32(16)).astype(np.float32)
     inp[1, 1, 5] = value                  # off the sampled rows (z = 8 mod 16, y = 16 mod 32)
