@@ -25,6 +25,12 @@ static thread_local std::string g_err;
 
 #include "cc_host.hpp"
 
+// integer from the environment (A/B knobs), read per call
+static inline long env_int(const char* name, long dflt) {
+    const char* e = std::getenv(name);
+    return (e && *e) ? std::atol(e) : dflt;
+}
+
 // host time spent in device allocations (instrumentation of the cold, first-call cost: reported by
 // cc_get_profile as the pseudo-kernel "host_alloc" -- count = hipMalloc calls, ms = their time)
 static std::atomic<int64_t> g_alloc_count{0}, g_alloc_ns{0};
@@ -363,7 +369,8 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             sa.t0 = t0;
             const unsigned ng = (unsigned)(t1 - t0);
             launch(c, "k_spec", [&] {
-#define CC_SPEC_LAUNCH(M, S) k_spec<M, S><<<ng, NTHREADS, 0, s>>>(g, sa, in, mask, BITS, FACES, COUNT, P, KR)
+#define CC_SPEC_LAUNCH(M, S) k_spec<M, S><<<ng, NTHREADS, spad, s>>>(g, sa, in, mask, BITS, FACES, COUNT, P, KR)
+                const unsigned spad = (unsigned)env_int("CC_LDS_PAD_SPEC", 0);   // A/B only, as CC_LDS_PAD_P2
                 if (mask) {
                     if (mode == MODE_GREATER) CC_SPEC_LAUNCH(true, 1);
                     else if (mode == MODE_LESS) CC_SPEC_LAUNCH(true, 2);
@@ -639,8 +646,19 @@ static void phase_map(cc_ctx* c, const u64* pairs, int64_t n) {
     int m = 0;
     u64 id_max = 0;
     if (2 * n <= prims::SU_MAX) {
-        // a few thousand ids: one workgroup sorts and dedups them in LDS
-        launch(c, "seam_sort_small", [&] { prims::k_sort_unique_small<<<1, prims::SU_T, 0, s>>>(pairs, (int)(2 * n), ids, nsel); });
+        // a few thousand ids: the whole map (distinct ids, unions, representatives) in one
+        // workgroup in LDS
+        c->map_vals.ensure(2 * n * sizeof(u64));
+        launch(c, "k_seam_map_small", [&] {
+            prims::k_seam_map_small<<<1, prims::SU_T, 0, s>>>(pairs, (int)n, ids, c->map_vals.as<u64>(), nsel);
+        });
+        {
+            Readback rb(c, 64);
+            rb.add(&m, nsel, sizeof(int));
+            rb.wait();
+        }
+        st.n_map = m;
+        return;
     } else {
         unsigned long long* dmax = (unsigned long long*)c->scalars2.p + 1;
         HIP_OK(hipMemsetAsync(dmax, 0, sizeof(u64), s));
@@ -716,8 +734,10 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
         // (CC_PASS2_ORDER = 0 / 1 forces one, A/B only)
         int order = g.X >= 4096 ? 1 : 0;
         if (const char* e = std::getenv("CC_PASS2_ORDER"); e && *e) order = std::atoi(e) ? 1 : 0;
-        if (st.local_only) k_pass2<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, FIN, nullptr, nullptr, 0, 0, out, order);
-        else k_pass2<true><<<(unsigned)nt, NTHREADS, 0, s>>>(g, c->bits.as<u64>(), COUNT, KR, P, c->lut.as<u64>(), st.base, m, out, order);
+        // CC_LDS_PAD_P2 (A/B only): extra dynamic LDS per workgroup, i.e. fewer tiles per CU
+        const unsigned pad = (unsigned)env_int("CC_LDS_PAD_P2", 0);
+        if (st.local_only) k_pass2<false><<<(unsigned)nt, NTHREADS, pad, s>>>(g, c->bits.as<u64>(), COUNT, FIN, nullptr, nullptr, 0, 0, out, order);
+        else k_pass2<true><<<(unsigned)nt, NTHREADS, pad, s>>>(g, c->bits.as<u64>(), COUNT, KR, P, c->lut.as<u64>(), st.base, m, out, order);
     });
 
     u64 sc[4] = {0, 0, 0, 0};

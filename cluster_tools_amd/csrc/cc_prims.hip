@@ -315,19 +315,6 @@ __device__ __forceinline__ int su_unique(SortSmallLDS& L, const u64* k, int n, E
     return carry;
 }
 
-// sorted distinct values of in[0, n) (n <= SU_MAX) -> out, *nsel = their count
-__global__ __launch_bounds__(SU_T) void k_sort_unique_small(const u64* __restrict__ in, int n, u64* out, int* nsel) {
-    __shared__ SortSmallLDS L;
-    for (int i = threadIdx.x; i < n; i += SU_T) L.a[i] = in[i];
-    __syncthreads();
-    const u64 mx = su_max(L, n);
-    int bits = 0;
-    while (bits < 64 && (mx >> bits)) ++bits;
-    const u64* k = su_sort(L, n, bits);
-    const int m = su_unique(L, k, n, [&](int pos, u64 v) { out[pos] = v; });
-    if (threadIdx.x == 0) *nsel = m;
-}
-
 // sorted distinct (a, b) pairs of pa / pb [0, n) (n <= SU_MAX, every id < 2^nb) -> pairs
 // ([m][2], at most cap written; qa / qb, if given, get them too), *nsel = m
 __global__ __launch_bounds__(SU_T) void k_pairs_sort_unique_small(const u64* __restrict__ pa, const u64* __restrict__ pb,
@@ -344,6 +331,40 @@ __global__ __launch_bounds__(SU_T) void k_pairs_sort_unique_small(const u64* __r
         if (qa) { qa[pos] = a; qb[pos] = b; }
     });
     if (threadIdx.x == 0) *nsel = m;
+}
+
+// The seam map of cc_shard_finish in one workgroup (2 n <= SU_MAX ids; the multi-kernel form is
+// phase_map's: sort, unique, pairs -> indices, iota, unions, resolve, map = 7+ launches): U = the
+// sorted distinct ids of the n pairs, a union-find over indices into U in LDS (the smaller index
+// wins, so a component's root is its smallest id), V[i] = U[root(i)]; *m_out = |U|.
+__global__ __launch_bounds__(SU_T) void k_seam_map_small(const u64* __restrict__ pairs, int n, u64* U, u64* V,
+                                                         int* m_out) {
+    __shared__ SortSmallLDS L;
+    const int n2 = 2 * n, tid = threadIdx.x;
+    for (int i = tid; i < n2; i += SU_T) L.a[i] = pairs[i];
+    __syncthreads();
+    const u64 mx = su_max(L, n2);
+    int bits = 0;
+    while (bits < 64 && (mx >> bits)) ++bits;
+    u64* k = su_sort(L, n2, bits);
+    u64* ub = k == L.a ? L.b : L.a;                  // distinct ids; k's buffer becomes the parents
+    const int m = su_unique(L, k, n2, [&](int pos, u64 v) { ub[pos] = v; U[pos] = v; });
+    __syncthreads();
+    u32* par = reinterpret_cast<u32*>(k);
+    for (int i = tid; i < m; i += SU_T) par[i] = (u32)i;
+    __syncthreads();
+    auto index_of = [&](u64 v) -> u32 {              // v is in ub[0, m)
+        int lo = 0, hi = m - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (ub[mid] < v) lo = mid + 1; else hi = mid;
+        }
+        return (u32)lo;
+    };
+    for (int i = tid; i < n; i += SU_T) lunion(par, index_of(pairs[2 * i]), index_of(pairs[2 * i + 1]));
+    __syncthreads();
+    for (int i = tid; i < m; i += SU_T) V[i] = ub[lfind_ro(as_lds(par), (u32)i)];
+    if (tid == 0) *m_out = m;
 }
 
 // ---- host side: temporaries carved from one caller buffer (the context's cub_tmp) ----------
