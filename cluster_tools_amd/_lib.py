@@ -26,6 +26,7 @@ EXPORTS = (
     'cc_seam_pairs32', 'cc_shard_top_cubes32', 'cc_seam_pairs_cubes32',
     'cc_evaluate', 'cc_get_overlaps', 'cc_relabel_consecutive', 'cc_set_option', 'cc_channel_mean',
     'cc_gaussian_smooth_blocks', 'cc_gaussian_taps', 'cc_result_size', 'cc_resize_mask_nearest',
+    'cc_watershed_from_seeds',
 )
 # CC_DTYPE_* of include/cc_mi355x.h (cc_channel_mean)
 DTYPES = {'float32': 0, 'float64': 1, 'uint8': 2, 'int8': 3, 'uint16': 4, 'int16': 5, 'uint32': 6,
@@ -117,6 +118,7 @@ def load():
         'cc_gaussian_taps': (I, [ctypes.c_double, P, I]),
         'cc_result_size': (i64, []),
         'cc_resize_mask_nearest': (I, [P, P, P, P, i64, i64, P]),
+        'cc_watershed_from_seeds': (I, [P, P, P, P, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -355,6 +357,28 @@ class Context:
         _check(load().cc_threshold(self._h, _ptr(inp), _ptr(shape), _ptr(bs), float(threshold),
                                    mode_id(mode), _ptr(out)))
         return out
+
+    def watershed_from_seeds(self, inp, seeds, block_shape, mask=None, out=None):
+        """WatershedFromSeeds (watershed/watershed_from_seeds.py:143-273) on device: the seeds
+        (uint64 ids < 2^32 - 1, torch int64) grow over the per-block normalized float32 input,
+        6-connected inside each block; mask (uint8) -> input 1.0 / output 0 outside it.  out may
+        be `seeds` (in place).  Returns (labels, relaxation rounds).  See include/cc_mi355x.h for
+        the definition (the reference's vu.watershed does not exist: parity unpinned)."""
+        import torch
+        assert hasattr(inp, 'data_ptr') and inp.is_cuda and inp.dtype == torch.float32 and inp.is_contiguous()
+        assert seeds.is_cuda and seeds.element_size() == 8 and seeds.shape == inp.shape and seeds.is_contiguous()
+        if mask is not None:
+            assert mask.is_cuda and mask.dtype == torch.uint8 and mask.shape == inp.shape and mask.is_contiguous()
+        shape = _i64(inp.shape)
+        bs = _i64(block_shape)
+        assert len(shape) == 3 and len(bs) == 3
+        if out is None:
+            out = torch.empty(tuple(inp.shape), dtype=torch.int64, device=inp.device)
+        assert out.element_size() == 8 and out.shape == inp.shape and out.is_contiguous()
+        rounds = np.zeros(1, dtype=np.int64)
+        _check(load().cc_watershed_from_seeds(self._h, _ptr(inp), _ptr(seeds), _ptr(mask), _ptr(shape), _ptr(bs),
+                                              _ptr(out), _ptr(rounds)))
+        return out, int(rounds[0])
 
     def evaluate(self, seg, gt, block_shape, ignore_label=0):
         """EvaluationWorkflow (evaluation/evaluation_workflow.py:46-84) on device: overlaps per

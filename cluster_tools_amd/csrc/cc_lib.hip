@@ -101,7 +101,8 @@ struct cc_ctx {
         rl_wg,                                            // relabel: per-workgroup id lists
         gs1, gs2, gs_tab,                                 // Gaussian prefilter temporaries (cc_prefilter.hip)
         mask_xmap,                                        // resized masks (cc_mask.hip)
-        seam_hash;                                        // seam pair hash set (k_seam_pairs)
+        seam_hash,                                        // seam pair hash set (k_seam_pairs)
+        ws_tab, ws_buf;                                   // seeded watershed (cc_watershed.hip)
     int64_t ev_cap = 0;      // entries per evaluation hash table of the last cc_evaluate
     int64_t rl_cap = 0;      // id-set slots of the last cc_relabel_consecutive
     // last run
@@ -825,7 +826,7 @@ void cc_destroy(cc_ctx* c) {
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
                       &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec, &c->mark, &c->bflag,
                       &c->ev_main, &c->ev_z, &c->ev_seg, &c->ev_gt, &c->ev_flag, &c->ev_part, &c->rl_wg,
-                      &c->gs1, &c->gs2, &c->gs_tab, &c->mask_xmap, &c->seam_hash};
+                      &c->gs1, &c->gs2, &c->gs_tab, &c->mask_xmap, &c->seam_hash, &c->ws_tab, &c->ws_buf};
     for (DevBuf* b : bufs) b->release();
     c->pin.release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
@@ -1089,3 +1090,4 @@ int cc_get_profile(cc_ctx* c, char* names, int names_cap, int64_t* counts, doubl
 #include "cc_eval.hip"
 #include "cc_relabel.hip"
 #include "cc_prefilter.hip"
+#include "cc_watershed.hip"

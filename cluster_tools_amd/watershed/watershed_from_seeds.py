@@ -1,0 +1,128 @@
+#! /usr/bin/python
+"""WatershedFromSeeds task + job (reference: cluster_tools/watershed/watershed_from_seeds.py).
+
+Same task surface as the reference (:20-128): parameters input_path / input_key / seeds_path /
+seeds_key / output_path / output_key / mask_path / mask_key / dependency, the task config
+(channel_begin, channel_end, agglomerate_channels, size_filter), the uint64 output dataset with
+chunks block_shape // 2 clipped to the shape (gzip), and the job's block contract: per block of the
+blocking the seeds grow over the normalized input (_ws_block, :143-166), masked blocks without a
+mask voxel are skipped and the result is zeroed outside the mask (_ws_block_masked, :169-206).  The
+job's compute runs on the MI355X through cc_watershed_from_seeds, one GPU job for the volume.
+
+The reference's watershed call (`vu.watershed`) does not exist in its volume_utils; the watershed
+here is defined in include/cc_mi355x.h (minimax path cost from the seeds, smallest label among the
+optimal predecessors, 6-connected inside each block) -- parity unpinned.  Not supported (raise):
+4-D (channel) input, size_filter > 0.
+"""
+import json
+import os
+
+import numpy as np
+
+from cluster_tools_amd.luigi_compat import Task, Parameter, TaskParameter
+from cluster_tools_amd.cluster_tasks import LocalTask, DummyTask
+import cluster_tools_amd.utils.volume_utils as vu
+import cluster_tools_amd.utils.function_utils as fu
+
+
+class WatershedFromSeedsBase(Task):
+    task_name = 'watershed_from_seeds'
+    src_file = os.path.abspath(__file__)
+
+    input_path = Parameter()
+    input_key = Parameter()
+    seeds_path = Parameter()
+    seeds_key = Parameter()
+    output_path = Parameter()
+    output_key = Parameter()
+    mask_path = Parameter(default='')
+    mask_key = Parameter(default='')
+    dependency = TaskParameter(default=DummyTask())
+
+    def requires(self):
+        return self.dependency
+
+    @staticmethod
+    def default_task_config():
+        config = LocalTask.default_task_config()
+        config.update({'channel_begin': 0, 'channel_end': None,
+                       'agglomerate_channels': 'mean', 'size_filter': 0})
+        return config
+
+    def run_impl(self):
+        shebang, block_shape, roi_begin, roi_end = self.global_config_values()
+        self.init(shebang)
+        shape = vu.get_shape(self.input_path, self.input_key)
+        if len(shape) == 4:
+            raise NotImplementedError('WatershedFromSeeds on the MI355X takes 3-D input only')
+        config = self.get_task_config()
+        if config.get('size_filter', 0):
+            raise NotImplementedError('size_filter > 0 is not supported (the reference watershed is undefined)')
+        chunks = tuple(bs // 2 for bs in block_shape)
+        chunks = tuple(max(1, min(ch, sh)) for ch, sh in zip(chunks, shape))
+        with vu.file_reader(self.output_path) as f:
+            f.require_dataset(self.output_key, shape=shape, chunks=chunks, compression='gzip', dtype='uint64')
+        config.update({'input_path': self.input_path, 'input_key': self.input_key,
+                       'seeds_path': self.seeds_path, 'seeds_key': self.seeds_key,
+                       'output_path': self.output_path, 'output_key': self.output_key,
+                       'block_shape': block_shape})
+        if self.mask_path != '':
+            assert self.mask_key != ''
+            config.update({'mask_path': self.mask_path, 'mask_key': self.mask_key})
+        block_list = vu.blocks_in_volume(shape, block_shape, roi_begin, roi_end)
+        self._write_log('scheduling %i blocks to be processed' % len(block_list))
+        n_jobs = 1                     # one GPU job grows the whole volume
+        self.prepare_jobs(n_jobs, block_list, config)
+        self.submit_jobs(n_jobs)
+        self.wait_for_jobs()
+        self.check_jobs(n_jobs)
+
+
+class WatershedFromSeedsLocal(WatershedFromSeedsBase, LocalTask):
+    pass
+
+
+def watershed_from_seeds(job_id, config_path):
+    import torch
+    from cluster_tools_amd import _lib
+    from cluster_tools_amd.thresholded_components.block_components import _read, read_mask, device_mask
+    fu.log('start processing job %i' % job_id)
+    fu.log('reading config from %s' % config_path)
+    with open(config_path) as f:
+        config = json.load(f)
+    block_list = config['block_list']
+    block_shape = config['block_shape']
+    shape = list(vu.get_shape(config['input_path'], config['input_key']))
+    x = _read(config['input_path'], config['input_key'], dtype=np.float32)    # normalize's astype('float32')
+    seeds = _read(config['seeds_path'], config['seeds_key'], dtype=np.uint64)
+    mask, resized = read_mask(config, shape)
+    device = int(os.environ.get('CC_DEVICE', '0'))
+    dev = torch.device('cuda', device)
+    torch.cuda.set_device(dev)
+    with _lib.Context(device) as ctx:
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        md = device_mask(ctx, mask, resized, shape, dev)
+        sd = torch.from_numpy(seeds.view(np.int64)).to(dev)
+        out, rounds = ctx.watershed_from_seeds(torch.from_numpy(x).to(dev), sd, block_shape, md, out=sd)
+        out = out.cpu().numpy().view(np.uint64)
+        mh = None if md is None else md.cpu().numpy()
+    fu.log('watershed: %d relaxation rounds' % rounds)
+    blocking = vu.Blocking([0, 0, 0], shape, block_shape)
+    with vu.file_reader(config['output_path']) as f:
+        ds = f[config['output_key']]
+        for b in block_list:
+            bb = vu.block_to_bb(blocking.getBlock(b))
+            if mh is not None and not mh[bb].any():          # _ws_block_masked: nothing to do
+                fu.log_block_success(b)
+                continue
+            ds[bb] = out[bb]
+            fu.log_block_success(b)
+    fu.log_job_success(job_id)
+
+
+if __name__ == '__main__':
+    import sys
+    path = sys.argv[1]
+    assert os.path.exists(path), path
+    job_id = int(os.path.split(path)[1].split('.')[0].split('_')[-1])
+    watershed_from_seeds(job_id, path)

@@ -283,6 +283,21 @@ int64_t cc_get_overlaps(cc_ctx* ctx, uint64_t* seg_ids, uint64_t* gt_ids, uint64
 int cc_relabel_consecutive(cc_ctx* ctx, const uint64_t* labels_dev, uint64_t* out_dev, int64_t n,
                            uint64_t* n_unique, uint64_t* start_label, uint64_t* uniques_host, int64_t cap);
 
+/* Seeded watershed per block (watershed/watershed_from_seeds.py:143-273, the WatershedFromSeeds
+ * task of ThresholdAndWatershedWorkflow, thresholded_components_workflow.py:107-144): the seeds
+ * (uint64 ids < 2^32 - 1, 0 = none; e.g. the thresholded components) grow over the input
+ * normalized per block (volume_utils.py:98-105), 6-connected inside each block (no halo).  The
+ * reference calls vu.watershed, which its volume_utils does not define (parity unpinned):
+ * cost(v) = min over paths from a seed of the max normalized value on the path (seed excluded),
+ * label(v) = the smallest label among the neighbours an optimal path can come through
+ * (max(cost(u), f(v)) == cost(v)); 0 where no seed of the block reaches v.  mask_dev (optional,
+ * uint8, same shape): the input is 1.0 outside the mask and the output 0 there
+ * (_ws_block_masked).  out_dev may be seeds_dev (in place, as the workflow writes).  *rounds
+ * (optional): relaxation rounds run. */
+int cc_watershed_from_seeds(cc_ctx* ctx, const float* in_dev, const uint64_t* seeds_dev, const uint8_t* mask_dev,
+                            const int64_t shape[3], const int64_t block_shape[3], uint64_t* out_dev,
+                            int64_t* rounds);
+
 #ifdef __cplusplus
 }
 #endif
