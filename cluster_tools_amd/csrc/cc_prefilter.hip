@@ -143,6 +143,8 @@ struct NormP {                     // vu.normalize of one block: y = x - mn; if 
 };
 constexpr int GS_ZY_OUT = 64;      // outputs per z / y tile (x: 64 lanes)
 constexpr int GS_X_OUT = 256;      // outputs per x tile (one row per wave)
+constexpr int GS_U = 8;            // z / y lines loaded per wave before their LDS stores
+constexpr int GS_UX = 5;           // x: (256 + 2 r) / 64 <= 5 loads per lane for r <= 32
 
 __global__ void k_norm_params(int64_t nb, const u32* smin, const u32* smax, const u32* sflag, NormP* np) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -192,12 +194,22 @@ __global__ __launch_bounds__(256) void k_gauss_zy(const float* __restrict__ in, 
         static_assert(!NORM || AX == 0, "the first (normalizing) pass runs along z");
         P = np[((int64_t)S.blk * nby + o / by) * nbx + xs / bx];
     }
-    for (int p = wave; p < S.n + 2 * r; p += 4) {
-        const int64_t c = S.b0 + gs_reflect(S.a0 - S.b0 - r + p, S.w);
-        const int64_t idx = AX == 0 ? (c * Y + o) * X + xs : (o * Y + c) * X + xs;
-        float v = in[idx];
-        if (NORM) v = gs_norm(v, P);
-        gbuf[p * 64 + lane] = v;
+    // GS_U lines in flight per wave (one load at a time, each waited for before the LDS store,
+    // left the passes latency-bound at 2.7-4.2 TB/s)
+    const int np_ = S.n + 2 * r;
+    for (int p0 = wave; p0 < np_; p0 += 4 * GS_U) {
+        float v[GS_U];
+#pragma unroll
+        for (int u = 0; u < GS_U; ++u) {
+            const int p = p0 + 4 * u;
+            const int64_t c = S.b0 + gs_reflect(S.a0 - S.b0 - r + (p < np_ ? p : np_ - 1), S.w);
+            v[u] = in[AX == 0 ? (c * Y + o) * X + xs : (o * Y + c) * X + xs];
+        }
+#pragma unroll
+        for (int u = 0; u < GS_U; ++u) {
+            const int p = p0 + 4 * u;
+            if (p < np_) gbuf[p * 64 + lane] = NORM ? gs_norm(v[u], P) : v[u];
+        }
     }
     __syncthreads();
     if (!xin) return;
@@ -221,8 +233,20 @@ __global__ __launch_bounds__(256) void k_gauss_x(const float* __restrict__ in, f
     const bool ok = row < rows;                   // wave-uniform
     float* b = gbuf + wave * (GS_X_OUT + 2 * GS_RMAX);
     const float* src = in + (ok ? row : 0) * X;
-    if (ok)
-        for (int p = lane; p < S.n + 2 * r; p += 64) b[p] = src[S.b0 + gs_reflect(S.a0 - S.b0 - r + p, S.w)];
+    if (ok) {
+        const int np_ = S.n + 2 * r;
+        for (int p0 = lane; p0 < np_; p0 += 64 * GS_UX) {
+            float v[GS_UX];
+#pragma unroll
+            for (int u = 0; u < GS_UX; ++u) {
+                const int p = p0 + 64 * u;
+                v[u] = src[S.b0 + gs_reflect(S.a0 - S.b0 - r + (p < np_ ? p : np_ - 1), S.w)];
+            }
+#pragma unroll
+            for (int u = 0; u < GS_UX; ++u)
+                if (p0 + 64 * u < np_) b[p0 + 64 * u] = v[u];
+        }
+    }
     __syncthreads();
     if (!ok) return;
     for (int q = lane; q < S.n; q += 64) {
