@@ -110,6 +110,7 @@ struct cc_ctx {
     uint64_t n_labels = 0;
     std::vector<uint64_t> h_values, h_offsets;
     std::vector<int32_t> h_tab;
+    std::vector<int32_t> h_gs;   // Gaussian segment tables (cc_prefilter.hip AxSeg), alive until copied
     HostPin pin;             // small read-backs (see HostPin)
     bool lut_valid = false;
     // profiling

@@ -222,6 +222,62 @@ __global__ __launch_bounds__(256) void k_gauss_zy(const float* __restrict__ in, 
     }
 }
 
+// z (AX = 0) or y (AX = 1) lines without LDS: one wave per (segment, row o, 256 x-adjacent
+// columns), a lane owns 4 columns (float4) and walks its segment's outputs with the 2R + 1 taps'
+// window in registers (R <= GS_WIN_RMAX, X % 4 == 0); 8 outputs' new values are loaded before
+// they are used (8 float4 loads in flight per lane).  Same sums, same order as k_gauss_zy.
+constexpr int GS_WIN_RMAX = 8, GS_WIN_CH = 8;
+template <int AX, int R, bool NORM>
+__global__ __launch_bounds__(64) void k_gauss_win(const float* __restrict__ in, float* __restrict__ out, int64_t Y,
+                                                  int64_t X, int64_t by, int64_t bx, int nby, int nbx,
+                                                  const AxSeg* __restrict__ segs, int64_t other, int64_t nxc,
+                                                  const NormP* __restrict__ np, GaussTaps tp) {
+    const int lane = threadIdx.x;
+    const int64_t id = blockIdx.x;
+    const int64_t xc = id % nxc, rest = id / nxc;
+    const int64_t o = rest % other, sg = rest / other;
+    const AxSeg S = segs[sg];
+    const int64_t x = (xc * 64 + lane) * 4;
+    if (x >= X) return;
+    NormP P[4];
+    if (NORM) {
+        static_assert(!NORM || AX == 0, "the first (normalizing) pass runs along z");
+#pragma unroll
+        for (int c = 0; c < 4; ++c) P[c] = np[((int64_t)S.blk * nby + o / by) * nbx + (x + c) / bx];
+    }
+    auto at = [&](int p) -> float4 {                 // p-th value of the window sequence (reflected)
+        const int64_t cpos = S.b0 + gs_reflect(S.a0 - S.b0 - R + p, S.w);
+        float4 v = *reinterpret_cast<const float4*>(in + (AX == 0 ? (cpos * Y + o) * X + x : (o * Y + cpos) * X + x));
+        if (NORM) { v.x = gs_norm(v.x, P[0]); v.y = gs_norm(v.y, P[1]); v.z = gs_norm(v.z, P[2]); v.w = gs_norm(v.w, P[3]); }
+        return v;
+    };
+    float4 w[2 * R + 1];
+#pragma unroll
+    for (int j = 0; j < 2 * R; ++j) w[j] = at(j);
+    for (int q0 = 0; q0 < S.n; q0 += GS_WIN_CH) {
+        float4 nv[GS_WIN_CH];
+#pragma unroll
+        for (int u = 0; u < GS_WIN_CH; ++u) nv[u] = q0 + u < S.n ? at(q0 + u + 2 * R) : make_float4(0, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < GS_WIN_CH; ++u) {
+            if (q0 + u >= S.n) break;
+            w[2 * R] = nv[u];
+            float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int j = 0; j <= 2 * R; ++j) {
+#pragma clang fp contract(off)
+                const float k = tp.k[2 * R - j];
+                sum.x = sum.x + k * w[j].x; sum.y = sum.y + k * w[j].y;
+                sum.z = sum.z + k * w[j].z; sum.w = sum.w + k * w[j].w;
+            }
+            const int64_t c = S.a0 + q0 + u;
+            *reinterpret_cast<float4*>(out + (AX == 0 ? (c * Y + o) * X + x : (o * Y + c) * X + x)) = sum;
+#pragma unroll
+            for (int j = 0; j < 2 * R; ++j) w[j] = w[j + 1];
+        }
+    }
+}
+
 // x lines: one row per wave, GS_X_OUT outputs of one block segment per workgroup row
 __global__ __launch_bounds__(256) void k_gauss_x(const float* __restrict__ in, float* __restrict__ out, int64_t rows,
                                                  int64_t X, const AxSeg* __restrict__ segs, GaussTaps tp) {
@@ -257,6 +313,42 @@ __global__ __launch_bounds__(256) void k_gauss_x(const float* __restrict__ in, f
     }
 }
 
+// x lines with 16-B accesses (X and the x block a multiple of 4, 16-B aligned rows): the segment's
+// own values are one float4 per lane into LDS (the 2r reflected halo values scalar), each lane
+// computes 4 consecutive outputs and stores them as one float4.  Same sums, same order.
+__global__ __launch_bounds__(256) void k_gauss_x4(const float* __restrict__ in, float* __restrict__ out, int64_t rows,
+                                                  int64_t X, const AxSeg* __restrict__ segs, GaussTaps tp) {
+    extern __shared__ float gbuf[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = tp.r;
+    const AxSeg S = segs[blockIdx.y];
+    const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+    const bool ok = row < rows;                   // wave-uniform
+    float* b = gbuf + wave * (GS_X_OUT + 2 * GS_RMAX);
+    const float* src = in + (ok ? row : 0) * X;
+    if (ok) {
+        if (4 * lane < S.n) {
+            const float4 v = *reinterpret_cast<const float4*>(src + S.a0 + 4 * lane);
+            b[r + 4 * lane] = v.x; b[r + 4 * lane + 1] = v.y; b[r + 4 * lane + 2] = v.z; b[r + 4 * lane + 3] = v.w;
+        }
+        for (int h = lane; h < 2 * r; h += 64) {                      // halo: p in [0, r) and [n + r, n + 2r)
+            const int p = h < r ? h : S.n + h;
+            b[p] = src[S.b0 + gs_reflect(S.a0 - S.b0 - r + p, S.w)];
+        }
+    }
+    __syncthreads();
+    if (!ok || 4 * lane >= S.n) return;
+    float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* bq = b + 4 * lane;
+    for (int j = 0; j <= 2 * r; ++j) {
+#pragma clang fp contract(off)
+        const float k = tp.k[2 * r - j];
+        sum.x = sum.x + k * bq[j]; sum.y = sum.y + k * bq[j + 1];
+        sum.z = sum.z + k * bq[j + 2]; sum.w = sum.w + k * bq[j + 3];
+    }
+    *reinterpret_cast<float4*>(out + row * X + S.a0 + 4 * lane) = sum;
+}
+
 }  // namespace cc
 
 namespace cc {
@@ -281,6 +373,28 @@ static int gauss_taps(double sigma, GaussTaps& t) {
     for (int i = 2 * radius + 1; i <= 2 * GS_RMAX; ++i) t.k[i] = 0.0f;
     t.r = radius;
     return radius;
+}
+
+// the register-window z and y passes for taps radius R
+struct WinArgs {
+    const float* in; float* A; float* B;
+    int64_t Y, X, Z, by, bx;
+    int nby, nbx;
+    const AxSeg* sz; const AxSeg* sy;
+    int64_t gz, gy, nxc;
+    const NormP* np;
+};
+template <int R>
+static void gauss_win_passes(cc_ctx* c, const WinArgs& w, const GaussTaps& tp) {
+    hipStream_t s = cstream(c);
+    launch(c, "k_gauss_z", [&] {
+        k_gauss_win<0, R, true><<<(unsigned)w.gz, 64, 0, s>>>(w.in, w.A, w.Y, w.X, w.by, w.bx, w.nby, w.nbx, w.sz, w.Y,
+                                                              w.nxc, w.np, tp);
+    });
+    launch(c, "k_gauss_y", [&] {
+        k_gauss_win<1, R, false><<<(unsigned)w.gy, 64, 0, s>>>(w.A, w.B, w.Y, w.X, w.by, w.bx, w.nby, w.nbx, w.sy, w.Z,
+                                                               w.nxc, w.np, tp);
+    });
 }
 
 // tiles of `out_per` outputs inside each block segment of an axis of length n, blocks of bs
@@ -346,50 +460,75 @@ int cc_gaussian_smooth_blocks(cc_ctx* c, const float* in, const int64_t shape[3]
         HIP_OK(hipMemsetAsync(smin, 0xFF, nb * sizeof(u32), s));
         HIP_OK(hipMemsetAsync(smax, 0x00, 2 * nb * sizeof(u32), s));
         launch(c, "k_block_stats", [&] { k_block_stats<<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, smin, smax, sflag); });
+        // register-window z / y passes (k_gauss_win) when the taps fit and rows are 16-B aligned;
+        // else the LDS-staged k_gauss_zy
+        const bool win = r <= GS_WIN_RMAX && X % 4 == 0 && ((uintptr_t)in | (uintptr_t)out) % 16 == 0;
         std::vector<AxSeg> sz, sy, sx;
-        axis_segs(Z, block_shape[0], GS_ZY_OUT, sz);
-        axis_segs(Y, block_shape[1], GS_ZY_OUT, sy);
+        axis_segs(Z, block_shape[0], win ? 64 : GS_ZY_OUT, sz);
+        axis_segs(Y, block_shape[1], win ? 128 : GS_ZY_OUT, sy);
         axis_segs(X, block_shape[2], GS_X_OUT, sx);
         CC_REQUIRE(sx.size() < 65536, "too many x segments");
         const size_t nseg = sz.size() + sy.size() + sx.size();
         c->gs_tab.ensure(nseg * sizeof(AxSeg) + nb * sizeof(NormP));
         AxSeg* dseg = c->gs_tab.as<AxSeg>();
         NormP* np = (NormP*)(dseg + nseg);
-        std::vector<AxSeg> all(sz);
-        all.insert(all.end(), sy.begin(), sy.end());
-        all.insert(all.end(), sx.begin(), sx.end());
-        HIP_OK(hipMemcpyAsync(dseg, all.data(), nseg * sizeof(AxSeg), hipMemcpyHostToDevice, s));
+        static_assert(sizeof(AxSeg) % sizeof(int32_t) == 0, "AxSeg as int32 words");
+        c->h_gs.resize(nseg * sizeof(AxSeg) / sizeof(int32_t));    // kept alive until the stream has read it
+        {
+            char* h = reinterpret_cast<char*>(c->h_gs.data());
+            std::memcpy(h, sz.data(), sz.size() * sizeof(AxSeg));
+            std::memcpy(h + sz.size() * sizeof(AxSeg), sy.data(), sy.size() * sizeof(AxSeg));
+            std::memcpy(h + (sz.size() + sy.size()) * sizeof(AxSeg), sx.data(), sx.size() * sizeof(AxSeg));
+        }
+        HIP_OK(hipMemcpyAsync(dseg, c->h_gs.data(), nseg * sizeof(AxSeg), hipMemcpyHostToDevice, s));
         launch(c, "k_norm_params", [&] { k_norm_params<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, smin, smax, sflag, np); });
         c->gs1.ensure(n * sizeof(float));
         c->gs2.ensure(n * sizeof(float));
         float* A = c->gs1.as<float>();
         float* B = c->gs2.as<float>();
-        const int64_t nxt = (X + 63) / 64;
         const int nby = (int)g.nb[1], nbx = (int)g.nb[2];
-        const size_t lds_zy = (size_t)(GS_ZY_OUT + 2 * r) * 64 * sizeof(float);
-        {
-            const int64_t grid = (int64_t)sz.size() * Y * nxt;
-            CC_REQUIRE(grid < (1ll << 31), "volume too large for the z pass grid");
+        if (win) {
+            const int64_t nxc = (X / 4 + 63) / 64;
+            const int64_t gz = (int64_t)sz.size() * Y * nxc, gy = (int64_t)sy.size() * Z * nxc;
+            CC_REQUIRE(gz < (1ll << 31) && gy < (1ll << 31), "volume too large for the z / y pass grid");
+            const WinArgs wa{in, A, B, Y, X, Z, block_shape[1], block_shape[2], nby, nbx, dseg,
+                             dseg + sz.size(), gz, gy, nxc, np};
+            switch (r) {
+                case 1: gauss_win_passes<1>(c, wa, tp); break;
+                case 2: gauss_win_passes<2>(c, wa, tp); break;
+                case 3: gauss_win_passes<3>(c, wa, tp); break;
+                case 4: gauss_win_passes<4>(c, wa, tp); break;
+                case 5: gauss_win_passes<5>(c, wa, tp); break;
+                case 6: gauss_win_passes<6>(c, wa, tp); break;
+                case 7: gauss_win_passes<7>(c, wa, tp); break;
+                default: gauss_win_passes<8>(c, wa, tp); break;
+            }
+        } else {
+            const int64_t nxt = (X + 63) / 64;
+            const size_t lds_zy = (size_t)(GS_ZY_OUT + 2 * r) * 64 * sizeof(float);
+            const int64_t grid_z = (int64_t)sz.size() * Y * nxt, grid_y = (int64_t)sy.size() * Z * nxt;
+            CC_REQUIRE(grid_z < (1ll << 31) && grid_y < (1ll << 31), "volume too large for the z / y pass grid");
             launch(c, "k_gauss_z", [&] {
-                k_gauss_zy<0, true><<<(unsigned)grid, 256, lds_zy, s>>>(in, A, Z, Y, X, block_shape[1], block_shape[2],
-                                                                        nby, nbx, dseg, Y, nxt, np, tp);
+                k_gauss_zy<0, true><<<(unsigned)grid_z, 256, lds_zy, s>>>(in, A, Z, Y, X, block_shape[1], block_shape[2],
+                                                                          nby, nbx, dseg, Y, nxt, np, tp);
             });
-        }
-        {
-            const int64_t grid = (int64_t)sy.size() * Z * nxt;
-            CC_REQUIRE(grid < (1ll << 31), "volume too large for the y pass grid");
             launch(c, "k_gauss_y", [&] {
-                k_gauss_zy<1, false><<<(unsigned)grid, 256, lds_zy, s>>>(A, B, Z, Y, X, block_shape[1], block_shape[2],
-                                                                         nby, nbx, dseg + sz.size(), Z, nxt, np, tp);
+                k_gauss_zy<1, false><<<(unsigned)grid_y, 256, lds_zy, s>>>(A, B, Z, Y, X, block_shape[1], block_shape[2],
+                                                                           nby, nbx, dseg + sz.size(), Z, nxt, np, tp);
             });
         }
         {
             const int64_t rows = Z * Y, gx = (rows + 3) / 4;
             CC_REQUIRE(gx < (1ll << 31), "volume too large for the x pass grid");
             const size_t lds_x = (size_t)4 * (GS_X_OUT + 2 * GS_RMAX) * sizeof(float);
+            const bool x4 = X % 4 == 0 && block_shape[2] % 4 == 0 && ((uintptr_t)out % 16) == 0;
             launch(c, "k_gauss_x", [&] {
-                k_gauss_x<<<dim3((unsigned)gx, (unsigned)sx.size()), 256, lds_x, s>>>(B, out, rows, X,
-                                                                                   dseg + sz.size() + sy.size(), tp);
+                if (x4)
+                    k_gauss_x4<<<dim3((unsigned)gx, (unsigned)sx.size()), 256, lds_x, s>>>(B, out, rows, X,
+                                                                                        dseg + sz.size() + sy.size(), tp);
+                else
+                    k_gauss_x<<<dim3((unsigned)gx, (unsigned)sx.size()), 256, lds_x, s>>>(B, out, rows, X,
+                                                                                       dseg + sz.size() + sy.size(), tp);
             });
         }
         sync(c);

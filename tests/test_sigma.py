@@ -81,7 +81,12 @@ def test_gpu_matches_reference(ctx, name):
 @pytest.mark.parametrize('shape,bs,sigma', [((70, 140, 300), (32, 64, 128), 1.3),      # ragged blocks / tiles (last block lines > r)
                                             ((40, 64, 520), (40, 64, 520), 4.0),       # x segments > 256
                                             ((33, 65, 129), (11, 13, 43), 1.0),        # odd everything
-                                            ((24, 40, 70), (24, 40, 70), 7.5)])        # r = 23
+                                            ((24, 40, 70), (24, 40, 70), 7.5),         # r = 23
+                                            # register-window z / y passes (r <= 8, X % 4 == 0):
+                                            ((48, 100, 256), (20, 36, 128), 2.0),      # r = 6, ragged z / y blocks
+                                            ((33, 64, 132), (11, 32, 46), 0.7),        # r = 2, x blocks not a multiple of 4
+                                            ((70, 300, 64), (70, 300, 64), 2.6),       # r = 8, y segments of 128 + a ragged one
+                                            ((20, 30, 600), (20, 30, 300), 3.4)])      # float4 x pass: x segments 256 + 44, r = 10
 def test_gpu_smooth_vs_oracle(ctx, shape, bs, sigma):
     import torch
     x = O.boundary_map(shape, origin=(3, 5, 7), dither=True)
