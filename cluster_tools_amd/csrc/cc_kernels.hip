@@ -508,18 +508,6 @@ __global__ void k_block_params(int64_t nb, const u32* smin, const u32* smax, con
         : "+v"(lo), "+v"(hi)                                                                      \
         : "s"(blo), "s"(bhi), "i"(j))
 
-// the four ballots of one float4 plane into lane j of R[0..7] behind ONE set of wait states (the
-// SGPR hazard of CC_WRITELANE2 is counted from the last ballot; four pairs behind four s_nops
-// stalled the wave three times more)
-#define CC_WRITELANE8(R, b0, b1, b2, b3, j)                                                        \
-    asm("s_nop 3\n\tv_writelane_b32 %0, %8, %16\n\tv_writelane_b32 %1, %9, %16\n\t"                \
-        "v_writelane_b32 %2, %10, %16\n\tv_writelane_b32 %3, %11, %16\n\t"                           \
-        "v_writelane_b32 %4, %12, %16\n\tv_writelane_b32 %5, %13, %16\n\t"                           \
-        "v_writelane_b32 %6, %14, %16\n\tv_writelane_b32 %7, %15, %16"                                 \
-        : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]), "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]) \
-        : "s"((u32)(b0)), "s"((u32)((b0) >> 32)), "s"((u32)(b1)), "s"((u32)((b1) >> 32)),                \
-          "s"((u32)(b2)), "s"((u32)((b2) >> 32)), "s"((u32)(b3)), "s"((u32)((b3) >> 32)), "i"(j))
-
 // natural bit row (bit x <-> voxel x) -> split row (even voxels low, odd voxels high): the
 // inverse perfect shuffle, once per row after the (coalesced, lane = x) loads
 __device__ __forceinline__ u64 split_row(u64 x) {
@@ -753,15 +741,6 @@ __device__ __forceinline__ TileInfo uniform_ti(TileInfo ti) {
 // bounds miss the exact ones by about the extremes' sampling error, so a denser sample leaves
 // fewer tiles with a voxel in between; 1/512 left 8 % of the C3 tiles to k_fix)
 constexpr int SAMPLE_DZ = 4, SAMPLE_DY = 16;
-#ifndef CC_F4_SERIAL
-#define CC_F4_SERIAL 1
-#endif
-#ifndef CC_F4_PREFETCH
-#define CC_F4_PREFETCH 0
-#endif
-#ifndef CC_WL_BATCH
-#define CC_WL_BATCH 0
-#endif
 
 __device__ __forceinline__ void block_extent(const Geom& g, int64_t b, int e0[3], int el[3]) {
     const int bi[3] = {(int)(b / ((int64_t)g.nb[2] * g.nb[1])), (int)((b / g.nb[2]) % g.nb[1]), (int)(b % g.nb[2])};
@@ -971,34 +950,11 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
             bool fg[4];
             quad(v, mk, fg);
             const u64 b0 = __ballot(fg[0]), b1 = __ballot(fg[1]), b2 = __ballot(fg[2]), b3 = __ballot(fg[3]);
-#if CC_WL_BATCH
-            CC_WRITELANE8(R, b0, b1, b2, b3, z);
-#else
             CC_WRITELANE2(R[0], R[1], (u32)b0, (u32)(b0 >> 32), z);
             CC_WRITELANE2(R[2], R[3], (u32)b1, (u32)(b1 >> 32), z);
             CC_WRITELANE2(R[4], R[5], (u32)b2, (u32)(b2 >> 32), z);
             CC_WRITELANE2(R[6], R[7], (u32)b3, (u32)(b3 >> 32), z);
-#endif
         };
-#if CC_F4_PREFETCH
-        // two loads in flight per wave: plane z + 1 is issued before plane z is processed
-        float4 cur = *reinterpret_cast<const float4*>(pz);
-        uchar4 cmk = HAS_MASK ? *reinterpret_cast<const uchar4*>(mz) : uchar4{};
-#pragma unroll
-        for (int z = 0; z < TZ; ++z) {
-            float4 nxt = cur;
-            uchar4 nmk = cmk;
-            if (z + 1 < TZ) {
-                asm volatile("" ::: "memory");
-                nxt = *reinterpret_cast<const float4*>(pz + (z + 1) * sz);
-                if (HAS_MASK) nmk = *reinterpret_cast<const uchar4*>(mz + (z + 1) * sz);
-            }
-            plane_bits(z, cur, cmk);
-            cur = nxt;
-            cmk = nmk;
-        }
-        if (false)
-#endif
 #pragma unroll
         for (int z0 = 0; z0 < TZ; z0 += RZ4) {
             float4 v[RZ4];
@@ -1007,17 +963,13 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
                 v[a] = *reinterpret_cast<const float4*>(pz + (z0 + a) * sz);
                 if (HAS_MASK) mk[a] = *reinterpret_cast<const uchar4*>(mz + (z0 + a) * sz);
             };
-            if (!CC_F4_SERIAL)
-#pragma unroll
-                for (int a = 0; a < RZ4; ++a) ld(a);
 #pragma unroll
             for (int a = 0; a < RZ4; ++a) {
-                if (CC_F4_SERIAL) {
-                    // each load issued right before its use, one in flight per wave (an empty asm
-                    // with a memory clobber keeps the next load below the previous processing)
-                    asm volatile("" ::: "memory");
-                    ld(a);
-                }
+                // each load issued right before its use, one in flight per wave (an empty asm
+                // with a memory clobber keeps the next load below the previous processing; two or
+                // four in flight measured slower)
+                asm volatile("" ::: "memory");
+                ld(a);
                 plane_bits(z0 + a, v[a], HAS_MASK ? mk[a] : uchar4{});
             }
         }
