@@ -140,9 +140,12 @@ __global__ __launch_bounds__(256) void k_ev_overlaps(const u64* __restrict__ seg
             }
             u64 key = EV_EMPTY;
             if (valid && !(use_ignore && g == ignore)) {
-                key = s == 0 ? (EV_ZTAG | (bid << 32) | g) : ((s << 32) | g);
+                // ids beyond the packing make no key (a seg id >= 2^31 would carry EV_ZTAG and a
+                // garbage block index into k_ev_fold): the call reports them and the caller
+                // relabels (Context.evaluate)
                 if (s >> 31) err |= EV_ERR_SEG;
                 if (g >= 0xFFFFFFFFull) err |= EV_ERR_GT;
+                if (!(s >> 31) && g < 0xFFFFFFFFull) key = s == 0 ? (EV_ZTAG | (bid << 32) | g) : ((s << 32) | g);
             }
             const u64 prev = (u64)__shfl_up((unsigned long long)key, 1);
             const bool head = lane == 0 || key != prev;

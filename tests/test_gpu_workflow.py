@@ -241,7 +241,7 @@ def test_integration_binding_runs_as_documented():
     assert max_id == int(d['max_id'])
     # the Threshold / evaluation blocks extend the same module namespace
     for b in integration_blocks():
-        if 'def threshold_volume' in b or 'def measures_on_device' in b:
+        if 'def threshold_volume' in b or 'def measures_on_device' in b or 'def watershed_from_seeds' in b:
             exec(compile(b, 'INTEGRATION.md', 'exec'), ns)
     L = ns['_L']
     ctx = ctypes.c_void_p()
@@ -258,6 +258,15 @@ def test_integration_binding_runs_as_documented():
         torch.cuda.synchronize()
         m = ns['measures_on_device'](ctx, seg.data_ptr(), seg.data_ptr(), seg.shape, meta['block_shape'])
         assert abs(m['rand-index'] - 1.0) < 1e-12 and abs(m['vi-split']) < 1e-12 and abs(m['vi-merge']) < 1e-12
+        # the watershed block: the labels as seeds, grown over the input (oracle/watershed.py)
+        from oracle import watershed as W
+        ws = torch.empty_like(seg)
+        mk = torch.from_numpy((d['mask'] != 0).astype(np.uint8)).cuda()
+        torch.cuda.synchronize()
+        ns['watershed_from_seeds'](ctx, x.data_ptr(), seg.data_ptr(), mk.data_ptr(), x.shape, meta['block_shape'],
+                                   ws.data_ptr())
+        want = W.watershed_from_seeds(d['input'], out, meta['block_shape'], (d['mask'] != 0).astype(np.uint8))
+        np.testing.assert_array_equal(ws.cpu().numpy().view(np.uint64), want)
     finally:
         L.cc_destroy(ctx)
 
