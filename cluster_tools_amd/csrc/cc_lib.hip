@@ -270,6 +270,7 @@ struct RunState {
     int stage = 0;             // 1 local done, 2 rid done, 3 final done
     bool rid0 = false;         // k_emit_roots already wrote the roots' ids for base 0
     bool sum_known = false;    // sum_v already read back (phase_local's fast path)
+    bool any_iovf = true;      // some tile's block-face pair list overflowed (or not read back)
 };
 
 static RunState& state(cc_ctx* c) {
@@ -450,25 +451,32 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             k_block_uf<<<(unsigned)nb, SB_THREADS, 0, s>>>(g, COUNT, c->pairsl.as<u64>(), c->pc.as<u32>(), P, KR, big, RL, RCB);
         });
     }
-    const unsigned stitch_grid = (unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, 2048);
-    launch(c, "k_stitch_intra", [&] { k_stitch<false><<<stitch_grid, SP_WAVES * 64, 0, s>>>(g, FACES, P, KR, big, nullptr); });
-
-    // one mid-run host read: whether any block took the fallback, and the number of roots (it
-    // sizes the root arrays / LUT)
+    // one mid-run host read: whether any block took the fallback, the number of roots (it sizes
+    // the root arrays / LUT) and whether any tile's block-face pair list overflowed (iovf[nt]: the
+    // block-face fallback k_stitch<true> is launched only then)
     u8 any_big = 1;
     u64 nr_blocks = 0;
+    st.any_iovf = true;
     if (block_uf) {
         launch(c, "k_block_scan", [&] { k_block_scan<<<1, SB_THREADS, 0, s>>>(nb, RCB, ROFFB, values, offsets, big, scalars); });
         u64 sc[4] = {0, 0, 0, 1};
+        u8 ovf = 1;
         Readback rb(c, 64);
         rb.add(sc, scalars, 4 * sizeof(u64));             // sum of values, -, roots, "any block big" (k_block_scan)
+        rb.add(&ovf, c->iovf.as<u8>() + nt, 1);
         rb.wait();
         nr_blocks = sc[2];
         any_big = sc[3] ? 1 : 0;
+        st.any_iovf = ovf != 0;
         if (!any_big) {                                   // the slab's sum of block values (cc_shard_begin)
             st.sum_v = sc[0];
             st.sum_known = true;
         }
+    }
+    // intra-block fallback (blocks the LDS union-find could not take): only when some block needs it
+    if (any_big) {
+        const unsigned stitch_grid = (unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, 2048);
+        launch(c, "k_stitch_intra", [&] { k_stitch<false><<<stitch_grid, SP_WAVES * 64, 0, s>>>(g, FACES, P, KR, big, nullptr); });
     }
     if (!any_big) {
         const int64_t nr = (int64_t)nr_blocks;
@@ -568,7 +576,7 @@ static void phase_rid(cc_ctx* c, uint64_t base) {
         });
         // tiles whose block-face pairs overflowed their list (and every tile under CC_DEBUG_GLOBAL_STITCH)
         const unsigned stitch_grid = (unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, 2048);
-        launch(c, "k_stitch_inter", [&] { k_stitch<true><<<stitch_grid, SP_WAVES * 64, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), c->big.as<u8>(), c->iovf.as<u8>()); });
+        if (st.any_iovf) launch(c, "k_stitch_inter", [&] { k_stitch<true><<<stitch_grid, SP_WAVES * 64, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), c->big.as<u8>(), c->iovf.as<u8>()); });
     }
     st.n_map = 0;
     st.stage = 2;

@@ -274,6 +274,31 @@ def test_white_noise_large_block(ctx):
     _check_against_oracle(ctx, inp, (32, 96, 128), 0.3, 'less')
 
 
+@pytest.mark.parametrize('kind', ['inter_overflow', 'block_lcap_overflow', 'both'])
+def test_fallback_paths_structured(ctx, kind):
+    """Patterns that overflow the LDS lists by construction, so the launch-only-when-flagged
+    fallbacks (k_stitch<false> when a block exceeds the LDS union-find, k_stitch<true> when a
+    tile's block-face pair list overflows) run next to the LDS paths of other blocks / tiles:
+      inter_overflow: 2-voxel columns on a 2-lattice across each z block face (512 distinct
+        6-connected pairs per tile face > 256 slots);
+      block_lcap_overflow: isolated voxels on a 2-lattice in the first block only (16 k
+        components > 8 k LDS slots), ordinary data elsewhere."""
+    shape, bs = (64, 128, 256), (16, 64, 128)
+    base = O.boundary_map(shape, origin=(1, 2, 3))
+    inp = np.ones(shape, dtype=np.float32)
+    z, y, x = np.meshgrid(np.arange(shape[0]), np.arange(shape[1]), np.arange(shape[2]), indexing='ij')
+    lat = (y % 2 == 0) & (x % 2 == 0)
+    if kind in ('inter_overflow', 'both'):
+        face = (z % bs[0] == 0) | (z % bs[0] == bs[0] - 1)        # the two voxel planes at each z block face
+        inp[face & lat] = 0.0
+    if kind in ('block_lcap_overflow', 'both'):
+        first = (z < bs[0]) & (y < bs[1]) & (x < bs[2])
+        inp[first] = 1.0
+        inp[first & lat & (z % 2 == 0)] = 0.0
+        inp[~first & (z >= 2 * bs[0])] = base[~first & (z >= 2 * bs[0])]
+    _check_against_oracle(ctx, inp, bs, 0.5, 'less')
+
+
 def _full_size_vs_oracle(ctx, shape, bs, mode, masked=False, dither=False):
     """The fused path on the device against the C oracle on the same synthetic volume, at a
     BASELINE size: raw uint64 labels compared on the device, block values / offsets / n_labels /

@@ -62,6 +62,31 @@ def test_two_ranks_one_gpu_gloo(tmp_path, mode, block_shape):
         assert int(np.load(str(tmp_path / ('nl_%d.npy' % k)))[0]) == ref['n_labels']
 
 
+def test_one_rank_rccl(tmp_path):
+    """The production communicator (TorchComm over backend 'nccl' = RCCL, GPU tensors, device_id
+    bound at init) through the whole ShardedLabeler schedule with one rank: the collectives
+    (all_gather of counts and pairs) run on RCCL; the result equals the oracle's labelling."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    shape, block_shape = (48, 150, 200), (16, 64, 64)
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '1',
+           '--master-addr', '127.0.0.1', '--master-port', str(port),
+           os.path.join(root, 'tests', '_sharded_worker.py'), str(tmp_path), 'greater',
+           ','.join(map(str, shape)), ','.join(map(str, block_shape)), 'nccl']
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    got = np.load(str(tmp_path / 'slab_0.npy')).astype(np.uint64)
+    ref = O.label_volume(O.boundary_map(shape, n_threads=1), block_shape, 0.5, 'greater')
+    np.testing.assert_array_equal(got, ref['labels'])
+    assert int(np.load(str(tmp_path / 'nl_0.npy'))[0]) == ref['n_labels']
+
+
 @pytest.mark.parametrize('mode,masked,form', [('less', True, None), ('greater', False, None),
                                               ('greater', True, 'voxel32')])
 def test_sharded_c4_scale_vs_oracle(mode, masked, form):
