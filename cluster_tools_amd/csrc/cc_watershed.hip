@@ -17,8 +17,9 @@
 //              seed reaches v (a block without seeds) and outside the mask.
 // Both fixpoints are unique (min over a fixed, monotone system), so any update order reaches
 // them: here tiles of 8 x 8 x 32 voxels (inside one block) relax in LDS to their local fixpoint
-// given the halo, rounds of launches over the tiles whose neighbours changed until none changes
-// (phase 1: costs; phase 2: labels on the converged costs).
+// given the halo (voxel-by-voxel sweeps), rounds of launches over the tiles whose neighbours
+// changed until none changes (phase 1: costs; phase 2: labels on the converged costs).  Every
+// round after a phase's first visits only the tiles the previous round listed.
 namespace cc {
 
 constexpr int WS_Z = 8, WS_Y = 8, WS_X = 32, WS_T = 256;
@@ -60,10 +61,12 @@ template <int PHASE>
 __global__ __launch_bounds__(WS_T) void k_ws_relax(WsGeom g, const float* __restrict__ in, const u8* __restrict__ mask,
                                                    const u32* __restrict__ smin, const u32* __restrict__ smax,
                                                    const u32* __restrict__ sflag, u32* cost, u32* lab,
-                                                   const u8* __restrict__ act_in, u8* act_out, u32* any) {
-    __shared__ u32 C[WS_HN], L[WS_HN], F[WS_Z * WS_Y * WS_X];
-    const int64_t t = blockIdx.x;
-    if (!act_in[t]) return;
+                                                   const u32* __restrict__ list_in, u32* stamp, u32 round,
+                                                   u32* list_out, u32* n_out) {
+    __shared__ u32 C[WS_HN], F[WS_Z * WS_Y * WS_X];
+    __shared__ u32 Lsh[PHASE == 2 ? WS_HN : 1];
+    // the round's tiles: all (list_in NULL, the first round of a phase) or the listed ones
+    const int64_t t = list_in ? (int64_t)list_in[blockIdx.x] : (int64_t)blockIdx.x;
     const int tid = threadIdx.x;
     const u32 tt = (u32)t, n2 = (u32)g.nt[2], n1 = (u32)g.nt[1];
     const u32 q = tt / n2;
@@ -92,10 +95,10 @@ __global__ __launch_bounds__(WS_T) void k_ws_relax(WsGeom g, const float* __rest
         if (inside_tile || halo) {
             const int64_t o = z * YX + y * g.S[2] + x;
             c = cost[o];
-            l = lab[o];
+            if (PHASE == 2) l = lab[o];
         }
         C[i] = c;
-        L[i] = l;
+        if (PHASE == 2) Lsh[i] = l;
     }
     for (int j = tid; j < WS_Z * WS_Y * WS_X; j += WS_T) {
         const int vz = j / (WS_Y * WS_X), vy = (j / WS_X) % WS_Y, vx = j % WS_X;
@@ -109,6 +112,7 @@ __global__ __launch_bounds__(WS_T) void k_ws_relax(WsGeom g, const float* __rest
     __syncthreads();
     constexpr int DZ = WS_HY * WS_HX, DY = WS_HX;
     bool tile_changed = false;
+    // voxel-by-voxel (Gauss-Seidel) sweeps: each voxel against its six neighbours
     for (;;) {
         bool chg = false;
 #pragma unroll
@@ -128,12 +132,12 @@ __global__ __launch_bounds__(WS_T) void k_ws_relax(WsGeom g, const float* __rest
             } else {
                 if (c == WS_INF) continue;
                 const int off[6] = {-DZ, DZ, -DY, DY, -1, 1};
-                u32 l = L[h];
+                u32 l = Lsh[h];
                 const u32 l0 = l;
 #pragma unroll
                 for (int d = 0; d < 6; ++d)
-                    if (nb[d] != WS_INF && max(nb[d], f) == c) l = min(l, L[h + off[d]]);
-                if (l < l0) { L[h] = l; chg = true; }
+                    if (nb[d] != WS_INF && max(nb[d], f) == c) l = min(l, Lsh[h + off[d]]);
+                if (l < l0) { Lsh[h] = l; chg = true; }
             }
         }
         if (!__syncthreads_or(chg)) break;
@@ -145,17 +149,23 @@ __global__ __launch_bounds__(WS_T) void k_ws_relax(WsGeom g, const float* __rest
         if (vz >= lz || vy >= ly || vx >= lx) continue;
         const int h = ((vz + 1) * WS_HY + vy + 1) * WS_HX + vx + 1;
         const int64_t o = (int64_t)(z0 + vz) * YX + (int64_t)(y0 + vy) * g.S[2] + (x0 + vx);
-        if (PHASE == 1) cost[o] = C[h]; else lab[o] = L[h];
+        if (PHASE == 1) cost[o] = C[h]; else lab[o] = Lsh[h];
     }
-    if (tid == 0) {
-        // the six neighbour tiles of the same block see a new halo
-        if (iz > 0 && g.tblk[0][iz - 1] == bz) act_out[t - (int64_t)n1 * n2] = 1;
-        if (iz + 1 < g.nt[0] && g.tblk[0][iz + 1] == bz) act_out[t + (int64_t)n1 * n2] = 1;
-        if (iy > 0 && g.tblk[1][iy - 1] == by) act_out[t - n2] = 1;
-        if (iy + 1 < g.nt[1] && g.tblk[1][iy + 1] == by) act_out[t + n2] = 1;
-        if (ix > 0 && g.tblk[2][ix - 1] == bx) act_out[t - 1] = 1;
-        if (ix + 1 < g.nt[2] && g.tblk[2][ix + 1] == bx) act_out[t + 1] = 1;
-        atomicOr(any, 1u);
+    if (tid < 6) {
+        // the six neighbour tiles of the same block see a new halo: each goes on the next round's
+        // list once (stamp = the round that listed it)
+        const int64_t zs = (int64_t)n1 * n2;
+        bool ok = false;
+        int64_t u = 0;
+        switch (tid) {
+            case 0: ok = iz > 0 && g.tblk[0][iz - 1] == bz; u = t - zs; break;
+            case 1: ok = iz + 1 < g.nt[0] && g.tblk[0][iz + 1] == bz; u = t + zs; break;
+            case 2: ok = iy > 0 && g.tblk[1][iy - 1] == by; u = t - n2; break;
+            case 3: ok = iy + 1 < g.nt[1] && g.tblk[1][iy + 1] == by; u = t + n2; break;
+            case 4: ok = ix > 0 && g.tblk[2][ix - 1] == bx; u = t - 1; break;
+            default: ok = ix + 1 < g.nt[2] && g.tblk[2][ix + 1] == bx; u = t + 1; break;
+        }
+        if (ok && atomicExch(&stamp[u], round) != round) list_out[atomicAdd(n_out, 1u)] = (u32)u;
     }
 }
 
@@ -226,28 +236,35 @@ extern "C" int cc_watershed_from_seeds(cc_ctx* c, const float* in, const uint64_
                 g.tblk[a] = p; p += g.nt[a];
             }
         }
-        // state: cost | label per voxel, two activity maps, flags
-        c->ws_buf.ensure((size_t)n * 2 * sizeof(u32) + 2 * (size_t)nt + 64);
+        // state: cost | label per voxel; per tile the round that last listed it, two tile lists
+        c->ws_buf.ensure((size_t)n * 2 * sizeof(u32) + 3 * (size_t)nt * sizeof(u32) + 64);
         u32* cost = c->ws_buf.as<u32>();
         u32* lab = cost + n;
-        u8* act0 = (u8*)(lab + n);
-        u8* act1 = act0 + nt;
+        u32* stamp = lab + n;
+        u32* list0 = stamp + nt;
+        u32* list1 = list0 + nt;
         c->counter.ensure(4 * sizeof(u32));
-        u32* flags = c->counter.as<u32>();            // [0] seed id overflow, [1] any tile changed
+        u32* flags = c->counter.as<u32>();            // [0] seed id overflow, [1] tiles listed for the next round
         HIP_OK(hipMemsetAsync(flags, 0, 4 * sizeof(u32), s));
+        HIP_OK(hipMemsetAsync(stamp, 0, nt * sizeof(u32), s));
         launch(c, "k_ws_init", [&] { k_ws_init<<<grid_stride(n), 256, 0, s>>>(n, seeds, cost, lab, flags); });
         int64_t total_rounds = 0;
+        u32 round = 0;
         for (int phase = 1; phase <= 2; ++phase) {
-            HIP_OK(hipMemsetAsync(act0, 1, nt, s));
-            for (int64_t r = 0;; ++r) {
+            // the first round of a phase visits every tile, later rounds the tiles listed by the last
+            const u32* lin = nullptr;
+            int64_t ntile = nt;
+            for (int64_t r = 0; ntile > 0; ++r) {
                 CC_REQUIRE(r < 4 * n + 16, "watershed did not converge");
-                HIP_OK(hipMemsetAsync(act1, 0, nt, s));
+                ++round;
                 HIP_OK(hipMemsetAsync(flags + 1, 0, sizeof(u32), s));
                 launch(c, phase == 1 ? "k_ws_relax_cost" : "k_ws_relax_label", [&] {
                     if (phase == 1)
-                        k_ws_relax<1><<<(unsigned)nt, WS_T, 0, s>>>(g, in, mask, smin, smax, sflag, cost, lab, act0, act1, flags + 1);
+                        k_ws_relax<1><<<(unsigned)ntile, WS_T, 0, s>>>(g, in, mask, smin, smax, sflag, cost, lab, lin, stamp,
+                                                                      round, list1, flags + 1);
                     else
-                        k_ws_relax<2><<<(unsigned)nt, WS_T, 0, s>>>(g, in, mask, smin, smax, sflag, cost, lab, act0, act1, flags + 1);
+                        k_ws_relax<2><<<(unsigned)ntile, WS_T, 0, s>>>(g, in, mask, smin, smax, sflag, cost, lab, lin, stamp,
+                                                                      round, list1, flags + 1);
                 });
                 u32 fl[2] = {0, 0};
                 {
@@ -257,8 +274,10 @@ extern "C" int cc_watershed_from_seeds(cc_ctx* c, const float* in, const uint64_
                 }
                 CC_REQUIRE(!(fl[0] & 1u), "seed ids must be < 2^32 - 1 (the reference casts seeds to uint32)");
                 ++total_rounds;
-                std::swap(act0, act1);
-                if (!fl[1]) break;
+                CC_REQUIRE(fl[1] <= (u32)nt, "watershed tile list overflow");
+                std::swap(list0, list1);
+                lin = list0;
+                ntile = fl[1];
             }
         }
         launch(c, "k_ws_write", [&] { k_ws_write<<<grid_stride(n), 256, 0, s>>>(n, lab, mask, out); });
