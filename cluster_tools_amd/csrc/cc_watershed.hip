@@ -56,116 +56,200 @@ __global__ void k_ws_init(int64_t n, const u64* __restrict__ seeds, u32* cost, u
     }
 }
 
-// one round over the active tiles; PHASE 1 relaxes costs, PHASE 2 labels
-template <int PHASE>
-__global__ __launch_bounds__(WS_T) void k_ws_relax(WsGeom g, const float* __restrict__ in, const u8* __restrict__ mask,
-                                                   const u32* __restrict__ smin, const u32* __restrict__ smax,
-                                                   const u32* __restrict__ sflag, u32* cost, u32* lab,
-                                                   const u32* __restrict__ list_in, u32* stamp, u32 round,
-                                                   u32* list_out, u32* n_out) {
-    __shared__ u32 C[WS_HN], F[WS_Z * WS_Y * WS_X];
-    __shared__ u32 Lsh[PHASE == 2 ? WS_HN : 1];
-    // the round's tiles: all (list_in NULL, the first round of a phase) or the listed ones
-    const int64_t t = list_in ? (int64_t)list_in[blockIdx.x] : (int64_t)blockIdx.x;
-    const int tid = threadIdx.x;
+// a watershed tile: position, extent, block and the block's extent (neighbours outside the block
+// are not neighbours: blocks are independent)
+struct WsTile {
+    int ix, iy, iz, z0, y0, x0, lz, ly, lx, bz, by, bx;
+    int64_t b, e0[3], e1[3];
+};
+
+__device__ __forceinline__ WsTile ws_tile(const WsGeom& g, int64_t t) {
+    WsTile w;
     const u32 tt = (u32)t, n2 = (u32)g.nt[2], n1 = (u32)g.nt[1];
     const u32 q = tt / n2;
-    const int ix = (int)(tt - q * n2), iy = (int)(q % n1), iz = (int)(q / n1);
-    const int z0 = g.tstart[0][iz], y0 = g.tstart[1][iy], x0 = g.tstart[2][ix];
-    const int lz = g.tlen[0][iz], ly = g.tlen[1][iy], lx = g.tlen[2][ix];
-    const int bz = g.tblk[0][iz], by = g.tblk[1][iy], bx = g.tblk[2][ix];
-    const int64_t b = ((int64_t)bz * g.nb[1] + by) * g.nb[2] + bx;
-    // the block's extent: neighbours outside it are not neighbours (blocks are independent)
-    const int64_t e0[3] = {bz * g.B[0], by * g.B[1], bx * g.B[2]};
-    int64_t e1[3];
+    w.ix = (int)(tt - q * n2); w.iy = (int)(q % n1); w.iz = (int)(q / n1);
+    w.z0 = g.tstart[0][w.iz]; w.y0 = g.tstart[1][w.iy]; w.x0 = g.tstart[2][w.ix];
+    w.lz = g.tlen[0][w.iz]; w.ly = g.tlen[1][w.iy]; w.lx = g.tlen[2][w.ix];
+    w.bz = g.tblk[0][w.iz]; w.by = g.tblk[1][w.iy]; w.bx = g.tblk[2][w.ix];
+    w.b = ((int64_t)w.bz * g.nb[1] + w.by) * g.nb[2] + w.bx;
+    w.e0[0] = w.bz * g.B[0]; w.e0[1] = w.by * g.B[1]; w.e0[2] = w.bx * g.B[2];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) e1[a] = e0[a] + g.B[a] < g.S[a] ? e0[a] + g.B[a] : g.S[a];
-    // normalize parameters of the block (as block_param: numpy's min / max(x - min), NaN blocks)
-    const u32 omn = smin[b], omx = smax[b];
-    const bool nan = sflag[b] & 1u;
-    const float mn = __uint_as_float(ord2f(omn)), mxv = __uint_as_float(ord2f(omx));
-    const float m = (isinf(mn) || isinf(mxv)) ? (isinf(mn) ? __uint_as_float(0x7FC00000u) : mxv - mn) : mxv - mn;
+    for (int a = 0; a < 3; ++a) w.e1[a] = w.e0[a] + g.B[a] < g.S[a] ? w.e0[a] + g.B[a] : g.S[a];
+    return w;
+}
+
+// the tile's state with its halo into LDS (WS_INF outside the block)
+__device__ __forceinline__ void ws_load_halo(const WsGeom& g, const WsTile& w, const u32* __restrict__ src, u32* H) {
     const int64_t YX = g.S[1] * g.S[2];
-    for (int i = tid; i < WS_HN; i += WS_T) {
+    for (int i = threadIdx.x; i < WS_HN; i += WS_T) {
         const int hz = i / (WS_HY * WS_HX), hy = (i / WS_HX) % WS_HY, hx = i % WS_HX;
-        const int64_t z = z0 - 1 + hz, y = y0 - 1 + hy, x = x0 - 1 + hx;
-        const bool inside_tile = hz >= 1 && hy >= 1 && hx >= 1 && hz <= lz && hy <= ly && hx <= lx;
-        const bool halo = !inside_tile && z >= e0[0] && z < e1[0] && y >= e0[1] && y < e1[1] && x >= e0[2] && x < e1[2];
-        u32 c = WS_INF, l = WS_INF;
-        if (inside_tile || halo) {
-            const int64_t o = z * YX + y * g.S[2] + x;
-            c = cost[o];
-            if (PHASE == 2) l = lab[o];
-        }
-        C[i] = c;
-        if (PHASE == 2) Lsh[i] = l;
+        const int64_t z = w.z0 - 1 + hz, y = w.y0 - 1 + hy, x = w.x0 - 1 + hx;
+        const bool inside_tile = hz >= 1 && hy >= 1 && hx >= 1 && hz <= w.lz && hy <= w.ly && hx <= w.lx;
+        const bool halo = !inside_tile && z >= w.e0[0] && z < w.e1[0] && y >= w.e0[1] && y < w.e1[1] &&
+                          x >= w.e0[2] && x < w.e1[2];
+        H[i] = (inside_tile || halo) ? src[z * YX + y * g.S[2] + x] : WS_INF;
     }
-    for (int j = tid; j < WS_Z * WS_Y * WS_X; j += WS_T) {
-        const int vz = j / (WS_Y * WS_X), vy = (j / WS_X) % WS_Y, vx = j % WS_X;
-        u32 f = WS_INF;
-        if (vz < lz && vy < ly && vx < lx) {
-            const int64_t o = (int64_t)(z0 + vz) * YX + (int64_t)(y0 + vy) * g.S[2] + (x0 + vx);
-            f = ws_f(in[o], mn, m, nan, mask == nullptr || mask[o] != 0);
-        }
-        F[j] = f;
+}
+
+// the six neighbour tiles of the same block see a new halo: each goes on the next round's list
+// once (stamp = the round that listed it)
+__device__ __forceinline__ void ws_list_neighbours(const WsGeom& g, const WsTile& w, int64_t t, u32* stamp, u32 round,
+                                                   u32* list_out, u32* n_out) {
+    const int tid = threadIdx.x;
+    if (tid >= 6) return;
+    const int64_t n2 = g.nt[2], zs = (int64_t)g.nt[1] * n2;
+    bool ok = false;
+    int64_t u = 0;
+    switch (tid) {
+        case 0: ok = w.iz > 0 && g.tblk[0][w.iz - 1] == w.bz; u = t - zs; break;
+        case 1: ok = w.iz + 1 < g.nt[0] && g.tblk[0][w.iz + 1] == w.bz; u = t + zs; break;
+        case 2: ok = w.iy > 0 && g.tblk[1][w.iy - 1] == w.by; u = t - n2; break;
+        case 3: ok = w.iy + 1 < g.nt[1] && g.tblk[1][w.iy + 1] == w.by; u = t + n2; break;
+        case 4: ok = w.ix > 0 && g.tblk[2][w.ix - 1] == w.bx; u = t - 1; break;
+        default: ok = w.ix + 1 < g.nt[2] && g.tblk[2][w.ix + 1] == w.bx; u = t + 1; break;
     }
-    __syncthreads();
-    constexpr int DZ = WS_HY * WS_HX, DY = WS_HX;
+    if (ok && atomicExch(&stamp[u], round) != round) list_out[atomicAdd(n_out, 1u)] = (u32)u;
+}
+
+constexpr int WS_DZ = WS_HY * WS_HX, WS_DY = WS_HX;
+
+// label sweeps over the predecessor masks (bit d: the neighbour in direction d, in the order
+// -z, +z, -y, +y, -x, +x, is an optimal predecessor) to the tile's fixpoint; true if any changed
+__device__ __forceinline__ bool ws_label_sweeps(const WsTile& w, u32* L, const u8* PM) {
+    const int tid = threadIdx.x;
     bool tile_changed = false;
-    // voxel-by-voxel (Gauss-Seidel) sweeps: each voxel against its six neighbours
     for (;;) {
         bool chg = false;
 #pragma unroll
         for (int k = 0; k < WS_VPT; ++k) {
             const int j = tid + k * WS_T;
+            const u32 pm = PM[j];
+            if (!pm) continue;
             const int vz = j / (WS_Y * WS_X), vy = (j / WS_X) % WS_Y, vx = j % WS_X;
-            if (vz >= lz || vy >= ly || vx >= lx) continue;
             const int h = ((vz + 1) * WS_HY + vy + 1) * WS_HX + vx + 1;
-            const u32 c = C[h];
-            if (c == 0u) continue;                               // a seed
-            const u32 f = F[j];
-            const u32 nb[6] = {C[h - DZ], C[h + DZ], C[h - DY], C[h + DY], C[h - 1], C[h + 1]};
-            if (PHASE == 1) {
-                u32 best = min(min(min(nb[0], nb[1]), min(nb[2], nb[3])), min(nb[4], nb[5]));
-                const u32 cand = best == WS_INF ? WS_INF : max(best, f);
-                if (cand < c) { C[h] = cand; chg = true; }
-            } else {
-                if (c == WS_INF) continue;
-                const int off[6] = {-DZ, DZ, -DY, DY, -1, 1};
-                u32 l = Lsh[h];
-                const u32 l0 = l;
-#pragma unroll
-                for (int d = 0; d < 6; ++d)
-                    if (nb[d] != WS_INF && max(nb[d], f) == c) l = min(l, Lsh[h + off[d]]);
-                if (l < l0) { Lsh[h] = l; chg = true; }
-            }
+            u32 l = L[h];
+            const u32 l0 = l;
+            if (pm & 1u) l = min(l, L[h - WS_DZ]);
+            if (pm & 2u) l = min(l, L[h + WS_DZ]);
+            if (pm & 4u) l = min(l, L[h - WS_DY]);
+            if (pm & 8u) l = min(l, L[h + WS_DY]);
+            if (pm & 16u) l = min(l, L[h - 1]);
+            if (pm & 32u) l = min(l, L[h + 1]);
+            if (l < l0) { L[h] = l; chg = true; }
         }
         if (!__syncthreads_or(chg)) break;
         tile_changed = true;
     }
-    if (!tile_changed) return;
+    return tile_changed;
+}
+
+__device__ __forceinline__ void ws_store(const WsGeom& g, const WsTile& w, const u32* H, u32* dst) {
+    const int64_t YX = g.S[1] * g.S[2];
+    for (int j = threadIdx.x; j < WS_Z * WS_Y * WS_X; j += WS_T) {
+        const int vz = j / (WS_Y * WS_X), vy = (j / WS_X) % WS_Y, vx = j % WS_X;
+        if (vz >= w.lz || vy >= w.ly || vx >= w.lx) continue;
+        const int h = ((vz + 1) * WS_HY + vy + 1) * WS_HX + vx + 1;
+        dst[(int64_t)(w.z0 + vz) * YX + (int64_t)(w.y0 + vy) * g.S[2] + (w.x0 + vx)] = H[h];
+    }
+}
+
+// PHASE 1: one round of the costs over the round's tiles.  PHASE 2: every tile once on the
+// converged costs: each voxel's predecessor mask (pm), which is all the label rounds (k_ws_label)
+// read besides the labels (half their LDS, twice the resident tiles).
+template <int PHASE>
+__global__ __launch_bounds__(WS_T) void k_ws_relax(WsGeom g, const float* __restrict__ in, const u8* __restrict__ mask,
+                                                   const u32* __restrict__ smin, const u32* __restrict__ smax,
+                                                   const u32* __restrict__ sflag, u32* cost, u32* lab, u8* pm,
+                                                   const u32* __restrict__ list_in, u32* stamp, u32 round,
+                                                   u32* list_out, u32* n_out) {
+    __shared__ u32 C[WS_HN], F[WS_Z * WS_Y * WS_X];
+    // the round's tiles: all (list_in NULL, the first round of a phase) or the listed ones
+    const int64_t t = list_in ? (int64_t)list_in[blockIdx.x] : (int64_t)blockIdx.x;
+    const int tid = threadIdx.x;
+    const WsTile w = ws_tile(g, t);
+    // normalize parameters of the block (as block_param: numpy's min / max(x - min), NaN blocks)
+    const u32 omn = smin[w.b], omx = smax[w.b];
+    const bool nan = sflag[w.b] & 1u;
+    const float mn = __uint_as_float(ord2f(omn)), mxv = __uint_as_float(ord2f(omx));
+    const float m = (isinf(mn) || isinf(mxv)) ? (isinf(mn) ? __uint_as_float(0x7FC00000u) : mxv - mn) : mxv - mn;
+    const int64_t YX = g.S[1] * g.S[2];
+    ws_load_halo(g, w, cost, C);
     for (int j = tid; j < WS_Z * WS_Y * WS_X; j += WS_T) {
         const int vz = j / (WS_Y * WS_X), vy = (j / WS_X) % WS_Y, vx = j % WS_X;
-        if (vz >= lz || vy >= ly || vx >= lx) continue;
-        const int h = ((vz + 1) * WS_HY + vy + 1) * WS_HX + vx + 1;
-        const int64_t o = (int64_t)(z0 + vz) * YX + (int64_t)(y0 + vy) * g.S[2] + (x0 + vx);
-        if (PHASE == 1) cost[o] = C[h]; else lab[o] = Lsh[h];
-    }
-    if (tid < 6) {
-        // the six neighbour tiles of the same block see a new halo: each goes on the next round's
-        // list once (stamp = the round that listed it)
-        const int64_t zs = (int64_t)n1 * n2;
-        bool ok = false;
-        int64_t u = 0;
-        switch (tid) {
-            case 0: ok = iz > 0 && g.tblk[0][iz - 1] == bz; u = t - zs; break;
-            case 1: ok = iz + 1 < g.nt[0] && g.tblk[0][iz + 1] == bz; u = t + zs; break;
-            case 2: ok = iy > 0 && g.tblk[1][iy - 1] == by; u = t - n2; break;
-            case 3: ok = iy + 1 < g.nt[1] && g.tblk[1][iy + 1] == by; u = t + n2; break;
-            case 4: ok = ix > 0 && g.tblk[2][ix - 1] == bx; u = t - 1; break;
-            default: ok = ix + 1 < g.nt[2] && g.tblk[2][ix + 1] == bx; u = t + 1; break;
+        u32 f = WS_INF;
+        if (vz < w.lz && vy < w.ly && vx < w.lx) {
+            const int64_t o = (int64_t)(w.z0 + vz) * YX + (int64_t)(w.y0 + vy) * g.S[2] + (w.x0 + vx);
+            f = ws_f(in[o], mn, m, nan, mask == nullptr || mask[o] != 0);
         }
-        if (ok && atomicExch(&stamp[u], round) != round) list_out[atomicAdd(n_out, 1u)] = (u32)u;
+        F[j] = f;
+    }
+    __syncthreads();
+    bool tile_changed = false;
+    if (PHASE == 1) {
+        // voxel-by-voxel (Gauss-Seidel) sweeps: each voxel against its six neighbours
+        for (;;) {
+            bool chg = false;
+#pragma unroll
+            for (int k = 0; k < WS_VPT; ++k) {
+                const int j = tid + k * WS_T;
+                const int vz = j / (WS_Y * WS_X), vy = (j / WS_X) % WS_Y, vx = j % WS_X;
+                if (vz >= w.lz || vy >= w.ly || vx >= w.lx) continue;
+                const int h = ((vz + 1) * WS_HY + vy + 1) * WS_HX + vx + 1;
+                const u32 c = C[h];
+                if (c == 0u) continue;                               // a seed
+                const u32 best = min(min(min(C[h - WS_DZ], C[h + WS_DZ]), min(C[h - WS_DY], C[h + WS_DY])),
+                                     min(C[h - 1], C[h + 1]));
+                const u32 cand = best == WS_INF ? WS_INF : max(best, F[j]);
+                if (cand < c) { C[h] = cand; chg = true; }
+            }
+            if (!__syncthreads_or(chg)) break;
+            tile_changed = true;
+        }
+        if (tile_changed) ws_store(g, w, C, cost);
+    } else {
+        for (int j = tid; j < WS_Z * WS_Y * WS_X; j += WS_T) {
+            const int vz = j / (WS_Y * WS_X), vy = (j / WS_X) % WS_Y, vx = j % WS_X;
+            if (vz >= w.lz || vy >= w.ly || vx >= w.lx) continue;
+            const int h = ((vz + 1) * WS_HY + vy + 1) * WS_HX + vx + 1;
+            const u32 c = C[h], f = F[j];
+            u32 bits = 0;
+            if (c != 0u && c != WS_INF) {
+                const int off[6] = {-WS_DZ, WS_DZ, -WS_DY, WS_DY, -1, 1};
+#pragma unroll
+                for (int d = 0; d < 6; ++d) {
+                    const u32 cu = C[h + off[d]];
+                    if (cu != WS_INF && max(cu, f) == c) bits |= 1u << d;
+                }
+            }
+                pm[(int64_t)(w.z0 + vz) * YX + (int64_t)(w.y0 + vy) * g.S[2] + (w.x0 + vx)] = (u8)bits;
+        }
+        return;                                       // the label rounds are k_ws_label's
+    }
+    if (tile_changed) ws_list_neighbours(g, w, t, stamp, round, list_out, n_out);
+}
+
+// a label round over the listed tiles (list_in NULL: every tile): labels with halo and the
+// predecessor masks
+__global__ __launch_bounds__(WS_T) void k_ws_label(WsGeom g, const u8* __restrict__ pm, u32* lab,
+                                                   const u32* __restrict__ list_in, u32* stamp, u32 round,
+                                                   u32* list_out, u32* n_out) {
+    __shared__ u32 Lsh[WS_HN];
+    __shared__ u8 PM[WS_Z * WS_Y * WS_X];
+    const int64_t t = list_in ? (int64_t)list_in[blockIdx.x] : (int64_t)blockIdx.x;
+    const WsTile w = ws_tile(g, t);
+    const int64_t YX = g.S[1] * g.S[2];
+    ws_load_halo(g, w, lab, Lsh);
+    for (int j = threadIdx.x; j < WS_Z * WS_Y * WS_X; j += WS_T) {
+        const int vz = j / (WS_Y * WS_X), vy = (j / WS_X) % WS_Y, vx = j % WS_X;
+        u8 bits = 0;
+        if (vz < w.lz && vy < w.ly && vx < w.lx)
+            bits = pm[(int64_t)(w.z0 + vz) * YX + (int64_t)(w.y0 + vy) * g.S[2] + (w.x0 + vx)];
+        PM[j] = bits;
+    }
+    __syncthreads();
+    if (ws_label_sweeps(w, Lsh, PM)) {
+        ws_store(g, w, Lsh, lab);
+        ws_list_neighbours(g, w, t, stamp, round, list_out, n_out);
     }
 }
 
@@ -237,12 +321,13 @@ extern "C" int cc_watershed_from_seeds(cc_ctx* c, const float* in, const uint64_
             }
         }
         // state: cost | label per voxel; per tile the round that last listed it, two tile lists
-        c->ws_buf.ensure((size_t)n * 2 * sizeof(u32) + 3 * (size_t)nt * sizeof(u32) + 64);
+        c->ws_buf.ensure((size_t)n * 2 * sizeof(u32) + 3 * (size_t)nt * sizeof(u32) + (size_t)n + 64);
         u32* cost = c->ws_buf.as<u32>();
         u32* lab = cost + n;
         u32* stamp = lab + n;
         u32* list0 = stamp + nt;
         u32* list1 = list0 + nt;
+        u8* pm = (u8*)(list1 + nt);                   // predecessor masks (the first label round)
         c->counter.ensure(4 * sizeof(u32));
         u32* flags = c->counter.as<u32>();            // [0] seed id overflow, [1] tiles listed for the next round
         HIP_OK(hipMemsetAsync(flags, 0, 4 * sizeof(u32), s));
@@ -250,21 +335,27 @@ extern "C" int cc_watershed_from_seeds(cc_ctx* c, const float* in, const uint64_
         launch(c, "k_ws_init", [&] { k_ws_init<<<grid_stride(n), 256, 0, s>>>(n, seeds, cost, lab, flags); });
         int64_t total_rounds = 0;
         u32 round = 0;
+        const bool trace = std::getenv("CC_WS_TRACE") != nullptr;
+        auto tr0 = std::chrono::steady_clock::now();
         for (int phase = 1; phase <= 2; ++phase) {
             // the first round of a phase visits every tile, later rounds the tiles listed by the last
             const u32* lin = nullptr;
             int64_t ntile = nt;
+            if (phase == 2)
+                launch(c, "k_ws_preds", [&] {
+                    k_ws_relax<2><<<(unsigned)nt, WS_T, 0, s>>>(g, in, mask, smin, smax, sflag, cost, lab, pm, nullptr,
+                                                               stamp, round, list1, flags + 1);
+                });
             for (int64_t r = 0; ntile > 0; ++r) {
                 CC_REQUIRE(r < 4 * n + 16, "watershed did not converge");
                 ++round;
                 HIP_OK(hipMemsetAsync(flags + 1, 0, sizeof(u32), s));
                 launch(c, phase == 1 ? "k_ws_relax_cost" : "k_ws_relax_label", [&] {
                     if (phase == 1)
-                        k_ws_relax<1><<<(unsigned)ntile, WS_T, 0, s>>>(g, in, mask, smin, smax, sflag, cost, lab, lin, stamp,
-                                                                      round, list1, flags + 1);
+                        k_ws_relax<1><<<(unsigned)ntile, WS_T, 0, s>>>(g, in, mask, smin, smax, sflag, cost, lab, pm, lin,
+                                                                      stamp, round, list1, flags + 1);
                     else
-                        k_ws_relax<2><<<(unsigned)ntile, WS_T, 0, s>>>(g, in, mask, smin, smax, sflag, cost, lab, lin, stamp,
-                                                                      round, list1, flags + 1);
+                        k_ws_label<<<(unsigned)ntile, WS_T, 0, s>>>(g, pm, lab, lin, stamp, round, list1, flags + 1);
                 });
                 u32 fl[2] = {0, 0};
                 {
@@ -277,6 +368,12 @@ extern "C" int cc_watershed_from_seeds(cc_ctx* c, const float* in, const uint64_
                 CC_REQUIRE(fl[1] <= (u32)nt, "watershed tile list overflow");
                 std::swap(list0, list1);
                 lin = list0;
+                if (trace) {                          // dev hook: tiles and host ms per round
+                    const auto now = std::chrono::steady_clock::now();
+                    std::fprintf(stderr, "ws phase %d round %ld tiles %ld ms %.3f\n", phase, (long)r, (long)ntile,
+                                 std::chrono::duration<double, std::milli>(now - tr0).count());
+                    tr0 = now;
+                }
                 ntile = fl[1];
             }
         }
