@@ -22,7 +22,15 @@
 // round after a phase's first visits only the tiles the previous round listed.
 namespace cc {
 
-constexpr int WS_Z = 8, WS_Y = 8, WS_X = 32, WS_T = 256;
+// tile shape and threads (CC_WS_TZ / TY / TX / TT at build time: A/B only)
+#ifndef CC_WS_TZ
+#define CC_WS_TZ 8
+#define CC_WS_TY 8
+#define CC_WS_TX 32
+#define CC_WS_TT 256
+#endif
+constexpr int WS_Z = CC_WS_TZ, WS_Y = CC_WS_TY, WS_X = CC_WS_TX, WS_T = CC_WS_TT;
+static_assert(WS_Z * WS_Y * WS_X % WS_T == 0, "whole voxels per thread");
 constexpr int WS_HZ = WS_Z + 2, WS_HY = WS_Y + 2, WS_HX = WS_X + 2, WS_HN = WS_HZ * WS_HY * WS_HX;
 constexpr int WS_VPT = WS_Z * WS_Y * WS_X / WS_T;      // interior voxels per thread
 constexpr u32 WS_INF = 0xFFFFFFFFu;
