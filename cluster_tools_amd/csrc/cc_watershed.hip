@@ -31,6 +31,9 @@ namespace cc {
 #endif
 constexpr int WS_Z = CC_WS_TZ, WS_Y = CC_WS_TY, WS_X = CC_WS_TX, WS_T = CC_WS_TT;
 static_assert(WS_Z * WS_Y * WS_X % WS_T == 0, "whole voxels per thread");
+#ifndef CC_WS_ALT
+#define CC_WS_ALT 0        // A/B only: odd sweeps walk a thread's voxels in reverse order
+#endif
 constexpr int WS_HZ = WS_Z + 2, WS_HY = WS_Y + 2, WS_HX = WS_X + 2, WS_HN = WS_HZ * WS_HY * WS_HX;
 constexpr int WS_VPT = WS_Z * WS_Y * WS_X / WS_T;      // interior voxels per thread
 constexpr u32 WS_INF = 0xFFFFFFFFu;
@@ -126,11 +129,11 @@ constexpr int WS_DZ = WS_HY * WS_HX, WS_DY = WS_HX;
 __device__ __forceinline__ bool ws_label_sweeps(const WsTile& w, u32* L, const u8* PM) {
     const int tid = threadIdx.x;
     bool tile_changed = false;
-    for (;;) {
+    for (int sweep = 0;; ++sweep) {
         bool chg = false;
 #pragma unroll
         for (int k = 0; k < WS_VPT; ++k) {
-            const int j = tid + k * WS_T;
+            const int j = tid + (CC_WS_ALT && (sweep & 1) ? WS_VPT - 1 - k : k) * WS_T;
             const u32 pm = PM[j];
             if (!pm) continue;
             const int vz = j / (WS_Y * WS_X), vy = (j / WS_X) % WS_Y, vx = j % WS_X;
@@ -195,11 +198,11 @@ __global__ __launch_bounds__(WS_T) void k_ws_relax(WsGeom g, const float* __rest
     bool tile_changed = false;
     if (PHASE == 1) {
         // voxel-by-voxel (Gauss-Seidel) sweeps: each voxel against its six neighbours
-        for (;;) {
+        for (int sweep = 0;; ++sweep) {
             bool chg = false;
 #pragma unroll
             for (int k = 0; k < WS_VPT; ++k) {
-                const int j = tid + k * WS_T;
+                const int j = tid + (CC_WS_ALT && (sweep & 1) ? WS_VPT - 1 - k : k) * WS_T;
                 const int vz = j / (WS_Y * WS_X), vy = (j / WS_X) % WS_Y, vx = j % WS_X;
                 if (vz >= w.lz || vy >= w.ly || vx >= w.lx) continue;
                 const int h = ((vz + 1) * WS_HY + vy + 1) * WS_HX + vx + 1;
