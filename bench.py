@@ -6,17 +6,26 @@ One step = the full five-stage path (block_components -> merge_offsets -> block_
 merge_assignments -> write) over one synthetic volume that is already resident in HBM,
 ending with the final uint64 labels resident in HBM.
 
-Workloads (--workload):
-  c3 (default at N = 1)  (1024, 2048, 2048) float32, block (64, 512, 512), threshold 0.5 'greater'
-  c4   C3 + the ellipsoid uint8 mask, strong-scaled: z-slabs of the one volume over N ranks
-  c5 (default at N > 1)  weak scaling: each rank owns a (256, 4096, 4096) slab of a
-       (256 N, 4096, 4096) volume -- at N = 8 this is C5, (2048, 4096, 4096)
+Workloads (--workload).  One workload keeps its meaning at every N, so a
+1 -> 2 -> 4 -> 8 series is one curve:
+  c3 (default, every N)  (1024, 2048, 2048) float32, block (64, 512, 512), threshold 0.5 'greater';
+       strong scaling: the one volume split into N z-slabs (N = 1: the headline single-GPU case)
+  c4   C3 + the ellipsoid uint8 mask, strong-scaled the same way (BASELINE config 4)
+  c5   weak scaling: each rank owns a (256, 4096, 4096) slab of a (256 N, 4096, 4096) volume --
+       N = 1 is one such slab, N = 8 is C5, (2048, 4096, 4096)
   c2   (512, 512, 512), block (128, 128, 128)
   c1   (125, 1250, 1250), block (50, 512, 512): BASELINE config 1's geometry; the line also carries
        `cold_start`: a fresh process (a child of this one, input handed over as a .npy file) timing
        its FIRST cc_label_volume -- what every one-shot target='local' job pays -- and the warm calls
   --dither: continuous input (the map plus a sub-2^-8 dither).  N > 1 runs one process per GPU;
   seams are stitched over RCCL (cluster_tools_amd/distributed.py).
+
+Launch: `python bench.py --gpus N` starts its own N ranks when it is not already one of them
+(WORLD_SIZE unset): a child `python -m torch.distributed.run --nproc-per-node N bench.py ...` is
+started BEFORE this process imports torch or loads the library (a subprocess, never an exec), its
+stdout (rank 0's JSON line) is relayed, and the exit code is non-zero if any rank failed -- the
+analogue of the reference's LocalTask pool (cluster_tools/cluster_tasks.py:545-551).  Under
+`torch.distributed.run` (WORLD_SIZE set) this process is one rank.
 Rank 0 prints one JSON line.
 """
 import argparse
@@ -44,7 +53,7 @@ WORKLOADS = {
 }
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--timed-prof', type=int, default=2,
@@ -57,9 +66,9 @@ def parse():
     p.add_argument('--dither', action='store_true',
                    help='continuous input: the synthetic map plus a deterministic sub-2^-8 dither (not quantized)')
     p.add_argument('--shape', default=None, help='override Z,Y,X (per-rank slab for N > 1)')
-    p.add_argument('--workload', default=None, choices=sorted(WORKLOADS),
-                   help='c3 (default at N=1), c4 (C3 + mask, strong-scaled z-slabs), c5 (default at N>1: '
-                        '(256N,4096,4096), weak), c2 (512^3, block 128^3), c1 (125x1250x1250, block '
+    p.add_argument('--workload', default='c3', choices=sorted(WORKLOADS),
+                   help='c3 (default; strong-scaled z-slabs at N>1), c4 (C3 + mask, strong-scaled z-slabs), '
+                        'c5 ((256N,4096,4096), weak), c2 (512^3, block 128^3), c1 (125x1250x1250, block '
                         '50x512x512, + cold_start)')
     p.add_argument('--block-shape', default=None)
     p.add_argument('--no-cpu-baseline', action='store_true')
@@ -68,7 +77,36 @@ def parse():
     p.add_argument('--traffic-json', default=None,
                    help='tools/prof_summary.py output (rocprofv3 FETCH_SIZE / WRITE_SIZE passes) to fill '
                         'roofline.traffic; default profiles/traffic_<workload tag>.json when present')
-    return p.parse_args()
+    return p.parse_args(argv)
+
+
+def launcher_cmd(gpus, argv, port, script=None):
+    """The torch.distributed.run command that starts `gpus` ranks of this script with the same
+    arguments (one process per GPU; rendezvous on 127.0.0.1)."""
+    return [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(gpus),
+            '--master-addr', '127.0.0.1', '--master-port', str(port),
+            script or os.path.abspath(__file__)] + list(argv)
+
+
+def needs_launch(gpus, env=None):
+    """True when `--gpus N > 1` was asked for outside torch.distributed.run."""
+    env = os.environ if env is None else env
+    return gpus > 1 and 'WORLD_SIZE' not in env
+
+
+def self_launch(gpus, argv):
+    """Start the N ranks as a CHILD process (torch.distributed.run) and wait for it.  Runs before
+    anything in this process touches torch or the GPU; the ranks inherit stdout, so rank 0's JSON
+    line reaches the caller unchanged.  Returns the child's exit code (non-zero if any rank failed)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')      # dmabuf IPC only on these hosts (RCCL)
+    r = subprocess.run(launcher_cmd(gpus, argv, port), env=env)
+    return r.returncode
 
 
 def cpu_baseline(args, block_shape, shape_yx, nz):
@@ -144,6 +182,8 @@ def main():
     args = parse()
     if args.cold_child:
         return cold_child(args)
+    if needs_launch(args.gpus):
+        return self_launch(args.gpus, sys.argv[1:])
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -171,7 +211,7 @@ def main():
 
     # workloads: strong = the volume is fixed and split into z-slabs over the N
     # ranks; weak = every rank owns a slab of the same size
-    wl = args.workload or ('c3' if world == 1 else 'c5')
+    wl = args.workload
     spec = dict(WORKLOADS[wl])
     if args.mask:
         spec['mask'] = True
@@ -317,4 +357,4 @@ def main():
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main() or 0)

@@ -87,12 +87,15 @@ def test_one_rank_rccl(tmp_path):
     assert int(np.load(str(tmp_path / 'nl_0.npy'))[0]) == ref['n_labels']
 
 
-@pytest.mark.parametrize('mode,masked,form', [('less', True, None), ('greater', False, None),
-                                              ('greater', True, 'voxel32')])
-def test_sharded_c4_scale_vs_oracle(mode, masked, form):
+@pytest.mark.parametrize('n_slabs,mode,masked,form', [
+    (4, 'less', True, None), (4, 'greater', False, None), (4, 'greater', True, 'voxel32'),
+    # the 8-GPU strong-scaling split: 8 slabs of (128, 2048, 2048), seams every 128 planes
+    (8, 'greater', True, None), (8, 'less', False, None)])
+def test_sharded_c4_scale_vs_oracle(n_slabs, mode, masked, form):
     """SURVEY.md §8d parity at scale for the sharded configs: C4 (C3 + ellipsoid mask) over 4
-    z-slabs on one GPU, with the cubes32 seam planes the ranks exchange over xGMI (or the
-    per-voxel uint32 fallback), against the C oracle on the whole volume: raw labels identical
+    or 8 z-slabs on one GPU (8: the strong-scaling split of the 8-GPU run), with the cubes32 seam
+    planes the ranks exchange over xGMI (or the per-voxel uint32 fallback), against the C oracle
+    on the whole volume (6-connected seams: block_faces.py:87-113): raw labels identical
     (compared on the device), the assembled LUT identical, and the device contingency table of
     the two labellings a bijection (|unique(a, b)| == |unique(a)| == |unique(b)|)."""
     import os
@@ -101,7 +104,7 @@ def test_sharded_c4_scale_vs_oracle(mode, masked, form):
     from cluster_tools_amd.distributed import label_slabs_single_process, assemble_lut
     from cluster_tools_amd.synthetic import ellipsoid_mask_device
     shape, bs = (1024, 2048, 2048), (64, 512, 512)
-    ctxs = [_lib.Context(0) for _ in range(4)]
+    ctxs = [_lib.Context(0) for _ in range(n_slabs)]
     try:
         x = ctxs[0].generate_boundary_map(shape)
         mask = ellipsoid_mask_device(shape, 0, shape[0], x.device) if masked else None
@@ -177,3 +180,27 @@ def test_sharded_c5_geometry_vs_oracle(mode):
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_bench_self_launch_two_ranks_gloo():
+    """`python bench.py --gpus 2 --workload c4` exactly as the driver's scaling run calls it (no
+    torch.distributed.run around it): bench.py starts its two ranks itself; here both share
+    cuda:0 with gloo collectives staged through host memory (CC_DIST_BACKEND=gloo; RCCL refuses
+    two ranks on one device).  One JSON line with n_gpus 2, strong scaling over C4's volume."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CC_DIST_BACKEND='gloo')
+    env.pop('WORLD_SIZE', None)
+    cmd = [sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--workload', 'c4', '--steps', '2',
+           '--warmup', '1', '--no-cpu-baseline']
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d['n_gpus'] == 2 and d['scaling'] == 'strong' and d['config']['workload_id'] == 'c4'
+    assert d['config']['shape'] == [1024, 2048, 2048] and d['config']['slab'] == [512, 2048, 2048]
+    assert d['value'] > 0

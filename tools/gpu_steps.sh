@@ -1,0 +1,43 @@
+#!/bin/bash
+# One GPU-box session of named evidence steps, run in order; each GPU step has its own time
+# limit and the session stops at the first failure (no retries).  Outputs under gpurun_out/.
+# Usage (from this container): gpurun --timeout 1200 -- tools/gpu_steps.sh TAG STEP [STEP ...]
+#   bench          default bench line (C3, N = 1), CPU baseline skipped    -> bench_TAG.json
+#   bench_full     default bench line with the CPU baseline                 -> bench_full_TAG.json
+#   bench_c4 / bench_c2 / bench_c1 / bench_cont   other workloads on one GPU
+#   slabs8_c3 / slabs8_c4   the 8-slab strong-scaling schedule in one process (tools/bench_sharded_slabs.py)
+#   n2gloo         bench.py --gpus 2 --workload c4 self-launched, gloo on one GPU
+#   tests          the whole -m gpu suite                                   -> tests_TAG.log
+#   tests_sharded  tests/test_gpu_sharded.py only
+#   prof_c3 / prof_c3_mask   rocprofv3 trace + FETCH/WRITE passes (tools/profile.sh)
+#   trace_slabs8   rocprofv3 kernel trace of the 8-slab schedule
+set -e -o pipefail
+TAG=$1; shift
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+cd "$ROOT"
+mkdir -p gpurun_out
+O=gpurun_out
+PYT="python -u -m pytest -x -v --timeout 400 --timeout-method thread"
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+    bench)      timeout -k 10 240 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 > $O/bench_$TAG.json 2> $O/bench_$TAG.err; cat $O/bench_$TAG.json ;;
+    bench_full) timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench_full_$TAG.json 2> $O/bench_full_$TAG.err; cat $O/bench_full_$TAG.json ;;
+    bench_c4)   timeout -k 10 240 python -u bench.py --no-cpu-baseline --workload c4 --steps 20 --warmup 5 > $O/bench_c4_$TAG.json 2> $O/bench_c4_$TAG.err; cat $O/bench_c4_$TAG.json ;;
+    bench_c2)   timeout -k 10 240 python -u bench.py --no-cpu-baseline --workload c2 --steps 50 --warmup 10 > $O/bench_c2_$TAG.json 2> $O/bench_c2_$TAG.err; cat $O/bench_c2_$TAG.json ;;
+    bench_c1)   timeout -k 10 240 python -u bench.py --no-cpu-baseline --workload c1 --steps 50 --warmup 10 > $O/bench_c1_$TAG.json 2> $O/bench_c1_$TAG.err; cat $O/bench_c1_$TAG.json ;;
+    bench_cont) timeout -k 10 240 python -u bench.py --no-cpu-baseline --dither --steps 20 --warmup 5 > $O/bench_cont_$TAG.json 2> $O/bench_cont_$TAG.err; cat $O/bench_cont_$TAG.json ;;
+    slabs8_c3)  timeout -k 10 300 python -u tools/bench_sharded_slabs.py 8 c3 10 > $O/slabs8_c3_$TAG.json 2> $O/slabs8_c3_$TAG.err; cat $O/slabs8_c3_$TAG.json ;;
+    slabs8_c4)  timeout -k 10 300 python -u tools/bench_sharded_slabs.py 8 c4 10 > $O/slabs8_c4_$TAG.json 2> $O/slabs8_c4_$TAG.err; cat $O/slabs8_c4_$TAG.json ;;
+    n2gloo)     CC_DIST_BACKEND=gloo timeout -k 10 300 python -u bench.py --gpus 2 --workload c4 --steps 5 --warmup 2 --no-cpu-baseline > $O/n2gloo_$TAG.json 2> $O/n2gloo_$TAG.err; cat $O/n2gloo_$TAG.json ;;
+    tests)      timeout -k 10 1000 $PYT tests -m gpu > $O/tests_$TAG.log 2>&1 || { tail -40 $O/tests_$TAG.log; exit 1; }; tail -3 $O/tests_$TAG.log ;;
+    tests_sharded) timeout -k 10 900 $PYT tests/test_gpu_sharded.py > $O/tests_sharded_$TAG.log 2>&1 || { tail -40 $O/tests_sharded_$TAG.log; exit 1; }; tail -3 $O/tests_sharded_$TAG.log ;;
+    prof_c3)    tools/profile.sh "${TAG}_c3" --steps 10 --warmup 3 ;;
+    prof_c3_mask) tools/profile.sh "${TAG}_c3_mask" --steps 10 --warmup 3 --mask ;;
+    trace_slabs8) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                    -d "$ROOT/$O/trace_slabs8_$TAG" -o run -- python3 "$ROOT/tools/bench_sharded_slabs.py" 8 c3 3 \
+                    > "$ROOT/$O/trace_slabs8_$TAG.json" 2> "$ROOT/$O/trace_slabs8_$TAG.err") ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
