@@ -26,8 +26,11 @@ EXPORTS = (
     'cc_seam_pairs32', 'cc_shard_top_cubes32', 'cc_seam_pairs_cubes32',
     'cc_evaluate', 'cc_get_overlaps', 'cc_relabel_consecutive', 'cc_set_option', 'cc_channel_mean',
     'cc_gaussian_smooth_blocks', 'cc_gaussian_taps', 'cc_result_size', 'cc_resize_mask_nearest',
-    'cc_watershed_from_seeds',
+    'cc_watershed_from_seeds', 'cc_shard_dev_begin', 'cc_shard_dev_assign', 'cc_shard_dev_top_cubes',
+    'cc_shard_dev_seam_pairs', 'cc_shard_dev_finish',
 )
+# redo flags of the one-read-back schedule (RF_* in csrc/cc_kernels.hip)
+RF_BIG, RF_ROOTS, RF_CUBES, RF_PAIRS = 1, 2, 4, 8
 # CC_DTYPE_* of include/cc_mi355x.h (cc_channel_mean)
 DTYPES = {'float32': 0, 'float64': 1, 'uint8': 2, 'int8': 3, 'uint16': 4, 'int16': 5, 'uint32': 6,
           'int32': 7, 'uint64': 8, 'int64': 9}
@@ -110,6 +113,11 @@ def load():
         'cc_shard_planes': (I, [P, P, P]),
         'cc_seam_pairs': (i64, [P, P, P, i64, P, i64]),
         'cc_shard_finish': (I, [P, P, i64, P, ctypes.POINTER(CCResult)]),
+        'cc_shard_dev_begin': (I, [P, P, P, P, P, ctypes.c_double, I, i64, P]),
+        'cc_shard_dev_assign': (I, [P, P, I, I]),
+        'cc_shard_dev_top_cubes': (I, [P, P]),
+        'cc_shard_dev_seam_pairs': (I, [P, P, P, I, P, i64]),
+        'cc_shard_dev_finish': (I, [P, P, I, i64, P, P, ctypes.POINTER(CCResult), P]),
         'cc_evaluate': (I, [P, P, P, P, P, I, u64, ctypes.POINTER(CCEvalResult)]),
         'cc_get_overlaps': (i64, [P, P, P, P, i64]),
         'cc_relabel_consecutive': (I, [P, P, P, i64, P, P, P, i64]),
@@ -590,6 +598,35 @@ class Context:
         _check(load().cc_shard_finish(self._h, _ptr(pairs_dev) if n_pairs else None, int(n_pairs),
                                       _ptr(out_dev), ctypes.byref(res)))
         return res.as_dict()
+
+    # ---- z-slab shards, one-read-back schedule (distributed.py's default) ----
+    def shard_dev_begin(self, x_dev, block_shape, threshold, mode, z_offset, sum_dev, mask_dev=None):
+        """Local stages of the slab; its sum of block values goes to sum_dev (uint64 on the device)."""
+        shape, bs = _i64(x_dev.shape), _i64(block_shape)
+        _check(load().cc_shard_dev_begin(self._h, _ptr(x_dev), _ptr(mask_dev), _ptr(shape), _ptr(bs),
+                                         float(threshold), mode_id(mode), int(z_offset), _ptr(sum_dev)))
+
+    def shard_dev_assign(self, sums_dev, rank, world):
+        _check(load().cc_shard_dev_assign(self._h, _ptr(sums_dev), int(rank), int(world)))
+
+    def shard_dev_top_cubes(self, cubes_dev):
+        _check(load().cc_shard_dev_top_cubes(self._h, _ptr(cubes_dev)))
+
+    def shard_dev_seam_pairs(self, upper_cubes_dev, sums_dev, rank, hdr_pairs_dev):
+        """hdr_pairs_dev: [cap + 1, 2] int64 -- row 0 (count, redo flags), then the pairs."""
+        cap = hdr_pairs_dev.shape[0] - 1
+        _check(load().cc_shard_dev_seam_pairs(self._h, _ptr(upper_cubes_dev), _ptr(sums_dev), int(rank),
+                                              _ptr(hdr_pairs_dev), int(cap)))
+
+    def shard_dev_finish(self, all_dev, world, sums_dev, out_dev):
+        """all_dev: [world * (cap + 1), 2] (every slab's pair buffer).  Returns (result, status):
+        status = (redo flags, largest pair count of a slab, n_labels, id base)."""
+        cap = all_dev.shape[0] // int(world) - 1
+        res = CCResult()
+        st = np.zeros(4, dtype=np.uint64)
+        _check(load().cc_shard_dev_finish(self._h, _ptr(all_dev), int(world), int(cap), _ptr(sums_dev), _ptr(out_dev),
+                                          ctypes.byref(res), _ptr(st)))
+        return res.as_dict(), tuple(int(v) for v in st)
 
     def lut_local(self):
         """The LUT of the last run on this ctx: for a shard, its ids id_base .. id_base + sum."""

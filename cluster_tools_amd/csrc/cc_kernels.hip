@@ -71,6 +71,14 @@ __host__ __device__ constexpr u32 fsel(int sp, int sq) {
 // After tile_ccl: par[run] = root | k << 16 for every run, k in [0, R) the component's compact
 // index (roots in cube order).
 // ------------------------------------------------------------------------------------------
+// redo flags of the one-read-back schedule (scalars[3] of a run; bits of a shard's seam-pair
+// header): the launch sequence enqueued without read-backs was not valid for this input, and the
+// run is redone by the host-synchronised schedule (results never depend on which one ran)
+constexpr u64 RF_BIG = 1;       // some block needs the global-memory stitch fallback
+constexpr u64 RF_ROOTS = 2;     // more block-local roots than the root arrays hold
+constexpr u64 RF_CUBES = 4;     // the slab's ids do not fit the 28-bit cube form of its top plane
+constexpr u64 RF_PAIRS = 8;     // more seam pairs than the pair buffer holds
+
 constexpr int NCROW = CZ * CY;          // cube rows per tile
 constexpr int NRUN = NCROW * CX;        // a run per occupied cube at most (adjacent cubes need not link)
 static_assert(NTHREADS == 4 * NCROW, "tile_ccl maps one thread to each quarter cube row");
@@ -858,9 +866,12 @@ __global__ void k_guess(int64_t nb, const u32* part, float thr, int mode, BlockP
 // block min = ~0, max / NaN flag = 0, scalars, the k_fix count, seam overflow flags (+ their
 // "any" flags at big[nb] / iovf[nt]; fill = 1 sends everything to the global stitch), the
 // inter-pair counts, the root segments and the scan's extra element.
+// mflag / fchg (nullable, the device-gated k_fix of the one-read-back schedule): the seam marks
+// and their list count (mflag[nt]) and the changed-faces flags, which the host-synchronised
+// schedule clears only when the k_fix count it read back is non-zero.
 __global__ __launch_bounds__(256) void k_clear_front(int64_t nb, int64_t nt, u32* smin, u32* smax_flag,
                                                      u64* scalars, u32* FIX, u8* big, u8* iovf, u32* ipc,
-                                                     u32* seg, u32* rc_end, u8 fill) {
+                                                     u32* seg, u32* rc_end, u8 fill, u32* mflag, u8* fchg) {
     CC_FOR(i, (nt + 1 > 2 * nb + 1 ? nt + 1 : 2 * nb + 1)) {
         if (i < nb) smin[i] = 0xFFFFFFFFu;
         if (i < 2 * nb) { smax_flag[i] = 0u; seg[i] = 0u; }
@@ -869,6 +880,8 @@ __global__ __launch_bounds__(256) void k_clear_front(int64_t nb, int64_t nt, u32
         if (i < nt) ipc[i] = 0u;
         if (i < 4) scalars[i] = 0ull;
         if (i == 0) { FIX[0] = 0u; rc_end[0] = 0u; }
+        if (mflag && i <= nt) mflag[i] = 0u;
+        if (fchg && i < nt) fchg[i] = 0;
     }
 }
 
@@ -1086,6 +1099,51 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     if (!fresh && cc_tid() == 0) fchg[t] = 1;
     pass1_tile<HAS_MASK>(g, t, ti, p, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L, true,
                          fresh ? fchg : nullptr);
+}
+
+// the 14 tiles whose seams read the faces of tile f (f itself and the 13 that have it as a
+// lex-negative neighbour): d = 0 .. 13, each marked once (flag) and listed in LIST[1 .. LIST[0]]
+__device__ __forceinline__ void mark_seam(const Geom& g, u32 f, u32 d, u32* flag, u32* LIST) {
+    const TileInfo ti = tile_info(g, f);
+    int dz = 0, dy = 0, dx = 0;
+    if (d > 0) {
+        const int c = (int)d - 1;               // 0..12: (0,0,1), (0,1,-1..1), (1,-1..1,-1..1)
+        if (c == 0) { dx = 1; }
+        else if (c < 4) { dy = 1; dx = c - 2; }
+        else { dz = 1; dy = (c - 4) / 3 - 1; dx = (c - 4) % 3 - 1; }
+    }
+    const int iz = ti.iz + dz, iy = ti.iy + dy, ix = ti.ix + dx;
+    if (iz >= g.nt[0] || iy < 0 || iy >= g.nt[1] || ix < 0 || ix >= g.nt[2]) return;
+    const u32 t = (u32)(((int64_t)iz * g.nt[1] + iy) * g.nt[2] + ix);
+    if (atomicExch(&flag[t], 1u) == 0u) LIST[1 + atomicAdd(LIST, 1u)] = t;
+}
+
+// k_fix without a host read of the count (the one-read-back schedule): a fixed grid walks
+// FIX[1 .. FIX[0]], and a tile whose faces changed marks the seams to redo right away (what
+// k_mark_seams does after the host-gated k_fix).  fchg, flag and LIST[0] were cleared by
+// k_clear_front.  With nothing to fix every workgroup reads one word and leaves.
+// (no waves-per-EU bound: under the 64-VGPR bound of k_fix the loop spilled; this kernel sees
+// ~1 % of the tiles on continuous input and none on quantized input)
+template <bool HAS_MASK>
+__global__ __launch_bounds__(NTHREADS) void k_fix_dev(
+    Geom g, const u32* FIX, const BlockParam* bp, const BlockParam* guess, const float* __restrict__ in,
+    const u8* __restrict__ mask, float thr, int mode, u64* BITS, face_t* FACES, u32* COUNT, u32* P, u64* KEY,
+    u8* fchg, u32* flag, u32* LIST) {
+    __shared__ Pass1LDS L;
+    const u32 n = __builtin_amdgcn_readfirstlane(FIX[0]);
+#pragma nounroll
+    for (u32 i = blockIdx.x; i < n; i += gridDim.x) {
+        const int64_t t = __builtin_amdgcn_readfirstlane(FIX[1 + i]);
+        const TileInfo ti = uniform_ti(tile_info(g, t));
+        const BlockParam p = uniform_bp(bp[ti.block]);
+        const bool fresh = __builtin_amdgcn_readfirstlane(guess[ti.block].kind) == BP_INTERVAL;
+        if (!fresh && cc_tid() == 0) fchg[t] = 1;
+        pass1_tile<HAS_MASK>(g, t, ti, p, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L, true,
+                             fresh ? fchg : nullptr);
+        __syncthreads();                              // fchg[t] (thread 0) visible to the workgroup
+        if (cc_tid() < 14 && fchg[t]) mark_seam(g, (u32)t, (u32)cc_tid(), flag, LIST);
+        __syncthreads();                              // L is reused by the next tile
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1632,23 +1690,23 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const face_t* S, 
 // Tiles [t_begin, t_end): the seams of a z-layer chunk only read faces of that chunk and the
 // layers below it, so the library runs them on a side stream behind the k_spec chunks.
 // list (nullable): the tiles are list[1 .. list[0]] instead of the range (seams redone after k_fix)
+struct SeamsLDS {
+    alignas(16) face_t S[SP_WAVES][FACE_STRIDE];
+    u32 H[SP_WAVES][SEAM_HASH];
+    face_t E[SP_WAVES][EDGE_N];
+    u32 cnt[SP_WAVES][2];
+};
+
+// the seams of tile t (valid) for wave w; every wave of the workgroup calls it (one barrier)
 template <int STOP = 0>
-__global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* __restrict__ FACES, u64* PAIRS, u32* PC,
-                                                         u8* big, u64* IPAIRS, u32* IPC, u8* iovf,
-                                                         int64_t t_begin, int64_t t_end, const u32* list) {
-    __shared__ alignas(16) face_t Sall[SP_WAVES][FACE_STRIDE];
-    __shared__ u32 Hall[SP_WAVES][SEAM_HASH];
-    __shared__ face_t Eall[SP_WAVES][EDGE_N];
-    __shared__ u32 cnt[SP_WAVES][2];
+__device__ __forceinline__ void seams_tile(const Geom& g, const face_t* __restrict__ FACES, u64* PAIRS, u32* PC,
+                                           u8* big, u64* IPAIRS, u32* IPC, u8* iovf, int64_t t, bool valid,
+                                           SeamsLDS& LS) {
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t idx = (int64_t)blockIdx.x * SP_WAVES + w;
-    int64_t t = t_begin + idx;
-    bool valid = t < t_end;
-    if (list) {
-        const u32 nl = __builtin_amdgcn_readfirstlane(list[0]);
-        valid = idx < (int64_t)nl;
-        t = valid ? (int64_t)__builtin_amdgcn_readfirstlane(list[1 + idx]) : 0;
-    }
+    auto& Sall = LS.S;
+    auto& Hall = LS.H;
+    auto& Eall = LS.E;
+    auto& cnt = LS.cnt;
     face_t* S = Sall[w];
     u32* H = Hall[w];
     TileInfo ti;
@@ -1779,6 +1837,41 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* _
     }
 }
 
+template <int STOP = 0>
+__global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* __restrict__ FACES, u64* PAIRS, u32* PC,
+                                                         u8* big, u64* IPAIRS, u32* IPC, u8* iovf,
+                                                         int64_t t_begin, int64_t t_end, const u32* list) {
+    __shared__ SeamsLDS LS;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t idx = (int64_t)blockIdx.x * SP_WAVES + w;
+    int64_t t = t_begin + idx;
+    bool valid = t < t_end;
+    if (list) {
+        const u32 nl = __builtin_amdgcn_readfirstlane(list[0]);
+        valid = idx < (int64_t)nl;
+        t = valid ? (int64_t)__builtin_amdgcn_readfirstlane(list[1 + idx]) : 0;
+    }
+    seams_tile<STOP>(g, FACES, PAIRS, PC, big, IPAIRS, IPC, iovf, t, valid, LS);
+}
+
+// the listed tiles list[1 .. list[0]] with a fixed grid (the count stays on the device: the
+// one-read-back schedule); the loop's trip count is uniform per workgroup
+__global__ __launch_bounds__(SP_WAVES * 64) void k_seams_list(Geom g, const face_t* __restrict__ FACES, u64* PAIRS,
+                                                              u32* PC, u8* big, u64* IPAIRS, u32* IPC, u8* iovf,
+                                                              const u32* list) {
+    __shared__ SeamsLDS LS;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const u32 nl = __builtin_amdgcn_readfirstlane(list[0]);
+#pragma nounroll
+    for (int64_t i0 = (int64_t)blockIdx.x * SP_WAVES; i0 < (int64_t)nl; i0 += (int64_t)gridDim.x * SP_WAVES) {
+        const int64_t idx = i0 + w;
+        const bool valid = idx < (int64_t)nl;
+        const int64_t t = valid ? (int64_t)__builtin_amdgcn_readfirstlane(list[1 + idx]) : 0;
+        seams_tile<0>(g, FACES, PAIRS, PC, big, IPAIRS, IPC, iovf, t, valid, LS);
+        __syncthreads();
+    }
+}
+
 // Tiles whose seams read the faces of a relabelled tile whose faces changed (FIX[1 .. FIX[0]],
 // k_fix, fchg): the tile itself and the 13 tiles that have it as a lex-negative neighbour.  Each marked once (flag), listed in
 // LIST[1 .. LIST[0]] for k_seams.
@@ -1787,19 +1880,7 @@ __global__ void k_mark_seams(Geom g, const u32* FIX, const u8* fchg, u32* flag, 
     for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < 14 * n; i += gridDim.x * blockDim.x) {
         const u32 f = FIX[1 + i / 14], d = i % 14;
         if (!fchg[f]) continue;                    // same faces: every seam list still holds
-        const TileInfo ti = tile_info(g, f);
-        // d = 0: the tile; else the dependent at (+dz, dy, dx) over the 13 lex-positive offsets
-        int dz = 0, dy = 0, dx = 0;
-        if (d > 0) {
-            const int c = (int)d - 1;               // 0..12: (0,0,1), (0,1,-1..1), (1,-1..1,-1..1)
-            if (c == 0) { dx = 1; }
-            else if (c < 4) { dy = 1; dx = c - 2; }
-            else { dz = 1; dy = (c - 4) / 3 - 1; dx = (c - 4) % 3 - 1; }
-        }
-        const int iz = ti.iz + dz, iy = ti.iy + dy, ix = ti.ix + dx;
-        if (iz >= g.nt[0] || iy < 0 || iy >= g.nt[1] || ix < 0 || ix >= g.nt[2]) continue;
-        const u32 t = (u32)(((int64_t)iz * g.nt[1] + iy) * g.nt[2] + ix);
-        if (atomicExch(&flag[t], 1u) == 0u) LIST[1 + atomicAdd(LIST, 1u)] = t;
+        mark_seam(g, f, d, flag, LIST);
     }
 }
 
@@ -1958,13 +2039,14 @@ __global__ __launch_bounds__(SB_THREADS) void k_block_uf(Geom g, const u32* __re
     __shared__ u64 lkey[SB_LCAP];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t b = blockIdx.x;
-    if (big[b]) return;
+    // a block left to the global fallback ranks no roots here (RCB is read by k_block_scan)
+    if (big[b]) { if (tid == 0 && RCB) RCB[b] = 0; return; }
     const int bx = (int)(b % g.nb[2]), by = (int)((b / g.nb[2]) % g.nb[1]), bz = (int)(b / ((int64_t)g.nb[2] * g.nb[1]));
     const int iz0 = g.bt0[0][bz], iy0 = g.bt0[1][by], ix0 = g.bt0[2][bx];
     const int nz = g.btn[0][bz], ny = g.btn[1][by], nx = g.btn[2][bx];
     const int ntb = nz * ny * nx;
     if (ntb > SB_MAXT) {
-        if (tid == 0) { big[b] = 1; big[g.n_blocks] = 1; }
+        if (tid == 0) { big[b] = 1; big[g.n_blocks] = 1; if (RCB) RCB[b] = 0; }
         return;
     }
     auto tile_of = [&](int lt) -> int64_t {
@@ -1997,7 +2079,7 @@ __global__ __launch_bounds__(SB_THREADS) void k_block_uf(Geom g, const u32* __re
     __syncthreads();
     const u32 N = noff[ntb], M = poff[ntb];
     if (N > SB_LCAP) {
-        if (tid == 0) { big[b] = 1; big[g.n_blocks] = 1; }
+        if (tid == 0) { big[b] = 1; big[g.n_blocks] = 1; if (RCB) RCB[b] = 0; }
         return;
     }
     for (u32 i = tid; i < N; i += SB_THREADS) {
@@ -2068,8 +2150,11 @@ __global__ __launch_bounds__(SB_THREADS) void k_block_uf(Geom g, const u32* __re
 // their exclusive scan (merge_offsets.py:115-120) and that of the root counts; scalars[0] = sum of
 // the values, scalars[2] = number of roots, scalars[3] = whether any block took the global
 // fallback (big[nb]) -- the host reads [2..3] in one copy.  One workgroup, chunks of SB_THREADS blocks.
+// root_cap: capacity of the root arrays sized by the host before the count is known (the
+// one-read-back schedule); more roots set bit 1 of scalars[3] (the run is redone host-synchronised)
 __global__ __launch_bounds__(SB_THREADS) void k_block_scan(int64_t nb, const u32* __restrict__ RCB, u32* ROFFB,
-                                                           u64* values, u64* offsets, const u8* big, u64* scalars) {
+                                                           u64* values, u64* offsets, const u8* big, u64* scalars,
+                                                           u64 root_cap, u64* sum_out) {
     __shared__ u64 wsum[2][SB_THREADS / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     u64 carry_r = 0, carry_v = 0;
@@ -2098,7 +2183,12 @@ __global__ __launch_bounds__(SB_THREADS) void k_block_scan(int64_t nb, const u32
         carry_r += tr; carry_v += tv;
         __syncthreads();
     }
-    if (tid == 0) { scalars[0] = carry_v; scalars[2] = carry_r; scalars[3] = big[nb] ? 1ull : 0ull; }
+    if (tid == 0) {
+        scalars[0] = carry_v;
+        scalars[2] = carry_r;
+        scalars[3] = (big[nb] ? RF_BIG : 0ull) | (carry_r > root_cap ? RF_ROOTS : 0ull);
+        if (sum_out) *sum_out = carry_v;                // the slab's sum for the allgather
+    }
 }
 
 // the sorted per-block root lists as the (key, node) arrays of the generic path: keys2 = block <<
@@ -2107,10 +2197,11 @@ __global__ __launch_bounds__(SB_THREADS) void k_block_scan(int64_t nb, const u32
 // and written by its own thread only)
 __global__ __launch_bounds__(256) void k_emit_roots(const u32* __restrict__ RL, const u32* __restrict__ RCB,
                                                     const u32* __restrict__ ROFFB, u64* KEY, const u64* offsets,
-                                                    u64* keys2, u32* vals2, u32* seg_start, u32* seg_end) {
+                                                    u64* keys2, u32* vals2, u32* seg_start, u32* seg_end,
+                                                    u64 root_cap) {
     const int64_t b = blockIdx.x;
     const u32 R = RCB[b], off = ROFFB[b];
-    for (u32 r = threadIdx.x; r < R; r += 256) {
+    for (u32 r = threadIdx.x; r < R && off + (u64)r < root_cap; r += 256) {
         const u32 node = RL[(u64)b * SB_LCAP + r];
         keys2[off + r] = ((u64)b << KEY_BITS) | KEY[node];
         vals2[off + r] = node;
@@ -2203,6 +2294,41 @@ __device__ __forceinline__ u64 apply_map(u64 v, const u64* U, const u64* V, int6
     return (lo < m && U[lo] == v) ? V[lo] : v;
 }
 
+// Seam map of the one-read-back shard schedule: open addressing over the distinct seam ids
+// (keys, EMPTY = ~0; capacity mask + 1, at most a quarter full), par = union-find over slots
+// keyed by the ids (the smallest id of a set is its root), vals = the id of each slot's root.
+constexpr u64 HM_EMPTY = ~0ull;
+struct HashMap {
+    u64* keys = nullptr;
+    u32* par = nullptr;
+    u64* vals = nullptr;
+    u32 mask = 0;
+    __device__ __forceinline__ static u32 hash(u64 id) { return (u32)((id * 0x9E3779B97F4A7C15ull) >> 32); }
+    // slot of id, inserted if absent (the table never fills: sized for every id of the pairs)
+    __device__ __forceinline__ u32 insert(u64 id) const {
+        u32 h = hash(id) & mask;
+        while (true) {
+            u64 cur = __hip_atomic_load(keys + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur == HM_EMPTY) {
+                cur = atomicCAS((unsigned long long*)(keys + h), HM_EMPTY, (unsigned long long)id);
+                if (cur == HM_EMPTY) return h;
+            }
+            if (cur == id) return h;
+            h = (h + 1) & mask;
+        }
+    }
+    // the representative of id (id itself when it is not on any seam)
+    __device__ __forceinline__ u64 get(u64 id) const {
+        u32 h = hash(id) & mask;
+        while (true) {
+            const u64 cur = keys[h];
+            if (cur == id) return vals[h];
+            if (cur == HM_EMPTY) return id;
+            h = (h + 1) & mask;
+        }
+    }
+};
+
 // lut[i] = base + i for the ids of this volume (slab): i in [0, scalars[0]] (the last one is
 // the slack id n_labels - 1 on the last slab, merge_offsets.py:120)
 __global__ void k_lut_init(u64 cap, const u64* scalars, u64 base, u64* lut) {
@@ -2213,27 +2339,37 @@ __global__ void k_lut_init(u64 cap, const u64* scalars, u64 base, u64* lut) {
 // k_lut_init and k_lut in one launch, one thread per id of this volume (slab): id = base + i is
 // the rid of rank r = id - offsets[b] - 1 of the last block b whose range starts at or below it
 // (empty blocks share the next block's offset); a root's id maps to its component's
-// representative, every other id (label 0 of a block, the slack id) to itself
-__global__ void k_lut_all(u64 cap, int64_t nb, u64 base, const u64* __restrict__ offsets, const u64* __restrict__ values,
-                          const u32* __restrict__ seg_start, const u32* __restrict__ vals, u32* P, const u64* KR,
-                          const u64* U, const u64* V, int64_t m, u64* lut, u64* scalars) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= cap || i > scalars[0]) return;
-    const u64 id = base + i;
-    int64_t lo = 0, hi = nb - 1;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi + 1) >> 1;
-        if (offsets[mid] <= id) lo = mid; else hi = mid - 1;
+// representative, every other id (label 0 of a block, the slack id) to itself.  Grid-stride over
+// cap >= scalars[0] + 1 ids.  basep (nullable): the slab's id base on the device (the
+// one-read-back shard schedule); hm (keys != nullptr): the seam map as a hash table instead of U/V.
+__global__ void k_lut_all(u64 cap, int64_t nb, u64 base, const u64* basep, const u64* __restrict__ offsets,
+                          const u64* __restrict__ values, const u32* __restrict__ seg_start, const u32* __restrict__ vals,
+                          u64 nvals, u32* P, const u64* KR, const u64* U, const u64* V, int64_t m, HashMap hm,
+                          u64* lut, u64* scalars) {
+    if (basep) base = *basep;
+    const u64 n = scalars[0] + 1 < cap ? scalars[0] + 1 : cap;
+    u64 owned = 0;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        const u64 id = base + i;
+        int64_t lo = 0, hi = nb - 1;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) >> 1;
+            if (offsets[mid] <= id) lo = mid; else hi = mid - 1;
+        }
+        const u64 off = offsets[lo], v = values[lo];
+        u64 rep = id;
+        const u64 vi = (u64)seg_start[lo] + (id - off - 1);   // vals index (< nvals: the root arrays' size)
+        if (off < id && id - off < v && vi < nvals) {         // rank id - off - 1 in [0, v - 1)
+            const u32 node = vals[vi];
+            const u32 r = gfind(P, node);
+            rep = hm.keys ? hm.get(KR[r]) : apply_map(KR[r], U, V, m);
+            owned += (r == node && rep == KR[r]);          // components owned here
+        }
+        lut[i] = rep;
     }
-    const u64 off = offsets[lo], v = values[lo];
-    u64 rep = id;
-    if (off < id && id - off < v) {                       // rank id - off - 1 in [0, v - 1)
-        const u32 node = vals[seg_start[lo] + (u32)(id - off - 1)];
-        const u32 r = gfind(P, node);
-        rep = apply_map(KR[r], U, V, m);
-        if (r == node && rep == KR[r]) atomicAdd((unsigned long long*)&scalars[1], 1ull);   // components owned here
-    }
-    lut[i] = rep;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) owned += __shfl_xor(owned, o, 64);
+    if ((threadIdx.x & 63) == 0 && owned) atomicAdd((unsigned long long*)&scalars[1], (unsigned long long)owned);
 }
 
 __global__ void k_lut(int64_t n, const u32* vals, u32* P, const u64* KR, u64 base, const u64* U, const u64* V,
@@ -2479,8 +2615,18 @@ __global__ __launch_bounds__(SEAM_PAIR_THREADS) void k_seam_pairs(int64_t n, int
 // The top voxel plane as one u32 per 2x2 cube of the global cube grid (ceil(Y/2) x ceil(X/2);
 // needs even tile origins, i.e. even block_shape[1:]): (id - sub + 1) << 4 | the cube's 4
 // face-voxel bits, a quarter of the voxel plane's bytes.  One workgroup per top-layer tile.
+// subp (nullable): the id base on the device, and the 28-bit check of the one-read-back schedule
+// (scalars[0] = the slab's sum of block values; too many ids: RF_CUBES in scalars[3], plane unused)
 __global__ __launch_bounds__(NTHREADS) void k_top_cubes(Geom g, const face_t* __restrict__ FACES, u32* P,
-                                                        const u64* __restrict__ KR, u32* cubes, u64 sub) {
+                                                        const u64* __restrict__ KR, u32* cubes, u64 sub,
+                                                        const u64* subp, u64* scalars) {
+    if (subp) {
+        if (scalars[0] >= (1ull << 28) - 2) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr((unsigned long long*)&scalars[3], (unsigned long long)RF_CUBES);
+            return;
+        }
+        sub = *subp;
+    }
     const int64_t t = (int64_t)(g.nt[0] - 1) * g.nt[1] * g.nt[2] + blockIdx.x;
     const TileInfo ti = tile_info(g, t);
     const face_t* F = FACES + t * FACE_STRIDE + F_ZHI;
@@ -2495,6 +2641,139 @@ __global__ __launch_bounds__(NTHREADS) void k_top_cubes(Geom g, const face_t* __
         if (a) w = ((u32)(KR[gfind(P, base + (a & FK_MASK))] - sub + 1) << 4) | (a >> FK_BITS);
         cubes[(int64_t)(ti.y0 / 2 + cy) * CXg + ti.x0 / 2 + cx] = w;
     }
+}
+
+// ---- the one-read-back shard schedule (distributed.py fast path): everything below reads the
+// allgathered per-slab sums and seam-pair headers from device memory ------------------------
+
+// id base of slab `rank` = sum of the sums of the slabs below it; rebase this slab's block offsets
+// and the ids of its roots (k_emit_roots wrote them for base 0): offsets[b] += base,
+// KR[vals[i]] += base for the scalars[2] roots (capped at root_cap); thread 0 stores base
+__global__ void k_rebase(int64_t nb, u64* offsets, const u64* __restrict__ sums, int rank, const u32* vals, u64* KR,
+                         const u64* scalars, u64 root_cap, u64* base_out) {
+    u64 base = 0;
+    for (int r = 0; r < rank; ++r) base += sums[r];
+    const u64 nr = scalars[2] < root_cap ? scalars[2] : root_cap;
+    const u64 n = (u64)nb > nr ? (u64)nb : nr;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        if (i < (u64)nb) offsets[i] += base;
+        if (i < nr) KR[vals[i]] += base;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *base_out = base;
+}
+
+// Seam pairs of this slab's bottom face against the slab below's top plane in the cube form
+// (k_top_cubes), straight from the face planes of the bottom tile layer (no bottom voxel plane):
+// a 2x2 face cube holds one component id on each side, so each cube gives at most one pair
+// (upper id, lower id) when the two sides share a foreground voxel (6-connectivity,
+// block_faces.py:99-111).  A pair equal to the cube before it in x is dropped, the rest go
+// through the device hash set htab (key a << 32 | b; ids >= 2^32 or a full probe sequence are
+// appended anyway: the replicated union-find takes duplicates).  out = [cap + 1][2]: row 0 =
+// (count, redo flags), then the pairs; hdr[0] was zeroed.  One workgroup per bottom-layer tile.
+__global__ __launch_bounds__(NTHREADS) void k_seam_cube_pairs(Geom g, const face_t* __restrict__ FACES, u32* P,
+                                                              const u64* __restrict__ KR, const u32* __restrict__ upper,
+                                                              const u64* __restrict__ sums, int rank, u64* out, u64 cap,
+                                                              u64* htab, u32 hmask, const u64* scalars) {
+    const int64_t t = blockIdx.x;                    // bottom layer: tiles 0 .. nt[1] * nt[2] - 1
+    if (t == 0 && threadIdx.x == 0) out[1] = scalars[3];
+    const TileInfo ti = tile_info(g, t);
+    const face_t* F = FACES + t * FACE_STRIDE + F_ZLO;
+    const u32 base = (u32)(t * g.cap);
+    u64 ubase = 0;
+    for (int r = 0; r < rank - 1; ++r) ubase += sums[r];
+    const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2;
+    const int64_t CXg = (g.X + 1) / 2;
+    const int lane = threadIdx.x & 63;
+    for (int e0 = 0; e0 < ncy * CX; e0 += NTHREADS) {
+        const int e = e0 + threadIdx.x;
+        const int cy = e / CX, cx = e % CX;
+        bool emit = false;
+        u64 a = 0, b = 0;
+        if (e < ncy * CX && cx < ncx) {
+            const u32 f = F[e];
+            const u32 c = f ? upper[(int64_t)(ti.y0 / 2 + cy) * CXg + ti.x0 / 2 + cx] : 0u;
+            if (c & (f >> FK_BITS) & 0xFu) {
+                a = (u64)(c >> 4) - 1 + ubase;
+                b = KR[gfind(P, base + (f & FK_MASK))];
+                emit = true;
+                if (cx > 0) {                            // the cube before in x: same pair?
+                    const u32 fp = F[e - 1];
+                    const u32 cp = fp ? upper[(int64_t)(ti.y0 / 2 + cy) * CXg + ti.x0 / 2 + cx - 1] : 0u;
+                    if ((cp & (fp >> FK_BITS) & 0xFu) && (u64)(cp >> 4) - 1 + ubase == a &&
+                        KR[gfind(P, base + (fp & FK_MASK))] == b)
+                        emit = false;
+                }
+                if (emit && !((a | b) >> 32)) emit = seam_hash_insert(htab, hmask, (a << 32) | b) != 0;
+            }
+        }
+        const u64 bal = __ballot(emit);
+        if (bal) {
+            unsigned long long pos = 0;
+            if (lane == (int)(__ffsll((unsigned long long)bal) - 1)) pos = atomicAdd((unsigned long long*)out, (unsigned long long)__popcll(bal));
+            pos = __shfl(pos, (int)(__ffsll((unsigned long long)bal) - 1), 64) + (u64)__popcll(bal & ((1ull << lane) - 1));
+            if (emit && pos < cap) { out[2 + 2 * pos] = a; out[3 + 2 * pos] = b; }
+        }
+    }
+}
+
+// row 0 of a slab's pair buffer: hdr[1] = its redo flags (scalars[3]); hdr[0] (the count) is
+// written by k_seam_cube_pairs or stays 0 (slab 0)
+__global__ void k_seam_hdr(const u64* scalars, u64* hdr) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) hdr[1] = scalars[3];
+}
+
+// seam map over the allgathered pair buffers all[w] = [cap + 1][2] (w < world): clear, then
+// insert both ids of every pair and union their slots (smallest id = root), then resolve
+__global__ void k_map_clear(HashMap hm) {
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i <= hm.mask; i += (u64)gridDim.x * blockDim.x) {
+        hm.keys[i] = HM_EMPTY;
+        hm.par[i] = (u32)i;
+    }
+}
+
+__global__ void k_map_build(HashMap hm, const u64* __restrict__ all, int world, u64 cap) {
+    const u64 n = (u64)world * cap;
+    for (u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (u64)gridDim.x * blockDim.x) {
+        const u64 w = q / cap, j = q % cap;
+        const u64* buf = all + w * 2 * (cap + 1);
+        if (j >= buf[0]) continue;
+        const u32 sa = hm.insert(buf[2 + 2 * j]), sb = hm.insert(buf[3 + 2 * j]);
+        gunion(hm.par, hm.keys, sa, sb);
+    }
+}
+
+__global__ void k_map_resolve(HashMap hm) {
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i <= hm.mask; i += (u64)gridDim.x * blockDim.x) {
+        if (hm.keys[i] != HM_EMPTY) hm.vals[i] = hm.keys[gfind(hm.par, (u32)i)];
+    }
+}
+
+// The one read-back of a run, gathered into one contiguous buffer (one copy): out[0] = redo
+// flags (this run's scalars[3]; with shards, OR over every slab's header plus RF_PAIRS when a
+// slab had more pairs than cap and RF_CUBES when a slab's ids exceed the 28-bit cube form),
+// [1] = largest pair count of a slab, [2] = sum over the slabs (or this volume) of the block
+// values, [3] = this slab's id base, [4] = tiles k_fix relabelled, [5..8] = scalars[0..3],
+// [16 ..) = values[nb], then offsets[nb].  all == nullptr: a single volume.
+__global__ void k_status(const u64* scalars, const u32* FIX, const u64* all, int world, u64 cap, const u64* sums,
+                         const u64* basep, int64_t nb, const u64* values, const u64* offsets, u64* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        u64 flags = scalars[3], mx = 0, tot = scalars[0];
+        if (all) {
+            tot = 0;
+            for (int w = 0; w < world; ++w) {
+                const u64* h = all + (u64)w * 2 * (cap + 1);
+                flags |= h[1];
+                mx = h[0] > mx ? h[0] : mx;
+                tot += sums[w];
+                if (sums[w] >= (1ull << 28) - 2) flags |= RF_CUBES;
+            }
+            if (mx > cap) flags |= RF_PAIRS;
+        }
+        out[0] = flags; out[1] = mx; out[2] = tot; out[3] = basep ? *basep : 0ull; out[4] = FIX[0];
+        for (int k = 0; k < 4; ++k) out[5 + k] = scalars[k];
+    }
+    if (i < nb) { out[16 + i] = values[i]; out[16 + nb + i] = offsets[i]; }
 }
 
 // copy of the seam-pair ids with their largest value (atomicMax per workgroup into *mx): sizes the
@@ -2564,7 +2843,8 @@ __device__ __forceinline__ void store2(u64* __restrict__ out, int64_t idx, u64 v
 template <bool UF>
 __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restrict__ BITS, const u32* COUNT,
                                                     const u64* __restrict__ FIN, u32* P, const u64* lut, u64 id_base,
-                                                    int64_t m, u64* __restrict__ out, int order) {
+                                                    int64_t m, u64* __restrict__ out, int order,
+                                                    const u64* id_base_dev, const u64* lut_last) {
     __shared__ u64 rows[NROWS];             // split bit rows (see tile_ccl)
     __shared__ TileCCL T;
     __shared__ u64 lab[LABCAP];
@@ -2596,10 +2876,14 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
         return;
     }
     const u32 base = (u32)(t * g.cap);
+    if (UF && id_base_dev) id_base = __builtin_amdgcn_readfirstlane(*id_base_dev);
+    // lut_last (nullable): the LUT's last index on the device (the one-read-back shard schedule,
+    // whose ids are only checked after the run: a run to be redone must not read past the LUT)
+    const u64 lmax = (UF && lut_last) ? *lut_last : ~0ull;
     auto label = [&](u32 node) -> u64 {
         if (!UF) return FIN[node];
         const u64 v = FIN[gfind(P, node)];
-        return m ? lut[v - id_base] : v;
+        return m ? (v - id_base <= lmax ? lut[v - id_base] : v) : v;
     };
     constexpr int LPT = LABCAP / NTHREADS;
     u64 lv[LPT];

@@ -118,6 +118,13 @@ struct cc_ctx {
     int debug = 0;         // CC_DEBUG_* test hooks
     int front_chunks = 1;  // z-layer chunks of the speculative front (CC_FRONT_CHUNKS)
     int64_t quirk_jobs = 0;  // CC_OPT_EMPTY_JOB_QUIRK: emulate the reference's empty-job branch for max_jobs
+    // one-read-back schedule (see run_pipeline): capacity of the root arrays sized before the count
+    // is known (grown after a run that exceeded it), and whether the last volume of this geometry
+    // needed the global-stitch fallback (then the host-synchronised schedule runs directly)
+    uint64_t root_cap = 0;
+    bool fast_big = false;
+    std::vector<int32_t> fast_big_tab;
+    DevBuf status, dbase, hmap_keys, hmap_par, hmap_vals;
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, ProfEntry> prof_acc;
@@ -271,6 +278,10 @@ struct RunState {
     bool rid0 = false;         // k_emit_roots already wrote the roots' ids for base 0
     bool sum_known = false;    // sum_v already read back (phase_local's fast path)
     bool any_iovf = true;      // some tile's block-face pair list overflowed (or not read back)
+    bool fast = false;         // the one-read-back schedule: counts stay on the device
+    bool base_dev = false;     // the id base lives on the device (c->dbase; shards of the fast schedule)
+    uint64_t redo = 0;         // RF_* flags read back by phase_final (fast schedule): run again synchronised
+    uint64_t n_pairs_max = 0;  // largest seam-pair count of a slab (shards of the fast schedule)
 };
 
 static RunState& state(cc_ctx* c) {
@@ -279,11 +290,14 @@ static RunState& state(cc_ctx* c) {
 }
 
 // stats -> params -> pass1 -> intra-block stitch -> roots -> sort -> offsets (local)
+// fast: the one-read-back schedule -- no host read-back in this phase (the k_fix count, the root
+// count and the fallback flags stay on the device; see run_pipeline)
 static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const int64_t shape[3],
                         const int64_t block_shape[3], double threshold, int mode, int64_t zoff,
-                        bool local_only) {
+                        bool local_only, bool fast = false, uint64_t* sum_out = nullptr) {
     RunState& st = state(c);
     st = RunState();
+    st.fast = fast;
     st.hg = make_geom(shape, block_shape, zoff);
     upload_geom(c, st.hg);
     Geom& g = st.hg.g;
@@ -337,11 +351,14 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         c->iovf.ensure(nt + 1);
         c->rc.ensure((nt + 1) * sizeof(u32));
         c->roff.ensure((nt + 1) * sizeof(u32));
+        c->mark.ensure((size_t)(2 * nt + 1) * sizeof(u32) + nt);
         const bool lds_seams = !(c->debug & CC_DEBUG_GLOBAL_STITCH);
         launch(c, "k_clear_front", [&] {
+            u32* mflag = fast ? c->mark.as<u32>() : nullptr;
+            u8* mchg = fast ? (u8*)(c->mark.as<u32>() + 2 * nt + 1) : nullptr;
             k_clear_front<<<grid1d(std::max(nt + 1, 2 * nb + 1)), 256, 0, s>>>(
                 nb, nt, smin, smax, c->scalars.as<u64>(), FIX, c->big.as<u8>(), c->iovf.as<u8>(), c->ipc.as<u32>(),
-                c->seg.as<u32>(), c->rc.as<u32>() + nt, lds_seams ? 0 : 1);
+                c->seg.as<u32>(), c->rc.as<u32>() + nt, lds_seams ? 0 : 1, mflag, mchg);
         });
         launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART); });
         launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, mode, guess); });
@@ -393,12 +410,25 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         launch(c, "k_params_verify", [&] {
             k_params_verify<<<grid_stride(nt), 256, 0, s>>>(g, guess, smin, smax, sflag, thr, mode, bp, TB, FIX);
         });
-        c->mark.ensure((size_t)(2 * nt + 1) * sizeof(u32) + nt);
         u32* flag = c->mark.as<u32>();
         u32* list = flag + nt;
         u8* fchg = (u8*)(list + nt + 1);
         u32 nfix = 0;
-        {
+        if (fast) {
+            // device-gated: a fixed grid walks the k_fix list (usually empty) and marks the seams
+            // of changed tiles; k_seams_list redoes the marked ones (k_clear_front cleared both)
+            launch(c, "k_fix", [&] {
+                const unsigned grid = (unsigned)std::min<int64_t>(nt, 1024);
+                if (mask) k_fix_dev<true><<<grid, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, mask, thr, mode, BITS, FACES, COUNT, P, KR, fchg, flag, list);
+                else k_fix_dev<false><<<grid, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR, fchg, flag, list);
+            });
+            if (lds_seams)
+                launch(c, "k_seams", [&] {
+                    const unsigned grid = (unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, 2048);
+                    k_seams_list<<<grid, SP_WAVES * 64, 0, s>>>(g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), c->big.as<u8>(),
+                                                               c->ipairs.as<u64>(), c->ipc.as<u32>(), c->iovf.as<u8>(), list);
+                });
+        } else {
             Readback rb(c, 64);
             rb.add(&nfix, FIX, sizeof(u32));
             rb.wait(false);
@@ -457,8 +487,27 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     u8 any_big = 1;
     u64 nr_blocks = 0;
     st.any_iovf = true;
+    if (fast) {
+        // no read-back: the root arrays get the context's capacity, k_block_scan flags a run that
+        // needs more (RF_ROOTS) or the global fallback (RF_BIG); phase_final reads the flags
+        CC_REQUIRE(block_uf, "the one-read-back schedule needs the LDS block union-find");
+        // (CC_ROOT_CAP: test hook, a context's first capacity)
+        if (c->root_cap == 0) c->root_cap = (uint64_t)env_int("CC_ROOT_CAP", std::max<int64_t>(1 << 16, 4 * nt));
+        const uint64_t cap = c->root_cap;
+        launch(c, "k_block_scan", [&] { k_block_scan<<<1, SB_THREADS, 0, s>>>(nb, RCB, ROFFB, values, offsets, big, scalars, cap, sum_out); });
+        st.nr = (int64_t)cap;
+        ensure_roots((int64_t)cap);
+        launch(c, "k_emit_roots", [&] {
+            k_emit_roots<<<(unsigned)nb, 256, 0, s>>>(RL, RCB, ROFFB, KR, offsets, c->keys2.as<u64>(), c->vals2.as<u32>(),
+                                                      seg_start, seg_end, cap);
+        });
+        st.rid0 = true;
+        st.stage = 1;
+        return;
+    }
+    CC_REQUIRE(sum_out == nullptr, "sum_out: fast schedule only");
     if (block_uf) {
-        launch(c, "k_block_scan", [&] { k_block_scan<<<1, SB_THREADS, 0, s>>>(nb, RCB, ROFFB, values, offsets, big, scalars); });
+        launch(c, "k_block_scan", [&] { k_block_scan<<<1, SB_THREADS, 0, s>>>(nb, RCB, ROFFB, values, offsets, big, scalars, ~0ull, nullptr); });
         u64 sc[4] = {0, 0, 0, 1};
         u8 ovf = 1;
         Readback rb(c, 64);
@@ -484,7 +533,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         ensure_roots(nr);
         launch(c, "k_emit_roots", [&] {
             k_emit_roots<<<(unsigned)nb, 256, 0, s>>>(RL, RCB, ROFFB, KR, offsets, c->keys2.as<u64>(), c->vals2.as<u32>(),
-                                                      seg_start, seg_end);
+                                                      seg_start, seg_end, ~0ull);
         });
         st.rid0 = true;
         st.stage = 1;
@@ -536,13 +585,15 @@ static uint64_t read_sum_v(cc_ctx* c) {
     return v;
 }
 
+static void rid_unions(cc_ctx* c);
+
 // global ids: offsets += base; rank -> rid; 6-connected unions across block faces
 static void phase_rid(cc_ctx* c, uint64_t base) {
     RunState& st = state(c);
     CC_REQUIRE(st.stage == 1, "phase order: call begin first");
     Geom& g = st.hg.g;
     hipStream_t s = cstream(c);
-    const int64_t nb = g.n_blocks, nr = st.nr, nt = g.n_tiles;
+    const int64_t nb = g.n_blocks, nr = st.nr;
     st.base = base;
     u64* offsets = c->offsets.as<u64>();
     if (base) launch(c, "k_add_base", [&] { k_add_base<<<grid1d(nb), 256, 0, s>>>(nb, offsets, base); });
@@ -551,6 +602,33 @@ static void phase_rid(cc_ctx* c, uint64_t base) {
             k_assign_rid<<<grid1d(nr), 256, 0, s>>>(nr, c->keys2.as<u64>(), c->vals2.as<u32>(), c->seg.as<u32>(),
                                                     offsets, c->KR.as<u64>());
         });
+    rid_unions(c);
+}
+
+// shards of the one-read-back schedule: the id base from the allgathered sums on the device
+static void phase_rid_dev(cc_ctx* c, const uint64_t* sums, int rank) {
+    RunState& st = state(c);
+    CC_REQUIRE(st.stage == 1 && st.fast, "phase order: call cc_shard_dev_begin first");
+    Geom& g = st.hg.g;
+    hipStream_t s = cstream(c);
+    const int64_t nb = g.n_blocks;
+    c->dbase.ensure(16);
+    st.base_dev = true;
+    st.base = 0;
+    launch(c, "k_rebase", [&] {
+        k_rebase<<<(unsigned)std::min<int64_t>(grid1d(std::max<int64_t>(nb, st.nr)), 1024), 256, 0, s>>>(
+            nb, c->offsets.as<u64>(), sums, rank, c->vals2.as<u32>(), c->KR.as<u64>(), c->scalars.as<u64>(),
+            (u64)st.nr, c->dbase.as<u64>());
+    });
+    rid_unions(c);
+}
+
+// 6-connected unions across the block faces of this volume / slab (and the empty-job emulation)
+static void rid_unions(cc_ctx* c) {
+    RunState& st = state(c);
+    Geom& g = st.hg.g;
+    hipStream_t s = cstream(c);
+    const int64_t nb = g.n_blocks, nt = g.n_tiles;
     st.identity_lut = false;
     if (!st.local_only && c->quirk_jobs > 0) {
         // reference empty-job branch (merge_assignments.py:115-123): block_faces job j owns blocks
@@ -705,8 +783,16 @@ static void phase_map(cc_ctx* c, const u64* pairs, int64_t n) {
     st.n_map = m;
 }
 
+// the seam map of the one-read-back shard schedule: every slab's pair buffer on the device
+struct SeamDev {
+    const u64* all = nullptr;   // [world][cap + 1][2]: (count, flags), then the pairs
+    int world = 0;
+    uint64_t cap = 0;
+    const u64* sums = nullptr;  // [world] sums of block values
+};
+
 // LUT, final label per node, bit rows -> uint64 labels; small artefacts to host
-static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
+static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev* sd = nullptr) {
     RunState& st = state(c);
     CC_REQUIRE(st.stage == 2, "phase order: call assign first");
     Geom& g = st.hg.g;
@@ -721,8 +807,30 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
     const u64* U = st.n_map ? c->map_ids.as<u64>() : nullptr;
     const u64* V = st.n_map ? c->map_vals.as<u64>() : nullptr;
     const int64_t m = st.n_map;
+    const u64* basep = st.base_dev ? c->dbase.as<u64>() : nullptr;
     u64* FIN = KR;
     const uint64_t lut_cap = (uint64_t)nr + (uint64_t)nb + 1;
+    HashMap hm;
+    if (sd) {
+        // seam map over every slab's pairs: slots for all their ids at <= 1/4 load
+        CC_REQUIRE(st.fast && basep, "phase order: the device seam map follows cc_shard_dev_assign");
+        uint64_t hc = 1024;
+        while (hc < 8 * (uint64_t)sd->world * sd->cap) hc <<= 1;
+        CC_REQUIRE(hc <= (1ull << 31), "seam map too large");
+        c->hmap_keys.ensure(hc * sizeof(u64));
+        c->hmap_par.ensure(hc * sizeof(u32));
+        c->hmap_vals.ensure(hc * sizeof(u64));
+        hm.keys = c->hmap_keys.as<u64>();
+        hm.par = c->hmap_par.as<u32>();
+        hm.vals = c->hmap_vals.as<u64>();
+        hm.mask = (u32)(hc - 1);
+        const unsigned gc = (unsigned)std::min<uint64_t>(1024, (hc + 255) / 256);
+        launch(c, "k_map_clear", [&] { k_map_clear<<<gc, 256, 0, s>>>(hm); });
+        launch(c, "k_map_build", [&] {
+            k_map_build<<<(unsigned)std::min<uint64_t>(1024, (sd->world * sd->cap + 255) / 256), 256, 0, s>>>(hm, sd->all, sd->world, sd->cap);
+        });
+        launch(c, "k_map_resolve", [&] { k_map_resolve<<<gc, 256, 0, s>>>(hm); });
+    }
     if (st.local_only) {
         c->FIN.ensure(nodes * sizeof(u64));
         FIN = c->FIN.as<u64>();
@@ -733,8 +841,10 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
         u64* lut = c->lut.as<u64>();
         const u64 base = st.base;
         launch(c, "k_lut_all", [&] {
-            k_lut_all<<<grid1d(lut_cap), 256, 0, s>>>(lut_cap, nb, base, offsets, c->values.as<u64>(), c->seg.as<u32>(),
-                                                      c->vals2.as<u32>(), P, KR, U, V, m, lut, scalars);
+            // grid-stride over the ids (their count scalars[0] + 1 is on the device)
+            k_lut_all<<<std::min<unsigned>(grid1d(lut_cap), 2048), 256, 0, s>>>(
+                lut_cap, nb, base, basep, offsets, c->values.as<u64>(), c->seg.as<u32>(), c->vals2.as<u32>(), (u64)nr, P, KR,
+                U, V, m, hm, lut, scalars);
         });
         c->lut_valid = true;
     }
@@ -746,14 +856,45 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
         if (const char* e = std::getenv("CC_PASS2_ORDER"); e && *e) order = std::atoi(e) ? 1 : 0;
         // CC_LDS_PAD_P2 (A/B only): extra dynamic LDS per workgroup, i.e. fewer tiles per CU
         const unsigned pad = (unsigned)env_int("CC_LDS_PAD_P2", 0);
-        if (st.local_only) k_pass2<false><<<(unsigned)nt, NTHREADS, pad, s>>>(g, c->bits.as<u64>(), COUNT, FIN, nullptr, nullptr, 0, 0, out, order);
-        else k_pass2<true><<<(unsigned)nt, NTHREADS, pad, s>>>(g, c->bits.as<u64>(), COUNT, KR, P, c->lut.as<u64>(), st.base, m, out, order);
+        // with a seam map every label goes through the slab's LUT (m = 1)
+        const int64_t mm = sd ? 1 : m;
+        if (st.local_only) k_pass2<false><<<(unsigned)nt, NTHREADS, pad, s>>>(g, c->bits.as<u64>(), COUNT, FIN, nullptr, nullptr, 0, 0, out, order, nullptr, nullptr);
+        else k_pass2<true><<<(unsigned)nt, NTHREADS, pad, s>>>(g, c->bits.as<u64>(), COUNT, KR, P, c->lut.as<u64>(), st.base, mm, out, order,
+                                                               basep, sd ? scalars : nullptr);
     });
 
     u64 sc[4] = {0, 0, 0, 0};
     c->h_values.resize(nb);
     c->h_offsets.resize(nb);
-    {
+    st.redo = 0;
+    uint64_t total = 0;
+    if (st.fast) {
+        // the one read-back of the run: flags, counts and the block values / offsets gathered by
+        // one kernel into one buffer, one copy
+        const size_t nst = 16 + 2 * (size_t)nb;
+        c->status.ensure(nst * sizeof(u64));
+        u64* stat = c->status.as<u64>();
+        const int64_t nth = std::max<int64_t>(nb, 1);
+        launch(c, "k_status", [&] {
+            k_status<<<grid1d(nth), 256, 0, s>>>(scalars, (const u32*)(c->spec.as<u32>() + 4 * nt + 4 * SAMPLE_PARTS * nb),
+                                                 sd ? sd->all : nullptr, sd ? sd->world : 0, sd ? sd->cap : 0,
+                                                 sd ? sd->sums : nullptr, basep, nb, c->values.as<u64>(), offsets, stat);
+        });
+        std::vector<u64> h(nst);
+        {
+            Readback rb(c, nst * sizeof(u64) + 64);
+            rb.add(h.data(), stat, nst * sizeof(u64));
+            rb.wait();
+        }
+        st.redo = h[0];
+        st.n_pairs_max = h[1];
+        total = h[2];
+        if (basep) st.base = h[3];
+        st.n_fix = h[4];
+        for (int k = 0; k < 4; ++k) sc[k] = h[5 + k];
+        std::memcpy(c->h_values.data(), h.data() + 16, nb * sizeof(u64));
+        std::memcpy(c->h_offsets.data(), h.data() + 16 + nb, nb * sizeof(u64));
+    } else {
         Readback rb(c, 4 * sizeof(u64) + 2 * nb * sizeof(u64) + 64);
         rb.add(sc, scalars, 4 * sizeof(u64));
         rb.add(c->h_values.data(), c->values.p, nb * sizeof(u64));
@@ -766,21 +907,53 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res) {
     c->n_labels = sc[0] + 1;        // LUT length of this volume (slab): ids base .. base + sum_v
     if (res) {
         res->n_blocks = nb;
-        res->n_labels = st.base + sc[0] + 1;   // global on the last slab / single GPU
+        res->n_labels = sd ? total + 1 : st.base + sc[0] + 1;   // global (every slab: the allgathered sums)
         res->max_id = res->n_labels - 1;       // lut[n_labels-1] = n_labels-1 is never merged
         res->n_components = st.local_only ? 0 : sc[1];
-        res->n_block_components = (uint64_t)nr;
+        res->n_block_components = st.fast ? sc[2] : (uint64_t)nr;
         res->n_relabelled_tiles = st.n_fix;
         res->identity_lut = st.identity_lut ? 1 : 0;
     }
 }
 
+// The default schedule of a single volume: every launch of the five stages is enqueued without
+// a host read-back (the k_fix count, the root count and the fallback flags stay on the device;
+// the root arrays get the context's capacity) and the run ends in ONE read-back (k_status).
+// If that read-back says the run needed more than the optimistic launch sequence covers -- the
+// global-stitch fallback of a block (RF_BIG) or more roots than the capacity (RF_ROOTS) -- the
+// volume is labelled again by the host-synchronised schedule, which sizes everything from
+// read-back counts; the output is fully rewritten, so which schedule ran never shows in the
+// result.  CC_FAST=0 (A/B, tests) forces the host-synchronised schedule.
+static bool fast_ok(cc_ctx* c) {
+    if (c->debug & CC_DEBUG_GLOBAL_STITCH) return false;
+    if (c->quirk_jobs > 0 || c->front_chunks > 1) return false;
+    return env_int("CC_FAST", 1) != 0;
+}
+
 static void run_pipeline(cc_ctx* c, const float* in, const uint8_t* mask, const int64_t shape[3],
                          const int64_t block_shape[3], double threshold, int mode, uint64_t* out,
                          bool local_only, cc_result* res) {
+    if (!local_only && fast_ok(c)) {
+        const HostGeom hg = make_geom(shape, block_shape, 0);
+        // a volume of this geometry needed the fallback last time: go synchronised directly
+        if (!(c->fast_big && c->fast_big_tab == hg.tab)) {
+            phase_local(c, in, mask, shape, block_shape, threshold, mode, 0, false, true);
+            phase_rid(c, 0);
+            phase_final(c, out, res);
+            const uint64_t redo = state(c).redo;
+            if (!redo) {
+                c->fast_big = false;
+                return;
+            }
+            c->fast_big = (redo & RF_BIG) != 0;
+            if (c->fast_big) c->fast_big_tab = hg.tab;
+        }
+    }
     phase_local(c, in, mask, shape, block_shape, threshold, mode, 0, local_only);
     phase_rid(c, 0);
     phase_final(c, out, res);
+    // the next optimistic run of this context gets room for this many roots
+    if (!state(c).local_only) c->root_cap = std::max<uint64_t>(c->root_cap, (uint64_t)state(c).nr + (uint64_t)state(c).nr / 4 + 1024);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -835,7 +1008,8 @@ void cc_destroy(cc_ctx* c) {
                       &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
                       &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec, &c->mark, &c->bflag,
                       &c->ev_main, &c->ev_z, &c->ev_seg, &c->ev_gt, &c->ev_flag, &c->ev_part, &c->rl_wg,
-                      &c->gs1, &c->gs2, &c->gs_tab, &c->mask_xmap, &c->seam_hash, &c->ws_tab, &c->ws_buf};
+                      &c->gs1, &c->gs2, &c->gs_tab, &c->mask_xmap, &c->seam_hash, &c->ws_tab, &c->ws_buf,
+                      &c->status, &c->dbase, &c->hmap_keys, &c->hmap_par, &c->hmap_vals};
     for (DevBuf* b : bufs) b->release();
     c->pin.release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }

@@ -177,6 +177,8 @@ int cc_shard_begin(cc_ctx* c, const float* in, const uint8_t* mask, const int64_
         HIP_OK(hipSetDevice(c->device));
         phase_local(c, in, mask, slab_shape, block_shape, threshold, to_mode(mode), z_offset, false);
         *sum_values = read_sum_v(c);
+        // room for this many roots in the next one-read-back step of this context
+        c->root_cap = std::max<uint64_t>(c->root_cap, (uint64_t)state(c).nr + (uint64_t)state(c).nr / 4 + 1024);
     })
 }
 
@@ -311,7 +313,7 @@ int cc_shard_top_cubes32(cc_ctx* c, uint32_t* cubes) {
         const unsigned nlayer = (unsigned)((int64_t)g.nt[1] * g.nt[2]);
         launch(c, "k_top_cubes", [&] {
             k_top_cubes<<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), cubes,
-                                                     (u64)st.base);
+                                                     (u64)st.base, nullptr, nullptr);
         });
     })
 }
@@ -343,3 +345,110 @@ int cc_shard_finish(cc_ctx* c, const uint64_t* pairs, int64_t n_pairs, uint64_t*
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// z-slab sharding, one-read-back schedule (distributed.py's default): the sums, the id base, the
+// seam planes and pairs stay on the device between the collectives; cc_shard_dev_finish is the
+// step's one host read-back.  Its status says whether every slab's optimistic assumptions held
+// (the same answer on every rank: it is computed from the allgathered pair headers and sums);
+// if not, the caller runs the host-synchronised schedule (cc_shard_begin ...) for this step.
+// ---------------------------------------------------------------------------------------------
+extern "C" {
+
+int cc_shard_dev_begin(cc_ctx* c, const float* in, const uint8_t* mask, const int64_t slab_shape[3],
+                       const int64_t block_shape[3], double threshold, int mode, int64_t z_offset,
+                       uint64_t* sum_dev) {
+    CC_TRY({
+        CC_REQUIRE(c && in && slab_shape && block_shape && sum_dev, "NULL argument");
+        CC_REQUIRE(z_offset >= 0 && z_offset % block_shape[0] == 0,
+                   "slab z offset must be a multiple of block_shape[0] (seams on block faces)");
+        CC_REQUIRE(fast_ok(c), "the one-read-back schedule is off on this context (debug flags / options)");
+        HIP_OK(hipSetDevice(c->device));
+        phase_local(c, in, mask, slab_shape, block_shape, threshold, to_mode(mode), z_offset, false, true, sum_dev);
+    })
+}
+
+int cc_shard_dev_assign(cc_ctx* c, const uint64_t* sums_dev, int rank, int world) {
+    CC_TRY({
+        CC_REQUIRE(c && sums_dev && rank >= 0 && rank < world, "bad arguments");
+        HIP_OK(hipSetDevice(c->device));
+        phase_rid_dev(c, sums_dev, rank);
+    })
+}
+
+int cc_shard_dev_top_cubes(cc_ctx* c, uint32_t* cubes_dev) {
+    CC_TRY({
+        CC_REQUIRE(c && cubes_dev, "NULL argument");
+        HIP_OK(hipSetDevice(c->device));
+        RunState& st = state(c);
+        CC_REQUIRE(st.stage == 2 && st.base_dev, "phase order: call cc_shard_dev_assign first");
+        Geom& g = st.hg.g;
+        for (int a = 1; a < 3; ++a)
+            CC_REQUIRE(g.nb[a] == 1 || st.bs[a] % 2 == 0, "cube form needs even tile origins (even block_shape[1:])");
+        hipStream_t s = cstream(c);
+        const unsigned nlayer = (unsigned)((int64_t)g.nt[1] * g.nt[2]);
+        launch(c, "k_top_cubes", [&] {
+            k_top_cubes<<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), cubes_dev,
+                                                     0, c->dbase.as<u64>(), c->scalars.as<u64>());
+        });
+    })
+}
+
+int cc_shard_dev_seam_pairs(cc_ctx* c, const uint32_t* upper_cubes_dev, const uint64_t* sums_dev, int rank,
+                            uint64_t* hdr_pairs_dev, int64_t cap) {
+    CC_TRY({
+        CC_REQUIRE(c && sums_dev && hdr_pairs_dev && cap >= 0, "bad arguments");
+        CC_REQUIRE(!upper_cubes_dev || rank > 0, "slab 0 has no slab below");
+        HIP_OK(hipSetDevice(c->device));
+        RunState& st = state(c);
+        CC_REQUIRE(st.stage == 2 && st.base_dev, "phase order: call cc_shard_dev_assign first");
+        Geom& g = st.hg.g;
+        hipStream_t s = cstream(c);
+        HIP_OK(hipMemsetAsync(hdr_pairs_dev, 0, 2 * sizeof(u64), s));
+        if (!upper_cubes_dev) {
+            launch(c, "k_seam_hdr", [&] { k_seam_hdr<<<1, 64, 0, s>>>(c->scalars.as<u64>(), hdr_pairs_dev); });
+            return 0;
+        }
+        for (int a = 1; a < 3; ++a)
+            CC_REQUIRE(g.nb[a] == 1 || st.bs[a] % 2 == 0, "cube form needs even tile origins (even block_shape[1:])");
+        constexpr int64_t HS = 1 << 16;              // the seam pair hash set (see k_seam_cube_pairs)
+        c->seam_hash.ensure(HS * sizeof(u64));
+        HIP_OK(hipMemsetAsync(c->seam_hash.p, 0xFF, HS * sizeof(u64), s));
+        const unsigned nlayer = (unsigned)((int64_t)g.nt[1] * g.nt[2]);
+        launch(c, "k_seam_cube_pairs", [&] {
+            k_seam_cube_pairs<<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(),
+                                                           upper_cubes_dev, sums_dev, rank, hdr_pairs_dev, (u64)cap,
+                                                           c->seam_hash.as<u64>(), (u32)(HS - 1), c->scalars.as<u64>());
+        });
+    })
+}
+
+// all_dev: [world][cap + 1][2] (every slab's buffer of cc_shard_dev_seam_pairs, allgathered);
+// status_host[4] (nullable): redo flags (RF_*: non-zero -> run this step host-synchronised), the
+// largest pair count of a slab, the global n_labels, this slab's id base
+int cc_shard_dev_finish(cc_ctx* c, const uint64_t* all_dev, int world, int64_t cap, const uint64_t* sums_dev,
+                        uint64_t* labels_dev, cc_result* res, uint64_t* status_host) {
+    CC_TRY({
+        CC_REQUIRE(c && all_dev && sums_dev && labels_dev && world >= 1 && cap >= 0, "bad arguments");
+        HIP_OK(hipSetDevice(c->device));
+        SeamDev sd;
+        sd.all = all_dev;
+        sd.world = world;
+        sd.cap = (uint64_t)cap;
+        sd.sums = sums_dev;
+        phase_final(c, labels_dev, res, &sd);
+        RunState& st = state(c);
+        if (status_host) {
+            status_host[0] = st.redo;
+            status_host[1] = st.n_pairs_max;
+            status_host[2] = res ? res->n_labels : 0;
+            status_host[3] = st.base;
+        }
+        // a slab with more roots than the capacity: room for them in the next step (the step is
+        // redone host-synchronised, which counts them)
+        if (st.redo & RF_ROOTS) c->root_cap = std::max<uint64_t>(c->root_cap, 2 * c->root_cap);
+    })
+}
+
+}  // extern "C"
+

@@ -19,6 +19,17 @@ what crosses GPUs is O(planes), never O(volume):
 
 The collectives go through torch.distributed: backend "nccl" is RCCL on ROCm (GPU tensors);
 "gloo" runs the same schedule on CPU tensors (tests/test_distributed_cpu.py).
+
+Default: the one-read-back schedule (cc_shard_dev_*).  The same eight steps, but the sums, the id
+base, the seam plane and the seam pairs never leave device memory: the allgathers and the
+point-to-point send run on device buffers in stream order behind the library's kernels, and the
+rank's only host synchronisation is the status read at the end of the step.  The pair buffers have
+a fixed capacity (row 0 of each = (count, redo flags)).  The status is computed from the
+allgathered headers and sums, so every rank reaches the same verdict; when an optimistic bound did
+not hold (more pairs than the capacity, ids beyond the cube form, a block needing the global
+stitch fallback, more roots than the context holds) every rank relabels the step with the
+host-synchronised schedule above, and the bound that failed is raised (pair capacity) or the
+schedule is left for good (the others).
 """
 import numpy as np
 
@@ -67,6 +78,11 @@ class TorchComm:
         return out, self.world * mx
 
 
+    def allgather_into(self, out, inp):
+        """out[world * n] = every rank's inp[n] (device tensors, stream-ordered: no host sync)."""
+        self.dist.all_gather_into_tensor(out, inp, group=self.group)
+
+
 class StagedComm(TorchComm):
     """TorchComm over a CPU-only backend ('gloo') for GPU tensors: each collective stages its
     operands through host memory.  Only for rehearsing the multi-process schedule where RCCL
@@ -105,6 +121,28 @@ class StagedComm(TorchComm):
         out = torch.empty((self.world * mx, 2), dtype=torch.int64)
         self.dist.all_gather_into_tensor(out, buf, group=self.group)
         return out.to(self.device), self.world * mx
+
+    def allgather_into(self, out, inp):
+        hout = torch_empty_like_cpu(out)
+        self.dist.all_gather_into_tensor(hout, inp.cpu(), group=self.group)
+        out.copy_(hout)
+
+
+def torch_empty_like_cpu(t):
+    import torch
+    return torch.empty(tuple(t.shape), dtype=t.dtype)
+
+
+# seam pairs per slab the one-read-back schedule's pair buffers hold at first (raised after a
+# step that needed more: the largest count seen, x2, every rank alike)
+PAIR_CAP = 2048
+
+
+def next_pow2(n):
+    p = 1
+    while p < n:
+        p <<= 1
+    return p
 
 
 def check_slabs(global_shape, block_shape, z0, zs):
@@ -158,6 +196,11 @@ class ShardedLabeler:
         self.sums = None
         self.form = None
         self.force_form = force_form          # tests: a wider seam-plane form than the ids need
+        # one-read-back schedule (cubes32 seam planes): device-resident sums and pair buffers
+        self.fast = self.cubes_ok and force_form is None
+        self.pair_cap = PAIR_CAP
+        self.redo_steps = 0                   # steps relabelled by the host-synchronised schedule
+        self._dev = None
 
     def _plane(self, form, which):
         """send / receive buffer of a seam-plane form ('cubes32', 'voxel32', 'voxel64')."""
@@ -181,11 +224,63 @@ class ShardedLabeler:
             return 'voxel32'
         return 'voxel64'
 
+    def _dev_buffers(self):
+        import torch
+        w = self.comm.world
+        if self._dev is None or self._dev['cap'] != self.pair_cap:
+            dev = self.device
+            self._dev = {'cap': self.pair_cap,
+                         'sum': torch.zeros(1, dtype=torch.int64, device=dev),
+                         'sums': torch.zeros(w, dtype=torch.int64, device=dev),
+                         'hdr': torch.zeros((self.pair_cap + 1, 2), dtype=torch.int64, device=dev),
+                         'all': torch.zeros((w * (self.pair_cap + 1), 2), dtype=torch.int64, device=dev)}
+        return self._dev
+
     def label(self, x, threshold, mode='greater', mask=None, out=None):
         import torch
-        ctx, comm = self.ctx, self.comm
         if out is None:
             out = torch.empty(tuple(x.shape), dtype=torch.int64, device=x.device)
+        if self.fast:
+            res = self._label_fast(x, threshold, mode, mask, out)
+            if res is not None:
+                return res
+            self.redo_steps += 1
+        return self._label_sync(x, threshold, mode, mask, out)
+
+    def _label_fast(self, x, threshold, mode, mask, out):
+        """One step of the one-read-back schedule; None when it must be redone synchronised."""
+        ctx, comm = self.ctx, self.comm
+        r, w = comm.rank, comm.world
+        b = self._dev_buffers()
+        ctx.shard_dev_begin(x, self.block_shape, threshold, mode, self.z0, b['sum'], mask)
+        comm.allgather_into(b['sums'], b['sum'])
+        ctx.shard_dev_assign(b['sums'], r, w)
+        top, upper = self._plane('cubes32', 'top'), self._plane('cubes32', 'upper')
+        if top is not None:
+            ctx.shard_dev_top_cubes(top)
+        comm.shift_up(top, upper)
+        ctx.shard_dev_seam_pairs(upper if r > 0 else None, b['sums'], r, b['hdr'])
+        comm.allgather_into(b['all'], b['hdr'])
+        res, (redo, max_pairs, n_labels, base) = ctx.shard_dev_finish(b['all'], w, b['sums'], out)
+        if redo:
+            from cluster_tools_amd import _lib
+            if redo & _lib.RF_PAIRS:          # every rank sees the same largest count
+                self.pair_cap = next_pow2(2 * max_pairs)
+            if redo & (_lib.RF_BIG | _lib.RF_CUBES):
+                self.fast = False             # a property of the input / id range: stay synchronised
+            return None
+        self.form = 'cubes32'
+        res['n_labels'] = n_labels
+        res['max_id'] = n_labels - 1
+        res['id_base'] = base
+        res['seam_form'] = 'cubes32'
+        res['schedule'] = 'one-read-back'
+        return res
+
+    def _label_sync(self, x, threshold, mode, mask, out):
+        """The host-synchronised schedule (every count read back; exact sizes)."""
+        import torch
+        ctx, comm = self.ctx, self.comm
         s = ctx.shard_begin(x, self.block_shape, threshold, mode, self.z0, mask)
         self.sums = comm.allgather_int(s)
         base = sum(self.sums[:comm.rank])
@@ -214,25 +309,73 @@ class ShardedLabeler:
         res['max_id'] = res['n_labels'] - 1
         res['id_base'] = base
         res['seam_form'] = form
+        res['schedule'] = 'synchronised'
         return res
 
 
+def _slabs_fast(ctxs, x, block_shape, threshold, mode, mask, bounds, out, cap):
+    """label_slabs_single_process with the one-read-back schedule (the collectives become device
+    copies in stream order); None when the status asks for the synchronised schedule."""
+    import torch
+    dev = x.device
+    n = len(ctxs)
+    Z, Y, X = x.shape
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for ctx in ctxs:
+        ctx.set_stream(stream)               # every slab's kernels in one stream order
+    sum_ts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(n)]
+    for r, (ctx, (z0, zs)) in enumerate(zip(ctxs, bounds)):
+        m = None if mask is None else mask[z0:z0 + zs]
+        ctx.shard_dev_begin(x[z0:z0 + zs], block_shape, threshold, mode, z0, sum_ts[r], m)
+    sums = torch.cat(sum_ts)                 # the allgather
+    for r, ctx in enumerate(ctxs):
+        ctx.shard_dev_assign(sums, r, n)
+    tops = [torch.empty(((Y + 1) // 2, (X + 1) // 2), dtype=torch.int32, device=dev) for _ in range(n - 1)]
+    for r in range(n - 1):
+        ctxs[r].shard_dev_top_cubes(tops[r])
+    allb = torch.zeros((n * (cap + 1), 2), dtype=torch.int64, device=dev)
+    for r, ctx in enumerate(ctxs):
+        ctx.shard_dev_seam_pairs(tops[r - 1] if r > 0 else None, sums, r, allb[r * (cap + 1):(r + 1) * (cap + 1)])
+    res, luts, redo = [], [], 0
+    for ctx, (z0, zs) in zip(ctxs, bounds):
+        q, st = ctx.shard_dev_finish(allb, n, sums, out[z0:z0 + zs])
+        redo |= st[0]
+        q['seam_form'] = 'cubes32'
+        q['schedule'] = 'one-read-back'
+        res.append(q)
+    if redo:
+        return None
+    for ctx in ctxs:
+        luts.append(ctx.lut_local())
+    return out, res, [int(v) for v in sums.cpu().tolist()], luts
+
+
 def label_slabs_single_process(ctxs, x, block_shape, threshold, mode='greater', mask=None, bounds=None,
-                               form=None):
+                               form=None, schedule=None, pair_cap=None):
     """The same schedule for several slabs on ONE device, phase by phase in one process (the
     collectives become list operations).  Used to test the sharded algorithm on one GPU.
     ctxs: one _lib.Context per slab.  form: the seam-plane form ('cubes32', 'voxel32', 'voxel64';
-    default: what ShardedLabeler picks).  Returns (labels, per-slab results, sums, luts)."""
+    default: what ShardedLabeler picks).  schedule: None (the one-read-back schedule when the
+    cube form applies, else -- or when its status asks for it -- the synchronised one), 'sync',
+    'fast' (the one-read-back schedule or an error).  Returns (labels, per-slab results, sums, luts)."""
     import torch
     Z, Y, X = x.shape
     bounds = bounds or slab_bounds(Z, block_shape[0], len(ctxs))
     out = torch.empty(tuple(x.shape), dtype=torch.int64, device=x.device)
+    nby, nbx = -(-Y // block_shape[1]), -(-X // block_shape[2])
+    cubes_ok = (nby == 1 or block_shape[1] % 2 == 0) and (nbx == 1 or block_shape[2] % 2 == 0)
+    if schedule != 'sync' and form in (None, 'cubes32') and cubes_ok:
+        r = _slabs_fast(ctxs, x, block_shape, threshold, mode, mask, bounds, out, pair_cap or PAIR_CAP)
+        if r is not None:
+            return r
+        if schedule == 'fast':
+            raise RuntimeError('the one-read-back schedule asked for the synchronised one')
+    elif schedule == 'fast':
+        raise ValueError('the one-read-back schedule needs the cube seam form (even block_shape[1:])')
     sums = []
     for ctx, (z0, zs) in zip(ctxs, bounds):
         m = None if mask is None else mask[z0:z0 + zs]
         sums.append(ctx.shard_begin(x[z0:z0 + zs], block_shape, threshold, mode, z0, m))
-    nby, nbx = -(-Y // block_shape[1]), -(-X // block_shape[2])
-    cubes_ok = (nby == 1 or block_shape[1] % 2 == 0) and (nbx == 1 or block_shape[2] % 2 == 0)
     form = form or ShardedLabeler.seam_form(cubes_ok, max(sums))
     if form == 'cubes32' and not cubes_ok:
         raise ValueError('cubes32 seam planes need even block_shape[1:]')
@@ -273,6 +416,7 @@ def label_slabs_single_process(ctxs, x, block_shape, threshold, mode='greater', 
     for ctx, (z0, zs) in zip(ctxs, bounds):
         o = out[z0:z0 + zs]
         r = ctx.shard_finish(allp.contiguous(), allp.shape[0], o)
+        r['schedule'] = 'synchronised'
         res.append(r)
         luts.append(ctx.lut_local())
     return out, res, sums, luts

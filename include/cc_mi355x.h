@@ -220,6 +220,39 @@ int64_t cc_seam_pairs_cubes32(cc_ctx* ctx, const uint32_t* upper_cubes_dev, uint
                               const uint64_t* lower_dev, int64_t Y, int64_t X, uint64_t* pairs_dev,
                               int64_t cap);
 
+/* One-read-back schedule of the z-slab shards (distributed.py's default).  The same collective
+ * schedule as above, but nothing comes back to the host until cc_shard_dev_finish: counts, the
+ * id base and the seam pairs stay in device memory between the collectives, which the caller
+ * runs on the ctx's stream (RCCL allgather / point-to-point on device buffers).
+ *   cc_shard_dev_begin      local stages; the slab's sum of block values -> sum_dev (1 uint64)
+ *   [allgather sum_dev -> sums_dev[world]]
+ *   cc_shard_dev_assign     id base = sum of sums_dev[0 .. rank) on the device; block-face unions
+ *   cc_shard_dev_top_cubes  the top plane in the cube form of cc_shard_top_cubes32 (even
+ *                           block_shape[1:] required)
+ *   [send it to rank + 1]
+ *   cc_shard_dev_seam_pairs hdr_pairs_dev[cap + 1][2]: row 0 = (pair count, redo flags), then up to
+ *                           cap seam pairs (upper id, lower id) of this slab's bottom face against
+ *                           the slab below's cube plane (upper_cubes_dev NULL on rank 0: header only)
+ *   [allgather hdr_pairs_dev -> all_dev[world][cap + 1][2]]
+ *   cc_shard_dev_finish     replicated union-find over every slab's pairs, LUT, final labels; the
+ *                           step's ONE host read-back.  status_host[4] = redo flags, the largest
+ *                           pair count of a slab, the global n_labels, this slab's id base.  Redo
+ *                           flags != 0 (identical on every rank: computed from the allgathered
+ *                           headers and sums) mean an optimistic bound did not hold -- more seam
+ *                           pairs than cap (8), ids beyond the 28-bit cube form (4), more roots than
+ *                           the context's root arrays (2), a block needing the global-stitch
+ *                           fallback (1) -- and the caller relabels this step with the schedule
+ *                           above (cc_shard_begin ...), which sizes everything from read-backs. */
+int cc_shard_dev_begin(cc_ctx* ctx, const float* in_dev, const uint8_t* mask_dev, const int64_t slab_shape[3],
+                       const int64_t block_shape[3], double threshold, int mode, int64_t z_offset,
+                       uint64_t* sum_dev);
+int cc_shard_dev_assign(cc_ctx* ctx, const uint64_t* sums_dev, int rank, int world);
+int cc_shard_dev_top_cubes(cc_ctx* ctx, uint32_t* cubes_dev);
+int cc_shard_dev_seam_pairs(cc_ctx* ctx, const uint32_t* upper_cubes_dev, const uint64_t* sums_dev, int rank,
+                            uint64_t* hdr_pairs_dev, int64_t cap);
+int cc_shard_dev_finish(cc_ctx* ctx, const uint64_t* all_dev, int world, int64_t cap, const uint64_t* sums_dev,
+                        uint64_t* labels_dev, cc_result* res, uint64_t* status_host);
+
 /* --- synthetic benchmark input (oracle/synth.py is its restatement) ---
  * dither = 0: q / 256 (quantized); dither = 1: (q * 2^16 + 16-bit hash dither) / 2^24, the
  * continuous variant (block extremes and threshold crossings no longer on a 2^-8 grid). */

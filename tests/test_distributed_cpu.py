@@ -68,6 +68,46 @@ class FakeShardCtx:
         pairs[:len(p)] = torch.from_numpy(p)
         return len(p)
 
+    # the one-read-back schedule's entry points (device buffers = CPU tensors here)
+    def shard_dev_begin(self, x, block_shape, threshold, mode, z0, sum_t, mask=None):
+        sum_t[0] = self.shard_begin(x, block_shape, threshold, mode, z0, mask)
+
+    def shard_dev_assign(self, sums, rank, world):
+        self.shard_assign(int(sums[:rank].sum()))
+
+    def shard_dev_top_cubes(self, cubes):
+        self.shard_top_cubes32(cubes)
+
+    def shard_dev_seam_pairs(self, upper, sums, rank, hdr):
+        cap = hdr.shape[0] - 1
+        hdr.zero_()
+        if upper is None:
+            return
+        Y, X = self.lab.shape[1:]
+        tmp = torch.zeros((Y * X, 2), dtype=torch.int64)
+        n = self.seam_pairs_cubes32(upper, int(sums[:rank - 1].sum()), torch.from_numpy(self.lab[0]), tmp)
+        hdr[0, 0] = n
+        m = min(n, cap)
+        hdr[1:1 + m] = tmp[:m]
+
+    def shard_dev_finish(self, all_, world, sums, out):
+        from cluster_tools_amd import _lib
+        cap = all_.shape[0] // world - 1
+        bufs = all_.reshape(world, cap + 1, 2)
+        counts = [int(b[0, 0]) for b in bufs]
+        redo = 0
+        for b in bufs:
+            redo |= int(b[0, 1])
+        if max(counts) > cap:
+            redo |= _lib.RF_PAIRS
+        n_labels = int(sums.sum()) + 1
+        if redo:
+            return {}, (redo, max(counts), n_labels, self.base)
+        p = torch.cat([b[1:1 + c] for b, c in zip(bufs, counts)])
+        res = self.shard_finish(p, p.shape[0], out)
+        res['n_labels'] = n_labels
+        return res, (0, max(counts), n_labels, self.base)
+
     def shard_finish(self, allp, n, out):
         mapping = {}
         if n:
@@ -97,7 +137,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, shape, block_shape, thr, mode, result_dir, form=None):
+def _worker(rank, world, port, shape, block_shape, thr, mode, result_dir, form=None, pair_cap=None):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
@@ -106,10 +146,18 @@ def _worker(rank, world, port, shape, block_shape, thr, mode, result_dir, form=N
     z0, zs = slab_bounds(shape[0], block_shape[0], world)[rank]
     lab = ShardedLabeler(FakeShardCtx(), shape, block_shape, z0, zs, device=None,
                          comm=TorchComm(device=None), force_form=form)
+    if pair_cap is not None:
+        lab.pair_cap = pair_cap
     out = torch.empty((zs,) + tuple(shape[1:]), dtype=torch.int64)
     res = lab.label(torch.from_numpy(x[z0:z0 + zs].copy()), thr, mode, out=out)
+    sched = [res['schedule']]
+    if pair_cap is not None:              # a too-small pair buffer: the step was redone synchronised,
+        res = lab.label(torch.from_numpy(x[z0:z0 + zs].copy()), thr, mode, out=out)   # the next fits
+        sched.append(res['schedule'])
     np.save(os.path.join(result_dir, 'slab_%d.npy' % rank), out.numpy())
     np.save(os.path.join(result_dir, 'nl_%d.npy' % rank), np.array([res['n_labels'], res['id_base']]))
+    with open(os.path.join(result_dir, 'sched_%d.txt' % rank), 'w') as f:
+        f.write(' '.join(sched) + ' %d' % lab.pair_cap)
     dist.destroy_process_group()
 
 
@@ -132,6 +180,30 @@ def test_gloo_sharded_schedule_matches_oracle(tmp_path, world, shape, block_shap
     np.testing.assert_array_equal(got, ref['labels'])
     for r in range(world):
         assert int(np.load(str(tmp_path / ('nl_%d.npy' % r)))[0]) == ref['n_labels']
+        sched = open(str(tmp_path / ('sched_%d.txt' % r))).read().split()
+        # even y/x blocks and no forced form: the one-read-back schedule, else the synchronised one
+        assert sched[0] == ('one-read-back' if form is None and block_shape[1] % 2 == 0 and
+                            block_shape[2] % 2 == 0 else 'synchronised')
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_gloo_pair_capacity_redo(tmp_path, world):
+    """A pair buffer too small for the seams: every rank sees the same header counts, relabels the
+    step with the synchronised schedule (same labels) and raises the capacity alike, so the next
+    step runs the one-read-back schedule again."""
+    shape, block_shape = (40, 64, 64), (8, 32, 32)
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, shape, block_shape, 0.5, 'less', str(tmp_path), None, 1), nprocs=world,
+             join=True)
+    got = np.concatenate([np.load(str(tmp_path / ('slab_%d.npy' % r))) for r in range(world)]).astype(np.uint64)
+    ref = O.label_volume(O.boundary_map(shape, n_threads=1), block_shape, 0.5, 'less')
+    np.testing.assert_array_equal(got, ref['labels'])
+    caps = set()
+    for r in range(world):
+        s = open(str(tmp_path / ('sched_%d.txt' % r))).read().split()
+        assert s[:2] == ['synchronised', 'one-read-back']
+        caps.add(int(s[2]))
+    assert len(caps) == 1 and caps.pop() > 1
 
 
 def test_seam_form_choice():

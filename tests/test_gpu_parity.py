@@ -407,3 +407,32 @@ def test_resized_mask_device_vs_oracle(ctx, mshape, shape):
     np.testing.assert_array_equal(ctx.resize_mask(m, shape, z0=7, nz=16).cpu().numpy(), want[7:23])
     inp = O.boundary_map(shape, origin=(2, 3, 4))
     _check_against_oracle(ctx, inp, (16, 32, 32), 0.5, 'less', want)
+
+
+@pytest.mark.parametrize('fast', ['0', '1'])
+@pytest.mark.parametrize('shape,bs,mode', SYNTH[:4])
+def test_both_schedules_vs_oracle(ctx, monkeypatch, fast, shape, bs, mode):
+    """The one-read-back schedule (default: every count stays on the device, one read-back per
+    run) and the host-synchronised schedule (CC_FAST=0) give the oracle's labels, quantized and
+    continuous input (the device-gated k_fix path)."""
+    monkeypatch.setenv('CC_FAST', fast)
+    x = O.boundary_map(shape, origin=(2, 5, 1))
+    _check_against_oracle(ctx, x, bs, 0.5, mode)
+    xc = O.boundary_map(shape, origin=(2, 5, 1), dither=True)
+    _check_against_oracle(ctx, xc, bs, 0.5, mode)
+
+
+def test_root_capacity_redo(monkeypatch):
+    """More block-local roots than a context's root arrays hold (CC_ROOT_CAP: the first capacity):
+    the one read-back carries RF_ROOTS, the run is redone host-synchronised (k_block_scan twice)
+    with the oracle's result, and the capacity is raised so the next run needs one pass."""
+    from cluster_tools_amd import _lib
+    monkeypatch.setenv('CC_ROOT_CAP', '8')
+    shape, bs = (64, 96, 160), (32, 48, 64)
+    x = O.boundary_map(shape, origin=(0, 3, 7))
+    with _lib.Context(0) as c:
+        c.set_profiling(1)
+        for passes in (2, 1):
+            c.reset_profile()
+            _check_against_oracle(c, x, bs, 0.5, 'less')
+            assert c.profile()['k_block_scan']['count'] == passes

@@ -9,6 +9,7 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize('schedule', ['fast', 'sync'])
 @pytest.mark.parametrize('n_slabs,shape,block_shape,mode', [
     (2, (64, 256, 256), (32, 128, 128), 'greater'),
     (2, (64, 256, 256), (32, 128, 128), 'less'),
@@ -16,14 +17,18 @@ pytestmark = pytest.mark.gpu
     (3, (75, 130, 170), (25, 64, 64), 'greater'),
     (8, (64, 96, 160), (8, 48, 64), 'less'),
 ])
-def test_sharded_single_gpu_vs_oracle(n_slabs, shape, block_shape, mode):
+def test_sharded_single_gpu_vs_oracle(n_slabs, shape, block_shape, mode, schedule):
+    """Both shard schedules: 'fast' = the one-read-back schedule (cc_shard_dev_*: sums, id
+    bases and seam pairs stay on the device), 'sync' = the host-synchronised one."""
     import torch
     from cluster_tools_amd import _lib
     from cluster_tools_amd.distributed import label_slabs_single_process, assemble_lut
     x = O.boundary_map(shape, origin=(3, 0, 9))
     ctxs = [_lib.Context(0) for _ in range(n_slabs)]
     try:
-        lab, res, sums, luts = label_slabs_single_process(ctxs, torch.from_numpy(x).cuda(), block_shape, 0.5, mode)
+        lab, res, sums, luts = label_slabs_single_process(ctxs, torch.from_numpy(x).cuda(), block_shape, 0.5, mode,
+                                                          schedule=schedule)
+        assert {r['schedule'] for r in res} == {'one-read-back' if schedule == 'fast' else 'synchronised'}
         ref = O.label_volume(x, block_shape, 0.5, mode, n_threads=8)
         np.testing.assert_array_equal(lab.cpu().numpy().view(np.uint64), ref['labels'])
         assert sum(sums) + 1 == ref['n_labels']
@@ -204,3 +209,23 @@ def test_bench_self_launch_two_ranks_gloo():
     assert d['n_gpus'] == 2 and d['scaling'] == 'strong' and d['config']['workload_id'] == 'c4'
     assert d['config']['shape'] == [1024, 2048, 2048] and d['config']['slab'] == [512, 2048, 2048]
     assert d['value'] > 0
+
+
+def test_sharded_pair_capacity_redo():
+    """Seam pair buffers too small (1 pair per slab): the status of the one-read-back step flags
+    RF_PAIRS on every slab and the synchronised schedule relabels the step -- same labels."""
+    import torch
+    from cluster_tools_amd import _lib
+    from cluster_tools_amd.distributed import label_slabs_single_process, assemble_lut
+    shape, bs = (96, 160, 192), (16, 64, 64)
+    x = O.boundary_map(shape, origin=(1, 2, 3))
+    ctxs = [_lib.Context(0) for _ in range(3)]
+    try:
+        lab, res, sums, luts = label_slabs_single_process(ctxs, torch.from_numpy(x).cuda(), bs, 0.5, 'less', pair_cap=1)
+        assert {r['schedule'] for r in res} == {'synchronised'}
+        ref = O.label_volume(x, bs, 0.5, 'less', n_threads=8)
+        np.testing.assert_array_equal(lab.cpu().numpy().view(np.uint64), ref['labels'])
+        np.testing.assert_array_equal(assemble_lut(luts, sums), ref['lut'])
+    finally:
+        for c in ctxs:
+            c.close()

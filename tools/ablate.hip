@@ -223,7 +223,7 @@ int main(int argc, char** argv) {
             r.push_back({"k_seams_zyx", time_ms(s, iters, [&] { SEAMS(4); })});
             r.push_back({"k_seams_full", time_ms(s, iters, [&] { SEAMS(0); })});
         }
-        r.push_back({"k_pass2", time_ms(s, iters, [&] { k_pass2<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, BITS, COUNT, FIN, nullptr, nullptr, 0, 0, out, 0); })});
+        r.push_back({"k_pass2", time_ms(s, iters, [&] { k_pass2<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, BITS, COUNT, FIN, nullptr, nullptr, 0, 0, out, 0, nullptr, nullptr); })});
         std::printf("{\"shape\": [%lld, %lld, %lld], \"block\": [%lld, %lld, %lld], \"mode\": %d, \"tiles\": %lld",
                     (long long)shape[0], (long long)shape[1], (long long)shape[2], (long long)bs[0], (long long)bs[1],
                     (long long)bs[2], mode, (long long)nt);
