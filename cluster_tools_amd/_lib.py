@@ -27,10 +27,11 @@ EXPORTS = (
     'cc_evaluate', 'cc_get_overlaps', 'cc_relabel_consecutive', 'cc_set_option', 'cc_channel_mean',
     'cc_gaussian_smooth_blocks', 'cc_gaussian_taps', 'cc_result_size', 'cc_resize_mask_nearest',
     'cc_watershed_from_seeds', 'cc_shard_dev_begin', 'cc_shard_dev_assign', 'cc_shard_dev_top_cubes',
-    'cc_shard_dev_seam_pairs', 'cc_shard_dev_finish',
+    'cc_shard_dev_seam_pairs', 'cc_shard_dev_finish', 'cc_normalize_channels',
 )
 # redo flags of the one-read-back schedule (RF_* in csrc/cc_kernels.hip)
 RF_BIG, RF_ROOTS, RF_CUBES, RF_PAIRS = 1, 2, 4, 8
+CC_ERR_ID_RANGE = -3          # cc_evaluate: ids beyond the key packing (include/cc_mi355x.h)
 # CC_DTYPE_* of include/cc_mi355x.h (cc_channel_mean)
 DTYPES = {'float32': 0, 'float64': 1, 'uint8': 2, 'int8': 3, 'uint16': 4, 'int16': 5, 'uint32': 6,
           'int32': 7, 'uint64': 8, 'int64': 9}
@@ -127,6 +128,7 @@ def load():
         'cc_result_size': (i64, []),
         'cc_resize_mask_nearest': (I, [P, P, P, P, i64, i64, P]),
         'cc_watershed_from_seeds': (I, [P, P, P, P, P, P, P, P]),
+        'cc_normalize_channels': (I, [P, P, i64, P, P, I, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -366,12 +368,30 @@ class Context:
                                    mode_id(mode), _ptr(out)))
         return out
 
-    def watershed_from_seeds(self, inp, seeds, block_shape, mask=None, out=None):
+    AGG = {'mean': 0, 'max': 1, 'min': 2}
+
+    def normalize_channels(self, inp, block_shape, agg='mean', out=None):
+        """4-D watershed input (_read_data, watershed_from_seeds.py:127-139) on device: inp =
+        the selected channels (C, Z, Y, X) float32 CUDA tensor; per block the 4-D block is
+        normalized as one array, then np.mean / np.max / np.min over the channels.  Returns the
+        (Z, Y, X) float32 tensor (the watershed input with prenormalized=True)."""
+        import torch
+        assert inp.is_cuda and inp.dtype == torch.float32 and inp.is_contiguous() and inp.dim() == 4
+        shape, bs = _i64(inp.shape[1:]), _i64(block_shape)
+        if out is None:
+            out = torch.empty(tuple(inp.shape[1:]), dtype=torch.float32, device=inp.device)
+        _check(load().cc_normalize_channels(self._h, _ptr(inp), int(inp.shape[0]), _ptr(shape), _ptr(bs),
+                                            self.AGG[agg], _ptr(out)))
+        return out
+
+    def watershed_from_seeds(self, inp, seeds, block_shape, mask=None, out=None, prenormalized=False):
         """WatershedFromSeeds (watershed/watershed_from_seeds.py:143-273) on device: the seeds
         (uint64 ids < 2^32 - 1, torch int64) grow over the per-block normalized float32 input,
         6-connected inside each block; mask (uint8) -> input 1.0 / output 0 outside it.  out may
-        be `seeds` (in place).  Returns (labels, relaxation rounds).  See include/cc_mi355x.h for
-        the definition (the reference's vu.watershed does not exist: parity unpinned)."""
+        be `seeds` (in place).  prenormalized: the input already holds the normalized values
+        (normalize_channels; CC_OPT_WS_PRENORMALIZED).  Returns (labels, relaxation rounds).  See
+        include/cc_mi355x.h for the definition (the reference's vu.watershed does not exist:
+        parity unpinned)."""
         import torch
         assert hasattr(inp, 'data_ptr') and inp.is_cuda and inp.dtype == torch.float32 and inp.is_contiguous()
         assert seeds.is_cuda and seeds.element_size() == 8 and seeds.shape == inp.shape and seeds.is_contiguous()
@@ -384,8 +404,12 @@ class Context:
             out = torch.empty(tuple(inp.shape), dtype=torch.int64, device=inp.device)
         assert out.element_size() == 8 and out.shape == inp.shape and out.is_contiguous()
         rounds = np.zeros(1, dtype=np.int64)
-        _check(load().cc_watershed_from_seeds(self._h, _ptr(inp), _ptr(seeds), _ptr(mask), _ptr(shape), _ptr(bs),
-                                              _ptr(out), _ptr(rounds)))
+        _check(load().cc_set_option(self._h, 2, int(bool(prenormalized))))
+        try:
+            _check(load().cc_watershed_from_seeds(self._h, _ptr(inp), _ptr(seeds), _ptr(mask), _ptr(shape), _ptr(bs),
+                                                  _ptr(out), _ptr(rounds)))
+        finally:
+            _check(load().cc_set_option(self._h, 2, 0))
         return out, int(rounds[0])
 
     def evaluate(self, seg, gt, block_shape, ignore_label=0):
@@ -414,13 +438,12 @@ class Context:
         # ids that fit the packing are the common case: the device reports ids out of range
         # (EV_ERR_SEG / EV_ERR_GT) and only then are the volumes relabelled (no host-side range
         # scan of the volumes: four reductions over C3's 34 GB tensors took ~40 ms per call)
-        try:
-            _check(load().cc_evaluate(self._h, _ptr(seg), _ptr(gt), _ptr(shape), _ptr(bs), int(use_ignore),
-                                      int(ignore_label) if use_ignore else 0, ctypes.byref(res)))
+        rc = load().cc_evaluate(self._h, _ptr(seg), _ptr(gt), _ptr(shape), _ptr(bs), int(use_ignore),
+                                int(ignore_label) if use_ignore else 0, ctypes.byref(res))
+        if rc == 0:
             return res.as_dict()
-        except RuntimeError as e:
-            if '2^31' not in str(e) and '2^32 - 1' not in str(e):
-                raise
+        if rc != CC_ERR_ID_RANGE:                      # CC_ERR_ID_RANGE: relabel and evaluate again
+            _check(rc)
 
         def too_large(a, limit):
             v = a.view(torch.int64)

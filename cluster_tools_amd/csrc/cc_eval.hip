@@ -264,11 +264,36 @@ static EvSums ev_table_sums(cc_ctx* c, const u64* keys, const u64* cnts, int64_t
     return r;
 }
 
+// ids beyond the 64-bit key packing: reported with their own status (CC_ERR_ID_RANGE) so a caller
+// can relabel and retry without parsing the message
+struct CCIdRangeError : CCError {};
+
+static int evaluate_impl(cc_ctx* c, const uint64_t* seg, const uint64_t* gt, const int64_t shape[3],
+                         const int64_t block_shape[3], int use_ignore, uint64_t ignore_label, cc_eval_result* out);
+
 extern "C" {
 
 int cc_evaluate(cc_ctx* c, const uint64_t* seg, const uint64_t* gt, const int64_t shape[3],
                 const int64_t block_shape[3], int use_ignore, uint64_t ignore_label, cc_eval_result* out) {
-    CC_TRY({
+    try {
+        return evaluate_impl(c, seg, gt, shape, block_shape, use_ignore, ignore_label, out);
+    } catch (const CCIdRangeError& e) {
+        g_err = e.msg;
+        return CC_ERR_ID_RANGE;
+    } catch (const CCError& e) {
+        g_err = e.msg;
+        return -1;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -2;
+    }
+}
+
+}  // extern "C"
+
+static int evaluate_impl(cc_ctx* c, const uint64_t* seg, const uint64_t* gt, const int64_t shape[3],
+                         const int64_t block_shape[3], int use_ignore, uint64_t ignore_label, cc_eval_result* out) {
+    {
         CC_REQUIRE(c && seg && gt && shape && block_shape && out, "bad arguments");
         HIP_OK(hipSetDevice(c->device));
         hipStream_t s = cstream(c);
@@ -318,8 +343,8 @@ int cc_evaluate(cc_ctx* c, const uint64_t* seg, const uint64_t* gt, const int64_
             u32 herr = 0;
             HIP_OK(hipMemcpyAsync(&herr, c->counter.p, sizeof(u32), hipMemcpyDeviceToHost, s));
             sync(c);
-            CC_REQUIRE(!(herr & EV_ERR_SEG), "segmentation id >= 2^31 (evaluation keys pack seg ids in 31 bits)");
-            CC_REQUIRE(!(herr & EV_ERR_GT), "ground-truth id >= 2^32 - 1 (evaluation keys pack gt ids in 32 bits)");
+            if (herr & EV_ERR_SEG) throw CCIdRangeError{{"segmentation id >= 2^31 (evaluation keys pack seg ids in 31 bits)"}};
+            if (herr & EV_ERR_GT) throw CCIdRangeError{{"ground-truth id >= 2^32 - 1 (evaluation keys pack gt ids in 32 bits)"}};
             u64* pu = c->ev_part.as<u64>();
             double* pf = (double*)(pu + 2 * EV_REDUCE_WG);
             EvSums m{};
@@ -353,8 +378,10 @@ int cc_evaluate(cc_ctx* c, const uint64_t* seg, const uint64_t* gt, const int64_
             out->sum_sq_seg = b.sq;
             return 0;
         }
-    })
+    }
 }
+
+extern "C" {
 
 int64_t cc_get_overlaps(cc_ctx* c, uint64_t* seg_ids, uint64_t* gt_ids, uint64_t* counts, int64_t cap) {
     try {

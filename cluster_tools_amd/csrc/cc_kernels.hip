@@ -79,6 +79,12 @@ constexpr u64 RF_ROOTS = 2;     // more block-local roots than the root arrays h
 constexpr u64 RF_CUBES = 4;     // the slab's ids do not fit the 28-bit cube form of its top plane
 constexpr u64 RF_PAIRS = 8;     // more seam pairs than the pair buffer holds
 
+// the run's device scalars: [0] sum of block values, [1] components owned, [2] block-local roots,
+// [3] redo flags, [4] k_lut_all workgroups done, [5] seam pairs appended, [6] k_seam_cube_pairs
+// workgroups done
+constexpr int SCALARS = 8;
+constexpr int64_t SEAM_SET = 1 << 16;   // slots of the seam pair hash set (k_seam_pairs, k_seam_cube_pairs)
+
 constexpr int NCROW = CZ * CY;          // cube rows per tile
 constexpr int NRUN = NCROW * CX;        // a run per occupied cube at most (adjacent cubes need not link)
 static_assert(NTHREADS == 4 * NCROW, "tile_ccl maps one thread to each quarter cube row");
@@ -869,16 +875,22 @@ __global__ void k_guess(int64_t nb, const u32* part, float thr, int mode, BlockP
 // mflag / fchg (nullable, the device-gated k_fix of the one-read-back schedule): the seam marks
 // and their list count (mflag[nt]) and the changed-faces flags, which the host-synchronised
 // schedule clears only when the k_fix count it read back is non-zero.
+// htab / hkeys + hpar (nullable, shards of the one-read-back schedule): the seam pair set and the
+// seam map of the previous step cleared for this one (n_clear = the longest of all the ranges)
 __global__ __launch_bounds__(256) void k_clear_front(int64_t nb, int64_t nt, u32* smin, u32* smax_flag,
                                                      u64* scalars, u32* FIX, u8* big, u8* iovf, u32* ipc,
-                                                     u32* seg, u32* rc_end, u8 fill, u32* mflag, u8* fchg) {
-    CC_FOR(i, (nt + 1 > 2 * nb + 1 ? nt + 1 : 2 * nb + 1)) {
+                                                     u32* seg, u32* rc_end, u8 fill, u32* mflag, u8* fchg,
+                                                     u64* htab, int64_t htab_n, u64* hkeys, u32* hpar, int64_t hm_n,
+                                                     int64_t n_clear) {
+    CC_FOR(i, n_clear) {
+        if (htab && i < htab_n) htab[i] = ~0ull;
+        if (hkeys && i < hm_n) { hkeys[i] = ~0ull; hpar[i] = (u32)i; }
         if (i < nb) smin[i] = 0xFFFFFFFFu;
         if (i < 2 * nb) { smax_flag[i] = 0u; seg[i] = 0u; }
         if (i <= nb) big[i] = fill;
         if (i <= nt) iovf[i] = fill;
         if (i < nt) ipc[i] = 0u;
-        if (i < 4) scalars[i] = 0ull;
+        if (i < SCALARS) scalars[i] = 0ull;
         if (i == 0) { FIX[0] = 0u; rc_end[0] = 0u; }
         if (mflag && i <= nt) mflag[i] = 0u;
         if (fchg && i < nt) fchg[i] = 0;
@@ -2301,7 +2313,6 @@ constexpr u64 HM_EMPTY = ~0ull;
 struct HashMap {
     u64* keys = nullptr;
     u32* par = nullptr;
-    u64* vals = nullptr;
     u32 mask = 0;
     __device__ __forceinline__ static u32 hash(u64 id) { return (u32)((id * 0x9E3779B97F4A7C15ull) >> 32); }
     // slot of id, inserted if absent (the table never fills: sized for every id of the pairs)
@@ -2317,17 +2328,58 @@ struct HashMap {
             h = (h + 1) & mask;
         }
     }
-    // the representative of id (id itself when it is not on any seam)
+    // the representative of id (id itself when it is not on any seam): the key of its slot's root
     __device__ __forceinline__ u64 get(u64 id) const {
         u32 h = hash(id) & mask;
         while (true) {
             const u64 cur = keys[h];
-            if (cur == id) return vals[h];
+            if (cur == id) return keys[gfind(par, h)];
             if (cur == HM_EMPTY) return id;
             h = (h + 1) & mask;
         }
     }
 };
+
+// the one read-back of a run (see phase_final), written by the last workgroup of k_lut_all:
+// out[0] = redo flags (the run's scalars[3]; with shards, OR over every slab's header plus
+// RF_PAIRS when a slab had more pairs than cap and RF_CUBES when a slab's ids exceed the 28-bit
+// cube form), [1] = largest pair count of a slab, [2] = sum over the slabs (or this volume) of
+// the block values, [3] = this slab's id base, [4] = tiles k_fix relabelled, [5..8] =
+// scalars[0..3], [16 ..) = values[nb], then offsets[nb] (+ base)
+struct StatusArgs {
+    u64* out = nullptr;          // nullptr: no status (the host-synchronised schedule)
+    const u32* FIX = nullptr;
+    const u64* all = nullptr;    // shards: every slab's pair buffer [world][cap + 1][2]
+    int world = 0;
+    u64 cap = 0;
+    const u64* values = nullptr;
+    const u64* offsets = nullptr;
+    int64_t nb = 0;
+};
+
+__device__ __forceinline__ void write_status(const StatusArgs& sa, const u64* scalars, const u64* sums, u64 base) {
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        u64 flags = scalars[3], mx = 0, tot = scalars[0];
+        if (sa.all) {
+            tot = 0;
+            for (int w = 0; w < sa.world; ++w) {
+                const u64* h = sa.all + (u64)w * 2 * (sa.cap + 1);
+                flags |= h[1];
+                mx = h[0] > mx ? h[0] : mx;
+                tot += sums[w];
+                if (sums[w] >= (1ull << 28) - 2) flags |= RF_CUBES;
+            }
+            if (mx > sa.cap) flags |= RF_PAIRS;
+        }
+        sa.out[0] = flags; sa.out[1] = mx; sa.out[2] = tot; sa.out[3] = base; sa.out[4] = sa.FIX[0];
+        for (int k = 0; k < 4; ++k) sa.out[5 + k] = scalars[k];
+    }
+    for (int64_t i = tid; i < sa.nb; i += blockDim.x) {
+        sa.out[16 + i] = sa.values[i];
+        sa.out[16 + sa.nb + i] = sa.offsets[i] + base;
+    }
+}
 
 // lut[i] = base + i for the ids of this volume (slab): i in [0, scalars[0]] (the last one is
 // the slack id n_labels - 1 on the last slab, merge_offsets.py:120)
@@ -2340,36 +2392,55 @@ __global__ void k_lut_init(u64 cap, const u64* scalars, u64 base, u64* lut) {
 // the rid of rank r = id - offsets[b] - 1 of the last block b whose range starts at or below it
 // (empty blocks share the next block's offset); a root's id maps to its component's
 // representative, every other id (label 0 of a block, the slack id) to itself.  Grid-stride over
-// cap >= scalars[0] + 1 ids.  basep (nullable): the slab's id base on the device (the
-// one-read-back shard schedule); hm (keys != nullptr): the seam map as a hash table instead of U/V.
-__global__ void k_lut_all(u64 cap, int64_t nb, u64 base, const u64* basep, const u64* __restrict__ offsets,
+// cap >= scalars[0] + 1 ids.  sums (nullable; the one-read-back shard schedule): offsets and KR are
+// this slab's own id space (base 0) and the global base = sum of sums[0 .. rank) is added here;
+// hm (keys != nullptr): the seam map.  st.out: the last workgroup writes the run's status.
+__global__ void k_lut_all(u64 cap, int64_t nb, u64 base, const u64* sums, int rank, const u64* __restrict__ offsets,
                           const u64* __restrict__ values, const u32* __restrict__ seg_start, const u32* __restrict__ vals,
                           u64 nvals, u32* P, const u64* KR, const u64* U, const u64* V, int64_t m, HashMap hm,
-                          u64* lut, u64* scalars) {
-    if (basep) base = *basep;
+                          u64* lut, u64* scalars, StatusArgs st) {
+    u64 gbase = base, obase = base;                           // ids = obase + i; reps + (gbase - obase)
+    if (sums) {
+        gbase = 0;
+        for (int r = 0; r < rank; ++r) gbase += sums[r];
+        obase = 0;
+    }
     const u64 n = scalars[0] + 1 < cap ? scalars[0] + 1 : cap;
     u64 owned = 0;
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-        const u64 id = base + i;
+        const u64 id = obase + i;
         int64_t lo = 0, hi = nb - 1;
         while (lo < hi) {
             const int64_t mid = (lo + hi + 1) >> 1;
             if (offsets[mid] <= id) lo = mid; else hi = mid - 1;
         }
         const u64 off = offsets[lo], v = values[lo];
-        u64 rep = id;
+        u64 rep = gbase + i;
         const u64 vi = (u64)seg_start[lo] + (id - off - 1);   // vals index (< nvals: the root arrays' size)
         if (off < id && id - off < v && vi < nvals) {         // rank id - off - 1 in [0, v - 1)
             const u32 node = vals[vi];
             const u32 r = gfind(P, node);
-            rep = hm.keys ? hm.get(KR[r]) : apply_map(KR[r], U, V, m);
-            owned += (r == node && rep == KR[r]);          // components owned here
+            const u64 kr = KR[r] + (gbase - obase);
+            rep = hm.keys ? hm.get(kr) : apply_map(kr, U, V, m);
+            owned += (r == node && rep == kr);                // components owned here
         }
         lut[i] = rep;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) owned += __shfl_xor(owned, o, 64);
     if ((threadIdx.x & 63) == 0 && owned) atomicAdd((unsigned long long*)&scalars[1], (unsigned long long)owned);
+    if (!st.out) return;
+    // the last workgroup to finish writes the status (every owned count is in by then)
+    __shared__ u32 last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd((unsigned long long*)&scalars[4], 1ull) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    write_status(st, scalars, sums, sums ? gbase : 0);
 }
 
 __global__ void k_lut(int64_t n, const u32* vals, u32* P, const u64* KR, u64 base, const u64* U, const u64* V,
@@ -2615,17 +2686,15 @@ __global__ __launch_bounds__(SEAM_PAIR_THREADS) void k_seam_pairs(int64_t n, int
 // The top voxel plane as one u32 per 2x2 cube of the global cube grid (ceil(Y/2) x ceil(X/2);
 // needs even tile origins, i.e. even block_shape[1:]): (id - sub + 1) << 4 | the cube's 4
 // face-voxel bits, a quarter of the voxel plane's bytes.  One workgroup per top-layer tile.
-// subp (nullable): the id base on the device, and the 28-bit check of the one-read-back schedule
-// (scalars[0] = the slab's sum of block values; too many ids: RF_CUBES in scalars[3], plane unused)
+// scalars (nullable): the one-read-back schedule (KR holds the slab's own ids, sub = 0) and its
+// 28-bit check (scalars[0] = the slab's sum of block values; too many ids: RF_CUBES in scalars[3],
+// plane unused)
 __global__ __launch_bounds__(NTHREADS) void k_top_cubes(Geom g, const face_t* __restrict__ FACES, u32* P,
                                                         const u64* __restrict__ KR, u32* cubes, u64 sub,
-                                                        const u64* subp, u64* scalars) {
-    if (subp) {
-        if (scalars[0] >= (1ull << 28) - 2) {
-            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr((unsigned long long*)&scalars[3], (unsigned long long)RF_CUBES);
-            return;
-        }
-        sub = *subp;
+                                                        u64* scalars) {
+    if (scalars && scalars[0] >= (1ull << 28) - 2) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr((unsigned long long*)&scalars[3], (unsigned long long)RF_CUBES);
+        return;
     }
     const int64_t t = (int64_t)(g.nt[0] - 1) * g.nt[1] * g.nt[2] + blockIdx.x;
     const TileInfo ti = tile_info(g, t);
@@ -2646,80 +2715,78 @@ __global__ __launch_bounds__(NTHREADS) void k_top_cubes(Geom g, const face_t* __
 // ---- the one-read-back shard schedule (distributed.py fast path): everything below reads the
 // allgathered per-slab sums and seam-pair headers from device memory ------------------------
 
-// id base of slab `rank` = sum of the sums of the slabs below it; rebase this slab's block offsets
-// and the ids of its roots (k_emit_roots wrote them for base 0): offsets[b] += base,
-// KR[vals[i]] += base for the scalars[2] roots (capped at root_cap); thread 0 stores base
-__global__ void k_rebase(int64_t nb, u64* offsets, const u64* __restrict__ sums, int rank, const u32* vals, u64* KR,
-                         const u64* scalars, u64 root_cap, u64* base_out) {
-    u64 base = 0;
-    for (int r = 0; r < rank; ++r) base += sums[r];
-    const u64 nr = scalars[2] < root_cap ? scalars[2] : root_cap;
-    const u64 n = (u64)nb > nr ? (u64)nb : nr;
-    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-        if (i < (u64)nb) offsets[i] += base;
-        if (i < nr) KR[vals[i]] += base;
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) *base_out = base;
-}
-
 // Seam pairs of this slab's bottom face against the slab below's top plane in the cube form
 // (k_top_cubes), straight from the face planes of the bottom tile layer (no bottom voxel plane):
 // a 2x2 face cube holds one component id on each side, so each cube gives at most one pair
 // (upper id, lower id) when the two sides share a foreground voxel (6-connectivity,
-// block_faces.py:99-111).  A pair equal to the cube before it in x is dropped, the rest go
+// block_faces.py:99-111).  A pair equal to that of the cube before it in x or above it in y is
+// dropped (the first cube of every distinct pair in raster order still emits), the rest go
 // through the device hash set htab (key a << 32 | b; ids >= 2^32 or a full probe sequence are
-// appended anyway: the replicated union-find takes duplicates).  out = [cap + 1][2]: row 0 =
-// (count, redo flags), then the pairs; hdr[0] was zeroed.  One workgroup per bottom-layer tile.
+// appended anyway: the replicated union-find takes duplicates).  Ids: KR holds this slab's own ids
+// (base 0); the global ones add the sums of the slabs below.  out = [cap + 1][2]: row 0 = (count,
+// redo flags) written by the last workgroup (scalars[5] counts, scalars[6] counts workgroups;
+// both zeroed by k_clear_front), then the pairs.  One workgroup per bottom-layer tile.
 __global__ __launch_bounds__(NTHREADS) void k_seam_cube_pairs(Geom g, const face_t* __restrict__ FACES, u32* P,
                                                               const u64* __restrict__ KR, const u32* __restrict__ upper,
                                                               const u64* __restrict__ sums, int rank, u64* out, u64 cap,
-                                                              u64* htab, u32 hmask, const u64* scalars) {
+                                                              u64* htab, u32 hmask, u64* scalars) {
     const int64_t t = blockIdx.x;                    // bottom layer: tiles 0 .. nt[1] * nt[2] - 1
-    if (t == 0 && threadIdx.x == 0) out[1] = scalars[3];
     const TileInfo ti = tile_info(g, t);
     const face_t* F = FACES + t * FACE_STRIDE + F_ZLO;
     const u32 base = (u32)(t * g.cap);
-    u64 ubase = 0;
-    for (int r = 0; r < rank - 1; ++r) ubase += sums[r];
+    u64 ubase = 0, own = 0;
+    for (int r = 0; r < rank; ++r) {
+        own += sums[r];
+        if (r < rank - 1) ubase += sums[r];
+    }
     const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2;
     const int64_t CXg = (g.X + 1) / 2;
+    const u32* U0 = upper + (int64_t)(ti.y0 / 2) * CXg + ti.x0 / 2;
     const int lane = threadIdx.x & 63;
+    // the raw pair of face cube e: (upper cube word >> 4, lower tile node k), 0 when the two
+    // sides share no foreground voxel; equal raw pairs are equal id pairs
+    auto raw_at = [&](int e) -> u64 {
+        const u32 f = F[e];
+        const u32 c = f ? U0[(int64_t)(e / CX) * CXg + e % CX] : 0u;
+        return (c & (f >> FK_BITS) & 0xFu) ? ((u64)(c >> 4) << 32) | ((f & FK_MASK) + 1) : 0ull;
+    };
     for (int e0 = 0; e0 < ncy * CX; e0 += NTHREADS) {
         const int e = e0 + threadIdx.x;
         const int cy = e / CX, cx = e % CX;
         bool emit = false;
         u64 a = 0, b = 0;
-        if (e < ncy * CX && cx < ncx) {
-            const u32 f = F[e];
-            const u32 c = f ? upper[(int64_t)(ti.y0 / 2 + cy) * CXg + ti.x0 / 2 + cx] : 0u;
-            if (c & (f >> FK_BITS) & 0xFu) {
-                a = (u64)(c >> 4) - 1 + ubase;
-                b = KR[gfind(P, base + (f & FK_MASK))];
-                emit = true;
-                if (cx > 0) {                            // the cube before in x: same pair?
-                    const u32 fp = F[e - 1];
-                    const u32 cp = fp ? upper[(int64_t)(ti.y0 / 2 + cy) * CXg + ti.x0 / 2 + cx - 1] : 0u;
-                    if ((cp & (fp >> FK_BITS) & 0xFu) && (u64)(cp >> 4) - 1 + ubase == a &&
-                        KR[gfind(P, base + (fp & FK_MASK))] == b)
-                        emit = false;
-                }
-                if (emit && !((a | b) >> 32)) emit = seam_hash_insert(htab, hmask, (a << 32) | b) != 0;
-            }
+        const u64 q = (e < ncy * CX && cx < ncx) ? raw_at(e) : 0ull;
+        if (q && !(cx > 0 && raw_at(e - 1) == q) && !(cy > 0 && raw_at(e - CX) == q)) {
+            a = (q >> 32) - 1 + ubase;
+            b = KR[gfind(P, base + (u32)(q & 0xFFFFFFFFu) - 1)] + own;
+            emit = ((a | b) >> 32) || seam_hash_insert(htab, hmask, (a << 32) | b) != 0;
         }
         const u64 bal = __ballot(emit);
         if (bal) {
+            const int first = (int)(__ffsll((unsigned long long)bal) - 1);
             unsigned long long pos = 0;
-            if (lane == (int)(__ffsll((unsigned long long)bal) - 1)) pos = atomicAdd((unsigned long long*)out, (unsigned long long)__popcll(bal));
-            pos = __shfl(pos, (int)(__ffsll((unsigned long long)bal) - 1), 64) + (u64)__popcll(bal & ((1ull << lane) - 1));
+            if (lane == first) pos = atomicAdd((unsigned long long*)&scalars[5], (unsigned long long)__popcll(bal));
+            pos = __shfl(pos, first, 64) + (u64)__popcll(bal & ((1ull << lane) - 1));
             if (emit && pos < cap) { out[2 + 2 * pos] = a; out[3 + 2 * pos] = b; }
+        }
+    }
+    // the last workgroup writes the header
+    __shared__ u32 last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd((unsigned long long*)&scalars[6], 1ull) == gridDim.x - 1;
+        if (last) {
+            __threadfence();
+            out[0] = __hip_atomic_load(&scalars[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            out[1] = scalars[3];
         }
     }
 }
 
-// row 0 of a slab's pair buffer: hdr[1] = its redo flags (scalars[3]); hdr[0] (the count) is
-// written by k_seam_cube_pairs or stays 0 (slab 0)
+// row 0 of slab 0's pair buffer (no slab below it): (0, its redo flags)
 __global__ void k_seam_hdr(const u64* scalars, u64* hdr) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) hdr[1] = scalars[3];
+    if (threadIdx.x == 0 && blockIdx.x == 0) { hdr[0] = 0; hdr[1] = scalars[3]; }
 }
 
 // seam map over the allgathered pair buffers all[w] = [cap + 1][2] (w < world): clear, then
@@ -2740,40 +2807,6 @@ __global__ void k_map_build(HashMap hm, const u64* __restrict__ all, int world, 
         const u32 sa = hm.insert(buf[2 + 2 * j]), sb = hm.insert(buf[3 + 2 * j]);
         gunion(hm.par, hm.keys, sa, sb);
     }
-}
-
-__global__ void k_map_resolve(HashMap hm) {
-    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i <= hm.mask; i += (u64)gridDim.x * blockDim.x) {
-        if (hm.keys[i] != HM_EMPTY) hm.vals[i] = hm.keys[gfind(hm.par, (u32)i)];
-    }
-}
-
-// The one read-back of a run, gathered into one contiguous buffer (one copy): out[0] = redo
-// flags (this run's scalars[3]; with shards, OR over every slab's header plus RF_PAIRS when a
-// slab had more pairs than cap and RF_CUBES when a slab's ids exceed the 28-bit cube form),
-// [1] = largest pair count of a slab, [2] = sum over the slabs (or this volume) of the block
-// values, [3] = this slab's id base, [4] = tiles k_fix relabelled, [5..8] = scalars[0..3],
-// [16 ..) = values[nb], then offsets[nb].  all == nullptr: a single volume.
-__global__ void k_status(const u64* scalars, const u32* FIX, const u64* all, int world, u64 cap, const u64* sums,
-                         const u64* basep, int64_t nb, const u64* values, const u64* offsets, u64* out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) {
-        u64 flags = scalars[3], mx = 0, tot = scalars[0];
-        if (all) {
-            tot = 0;
-            for (int w = 0; w < world; ++w) {
-                const u64* h = all + (u64)w * 2 * (cap + 1);
-                flags |= h[1];
-                mx = h[0] > mx ? h[0] : mx;
-                tot += sums[w];
-                if (sums[w] >= (1ull << 28) - 2) flags |= RF_CUBES;
-            }
-            if (mx > cap) flags |= RF_PAIRS;
-        }
-        out[0] = flags; out[1] = mx; out[2] = tot; out[3] = basep ? *basep : 0ull; out[4] = FIX[0];
-        for (int k = 0; k < 4; ++k) out[5 + k] = scalars[k];
-    }
-    if (i < nb) { out[16 + i] = values[i]; out[16 + nb + i] = offsets[i]; }
 }
 
 // copy of the seam-pair ids with their largest value (atomicMax per workgroup into *mx): sizes the

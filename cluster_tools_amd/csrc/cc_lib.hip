@@ -121,10 +121,12 @@ struct cc_ctx {
     // one-read-back schedule (see run_pipeline): capacity of the root arrays sized before the count
     // is known (grown after a run that exceeded it), and whether the last volume of this geometry
     // needed the global-stitch fallback (then the host-synchronised schedule runs directly)
+    bool ws_prenormalized = false;   // CC_OPT_WS_PRENORMALIZED
     uint64_t root_cap = 0;
     bool fast_big = false;
     std::vector<int32_t> fast_big_tab;
-    DevBuf status, dbase, hmap_keys, hmap_par, hmap_vals;
+    DevBuf status, hmap_keys, hmap_par;
+    uint64_t hm_slots = 0;   // slots of the seam map (shards): cleared by the next k_clear_front
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, ProfEntry> prof_acc;
@@ -279,9 +281,11 @@ struct RunState {
     bool sum_known = false;    // sum_v already read back (phase_local's fast path)
     bool any_iovf = true;      // some tile's block-face pair list overflowed (or not read back)
     bool fast = false;         // the one-read-back schedule: counts stay on the device
-    bool base_dev = false;     // the id base lives on the device (c->dbase; shards of the fast schedule)
+    bool base_dev = false;     // ids of this slab stay base 0; kernels add the allgathered sums below it
     uint64_t redo = 0;         // RF_* flags read back by phase_final (fast schedule): run again synchronised
     uint64_t n_pairs_max = 0;  // largest seam-pair count of a slab (shards of the fast schedule)
+    const uint64_t* sums = nullptr;   // the allgathered sums (shards of the fast schedule)
+    int rank = 0;
 };
 
 static RunState& state(cc_ctx* c) {
@@ -319,7 +323,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     c->seg.ensure(nb * 2 * sizeof(u32));
     c->values.ensure(nb * sizeof(u64));
     c->offsets.ensure(nb * sizeof(u64));
-    c->scalars.ensure(4 * sizeof(u64));
+    c->scalars.ensure(SCALARS * sizeof(u64));
 
     // block statistics (ordered min, max, NaN flag), accumulated by k_spec
     u32* smin = c->bstat.as<u32>();
@@ -353,12 +357,19 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         c->roff.ensure((nt + 1) * sizeof(u32));
         c->mark.ensure((size_t)(2 * nt + 1) * sizeof(u32) + nt);
         const bool lds_seams = !(c->debug & CC_DEBUG_GLOBAL_STITCH);
+        // shards of the one-read-back schedule: the seam pair set and the seam map are cleared here
+        const bool shard = fast && sum_out != nullptr;
+        if (shard) c->seam_hash.ensure(SEAM_SET * sizeof(u64));
+        const int64_t hs_n = shard ? SEAM_SET : 0, hm_n = shard ? (int64_t)c->hm_slots : 0;
         launch(c, "k_clear_front", [&] {
             u32* mflag = fast ? c->mark.as<u32>() : nullptr;
             u8* mchg = fast ? (u8*)(c->mark.as<u32>() + 2 * nt + 1) : nullptr;
-            k_clear_front<<<grid1d(std::max(nt + 1, 2 * nb + 1)), 256, 0, s>>>(
+            const int64_t n_clear = std::max<int64_t>({nt + 1, 2 * nb + 1, hs_n, hm_n});
+            k_clear_front<<<grid1d(n_clear), 256, 0, s>>>(
                 nb, nt, smin, smax, c->scalars.as<u64>(), FIX, c->big.as<u8>(), c->iovf.as<u8>(), c->ipc.as<u32>(),
-                c->seg.as<u32>(), c->rc.as<u32>() + nt, lds_seams ? 0 : 1, mflag, mchg);
+                c->seg.as<u32>(), c->rc.as<u32>() + nt, lds_seams ? 0 : 1, mflag, mchg,
+                shard ? c->seam_hash.as<u64>() : nullptr, hs_n, hm_n ? c->hmap_keys.as<u64>() : nullptr,
+                hm_n ? c->hmap_par.as<u32>() : nullptr, hm_n, n_clear);
         });
         launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART); });
         launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, mode, guess); });
@@ -605,21 +616,16 @@ static void phase_rid(cc_ctx* c, uint64_t base) {
     rid_unions(c);
 }
 
-// shards of the one-read-back schedule: the id base from the allgathered sums on the device
+// shards of the one-read-back schedule: the ids stay this slab's own (base 0) -- the unions are
+// keyed by id order, which a common base does not change -- and the kernels after the sums'
+// allgather add the base (the sums of the slabs below) themselves
 static void phase_rid_dev(cc_ctx* c, const uint64_t* sums, int rank) {
     RunState& st = state(c);
     CC_REQUIRE(st.stage == 1 && st.fast, "phase order: call cc_shard_dev_begin first");
-    Geom& g = st.hg.g;
-    hipStream_t s = cstream(c);
-    const int64_t nb = g.n_blocks;
-    c->dbase.ensure(16);
     st.base_dev = true;
     st.base = 0;
-    launch(c, "k_rebase", [&] {
-        k_rebase<<<(unsigned)std::min<int64_t>(grid1d(std::max<int64_t>(nb, st.nr)), 1024), 256, 0, s>>>(
-            nb, c->offsets.as<u64>(), sums, rank, c->vals2.as<u32>(), c->KR.as<u64>(), c->scalars.as<u64>(),
-            (u64)st.nr, c->dbase.as<u64>());
-    });
+    st.sums = sums;
+    st.rank = rank;
     rid_unions(c);
 }
 
@@ -807,29 +813,28 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
     const u64* U = st.n_map ? c->map_ids.as<u64>() : nullptr;
     const u64* V = st.n_map ? c->map_vals.as<u64>() : nullptr;
     const int64_t m = st.n_map;
-    const u64* basep = st.base_dev ? c->dbase.as<u64>() : nullptr;
     u64* FIN = KR;
     const uint64_t lut_cap = (uint64_t)nr + (uint64_t)nb + 1;
     HashMap hm;
     if (sd) {
-        // seam map over every slab's pairs: slots for all their ids at <= 1/4 load
-        CC_REQUIRE(st.fast && basep, "phase order: the device seam map follows cc_shard_dev_assign");
+        // seam map over every slab's pairs: slots for all their ids at <= 1/4 load (cleared by this
+        // step's k_clear_front unless its size changed)
+        CC_REQUIRE(st.fast && st.base_dev, "phase order: the device seam map follows cc_shard_dev_assign");
         uint64_t hc = 1024;
         while (hc < 8 * (uint64_t)sd->world * sd->cap) hc <<= 1;
         CC_REQUIRE(hc <= (1ull << 31), "seam map too large");
         c->hmap_keys.ensure(hc * sizeof(u64));
         c->hmap_par.ensure(hc * sizeof(u32));
-        c->hmap_vals.ensure(hc * sizeof(u64));
         hm.keys = c->hmap_keys.as<u64>();
         hm.par = c->hmap_par.as<u32>();
-        hm.vals = c->hmap_vals.as<u64>();
         hm.mask = (u32)(hc - 1);
-        const unsigned gc = (unsigned)std::min<uint64_t>(1024, (hc + 255) / 256);
-        launch(c, "k_map_clear", [&] { k_map_clear<<<gc, 256, 0, s>>>(hm); });
+        if (c->hm_slots != hc) {
+            launch(c, "k_map_clear", [&] { k_map_clear<<<(unsigned)std::min<uint64_t>(1024, (hc + 255) / 256), 256, 0, s>>>(hm); });
+            c->hm_slots = hc;
+        }
         launch(c, "k_map_build", [&] {
             k_map_build<<<(unsigned)std::min<uint64_t>(1024, (sd->world * sd->cap + 255) / 256), 256, 0, s>>>(hm, sd->all, sd->world, sd->cap);
         });
-        launch(c, "k_map_resolve", [&] { k_map_resolve<<<gc, 256, 0, s>>>(hm); });
     }
     if (st.local_only) {
         c->FIN.ensure(nodes * sizeof(u64));
@@ -840,11 +845,22 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
         c->lut.ensure(lut_cap * sizeof(u64));
         u64* lut = c->lut.as<u64>();
         const u64 base = st.base;
+        StatusArgs sa;
+        if (st.fast) {
+            c->status.ensure((16 + 2 * (size_t)nb) * sizeof(u64));
+            sa.out = c->status.as<u64>();
+            sa.FIX = c->spec.as<u32>() + 4 * nt + 4 * SAMPLE_PARTS * nb;
+            sa.values = c->values.as<u64>();
+            sa.offsets = offsets;
+            sa.nb = nb;
+            if (sd) { sa.all = sd->all; sa.world = sd->world; sa.cap = sd->cap; }
+        }
         launch(c, "k_lut_all", [&] {
-            // grid-stride over the ids (their count scalars[0] + 1 is on the device)
+            // grid-stride over the ids (their count scalars[0] + 1 is on the device); the last
+            // workgroup writes the run's status (one-read-back schedule)
             k_lut_all<<<std::min<unsigned>(grid1d(lut_cap), 2048), 256, 0, s>>>(
-                lut_cap, nb, base, basep, offsets, c->values.as<u64>(), c->seg.as<u32>(), c->vals2.as<u32>(), (u64)nr, P, KR,
-                U, V, m, hm, lut, scalars);
+                lut_cap, nb, base, st.base_dev ? st.sums : nullptr, st.rank, offsets, c->values.as<u64>(), c->seg.as<u32>(),
+                c->vals2.as<u32>(), (u64)nr, P, KR, U, V, m, hm, lut, scalars, sa);
         });
         c->lut_valid = true;
     }
@@ -860,7 +876,7 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
         const int64_t mm = sd ? 1 : m;
         if (st.local_only) k_pass2<false><<<(unsigned)nt, NTHREADS, pad, s>>>(g, c->bits.as<u64>(), COUNT, FIN, nullptr, nullptr, 0, 0, out, order, nullptr, nullptr);
         else k_pass2<true><<<(unsigned)nt, NTHREADS, pad, s>>>(g, c->bits.as<u64>(), COUNT, KR, P, c->lut.as<u64>(), st.base, mm, out, order,
-                                                               basep, sd ? scalars : nullptr);
+                                                               nullptr, sd ? scalars : nullptr);
     });
 
     u64 sc[4] = {0, 0, 0, 0};
@@ -869,17 +885,10 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
     st.redo = 0;
     uint64_t total = 0;
     if (st.fast) {
-        // the one read-back of the run: flags, counts and the block values / offsets gathered by
-        // one kernel into one buffer, one copy
+        // the one read-back of the run: flags, counts and the block values / offsets, gathered by
+        // k_lut_all's last workgroup into one buffer, one copy
         const size_t nst = 16 + 2 * (size_t)nb;
-        c->status.ensure(nst * sizeof(u64));
         u64* stat = c->status.as<u64>();
-        const int64_t nth = std::max<int64_t>(nb, 1);
-        launch(c, "k_status", [&] {
-            k_status<<<grid1d(nth), 256, 0, s>>>(scalars, (const u32*)(c->spec.as<u32>() + 4 * nt + 4 * SAMPLE_PARTS * nb),
-                                                 sd ? sd->all : nullptr, sd ? sd->world : 0, sd ? sd->cap : 0,
-                                                 sd ? sd->sums : nullptr, basep, nb, c->values.as<u64>(), offsets, stat);
-        });
         std::vector<u64> h(nst);
         {
             Readback rb(c, nst * sizeof(u64) + 64);
@@ -889,7 +898,7 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
         st.redo = h[0];
         st.n_pairs_max = h[1];
         total = h[2];
-        if (basep) st.base = h[3];
+        if (st.base_dev) st.base = h[3];
         st.n_fix = h[4];
         for (int k = 0; k < 4; ++k) sc[k] = h[5 + k];
         std::memcpy(c->h_values.data(), h.data() + 16, nb * sizeof(u64));
@@ -1009,7 +1018,7 @@ void cc_destroy(cc_ctx* c) {
                       &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec, &c->mark, &c->bflag,
                       &c->ev_main, &c->ev_z, &c->ev_seg, &c->ev_gt, &c->ev_flag, &c->ev_part, &c->rl_wg,
                       &c->gs1, &c->gs2, &c->gs_tab, &c->mask_xmap, &c->seam_hash, &c->ws_tab, &c->ws_buf,
-                      &c->status, &c->dbase, &c->hmap_keys, &c->hmap_par, &c->hmap_vals};
+                      &c->status, &c->hmap_keys, &c->hmap_par};
     for (DevBuf* b : bufs) b->release();
     c->pin.release();
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
@@ -1221,6 +1230,8 @@ int cc_set_option(cc_ctx* c, int option, int64_t value) {
         if (option == CC_OPT_EMPTY_JOB_QUIRK) {
             CC_REQUIRE(value >= 0, "max_jobs must be >= 0");
             c->quirk_jobs = value;
+        } else if (option == CC_OPT_WS_PRENORMALIZED) {
+            c->ws_prenormalized = value != 0;
         } else {
             CC_REQUIRE(false, "unknown option");
         }

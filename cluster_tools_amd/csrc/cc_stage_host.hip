@@ -23,7 +23,7 @@ int64_t cc_block_faces(cc_ctx* c, const uint64_t* labels, const int64_t shape[3]
         c->pairs.ensure(2 * capn * sizeof(u64));
         c->pairs2.ensure(2 * capn * sizeof(u64));
         c->counter.ensure(2 * sizeof(unsigned long long));
-        c->scalars.ensure(4 * sizeof(u64));
+        c->scalars.ensure(SCALARS * sizeof(u64));
         u64* pa = c->pairs.as<u64>();
         u64* pb = pa + capn;
         u64* qa = c->pairs2.as<u64>();
@@ -313,7 +313,7 @@ int cc_shard_top_cubes32(cc_ctx* c, uint32_t* cubes) {
         const unsigned nlayer = (unsigned)((int64_t)g.nt[1] * g.nt[2]);
         launch(c, "k_top_cubes", [&] {
             k_top_cubes<<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), cubes,
-                                                     (u64)st.base, nullptr, nullptr);
+                                                     (u64)st.base, nullptr);
         });
     })
 }
@@ -389,7 +389,7 @@ int cc_shard_dev_top_cubes(cc_ctx* c, uint32_t* cubes_dev) {
         const unsigned nlayer = (unsigned)((int64_t)g.nt[1] * g.nt[2]);
         launch(c, "k_top_cubes", [&] {
             k_top_cubes<<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), cubes_dev,
-                                                     0, c->dbase.as<u64>(), c->scalars.as<u64>());
+                                                     0, c->scalars.as<u64>());
         });
     })
 }
@@ -404,21 +404,18 @@ int cc_shard_dev_seam_pairs(cc_ctx* c, const uint32_t* upper_cubes_dev, const ui
         CC_REQUIRE(st.stage == 2 && st.base_dev, "phase order: call cc_shard_dev_assign first");
         Geom& g = st.hg.g;
         hipStream_t s = cstream(c);
-        HIP_OK(hipMemsetAsync(hdr_pairs_dev, 0, 2 * sizeof(u64), s));
         if (!upper_cubes_dev) {
             launch(c, "k_seam_hdr", [&] { k_seam_hdr<<<1, 64, 0, s>>>(c->scalars.as<u64>(), hdr_pairs_dev); });
             return 0;
         }
         for (int a = 1; a < 3; ++a)
             CC_REQUIRE(g.nb[a] == 1 || st.bs[a] % 2 == 0, "cube form needs even tile origins (even block_shape[1:])");
-        constexpr int64_t HS = 1 << 16;              // the seam pair hash set (see k_seam_cube_pairs)
-        c->seam_hash.ensure(HS * sizeof(u64));
-        HIP_OK(hipMemsetAsync(c->seam_hash.p, 0xFF, HS * sizeof(u64), s));
+        // the seam pair hash set (see k_seam_cube_pairs) was cleared by this step's k_clear_front
         const unsigned nlayer = (unsigned)((int64_t)g.nt[1] * g.nt[2]);
         launch(c, "k_seam_cube_pairs", [&] {
             k_seam_cube_pairs<<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(),
                                                            upper_cubes_dev, sums_dev, rank, hdr_pairs_dev, (u64)cap,
-                                                           c->seam_hash.as<u64>(), (u32)(HS - 1), c->scalars.as<u64>());
+                                                           c->seam_hash.as<u64>(), (u32)(SEAM_SET - 1), c->scalars.as<u64>());
         });
     })
 }

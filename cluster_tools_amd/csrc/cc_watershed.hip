@@ -22,15 +22,23 @@
 // round after a phase's first visits only the tiles the previous round listed.
 namespace cc {
 
-// tile shape and threads (CC_WS_TZ / TY / TX / TT at build time: A/B only)
+// tile shape and threads (CC_WS_TZ / TY / TX / TT at build time, each on its own: A/B only)
 #ifndef CC_WS_TZ
 #define CC_WS_TZ 8
+#endif
+#ifndef CC_WS_TY
 #define CC_WS_TY 8
+#endif
+#ifndef CC_WS_TX
 #define CC_WS_TX 32
+#endif
+#ifndef CC_WS_TT
 #define CC_WS_TT 256
 #endif
 constexpr int WS_Z = CC_WS_TZ, WS_Y = CC_WS_TY, WS_X = CC_WS_TX, WS_T = CC_WS_TT;
 static_assert(WS_Z * WS_Y * WS_X % WS_T == 0, "whole voxels per thread");
+static_assert(WS_T % 64 == 0 && WS_T >= 64, "whole waves per tile");
+static_assert(WS_T >= 6, "ws_list_neighbours lists the six face neighbours with one thread each");
 #ifndef CC_WS_ALT
 #define CC_WS_ALT 0        // A/B only: odd sweeps walk a thread's voxels in reverse order
 #endif
@@ -56,6 +64,11 @@ __device__ __forceinline__ u32 ws_f(float x, float mn, float m, bool nan, bool i
     const u32 b = __float_as_uint(y);
     if ((in_mask && nan) || (b & 0x7FFFFFFFu) > 0x7F800000u) return 0xFFFFFFFEu;
     return f2ord(b);
+}
+
+__global__ void k_fill_u32(int64_t n, u32* p, u32 v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
 }
 
 __global__ void k_ws_init(int64_t n, const u64* __restrict__ seeds, u32* cost, u32* lab, u32* err) {
@@ -271,7 +284,82 @@ __global__ void k_ws_write(int64_t n, const u32* __restrict__ lab, const u8* __r
     }
 }
 
+// ---- 4-D (channel) input of the watershed (_read_data, watershed_from_seeds.py:127-139): the
+// selected channels of the (C, Z, Y, X) block are normalized together (vu.normalize of the 4-D
+// block: one min / max over every channel of the block), then aggregated over the channels by
+// np.mean / np.max / np.min(axis=0) in channel order (float32; mean: sequential sum, then / C).
+// Per block: (mn, m) as block_param derives them; NaN blocks -> NaN everywhere (x - NaN).
+__global__ void k_norm_params(int64_t nb, const u32* smin, const u32* smax, const u32* sflag, float2* nm) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    float mn = __uint_as_float(ord2f(smin[b]));
+    const float mx = __uint_as_float(ord2f(smax[b]));
+    float m = isinf(mn) ? __uint_as_float(0x7FC00000u) : mx - mn;     // numpy: (x - mn).max()
+    if (sflag[b] & 1u) { mn = __uint_as_float(0x7FC00000u); m = mn; }  // NaN: x.min() is NaN
+    nm[b] = make_float2(mn, m);
+}
+
+template <int AGG>   // 0 mean, 1 max, 2 min
+__global__ void k_norm_agg(const float* __restrict__ in, int nc, int64_t Z, int64_t Y, int64_t X, int64_t Bz, int64_t By,
+                           int64_t Bx, int nby, int nbx, const float2* __restrict__ nm, float* __restrict__ out) {
+    const int64_t n = Z * Y * X;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = i % X, y = (i / X) % Y, z = i / (X * Y);
+        const float2 p = nm[((z / Bz) * nby + y / By) * nbx + x / Bx];
+        float acc = 0.0f;
+        for (int c = 0; c < nc; ++c) {
+            float v = __fsub_rn(in[(int64_t)c * n + i], p.x);          // vu.normalize, no contraction
+            if (p.y > 0.0f) v = __fdiv_rn(v, p.y);
+            if (c == 0) acc = v;
+            else if (AGG == 0) acc = __fadd_rn(acc, v);
+            else if (AGG == 1) acc = (acc >= v || isnan(acc)) ? acc : v;    // np.maximum: NaN propagates
+            else acc = (acc <= v || isnan(acc)) ? acc : v;                  // np.minimum
+        }
+        out[i] = AGG == 0 ? __fdiv_rn(acc, (float)nc) : acc;
+    }
+}
+
 }  // namespace cc
+
+extern "C" int cc_normalize_channels(cc_ctx* c, const float* in, int64_t n_channels, const int64_t shape[3],
+                                     const int64_t block_shape[3], int agg, float* out) {
+    CC_TRY({
+        CC_REQUIRE(c && in && out && shape && block_shape, "NULL argument");
+        CC_REQUIRE(n_channels >= 1 && n_channels < (1 << 20), "need at least one channel");
+        CC_REQUIRE(agg >= 0 && agg <= 2, "agg must be 0 (mean), 1 (max) or 2 (min)");
+        HIP_OK(hipSetDevice(c->device));
+        hipStream_t s = cstream(c);
+        RunState& st = state(c);
+        st = RunState();
+        st.hg = make_geom(shape, block_shape, 0);
+        upload_geom(c, st.hg);
+        Geom& gg = st.hg.g;
+        const int64_t nb = gg.n_blocks, n = shape[0] * shape[1] * shape[2];
+        c->bstat.ensure(nb * 3 * sizeof(u32));
+        u32* smin = c->bstat.as<u32>();
+        u32* smax = smin + nb;
+        u32* sflag = smax + nb;
+        HIP_OK(hipMemsetAsync(smin, 0xFF, nb * sizeof(u32), s));
+        HIP_OK(hipMemsetAsync(smax, 0x00, 2 * nb * sizeof(u32), s));
+        // the 4-D block's min / max: every channel's tiles fold into the same block statistics
+        for (int64_t ch = 0; ch < n_channels; ++ch)
+            launch(c, "k_block_stats", [&] { k_block_stats<<<(unsigned)gg.n_tiles, NTHREADS, 0, s>>>(gg, in + ch * n, smin, smax, sflag); });
+        c->gs_tab.ensure(nb * sizeof(float2));
+        float2* nm = c->gs_tab.as<float2>();
+        launch(c, "k_norm_params", [&] { k_norm_params<<<grid1d(nb), 256, 0, s>>>(nb, smin, smax, sflag, nm); });
+        const int nby = gg.nb[1], nbx = gg.nb[2];
+        launch(c, "k_norm_agg", [&] {
+            auto run = [&](auto kern) {
+                kern<<<grid_stride(n), 256, 0, s>>>(in, (int)n_channels, shape[0], shape[1], shape[2], block_shape[0],
+                                                   block_shape[1], block_shape[2], nby, nbx, nm, out);
+            };
+            if (agg == 0) run(k_norm_agg<0>);
+            else if (agg == 1) run(k_norm_agg<1>);
+            else run(k_norm_agg<2>);
+        });
+        sync(c);
+    })
+}
 
 extern "C" int cc_watershed_from_seeds(cc_ctx* c, const float* in, const uint64_t* seeds, const uint8_t* mask,
                                        const int64_t shape[3], const int64_t block_shape[3], uint64_t* out,
@@ -291,9 +379,17 @@ extern "C" int cc_watershed_from_seeds(cc_ctx* c, const float* in, const uint64_
         u32* smin = c->bstat.as<u32>();
         u32* smax = smin + nb;
         u32* sflag = smax + nb;
-        HIP_OK(hipMemsetAsync(smin, 0xFF, nb * sizeof(u32), s));
-        HIP_OK(hipMemsetAsync(smax, 0x00, 2 * nb * sizeof(u32), s));
-        launch(c, "k_block_stats", [&] { k_block_stats<<<(unsigned)gg.n_tiles, NTHREADS, 0, s>>>(gg, in, smin, smax, sflag); });
+        if (c->ws_prenormalized) {
+            // the input is already the normalized block (4-D input: cc_normalize_channels): min =
+            // max = +0 and no NaN flag make f(v) = x - 0 = x, no division (NaN voxels stay NaN)
+            HIP_OK(hipMemsetAsync(smin, 0x00, 2 * nb * sizeof(u32), s));
+            launch(c, "k_fill_u32", [&] { k_fill_u32<<<grid1d(2 * nb), 256, 0, s>>>(2 * nb, smin, 0x80000000u); });
+            HIP_OK(hipMemsetAsync(sflag, 0x00, nb * sizeof(u32), s));
+        } else {
+            HIP_OK(hipMemsetAsync(smin, 0xFF, nb * sizeof(u32), s));
+            HIP_OK(hipMemsetAsync(smax, 0x00, 2 * nb * sizeof(u32), s));
+            launch(c, "k_block_stats", [&] { k_block_stats<<<(unsigned)gg.n_tiles, NTHREADS, 0, s>>>(gg, in, smin, smax, sflag); });
+        }
         // the watershed tiles: per axis, tiles of WS_* from each block's origin
         WsGeom g;
         std::memset(&g, 0, sizeof(g));

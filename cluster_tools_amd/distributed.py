@@ -193,7 +193,7 @@ class ShardedLabeler:
         self.cubes_ok = ((nby == 1 or block_shape[1] % 2 == 0) and (nbx == 1 or block_shape[2] % 2 == 0))
         self.pairs = torch.empty((Y * X, 2), dtype=torch.int64, device=device) if r > 0 else None
         self._planes = {}
-        self.sums = None
+        self._sums = None
         self.form = None
         self.force_form = force_form          # tests: a wider seam-plane form than the ids need
         # one-read-back schedule (cubes32 seam planes): device-resident sums and pair buffers
@@ -223,6 +223,18 @@ class ShardedLabeler:
         if max_sum < 2 ** 32 - 2:
             return 'voxel32'
         return 'voxel64'
+
+    @property
+    def sums(self):
+        """Every slab's sum of block values of the last step (host list; read from the device on
+        first use after a one-read-back step)."""
+        if self._sums is not None and not isinstance(self._sums, list):
+            self._sums = [int(v) for v in self._sums.cpu().tolist()]
+        return self._sums
+
+    @sums.setter
+    def sums(self, v):
+        self._sums = v
 
     def _dev_buffers(self):
         import torch
@@ -270,6 +282,7 @@ class ShardedLabeler:
                 self.fast = False             # a property of the input / id range: stay synchronised
             return None
         self.form = 'cubes32'
+        self.sums = b['sums']                 # read back lazily (the sums property)
         res['n_labels'] = n_labels
         res['max_id'] = n_labels - 1
         res['id_base'] = base

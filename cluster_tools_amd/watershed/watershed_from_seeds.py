@@ -11,8 +11,12 @@ job's compute runs on the MI355X through cc_watershed_from_seeds, one GPU job fo
 
 The reference's watershed call (`vu.watershed`) does not exist in its volume_utils; the watershed
 here is defined in include/cc_mi355x.h (minimax path cost from the seeds, smallest label among the
-optimal predecessors, 6-connected inside each block) -- parity unpinned.  Not supported (raise):
-4-D (channel) input, size_filter > 0.
+optimal predecessors, 6-connected inside each block) -- parity unpinned.  4-D (channel) input
+follows the reference's _read_data (:127-139): the channels channel_begin:channel_end of each block
+are normalized together (one min / max over the 4-D block) and aggregated by np.mean / max / min
+over the channels (cc_normalize_channels, pinned by goldens made from the reference's own
+_read_data: tests/golden/make_golden_ws_read.py); the watershed then takes those values as its
+(already normalized) input.  Not supported (raise): size_filter > 0.
 """
 import json
 import os
@@ -53,9 +57,10 @@ class WatershedFromSeedsBase(Task):
         shebang, block_shape, roi_begin, roi_end = self.global_config_values()
         self.init(shebang)
         shape = vu.get_shape(self.input_path, self.input_key)
-        if len(shape) == 4:
-            raise NotImplementedError('WatershedFromSeeds on the MI355X takes 3-D input only')
+        if len(shape) == 4:                           # channels first (watershed_from_seeds.py:219-220)
+            shape = shape[1:]
         config = self.get_task_config()
+        assert config.get('agglomerate_channels', 'mean') in ('mean', 'max', 'min')
         if config.get('size_filter', 0):
             raise NotImplementedError('size_filter > 0 is not supported (the reference watershed is undefined)')
         chunks = tuple(bs // 2 for bs in block_shape)
@@ -93,7 +98,18 @@ def watershed_from_seeds(job_id, config_path):
     block_list = config['block_list']
     block_shape = config['block_shape']
     shape = list(vu.get_shape(config['input_path'], config['input_key']))
-    x = _read(config['input_path'], config['input_key'], dtype=np.float32)    # normalize's astype('float32')
+    four_d = len(shape) == 4
+    if four_d:
+        # _read_data (watershed_from_seeds.py:127-139): channels channel_begin:channel_end
+        n_ch = shape[0]
+        c0, c1, _ = slice(config.get('channel_begin', 0), config.get('channel_end', None)).indices(n_ch)
+        if c1 <= c0:
+            raise ValueError('empty channel range %s:%s' % (config.get('channel_begin', 0), config.get('channel_end')))
+        shape = shape[1:]
+        x = _read(config['input_path'], config['input_key'], box=[(c0, c1)] + [(0, s) for s in shape],
+                  dtype=np.float32)                   # normalize's astype('float32')
+    else:
+        x = _read(config['input_path'], config['input_key'], dtype=np.float32)    # normalize's astype('float32')
     seeds = _read(config['seeds_path'], config['seeds_key'], dtype=np.uint64)
     mask, resized = read_mask(config, shape)
     device = int(os.environ.get('CC_DEVICE', '0'))
@@ -103,7 +119,10 @@ def watershed_from_seeds(job_id, config_path):
         ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         md = device_mask(ctx, mask, resized, shape, dev)
         sd = torch.from_numpy(seeds.view(np.int64)).to(dev)
-        out, rounds = ctx.watershed_from_seeds(torch.from_numpy(x).to(dev), sd, block_shape, md, out=sd)
+        xd = torch.from_numpy(x).to(dev)
+        if four_d:
+            xd = ctx.normalize_channels(xd, block_shape, config.get('agglomerate_channels', 'mean'))
+        out, rounds = ctx.watershed_from_seeds(xd, sd, block_shape, md, out=sd, prenormalized=four_d)
         out = out.cpu().numpy().view(np.uint64)
         mh = None if md is None else md.cpu().numpy()
     fu.log('watershed: %d relaxation rounds' % rounds)

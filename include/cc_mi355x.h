@@ -275,6 +275,10 @@ int cc_reset_profile(cc_ctx* ctx);
  * merge_assignments drops every merge and writes the identity LUT (merge_assignments.py:115-123).
  * Fused single-volume path only. */
 #define CC_OPT_EMPTY_JOB_QUIRK 1
+/* CC_OPT_WS_PRENORMALIZED = 1: cc_watershed_from_seeds takes its input as the already normalized
+ * block values (4-D input: the output of cc_normalize_channels) instead of normalizing each block
+ * itself; 0 (the default) normalizes (3-D input, watershed_from_seeds.py:138). */
+#define CC_OPT_WS_PRENORMALIZED 2
 int cc_set_option(cc_ctx* ctx, int option, int64_t value);
 /* Test hook: CC_DEBUG_GLOBAL_STITCH routes every block's intra-block seams through the global
  * union-find fallback instead of the per-block LDS path (both must give identical results). */
@@ -300,6 +304,9 @@ typedef struct {
     double   sum_sq_pairs, sum_sq_gt, sum_sq_seg;
 } cc_eval_result;
 
+/* status CC_ERR_ID_RANGE: an id beyond the key packing (seg >= 2^31 or gt >= 2^32 - 1); relabel
+ * the volumes consecutively (cc_relabel_consecutive) and call again */
+#define CC_ERR_ID_RANGE (-3)
 int cc_evaluate(cc_ctx* ctx, const uint64_t* seg_dev, const uint64_t* gt_dev, const int64_t shape[3],
                 const int64_t block_shape[3], int use_ignore, uint64_t ignore_label, cc_eval_result* out);
 /* contingency table of the last cc_evaluate (unordered); returns its size (copies min(size, cap)) */
@@ -330,6 +337,14 @@ int cc_relabel_consecutive(cc_ctx* ctx, const uint64_t* labels_dev, uint64_t* ou
 int cc_watershed_from_seeds(cc_ctx* ctx, const float* in_dev, const uint64_t* seeds_dev, const uint8_t* mask_dev,
                             const int64_t shape[3], const int64_t block_shape[3], uint64_t* out_dev,
                             int64_t* rounds);
+/* 4-D (channel) input of the watershed (_read_data, watershed_from_seeds.py:127-139): in_dev =
+ * the selected channels (n_channels, Z, Y, X) as float32 (the reference's normalize casts first);
+ * per block of block_shape the 4-D block is normalized as one array (vu.normalize, one min / max
+ * over all its channels, volume_utils.py:98-105), then aggregated over the channels in order:
+ * agg 0 = np.mean (float32 sequential sum, then / n_channels), 1 = np.max, 2 = np.min (NaN
+ * propagates).  out_dev (Z, Y, X) float32: the watershed's input with CC_OPT_WS_PRENORMALIZED. */
+int cc_normalize_channels(cc_ctx* ctx, const float* in_dev, int64_t n_channels, const int64_t shape[3],
+                          const int64_t block_shape[3], int agg, float* out_dev);
 
 #ifdef __cplusplus
 }

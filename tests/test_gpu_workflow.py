@@ -338,3 +338,41 @@ def test_threshold_and_watershed_workflow(tmp_path, name):
                         want[bb] = seeds[bb]
     np.testing.assert_array_equal(ws, want)
     assert (tmp_path / 'tmp' / 'watershed_from_seeds.log').exists()
+
+
+@pytest.mark.parametrize('agg', ['mean', 'max'])
+def test_threshold_and_watershed_workflow_channels(tmp_path, agg):
+    """ThresholdAndWatershedWorkflow with `channel` on a 4-D (C, Z, Y, X) input: the components
+    from that channel (block_components.py:150-159), the watershed over _read_data's values
+    (the channels channel_begin:channel_end of each block normalized together, then
+    agglomerate_channels: watershed_from_seeds.py:127-139) -- against the oracle chain."""
+    import json
+    import os
+    from cluster_tools_amd import n5
+    from cluster_tools_amd.thresholded_components.thresholded_components_workflow import \
+        ThresholdAndWatershedWorkflow
+    from oracle import watershed as W
+    shape, bs = (32, 64, 80), [16, 32, 40]
+    x4 = np.stack([O.boundary_map(shape, origin=(0, 5 * c, 9 * c)) for c in range(3)])
+    data = str(tmp_path / 'data.n5')
+    with n5.open_file(data, 'a') as f:
+        f.create_dataset('volumes/boundaries', data=x4, chunks=(1, 16, 32, 40), compression='gzip')
+    from cluster_tools_amd.cluster_tasks import BaseClusterTask
+    cfg = str(tmp_path / 'config')
+    os.makedirs(cfg, exist_ok=True)
+    g = BaseClusterTask.default_global_config()
+    g['block_shape'] = bs
+    with open(os.path.join(cfg, 'global.config'), 'w') as fh:
+        json.dump(g, fh)
+    with open(os.path.join(cfg, 'watershed_from_seeds.config'), 'w') as fh:
+        json.dump({'channel_begin': 0, 'channel_end': 2, 'agglomerate_channels': agg}, fh)
+    t = ThresholdAndWatershedWorkflow(tmp_folder=str(tmp_path / 'tmp'), config_dir=cfg, target='local', max_jobs=4,
+                                      input_path=data, input_key='volumes/boundaries', output_path=data,
+                                      output_key='data', assignment_key='assignments', threshold=0.5,
+                                      threshold_mode='less', channel=1)     # luigi.IntParameter upstream
+    assert _build([t], tmp_path / 'tmp')
+    with n5.open_file(data, 'r') as f:
+        ws = f['data'][:]
+    seeds = O.label_volume(np.ascontiguousarray(x4[1]), bs, 0.5, 'less', n_threads=4)['labels']
+    want = W.watershed_from_seeds(x4, seeds, bs, None, 0, 2, agg)
+    np.testing.assert_array_equal(ws, want)

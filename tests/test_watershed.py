@@ -99,3 +99,63 @@ def test_gpu_watershed_rejects_wide_ids(ctx):
     s[0, 0, 0] = 2 ** 32 - 1
     with pytest.raises(RuntimeError, match='2\\^32'):
         ctx.watershed_from_seeds(x, s, (4, 8, 8))
+
+
+# ---- 4-D (channel) input: _read_data (watershed_from_seeds.py:127-139) ----
+def _ws_read_cases():
+    import json
+    import os
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+    with open(os.path.join(here, 'index_ws_read.json')) as f:
+        idx = json.load(f)
+    return here, sorted(idx.items())
+
+
+WS_READ_HERE, WS_READ_CASES = _ws_read_cases()
+
+
+def _ws_read_golden(name):
+    import os
+    d = np.load(os.path.join(WS_READ_HERE, 'ws_read_%s.npz' % name))
+    return d['input'], d['expected']
+
+
+@pytest.mark.parametrize('name,meta', WS_READ_CASES, ids=[c[0] for c in WS_READ_CASES])
+def test_oracle_read_data_golden(name, meta):
+    """oracle.watershed.read_data restates the reference's _read_data: equal (NaN-aware, bit for
+    bit) to the reference's own output on every golden case."""
+    x4, want = _ws_read_golden(name)
+    got = W.read_data(x4, meta['block_shape'], meta['channel_begin'], meta['channel_end'], meta['agg'])
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name,meta', WS_READ_CASES, ids=[c[0] for c in WS_READ_CASES])
+def test_gpu_normalize_channels_golden(ctx, name, meta):
+    """cc_normalize_channels against the reference's _read_data output, bit for bit (the host
+    casts to float32 first, as normalize's astype does; the channel range is sliced on the host,
+    as the job's read does)."""
+    import torch
+    x4, want = _ws_read_golden(name)
+    sel = np.ascontiguousarray(x4[meta['channel_begin']:meta['channel_end']].astype(np.float32))
+    got = ctx.normalize_channels(torch.from_numpy(sel).cuda(), meta['block_shape'], meta['agg'])
+    np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('agg', ['mean', 'max', 'min'])
+def test_gpu_watershed_4d_vs_oracle(ctx, agg):
+    """4-D input end to end: normalize_channels, then the watershed on those values as given
+    (prenormalized) -- against oracle.watershed_from_seeds on the 4-D array; also with a mask."""
+    import torch
+    shape, bs = (24, 64, 72), (12, 32, 36)
+    x4 = np.stack([O.boundary_map(shape, origin=(0, 7 * c, 3 * c)) for c in range(3)])
+    seeds = _seeds_from_ccl(ctx, np.ascontiguousarray(x4[0]), bs)
+    sh = seeds.cpu().numpy().view(np.uint64)
+    mask = (np.random.default_rng(5).random(shape) < 0.9).astype(np.uint8)
+    for m in (None, mask):
+        want = W.watershed_from_seeds(x4, sh, bs, m, 0, None, agg)
+        xn = ctx.normalize_channels(torch.from_numpy(x4).cuda(), bs, agg)
+        got, _ = ctx.watershed_from_seeds(xn, seeds, bs, None if m is None else torch.from_numpy(m).cuda(),
+                                          prenormalized=True)
+        np.testing.assert_array_equal(got.cpu().numpy().view(np.uint64), want)

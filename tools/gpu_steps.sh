@@ -8,7 +8,8 @@
 #   slabs8_c3 / slabs8_c4   the 8-slab strong-scaling schedule in one process (tools/bench_sharded_slabs.py)
 #   n2gloo         bench.py --gpus 2 --workload c4 self-launched, gloo on one GPU
 #   tests          the whole -m gpu suite                                   -> tests_TAG.log
-#   tests_sharded  tests/test_gpu_sharded.py only
+#   tests_sharded  tests/test_gpu_sharded.py only;  tests_parity  parity + watershed + workflow files
+#   bench_sync / bench_c2_sync   the host-synchronised schedule (CC_FAST=0), same-box A/B
 #   prof_c3 / prof_c3_mask   rocprofv3 trace + FETCH/WRITE passes (tools/profile.sh)
 #   trace_slabs8   rocprofv3 kernel trace of the 8-slab schedule
 set -e -o pipefail
@@ -27,6 +28,9 @@ for step in "$@"; do
     bench_c2)   timeout -k 10 240 python -u bench.py --no-cpu-baseline --workload c2 --steps 50 --warmup 10 > $O/bench_c2_$TAG.json 2> $O/bench_c2_$TAG.err; cat $O/bench_c2_$TAG.json ;;
     bench_c1)   timeout -k 10 240 python -u bench.py --no-cpu-baseline --workload c1 --steps 50 --warmup 10 > $O/bench_c1_$TAG.json 2> $O/bench_c1_$TAG.err; cat $O/bench_c1_$TAG.json ;;
     bench_cont) timeout -k 10 240 python -u bench.py --no-cpu-baseline --dither --steps 20 --warmup 5 > $O/bench_cont_$TAG.json 2> $O/bench_cont_$TAG.err; cat $O/bench_cont_$TAG.json ;;
+    bench_c2_sync) CC_FAST=0 timeout -k 10 240 python -u bench.py --no-cpu-baseline --workload c2 --steps 50 --warmup 10 > $O/bench_c2_sync_$TAG.json 2> $O/bench_c2_sync_$TAG.err; cat $O/bench_c2_sync_$TAG.json ;;
+    bench_sync) CC_FAST=0 timeout -k 10 240 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 > $O/bench_sync_$TAG.json 2> $O/bench_sync_$TAG.err; cat $O/bench_sync_$TAG.json ;;
+    tests_parity) timeout -k 10 900 $PYT tests/test_gpu_parity.py tests/test_watershed.py tests/test_gpu_workflow.py > $O/tests_parity_$TAG.log 2>&1 || { tail -40 $O/tests_parity_$TAG.log; exit 1; }; tail -3 $O/tests_parity_$TAG.log ;;
     slabs8_c3)  timeout -k 10 300 python -u tools/bench_sharded_slabs.py 8 c3 10 > $O/slabs8_c3_$TAG.json 2> $O/slabs8_c3_$TAG.err; cat $O/slabs8_c3_$TAG.json ;;
     slabs8_c4)  timeout -k 10 300 python -u tools/bench_sharded_slabs.py 8 c4 10 > $O/slabs8_c4_$TAG.json 2> $O/slabs8_c4_$TAG.err; cat $O/slabs8_c4_$TAG.json ;;
     n2gloo)     CC_DIST_BACKEND=gloo timeout -k 10 300 python -u bench.py --gpus 2 --workload c4 --steps 5 --warmup 2 --no-cpu-baseline > $O/n2gloo_$TAG.json 2> $O/n2gloo_$TAG.err; cat $O/n2gloo_$TAG.json ;;
