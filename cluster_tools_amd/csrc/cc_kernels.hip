@@ -927,6 +927,10 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     // the used voxels: o - lo puts every voxel at or above lo below every voxel under it, so
     // min k1 gives the smallest value >= lo and max k1 the largest value < lo (hi - o likewise);
     // no per-voxel select on the side of the bound (TB is derived once per tile below).
+    // The nearest values are taken over every voxel of the tile, masked or not: a superset of the
+    // used voxels only moves them closer to the bounds, so k_params_verify can only send more tiles
+    // to k_fix (a masked voxel between the guessed and the exact bound), never fewer -- and the
+    // masked kernel saves the per-voxel selects (8 per float4).
     u32 mn = 0xFFFFFFFFu, mx = 0u, K1N = 0xFFFFFFFFu, K1X = 0u, K2N = 0xFFFFFFFFu, K2X = 0u;
     auto fgp = [&](u32 o) -> bool { return SIDES == 1 ? o >= lo : SIDES == 2 ? o <= hi : (o >= lo && o <= hi); };
     // one voxel (partial tiles)
@@ -934,10 +938,9 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         const u32 o = f2ord(__float_as_uint(x));
         mn = min(mn, o);
         mx = max(mx, o);
-        const bool use = !HAS_MASK || mk != 0;
-        if (SIDES & 1) { const u32 k = o - lo; K1N = min(K1N, use ? k : ~0u); K1X = max(K1X, use ? k : 0u); }
-        if (SIDES & 2) { const u32 k = hi - o; K2N = min(K2N, use ? k : ~0u); K2X = max(K2X, use ? k : 0u); }
-        return use && fgp(o);
+        if (SIDES & 1) { const u32 k = o - lo; K1N = min(K1N, k); K1X = max(K1X, k); }
+        if (SIDES & 2) { const u32 k = hi - o; K2N = min(K2N, k); K2X = max(K2X, k); }
+        return (!HAS_MASK || mk != 0) && fgp(o);
     };
     // four voxels of one float4 (full tiles): the same, min / max folded three operands at a time
     auto quad = [&](float4 v, uchar4 mk, bool fg[4]) {
@@ -945,17 +948,17 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         const u32 o2 = f2ord(__float_as_uint(v.z)), o3 = f2ord(__float_as_uint(v.w));
         mn = min(min(min(min(mn, o0), o1), o2), o3);
         mx = max(max(max(max(mx, o0), o1), o2), o3);
-        const bool u0 = !HAS_MASK || mk.x, u1 = !HAS_MASK || mk.y, u2 = !HAS_MASK || mk.z, u3 = !HAS_MASK || mk.w;
         if (SIDES & 1) {
             const u32 k0 = o0 - lo, k1 = o1 - lo, k2 = o2 - lo, k3 = o3 - lo;
-            K1N = min(min(min(min(K1N, u0 ? k0 : ~0u), u1 ? k1 : ~0u), u2 ? k2 : ~0u), u3 ? k3 : ~0u);
-            K1X = max(max(max(max(K1X, u0 ? k0 : 0u), u1 ? k1 : 0u), u2 ? k2 : 0u), u3 ? k3 : 0u);
+            K1N = min(min(min(min(K1N, k0), k1), k2), k3);
+            K1X = max(max(max(max(K1X, k0), k1), k2), k3);
         }
         if (SIDES & 2) {
             const u32 k0 = hi - o0, k1 = hi - o1, k2 = hi - o2, k3 = hi - o3;
-            K2N = min(min(min(min(K2N, u0 ? k0 : ~0u), u1 ? k1 : ~0u), u2 ? k2 : ~0u), u3 ? k3 : ~0u);
-            K2X = max(max(max(max(K2X, u0 ? k0 : 0u), u1 ? k1 : 0u), u2 ? k2 : 0u), u3 ? k3 : 0u);
+            K2N = min(min(min(min(K2N, k0), k1), k2), k3);
+            K2X = max(max(max(max(K2X, k0), k1), k2), k3);
         }
+        const bool u0 = !HAS_MASK || mk.x, u1 = !HAS_MASK || mk.y, u2 = !HAS_MASK || mk.z, u3 = !HAS_MASK || mk.w;
         fg[0] = u0 && fgp(o0); fg[1] = u1 && fgp(o1); fg[2] = u2 && fgp(o2); fg[3] = u3 && fgp(o3);
     };
     const bool f4 = ti.lz == TZ && ti.ly == TY && ti.lx == TX && ((ti.x0 | (int)(g.X & 3)) & 3) == 0;

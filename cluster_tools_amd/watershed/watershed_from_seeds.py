@@ -87,6 +87,19 @@ class WatershedFromSeedsLocal(WatershedFromSeedsBase, LocalTask):
     pass
 
 
+def _blocks_box(shape, block_shape, block_list):
+    """The block-aligned bounding box of the listed blocks: blocks are independent (no halo), so
+    the watershed of the box's blocks equals theirs in the whole volume (the box starts on block
+    faces, so its own blocking is the volume's)."""
+    blocking = vu.Blocking([0, 0, 0], shape, block_shape)
+    beg, end = list(shape), [0, 0, 0]
+    for b in block_list:
+        bl = blocking.getBlock(b)
+        beg = [min(p, q) for p, q in zip(beg, bl.begin)]
+        end = [max(p, q) for p, q in zip(end, bl.end)]
+    return blocking, [(b, e) for b, e in zip(beg, end)]
+
+
 def watershed_from_seeds(job_id, config_path):
     import torch
     from cluster_tools_amd import _lib
@@ -100,24 +113,33 @@ def watershed_from_seeds(job_id, config_path):
     shape = list(vu.get_shape(config['input_path'], config['input_key']))
     four_d = len(shape) == 4
     if four_d:
+        shape = shape[1:]
+    if not block_list:
+        fu.log_job_success(job_id)
+        return
+    # only the listed blocks' bounding box is read and grown (not the whole volume)
+    blocking, box = _blocks_box(shape, block_shape, block_list)
+    bshape = [e - b for b, e in box]
+    if four_d:
         # _read_data (watershed_from_seeds.py:127-139): channels channel_begin:channel_end
-        n_ch = shape[0]
+        n_ch = vu.get_shape(config['input_path'], config['input_key'])[0]
         c0, c1, _ = slice(config.get('channel_begin', 0), config.get('channel_end', None)).indices(n_ch)
         if c1 <= c0:
             raise ValueError('empty channel range %s:%s' % (config.get('channel_begin', 0), config.get('channel_end')))
-        shape = shape[1:]
-        x = _read(config['input_path'], config['input_key'], box=[(c0, c1)] + [(0, s) for s in shape],
+        x = _read(config['input_path'], config['input_key'], box=[(c0, c1)] + box,
                   dtype=np.float32)                   # normalize's astype('float32')
     else:
-        x = _read(config['input_path'], config['input_key'], dtype=np.float32)    # normalize's astype('float32')
-    seeds = _read(config['seeds_path'], config['seeds_key'], dtype=np.uint64)
-    mask, resized = read_mask(config, shape)
+        x = _read(config['input_path'], config['input_key'], box=box, dtype=np.float32)
+    seeds = _read(config['seeds_path'], config['seeds_key'], box=box, dtype=np.uint64)
+    mask, resized = read_mask(config, shape, box)
     device = int(os.environ.get('CC_DEVICE', '0'))
     dev = torch.device('cuda', device)
     torch.cuda.set_device(dev)
     with _lib.Context(device) as ctx:
         ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-        md = device_mask(ctx, mask, resized, shape, dev)
+        md = device_mask(ctx, mask, resized, shape, dev, box[0][0], bshape[0])
+        if md is not None and resized:                # rows of the box, the full (Y, X): crop y / x
+            md = md[:, box[1][0]:box[1][1], box[2][0]:box[2][1]].contiguous()
         sd = torch.from_numpy(seeds.view(np.int64)).to(dev)
         xd = torch.from_numpy(x).to(dev)
         if four_d:
@@ -125,16 +147,16 @@ def watershed_from_seeds(job_id, config_path):
         out, rounds = ctx.watershed_from_seeds(xd, sd, block_shape, md, out=sd, prenormalized=four_d)
         out = out.cpu().numpy().view(np.uint64)
         mh = None if md is None else md.cpu().numpy()
-    fu.log('watershed: %d relaxation rounds' % rounds)
-    blocking = vu.Blocking([0, 0, 0], shape, block_shape)
+    fu.log('watershed: %d relaxation rounds over the box %s' % (rounds, box))
     with vu.file_reader(config['output_path']) as f:
         ds = f[config['output_key']]
         for b in block_list:
             bb = vu.block_to_bb(blocking.getBlock(b))
-            if mh is not None and not mh[bb].any():          # _ws_block_masked: nothing to do
+            lb = tuple(slice(s.start - o[0], s.stop - o[0]) for s, o in zip(bb, box))
+            if mh is not None and not mh[lb].any():          # _ws_block_masked: nothing to do
                 fu.log_block_success(b)
                 continue
-            ds[bb] = out[bb]
+            ds[bb] = out[lb]
             fu.log_block_success(b)
     fu.log_job_success(job_id)
 

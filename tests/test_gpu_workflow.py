@@ -376,3 +376,37 @@ def test_threshold_and_watershed_workflow_channels(tmp_path, agg):
     seeds = O.label_volume(np.ascontiguousarray(x4[1]), bs, 0.5, 'less', n_threads=4)['labels']
     want = W.watershed_from_seeds(x4, seeds, bs, None, 0, 2, agg)
     np.testing.assert_array_equal(ws, want)
+
+
+def test_watershed_job_block_subset(tmp_path):
+    """The WatershedFromSeeds job over a subset of the blocks reads and grows only their bounding
+    box: the listed blocks equal the oracle's, the others stay as they were (zeros)."""
+    import json
+    from cluster_tools_amd import n5
+    from cluster_tools_amd.watershed.watershed_from_seeds import watershed_from_seeds
+    from oracle import watershed as W
+    shape, bs = (40, 72, 88), [16, 32, 40]
+    x = O.boundary_map(shape, origin=(1, 2, 3))
+    seeds = O.label_volume(x, bs, 0.5, 'less', n_threads=4)['labels']
+    data = str(tmp_path / 'data.n5')
+    with n5.open_file(data, 'a') as f:
+        f.create_dataset('x', data=x, chunks=(8, 16, 20), compression='gzip')
+        f.create_dataset('seeds', data=seeds, chunks=(8, 16, 20), compression='gzip')
+        f.create_dataset('ws', shape=shape, chunks=(8, 16, 20), compression='gzip', dtype='uint64')
+    blocks = [4, 5, 13]                               # 3 x 3 x 3 blocks
+    cfg = str(tmp_path / 'watershed_from_seeds_job_0.config')
+    with open(cfg, 'w') as fh:
+        json.dump({'input_path': data, 'input_key': 'x', 'seeds_path': data, 'seeds_key': 'seeds',
+                   'output_path': data, 'output_key': 'ws', 'block_shape': bs, 'block_list': blocks}, fh)
+    watershed_from_seeds(0, cfg)
+    with n5.open_file(data, 'r') as f:
+        ws = f['ws'][:]
+    want = W.watershed_from_seeds(x, seeds, bs)
+    from cluster_tools_amd.utils import volume_utils as vu
+    blocking = vu.Blocking([0, 0, 0], shape, bs)
+    covered = np.zeros(shape, dtype=bool)
+    for b in blocks:
+        bb = vu.block_to_bb(blocking.getBlock(b))
+        np.testing.assert_array_equal(ws[bb], want[bb])
+        covered[bb] = True
+    assert not ws[~covered].any()

@@ -159,3 +159,16 @@ def test_gpu_watershed_4d_vs_oracle(ctx, agg):
         got, _ = ctx.watershed_from_seeds(xn, seeds, bs, None if m is None else torch.from_numpy(m).cuda(),
                                           prenormalized=True)
         np.testing.assert_array_equal(got.cpu().numpy().view(np.uint64), want)
+
+
+def test_blocks_box():
+    """The watershed job reads only the block-aligned bounding box of its blocks (blocks are
+    independent: the box's own blocking is the volume's)."""
+    from cluster_tools_amd.watershed.watershed_from_seeds import _blocks_box
+    shape, bs = (20, 30, 45), (8, 16, 20)          # 3 x 2 x 3 blocks, edge blocks clipped
+    _, box = _blocks_box(shape, bs, [4, 5])         # blocks (0, 1, 1) and (0, 1, 2)
+    assert box == [(0, 8), (16, 30), (20, 45)]
+    _, box = _blocks_box(shape, bs, list(range(18)))
+    assert box == [(0, 20), (0, 30), (0, 45)]
+    _, box = _blocks_box(shape, bs, [17])
+    assert box == [(16, 20), (16, 30), (40, 45)]
