@@ -267,6 +267,18 @@ def test_integration_binding_runs_as_documented():
                                    ws.data_ptr())
         want = W.watershed_from_seeds(d['input'], out, meta['block_shape'], (d['mask'] != 0).astype(np.uint8))
         np.testing.assert_array_equal(ws.cpu().numpy().view(np.uint64), want)
+        # the 4-D block (cc_normalize_channels + CC_OPT_WS_PRENORMALIZED): two channels, max
+        for b in integration_blocks():
+            if 'def watershed_4d' in b:
+                exec(compile(b, 'INTEGRATION.md', 'exec'), ns)
+        x4 = np.stack([d['input'], d['input'][:, ::-1, :].copy()])
+        s4 = torch.from_numpy(x4).cuda()
+        tmp = torch.empty(x.shape, dtype=torch.float32, device='cuda')
+        torch.cuda.synchronize()
+        ns['watershed_4d'](ctx, s4.data_ptr(), 2, x.shape, meta['block_shape'], 'max', tmp.data_ptr(), seg.data_ptr(),
+                           mk.data_ptr(), ws.data_ptr())
+        want = W.watershed_from_seeds(x4, out, meta['block_shape'], (d['mask'] != 0).astype(np.uint8), 0, None, 'max')
+        np.testing.assert_array_equal(ws.cpu().numpy().view(np.uint64), want)
     finally:
         L.cc_destroy(ctx)
 
