@@ -907,7 +907,10 @@ struct SpecArgs {
 // SIDES: bounds of the guessed interval that can move (1 lower: 'greater', 2 upper: 'less', 3 both)
 // ABL (kernel ablation harness tools/ablate.hip only; 0 in the library): 99 stop once the bit rows
 // are in LDS (loads, ballots, statistics), else as pass1_finish's ABL
-template <bool HAS_MASK, int SIDES, int ABL = 0>
+// INFL: float4 loads in flight per wave on full tiles -- 1 for volumes of many tile rounds (HBM
+// bound: more in flight measured slower), 4 for small volumes (a few rounds of
+// resident tiles in lockstep: each tile's sixteen dependent load round trips were the kernel)
+template <bool HAS_MASK, int SIDES, int ABL = 0, int INFL = 1>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_spec(
     Geom g, SpecArgs sa, const float* __restrict__ in, const u8* __restrict__ mask, u64* BITS, face_t* FACES,
     u32* COUNT, u32* P, u64* KEY) {
@@ -991,14 +994,21 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
                 v[a] = *reinterpret_cast<const float4*>(pz + (z0 + a) * sz);
                 if (HAS_MASK) mk[a] = *reinterpret_cast<const uchar4*>(mz + (z0 + a) * sz);
             };
+            if (INFL > 1) {
 #pragma unroll
-            for (int a = 0; a < RZ4; ++a) {
-                // each load issued right before its use, one in flight per wave (an empty asm
-                // with a memory clobber keeps the next load below the previous processing; two or
-                // four in flight measured slower)
-                asm volatile("" ::: "memory");
-                ld(a);
-                plane_bits(z0 + a, v[a], HAS_MASK ? mk[a] : uchar4{});
+                for (int a = 0; a < RZ4; ++a) ld(a);
+#pragma unroll
+                for (int a = 0; a < RZ4; ++a) plane_bits(z0 + a, v[a], HAS_MASK ? mk[a] : uchar4{});
+            } else {
+#pragma unroll
+                for (int a = 0; a < RZ4; ++a) {
+                    // each load issued right before its use, one in flight per wave (an empty asm
+                    // with a memory clobber keeps the next load below the previous processing;
+                    // two or four in flight measured slower on large volumes)
+                    asm volatile("" ::: "memory");
+                    ld(a);
+                    plane_bits(z0 + a, v[a], HAS_MASK ? mk[a] : uchar4{});
+                }
             }
         }
         // row m = 4 z + q: bits 16 q .. 16 q + 15 of ballot j are voxels x = 4 i + j, i = 0..15

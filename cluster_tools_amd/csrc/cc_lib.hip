@@ -133,6 +133,10 @@ struct cc_ctx {
     void* run = nullptr;     // RunState of the current labelling run
 };
 
+// k_spec launches of at most this many tiles take the four-loads-in-flight variant (8 rounds of
+// the 1024 tiles resident at 4 per CU on 256 CUs)
+constexpr int64_t SPEC_SMALL_TILES = 8 * 1024;
+
 // the context's stream: the caller's (cc_set_stream), else the null stream -- which is torch's
 // default stream too.  No stream of its own: creating one costs a hardware queue (10 ms in the
 // C1 cold-call trace, profiles/r03_c1_trace_*), paid by every one-shot job.
@@ -399,8 +403,13 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             const int64_t t0 = g.nt[0] * ci / n_chunks * layer, t1 = g.nt[0] * (ci + 1) / n_chunks * layer;
             sa.t0 = t0;
             const unsigned ng = (unsigned)(t1 - t0);
+            // small volumes (<= SPEC_SMALL_TILES tiles: a few rounds of resident tiles): four loads in
+            // flight per wave (CC_SPEC_INFL = 1 / 4 forces one, A/B only)
+            int infl = (int64_t)ng <= SPEC_SMALL_TILES ? 4 : 1;
+            if (const char* e = std::getenv("CC_SPEC_INFL"); e && *e) infl = std::atoi(e) > 1 ? 4 : 1;
             launch(c, "k_spec", [&] {
-#define CC_SPEC_LAUNCH(M, S) k_spec<M, S><<<ng, NTHREADS, spad, s>>>(g, sa, in, mask, BITS, FACES, COUNT, P, KR)
+#define CC_SPEC_LAUNCH(M, S) (infl > 1 ? k_spec<M, S, 0, 4><<<ng, NTHREADS, spad, s>>>(g, sa, in, mask, BITS, FACES, COUNT, P, KR) \
+                                         : k_spec<M, S, 0, 1><<<ng, NTHREADS, spad, s>>>(g, sa, in, mask, BITS, FACES, COUNT, P, KR))
                 const unsigned spad = (unsigned)env_int("CC_LDS_PAD_SPEC", 0);   // A/B only, as CC_LDS_PAD_P2
                 if (mask) {
                     if (mode == MODE_GREATER) CC_SPEC_LAUNCH(true, 1);

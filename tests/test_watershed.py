@@ -138,8 +138,12 @@ def test_gpu_normalize_channels_golden(ctx, name, meta):
     import torch
     x4, want = _ws_read_golden(name)
     sel = np.ascontiguousarray(x4[meta['channel_begin']:meta['channel_end']].astype(np.float32))
-    got = ctx.normalize_channels(torch.from_numpy(sel).cuda(), meta['block_shape'], meta['agg'])
-    np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32))
+    got = ctx.normalize_channels(torch.from_numpy(sel).cuda(), meta['block_shape'], meta['agg']).cpu().numpy()
+    # bit for bit, except that a NaN's sign / payload is not pinned (numpy's SIMD np.max returns the
+    # x86 default NaN, the mean path the propagated one; the watershed orders every NaN alike)
+    nan = np.isnan(want)
+    np.testing.assert_array_equal(np.isnan(got), nan)
+    np.testing.assert_array_equal(got.view(np.uint32)[~nan], want.view(np.uint32)[~nan])
 
 
 @pytest.mark.gpu

@@ -17,7 +17,7 @@ if [ -z "$2" ]; then
 fi
 P=tools/profile_cmd.sh
 $P ${TAG}_c3 bench.py --steps 20 --warmup 3 --no-cpu-baseline
-$P ${TAG}_c3_mask bench.py --steps 20 --warmup 3 --no-cpu-baseline --mask
+tools/profile.sh ${TAG}_c3_mask --steps 20 --warmup 3 --mask      # byte-wide mask reads: --narrow
 $P ${TAG}_c3_cont bench.py --steps 20 --warmup 3 --no-cpu-baseline --dither
 timeout -k 10 300 python -u bench.py --traffic-json gpurun_out/prof_${TAG}_c3/summary.json \
     > gpurun_out/final_bench.json 2> gpurun_out/final_bench.err

@@ -12,6 +12,9 @@
 #   bench_sync / bench_c2_sync   the host-synchronised schedule (CC_FAST=0), same-box A/B
 #   prof_c3 / prof_c3_mask   rocprofv3 trace + FETCH/WRITE passes (tools/profile.sh)
 #   trace_slabs8   rocprofv3 kernel trace of the 8-slab schedule
+#   evidence       rocprof summaries of the secondary kernels (threshold, stage path, 8-slab seams,
+#                  Gaussian prefilter, watershed);  prof_c4  C3 + mask with the --narrow correction
+#   roof / ablate  the box's streaming ceilings (tools/roof) and the k_spec ablation (tools/ablate)
 set -e -o pipefail
 TAG=$1; shift
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -39,6 +42,16 @@ for step in "$@"; do
     tests_sharded) timeout -k 10 900 $PYT tests/test_gpu_sharded.py > $O/tests_sharded_$TAG.log 2>&1 || { tail -40 $O/tests_sharded_$TAG.log; exit 1; }; tail -3 $O/tests_sharded_$TAG.log ;;
     prof_c3)    tools/profile.sh "${TAG}_c3" --steps 10 --warmup 3 ;;
     prof_c3_mask) tools/profile.sh "${TAG}_c3_mask" --steps 10 --warmup 3 --mask ;;
+    evidence)   # rocprof trace + FETCH / WRITE of the secondary kernels (tools/profile_cmd.sh)
+                P=tools/profile_cmd.sh
+                $P ${TAG}_threshold tools/bench_threshold.py
+                $P ${TAG}_stage tools/bench_stage.py
+                $P ${TAG}_slabs8 tools/bench_sharded_slabs.py 8 c3 3
+                $P ${TAG}_prefilter tools/bench_prefilter.py --steps 3
+                NO_PMC=1 $P ${TAG}_watershed tools/bench_watershed.py ;;
+    prof_c4)    CC_NVOX=4294967296 tools/profile.sh "${TAG}_c4" --workload c4 --steps 10 --warmup 3 --mask ;;
+    roof)       timeout -k 10 300 tools/roof 1024 2048 2048 5 > $O/roof_$TAG.txt 2>&1; tail -40 $O/roof_$TAG.txt ;;
+    ablate)     timeout -k 10 300 tools/ablate 1024 2048 2048 64 512 512 0 10 > $O/ablate_$TAG.txt 2>&1; tail -5 $O/ablate_$TAG.txt ;;
     trace_slabs8) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
                     -d "$ROOT/$O/trace_slabs8_$TAG" -o run -- python3 "$ROOT/tools/bench_sharded_slabs.py" 8 c3 3 \
                     > "$ROOT/$O/trace_slabs8_$TAG.json" 2> "$ROOT/$O/trace_slabs8_$TAG.err") ;;
