@@ -80,8 +80,7 @@ constexpr u64 RF_CUBES = 4;     // the slab's ids do not fit the 28-bit cube for
 constexpr u64 RF_PAIRS = 8;     // more seam pairs than the pair buffer holds
 
 // the run's device scalars: [0] sum of block values, [1] components owned, [2] block-local roots,
-// [3] redo flags, [4] k_lut_all workgroups done, [5] seam pairs appended, [6] k_seam_cube_pairs
-// workgroups done
+// [3] redo flags, [4] k_lut_all workgroups done, [5] seam pairs appended
 constexpr int SCALARS = 8;
 constexpr int64_t SEAM_SET = 1 << 16;   // slots of the seam pair hash set (k_seam_pairs, k_seam_cube_pairs)
 
@@ -793,7 +792,12 @@ __device__ __forceinline__ u32 block_reduce(u32 v, u32* red, Op op) {
 // (min, 0, max, 0); k_guess combines the parts of each block.
 constexpr int SAMPLE_PARTS = 8;
 
-__global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __restrict__ in, u32* part) {
+__device__ __forceinline__ BlockParam guess_of(const u32* q, float thr, int mode);
+
+// scnt (nullable): per-block count of finished parts (zeroed by k_clear_front); the last part of
+// a block turns the parts into the block's guess (what k_guess does: one launch less)
+__global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __restrict__ in, u32* part, u32* scnt = nullptr,
+                                                     float thr = 0.f, int mode = 0, BlockParam* guess = nullptr) {
     __shared__ u32 red[NTHREADS / 64];
     const int64_t b = blockIdx.x / SAMPLE_PARTS;
     const int pt = blockIdx.x % SAMPLE_PARTS;
@@ -853,19 +857,34 @@ __global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __rest
     if (tid == 0) {
         u32* q = part + 4 * blockIdx.x;
         q[0] = mn; q[1] = 0; q[2] = mx; q[3] = 0;
+        if (scnt) {
+            __threadfence();
+            if (atomicAdd(&scnt[b], 1u) == SAMPLE_PARTS - 1) {
+                __threadfence();
+                guess[b] = guess_of(part + 4 * SAMPLE_PARTS * b, thr, mode);
+            }
+        }
     }
+}
+
+// the guessed interval of a block from its SAMPLE_PARTS parts (agent-coherent loads: other
+// workgroups wrote them)
+__device__ __forceinline__ BlockParam guess_of(const u32* q, float thr, int mode) {
+    u32 mn = 0xFFFFFFFFu, mx = 0u;
+    for (int p = 0; p < SAMPLE_PARTS; ++p) {
+        mn = min(mn, __hip_atomic_load(q + 4 * p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        mx = max(mx, __hip_atomic_load(q + 4 * p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    const bool nan = mx > 0xFF800000u || mn < 0x007FFFFFu;
+    // On continuous data the sampled extremes are not the block's, so the guessed bound misses
+    // the exact one by a little: only tiles holding a voxel between the two are relabelled.
+    return widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
 }
 
 __global__ void k_guess(int64_t nb, const u32* part, float thr, int mode, BlockParam* guess) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
-    const u32* q = part + 4 * SAMPLE_PARTS * b;
-    u32 mn = 0xFFFFFFFFu, mx = 0u;
-    for (int p = 0; p < SAMPLE_PARTS; ++p) { mn = min(mn, q[4 * p]); mx = max(mx, q[4 * p + 2]); }
-    const bool nan = mx > 0xFF800000u || mn < 0x007FFFFFu;
-    // On continuous data the sampled extremes are not the block's, so the guessed bound misses
-    // the exact one by a little: only tiles holding a voxel between the two are relabelled.
-    guess[b] = widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
+    guess[b] = guess_of(part + 4 * SAMPLE_PARTS * b, thr, mode);
 }
 
 // One launch for the front's initial state (it replaced nine memsets of ~4 us each): ordered
@@ -881,8 +900,9 @@ __global__ __launch_bounds__(256) void k_clear_front(int64_t nb, int64_t nt, u32
                                                      u64* scalars, u32* FIX, u8* big, u8* iovf, u32* ipc,
                                                      u32* seg, u32* rc_end, u8 fill, u32* mflag, u8* fchg,
                                                      u64* htab, int64_t htab_n, u64* hkeys, u32* hpar, int64_t hm_n,
-                                                     int64_t n_clear) {
+                                                     int64_t n_clear, u32* scnt) {
     CC_FOR(i, n_clear) {
+        if (scnt && i < nb) scnt[i] = 0u;
         if (htab && i < htab_n) htab[i] = ~0ull;
         if (hkeys && i < hm_n) { hkeys[i] = ~0ull; hpar[i] = (u32)i; }
         if (i < nb) smin[i] = 0xFFFFFFFFu;
@@ -2735,14 +2755,19 @@ __global__ __launch_bounds__(NTHREADS) void k_top_cubes(Geom g, const face_t* __
 // block_faces.py:99-111).  A pair equal to that of the cube before it in x or above it in y is
 // dropped (the first cube of every distinct pair in raster order still emits), the rest go
 // through the device hash set htab (key a << 32 | b; ids >= 2^32 or a full probe sequence are
-// appended anyway: the replicated union-find takes duplicates).  Ids: KR holds this slab's own ids
+// appended anyway: the replicated union-find takes duplicates), after a per-workgroup LDS set
+// (the membrane component's pair recurs in every tile).  Ids: KR holds this slab's own ids
 // (base 0); the global ones add the sums of the slabs below.  out = [cap + 1][2]: row 0 = (count,
-// redo flags) written by the last workgroup (scalars[5] counts, scalars[6] counts workgroups;
-// both zeroed by k_clear_front), then the pairs.  One workgroup per bottom-layer tile.
+// redo flags), written by k_seam_hdr from scalars[5] (the count; zeroed by k_clear_front), then
+// the pairs.  One workgroup per bottom-layer tile.
 __global__ __launch_bounds__(NTHREADS) void k_seam_cube_pairs(Geom g, const face_t* __restrict__ FACES, u32* P,
                                                               const u64* __restrict__ KR, const u32* __restrict__ upper,
                                                               const u64* __restrict__ sums, int rank, u64* out, u64 cap,
                                                               u64* htab, u32 hmask, u64* scalars) {
+    static_assert(CY * CX <= NTHREADS, "one face cube per thread");
+    constexpr int LH = 1024;                         // per-workgroup pair set (LDS)
+    __shared__ u64 pa[CY * CX], pb[CY * CX];
+    __shared__ u64 lset[LH];
     const int64_t t = blockIdx.x;                    // bottom layer: tiles 0 .. nt[1] * nt[2] - 1
     const TileInfo ti = tile_info(g, t);
     const face_t* F = FACES + t * FACE_STRIDE + F_ZLO;
@@ -2754,52 +2779,50 @@ __global__ __launch_bounds__(NTHREADS) void k_seam_cube_pairs(Geom g, const face
     }
     const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2;
     const int64_t CXg = (g.X + 1) / 2;
-    const u32* U0 = upper + (int64_t)(ti.y0 / 2) * CXg + ti.x0 / 2;
-    const int lane = threadIdx.x & 63;
-    // the raw pair of face cube e: (upper cube word >> 4, lower tile node k), 0 when the two
-    // sides share no foreground voxel; equal raw pairs are equal id pairs
-    auto raw_at = [&](int e) -> u64 {
+    const int e = threadIdx.x, cy = e / CX, cx = e % CX;
+    const int lane = e & 63;
+    for (int i = e; i < LH; i += NTHREADS) lset[i] = ~0ull;
+    // the pair of this thread's face cube: (upper id, lower id), both global; 0 = none
+    u64 a = 0, b = 0;
+    if (e < CY * CX && cy < ncy && cx < ncx) {
         const u32 f = F[e];
-        const u32 c = f ? U0[(int64_t)(e / CX) * CXg + e % CX] : 0u;
-        return (c & (f >> FK_BITS) & 0xFu) ? ((u64)(c >> 4) << 32) | ((f & FK_MASK) + 1) : 0ull;
-    };
-    for (int e0 = 0; e0 < ncy * CX; e0 += NTHREADS) {
-        const int e = e0 + threadIdx.x;
-        const int cy = e / CX, cx = e % CX;
-        bool emit = false;
-        u64 a = 0, b = 0;
-        const u64 q = (e < ncy * CX && cx < ncx) ? raw_at(e) : 0ull;
-        if (q && !(cx > 0 && raw_at(e - 1) == q) && !(cy > 0 && raw_at(e - CX) == q)) {
-            a = (q >> 32) - 1 + ubase;
-            b = KR[gfind(P, base + (u32)(q & 0xFFFFFFFFu) - 1)] + own;
-            emit = ((a | b) >> 32) || seam_hash_insert(htab, hmask, (a << 32) | b) != 0;
-        }
-        const u64 bal = __ballot(emit);
-        if (bal) {
-            const int first = (int)(__ffsll((unsigned long long)bal) - 1);
-            unsigned long long pos = 0;
-            if (lane == first) pos = atomicAdd((unsigned long long*)&scalars[5], (unsigned long long)__popcll(bal));
-            pos = __shfl(pos, first, 64) + (u64)__popcll(bal & ((1ull << lane) - 1));
-            if (emit && pos < cap) { out[2 + 2 * pos] = a; out[3 + 2 * pos] = b; }
+        const u32 c = f ? upper[(int64_t)(ti.y0 / 2 + cy) * CXg + ti.x0 / 2 + cx] : 0u;
+        if (c & (f >> FK_BITS) & 0xFu) {
+            a = (u64)(c >> 4) - 1 + ubase;
+            b = KR[gfind(P, base + (f & FK_MASK))] + own;
         }
     }
-    // the last workgroup writes the header
-    __shared__ u32 last;
+    if (e < CY * CX) { pa[e] = a; pb[e] = b; }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        last = atomicAdd((unsigned long long*)&scalars[6], 1ull) == gridDim.x - 1;
-        if (last) {
-            __threadfence();
-            out[0] = __hip_atomic_load(&scalars[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            out[1] = scalars[3];
+    // the cube before in x or above in y with the same pair: dropped (the first cube of every
+    // distinct pair in raster order still emits); the rest through the workgroup's LDS set, then
+    // the device set: only pairs new to both are appended
+    bool emit = a && !(cx > 0 && pa[e - 1] == a && pb[e - 1] == b) && !(cy > 0 && pa[e - CX] == a && pb[e - CX] == b);
+    if (emit && !((a | b) >> 32)) {
+        const u64 key = (a << 32) | b;
+        u32 h = (u32)((key * 0x9E3779B97F4A7C15ull) >> 40) & (LH - 1);
+        for (int p = 0; p < 64; ++p) {
+            const u64 old = atomicCAS((unsigned long long*)&lset[h], ~0ull, (unsigned long long)key);
+            if (old == ~0ull) break;                 // new to the workgroup
+            if (old == key) { emit = false; break; }
+            h = (h + 1) & (LH - 1);
         }
+        if (emit) emit = seam_hash_insert(htab, hmask, key) != 0;
+    }
+    const u64 bal = __ballot(emit);
+    if (bal) {
+        const int first = (int)(__ffsll((unsigned long long)bal) - 1);
+        unsigned long long pos = 0;
+        if (lane == first) pos = atomicAdd((unsigned long long*)&scalars[5], (unsigned long long)__popcll(bal));
+        pos = __shfl(pos, first, 64) + (u64)__popcll(bal & ((1ull << lane) - 1));
+        if (emit && pos < cap) { out[2 + 2 * pos] = a; out[3 + 2 * pos] = b; }
     }
 }
 
-// row 0 of slab 0's pair buffer (no slab below it): (0, its redo flags)
+// row 0 of a slab's pair buffer: (pairs appended by k_seam_cube_pairs -- 0 on slab 0, which has
+// no slab below it --, the slab's redo flags)
 __global__ void k_seam_hdr(const u64* scalars, u64* hdr) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) { hdr[0] = 0; hdr[1] = scalars[3]; }
+    if (threadIdx.x == 0 && blockIdx.x == 0) { hdr[0] = scalars[5]; hdr[1] = scalars[3]; }
 }
 
 // seam map over the allgathered pair buffers all[w] = [cap + 1][2] (w < world): clear, then

@@ -346,10 +346,11 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         // speculative front: sample -> one read for statistics + pass 1 -> exact parameters ->
         // relabel the tiles whose guessed interval was not exact (see k_spec)
         BlockParam* guess = bp + nb;
-        c->spec.ensure((4 * nt + 4 * SAMPLE_PARTS * nb + nt + 1) * sizeof(u32));
+        c->spec.ensure((4 * nt + 4 * SAMPLE_PARTS * nb + nt + 1 + nb) * sizeof(u32));
         u32* TB = c->spec.as<u32>();
         u32* SPART = TB + 4 * nt;
         u32* FIX = SPART + 4 * SAMPLE_PARTS * nb;
+        u32* SCNT = FIX + nt + 1;                  // finished sample parts per block (k_sample)
         // seam outputs and flags (big[nb] / iovf[nt]: "any" flags of the global-stitch fallback)
         c->big.ensure(nb + 1);
         c->pairsl.ensure((size_t)nt * TPC * sizeof(u64));
@@ -373,10 +374,10 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
                 nb, nt, smin, smax, c->scalars.as<u64>(), FIX, c->big.as<u8>(), c->iovf.as<u8>(), c->ipc.as<u32>(),
                 c->seg.as<u32>(), c->rc.as<u32>() + nt, lds_seams ? 0 : 1, mflag, mchg,
                 shard ? c->seam_hash.as<u64>() : nullptr, hs_n, hm_n ? c->hmap_keys.as<u64>() : nullptr,
-                hm_n ? c->hmap_par.as<u32>() : nullptr, hm_n, n_clear);
+                hm_n ? c->hmap_par.as<u32>() : nullptr, hm_n, n_clear, SCNT);
         });
-        launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART); });
-        launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, mode, guess); });
+        // the sample and the guess in one launch (the last part of a block writes its guess)
+        launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART, SCNT, thr, mode, guess); });
         if (const char* e = std::getenv("CC_SPEC"); e && std::string(e) == "0")     // test hook: no guesses
             HIP_OK(hipMemsetAsync(guess, 0, nb * sizeof(BlockParam), s));
         SpecArgs sa;
@@ -438,13 +439,13 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             // device-gated: a fixed grid walks the k_fix list (usually empty) and marks the seams
             // of changed tiles; k_seams_list redoes the marked ones (k_clear_front cleared both)
             launch(c, "k_fix", [&] {
-                const unsigned grid = (unsigned)std::min<int64_t>(nt, 1024);
+                const unsigned grid = (unsigned)std::min<int64_t>(nt, 512);
                 if (mask) k_fix_dev<true><<<grid, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, mask, thr, mode, BITS, FACES, COUNT, P, KR, fchg, flag, list);
                 else k_fix_dev<false><<<grid, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR, fchg, flag, list);
             });
             if (lds_seams)
                 launch(c, "k_seams", [&] {
-                    const unsigned grid = (unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, 2048);
+                    const unsigned grid = (unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, 512);
                     k_seams_list<<<grid, SP_WAVES * 64, 0, s>>>(g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), c->big.as<u8>(),
                                                                c->ipairs.as<u64>(), c->ipc.as<u32>(), c->iovf.as<u8>(), list);
                 });
@@ -667,8 +668,9 @@ static void rid_unions(cc_ctx* c) {
         launch(c, "k_inter_union", [&] {
             k_inter_union<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(g, c->ipairs.as<u64>(), c->ipc.as<u32>(), c->P.as<u32>(), c->KR.as<u64>());
         });
-        // tiles whose block-face pairs overflowed their list (and every tile under CC_DEBUG_GLOBAL_STITCH)
-        const unsigned stitch_grid = (unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, 2048);
+        // tiles whose block-face pairs overflowed their list (and every tile under CC_DEBUG_GLOBAL_STITCH);
+        // the one-read-back schedule launches it unread (it checks the flag itself): a smaller grid
+        const unsigned stitch_grid = (unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, st.fast ? 256 : 2048);
         if (st.any_iovf) launch(c, "k_stitch_inter", [&] { k_stitch<true><<<stitch_grid, SP_WAVES * 64, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), c->big.as<u8>(), c->iovf.as<u8>()); });
     }
     st.n_map = 0;
@@ -867,7 +869,9 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
         launch(c, "k_lut_all", [&] {
             // grid-stride over the ids (their count scalars[0] + 1 is on the device); the last
             // workgroup writes the run's status (one-read-back schedule)
-            k_lut_all<<<std::min<unsigned>(grid1d(lut_cap), 2048), 256, 0, s>>>(
+            // (the one-read-back schedule sizes lut_cap by the root capacity, not the count: a
+            // smaller grid -- every workgroup takes part in the last-workgroup count)
+            k_lut_all<<<std::min<unsigned>(grid1d(lut_cap), st.fast ? 256 : 2048), 256, 0, s>>>(
                 lut_cap, nb, base, st.base_dev ? st.sums : nullptr, st.rank, offsets, c->values.as<u64>(), c->seg.as<u32>(),
                 c->vals2.as<u32>(), (u64)nr, P, KR, U, V, m, hm, lut, scalars, sa);
         });

@@ -417,6 +417,7 @@ int cc_shard_dev_seam_pairs(cc_ctx* c, const uint32_t* upper_cubes_dev, const ui
                                                            upper_cubes_dev, sums_dev, rank, hdr_pairs_dev, (u64)cap,
                                                            c->seam_hash.as<u64>(), (u32)(SEAM_SET - 1), c->scalars.as<u64>());
         });
+        launch(c, "k_seam_hdr", [&] { k_seam_hdr<<<1, 64, 0, s>>>(c->scalars.as<u64>(), hdr_pairs_dev); });
     })
 }
 
