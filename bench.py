@@ -147,6 +147,8 @@ def cold_child(args):
     ctx.label_volume(x, block_shape, args.threshold, args.mode, out=out)
     torch.cuda.synchronize()
     cold = time.perf_counter() - t0
+    host = {k: {'count': v['count'], 'ms': round(v['total_ms'], 3)} for k, v in ctx.profile().items()
+            if k.startswith('host_')}
     warm = []
     for _ in range(5):
         t0 = time.perf_counter()
@@ -154,7 +156,8 @@ def cold_child(args):
         torch.cuda.synchronize()
         warm.append(time.perf_counter() - t0)
     ctx.close()
-    print(json.dumps({'cold_ms': round(cold * 1e3, 3), 'warm_ms': round(min(warm) * 1e3, 3)}), flush=True)
+    print(json.dumps({'cold_ms': round(cold * 1e3, 3), 'warm_ms': round(min(warm) * 1e3, 3), 'first_call_host': host}),
+          flush=True)
 
 
 def cold_start(args, x, block_shape):

@@ -80,7 +80,7 @@ constexpr u64 RF_CUBES = 4;     // the slab's ids do not fit the 28-bit cube for
 constexpr u64 RF_PAIRS = 8;     // more seam pairs than the pair buffer holds
 
 // the run's device scalars: [0] sum of block values, [1] components owned, [2] block-local roots,
-// [3] redo flags, [4] k_lut_all workgroups done, [5] seam pairs appended
+// [3] redo flags, [5] seam pairs appended
 constexpr int SCALARS = 8;
 constexpr int64_t SEAM_SET = 1 << 16;   // slots of the seam pair hash set (k_seam_pairs, k_seam_cube_pairs)
 
@@ -792,12 +792,10 @@ __device__ __forceinline__ u32 block_reduce(u32 v, u32* red, Op op) {
 // (min, 0, max, 0); k_guess combines the parts of each block.
 constexpr int SAMPLE_PARTS = 8;
 
-__device__ __forceinline__ BlockParam guess_of(const u32* q, float thr, int mode);
-
-// scnt (nullable): per-block count of finished parts (zeroed by k_clear_front); the last part of
-// a block turns the parts into the block's guess (what k_guess does: one launch less)
-__global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __restrict__ in, u32* part, u32* scnt = nullptr,
-                                                     float thr = 0.f, int mode = 0, BlockParam* guess = nullptr) {
+// (the guess stays a launch of its own, k_guess: folding it in by a last-part-of-the-block count
+// needed an agent-scope fence per workgroup -- an L2 write-back on gfx950 -- and measured k_sample
+// 0.11 -> 0.25 ms at C3)
+__global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __restrict__ in, u32* part) {
     __shared__ u32 red[NTHREADS / 64];
     const int64_t b = blockIdx.x / SAMPLE_PARTS;
     const int pt = blockIdx.x % SAMPLE_PARTS;
@@ -857,34 +855,19 @@ __global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __rest
     if (tid == 0) {
         u32* q = part + 4 * blockIdx.x;
         q[0] = mn; q[1] = 0; q[2] = mx; q[3] = 0;
-        if (scnt) {
-            __threadfence();
-            if (atomicAdd(&scnt[b], 1u) == SAMPLE_PARTS - 1) {
-                __threadfence();
-                guess[b] = guess_of(part + 4 * SAMPLE_PARTS * b, thr, mode);
-            }
-        }
     }
-}
-
-// the guessed interval of a block from its SAMPLE_PARTS parts (agent-coherent loads: other
-// workgroups wrote them)
-__device__ __forceinline__ BlockParam guess_of(const u32* q, float thr, int mode) {
-    u32 mn = 0xFFFFFFFFu, mx = 0u;
-    for (int p = 0; p < SAMPLE_PARTS; ++p) {
-        mn = min(mn, __hip_atomic_load(q + 4 * p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        mx = max(mx, __hip_atomic_load(q + 4 * p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
-    const bool nan = mx > 0xFF800000u || mn < 0x007FFFFFu;
-    // On continuous data the sampled extremes are not the block's, so the guessed bound misses
-    // the exact one by a little: only tiles holding a voxel between the two are relabelled.
-    return widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
 }
 
 __global__ void k_guess(int64_t nb, const u32* part, float thr, int mode, BlockParam* guess) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
-    guess[b] = guess_of(part + 4 * SAMPLE_PARTS * b, thr, mode);
+    const u32* q = part + 4 * SAMPLE_PARTS * b;
+    u32 mn = 0xFFFFFFFFu, mx = 0u;
+    for (int p = 0; p < SAMPLE_PARTS; ++p) { mn = min(mn, q[4 * p]); mx = max(mx, q[4 * p + 2]); }
+    const bool nan = mx > 0xFF800000u || mn < 0x007FFFFFu;
+    // On continuous data the sampled extremes are not the block's, so the guessed bound misses
+    // the exact one by a little: only tiles holding a voxel between the two are relabelled.
+    guess[b] = widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
 }
 
 // One launch for the front's initial state (it replaced nine memsets of ~4 us each): ordered
@@ -900,9 +883,8 @@ __global__ __launch_bounds__(256) void k_clear_front(int64_t nb, int64_t nt, u32
                                                      u64* scalars, u32* FIX, u8* big, u8* iovf, u32* ipc,
                                                      u32* seg, u32* rc_end, u8 fill, u32* mflag, u8* fchg,
                                                      u64* htab, int64_t htab_n, u64* hkeys, u32* hpar, int64_t hm_n,
-                                                     int64_t n_clear, u32* scnt) {
+                                                     int64_t n_clear) {
     CC_FOR(i, n_clear) {
-        if (scnt && i < nb) scnt[i] = 0u;
         if (htab && i < htab_n) htab[i] = ~0ull;
         if (hkeys && i < hm_n) { hkeys[i] = ~0ull; hpar[i] = (u32)i; }
         if (i < nb) smin[i] = 0xFFFFFFFFu;
@@ -922,6 +904,7 @@ struct SpecArgs {
     u32* smin; u32* smax; u32* sflag;
     u32* TB;                  // 4 per tile (see above)
     int64_t t0;               // first tile of this launch (the front runs in z-layer chunks)
+    int prio = 0;             // A/B (CC_SPEC_PRIO): wave priority raised during the load phase
 };
 
 // SIDES: bounds of the guessed interval that can move (1 lower: 'greater', 2 upper: 'less', 3 both)
@@ -945,6 +928,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
     const int tid = cc_tid(), lane = tid & 63, wave = wave_id();
     const u32 lo = p.lo, hi = p.hi;
+    if (sa.prio) __builtin_amdgcn_s_setprio(3);     // loads first: the CCL phase of other tiles waits
     // Statistics: ordered min / max of every voxel, and the nearest values around the guessed
     // bounds as the min / max of the wrapped distances k1 = o - lo and k2 = hi - o (mod 2^32) over
     // the used voxels: o - lo puts every voxel at or above lo below every voxel under it, so
@@ -1089,6 +1073,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         u32* tb = sa.TB + 4 * t;
         tb[0] = A; tb[1] = B; tb[2] = C; tb[3] = D;
     }
+    if (sa.prio) __builtin_amdgcn_s_setprio(0);
     if (ABL == 99) return;
     pass1_finish<ABL % 99>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, true);
 }
@@ -1958,14 +1943,17 @@ __global__ __launch_bounds__(256) void k_block_face_flags(Geom g, const face_t* 
 // lists as one flat sequence, one pair per lane (a wave per tile left most lanes idle and paid
 // a dependent-load chain per tile); node pairs -> current roots (both finds together),
 // duplicate root pairs dropped per wave, union keyed by rid (the smaller rid becomes the root).
+// IU_TILES tiles per wave (lanes >= IU_TILES count no pairs): fewer than 64 puts more waves on the
+// dependent finds of small volumes / slabs (a C3 slab: 256 waves of 64 tiles on 256 CUs)
+constexpr int IU_TILES = 16;
 __global__ __launch_bounds__(256) void k_inter_union(Geom g, const u64* __restrict__ IPAIRS,
                                                      const u32* __restrict__ IPC, u32* P,
                                                      const u64* __restrict__ K) {
     const int lane = threadIdx.x & 63;
-    const int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+    const int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * IU_TILES;
     if (t0 >= g.n_tiles) return;
     const int64_t tl = t0 + lane;
-    const u32 cnt = tl < g.n_tiles ? IPC[tl] : 0u;
+    const u32 cnt = (lane < IU_TILES && tl < g.n_tiles) ? IPC[tl] : 0u;
     u32 incl = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -2373,7 +2361,7 @@ struct HashMap {
     }
 };
 
-// the one read-back of a run (see phase_final), written by the last workgroup of k_lut_all:
+// the one read-back of a run (see phase_final), written by k_status after k_lut_all:
 // out[0] = redo flags (the run's scalars[3]; with shards, OR over every slab's header plus
 // RF_PAIRS when a slab had more pairs than cap and RF_CUBES when a slab's ids exceed the 28-bit
 // cube form), [1] = largest pair count of a slab, [2] = sum over the slabs (or this volume) of
@@ -2421,59 +2409,58 @@ __global__ void k_lut_init(u64 cap, const u64* scalars, u64 base, u64* lut) {
     if (i < cap && i <= scalars[0]) lut[i] = base + i;
 }
 
-// k_lut_init and k_lut in one launch, one thread per id of this volume (slab): id = base + i is
-// the rid of rank r = id - offsets[b] - 1 of the last block b whose range starts at or below it
-// (empty blocks share the next block's offset); a root's id maps to its component's
-// representative, every other id (label 0 of a block, the slack id) to itself.  Grid-stride over
-// cap >= scalars[0] + 1 ids.  sums (nullable; the one-read-back shard schedule): offsets and KR are
+// k_lut_init and k_lut in one launch: the LUT entry of every id of this volume (slab) -- a root's
+// id maps to its component's representative, every other id (label 0 of a block, the slack id) to
+// itself; lut holds cap >= scalars[0] + 1 entries.  sums (nullable; the one-read-back shard schedule): offsets and KR are
 // this slab's own id space (base 0) and the global base = sum of sums[0 .. rank) is added here;
-// hm (keys != nullptr): the seam map.  st.out: the last workgroup writes the run's status.
+// hm (keys != nullptr): the seam map.
 __global__ void k_lut_all(u64 cap, int64_t nb, u64 base, const u64* sums, int rank, const u64* __restrict__ offsets,
                           const u64* __restrict__ values, const u32* __restrict__ seg_start, const u32* __restrict__ vals,
                           u64 nvals, u32* P, const u64* KR, const u64* U, const u64* V, int64_t m, HashMap hm,
-                          u64* lut, u64* scalars, StatusArgs st) {
+                          u64* lut, u64* scalars) {
     u64 gbase = base, obase = base;                           // ids = obase + i; reps + (gbase - obase)
     if (sums) {
         gbase = 0;
         for (int r = 0; r < rank; ++r) gbase += sums[r];
         obase = 0;
     }
+    // workgroup = block (grid-stride over the blocks), thread = one of the block's ids: no search
+    // for the block of an id.  Block b owns ids offsets[b] + [0, values[b]): + 0 its label 0, + r
+    // its root of rank r - 1; the slack id scalars[0] (n_labels - 1) maps to itself.
     const u64 n = scalars[0] + 1 < cap ? scalars[0] + 1 : cap;
     u64 owned = 0;
-    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-        const u64 id = obase + i;
-        int64_t lo = 0, hi = nb - 1;
-        while (lo < hi) {
-            const int64_t mid = (lo + hi + 1) >> 1;
-            if (offsets[mid] <= id) lo = mid; else hi = mid - 1;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && n) lut[n - 1] = gbase + n - 1;
+    for (int64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const u64 off = offsets[b] - obase, v = values[b];
+        const u64 s0 = seg_start[b];
+        for (u64 r = threadIdx.x; r < v; r += blockDim.x) {
+            const u64 i = off + r;
+            if (i >= n - 1) break;                            // capacity-bound (a run to be redone)
+            u64 rep = gbase + i;
+            const u64 vi = s0 + r - 1;                        // vals index (< nvals: the root arrays' size)
+            if (r > 0 && vi < nvals) {
+                const u32 node = vals[vi];
+                const u32 root = gfind(P, node);
+                const u64 kr = KR[root] + (gbase - obase);
+                rep = hm.keys ? hm.get(kr) : apply_map(kr, U, V, m);
+                owned += (root == node && rep == kr);         // components owned here
+            }
+            lut[i] = rep;
         }
-        const u64 off = offsets[lo], v = values[lo];
-        u64 rep = gbase + i;
-        const u64 vi = (u64)seg_start[lo] + (id - off - 1);   // vals index (< nvals: the root arrays' size)
-        if (off < id && id - off < v && vi < nvals) {         // rank id - off - 1 in [0, v - 1)
-            const u32 node = vals[vi];
-            const u32 r = gfind(P, node);
-            const u64 kr = KR[r] + (gbase - obase);
-            rep = hm.keys ? hm.get(kr) : apply_map(kr, U, V, m);
-            owned += (r == node && rep == kr);                // components owned here
-        }
-        lut[i] = rep;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) owned += __shfl_xor(owned, o, 64);
     if ((threadIdx.x & 63) == 0 && owned) atomicAdd((unsigned long long*)&scalars[1], (unsigned long long)owned);
-    if (!st.out) return;
-    // the last workgroup to finish writes the status (every owned count is in by then)
-    __shared__ u32 last;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        last = atomicAdd((unsigned long long*)&scalars[4], 1ull) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    write_status(st, scalars, sums, sums ? gbase : 0);
+}
+
+// the run's status (see StatusArgs) by one workgroup after k_lut_all (a last-workgroup count in
+// k_lut_all needed an agent-scope fence per workgroup: an L2 write-back each on gfx950, +0.04 ms
+// at C3's 256 blocks)
+__global__ __launch_bounds__(256) void k_status(StatusArgs st, const u64* scalars, const u64* sums, int rank) {
+    u64 gbase = 0;
+    if (sums)
+        for (int r = 0; r < rank; ++r) gbase += sums[r];
+    write_status(st, scalars, sums, gbase);
 }
 
 __global__ void k_lut(int64_t n, const u32* vals, u32* P, const u64* KR, u64 base, const u64* U, const u64* V,

@@ -346,11 +346,10 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         // speculative front: sample -> one read for statistics + pass 1 -> exact parameters ->
         // relabel the tiles whose guessed interval was not exact (see k_spec)
         BlockParam* guess = bp + nb;
-        c->spec.ensure((4 * nt + 4 * SAMPLE_PARTS * nb + nt + 1 + nb) * sizeof(u32));
+        c->spec.ensure((4 * nt + 4 * SAMPLE_PARTS * nb + nt + 1) * sizeof(u32));
         u32* TB = c->spec.as<u32>();
         u32* SPART = TB + 4 * nt;
         u32* FIX = SPART + 4 * SAMPLE_PARTS * nb;
-        u32* SCNT = FIX + nt + 1;                  // finished sample parts per block (k_sample)
         // seam outputs and flags (big[nb] / iovf[nt]: "any" flags of the global-stitch fallback)
         c->big.ensure(nb + 1);
         c->pairsl.ensure((size_t)nt * TPC * sizeof(u64));
@@ -374,16 +373,17 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
                 nb, nt, smin, smax, c->scalars.as<u64>(), FIX, c->big.as<u8>(), c->iovf.as<u8>(), c->ipc.as<u32>(),
                 c->seg.as<u32>(), c->rc.as<u32>() + nt, lds_seams ? 0 : 1, mflag, mchg,
                 shard ? c->seam_hash.as<u64>() : nullptr, hs_n, hm_n ? c->hmap_keys.as<u64>() : nullptr,
-                hm_n ? c->hmap_par.as<u32>() : nullptr, hm_n, n_clear, SCNT);
+                hm_n ? c->hmap_par.as<u32>() : nullptr, hm_n, n_clear);
         });
-        // the sample and the guess in one launch (the last part of a block writes its guess)
-        launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART, SCNT, thr, mode, guess); });
+        launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART); });
+        launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, mode, guess); });
         if (const char* e = std::getenv("CC_SPEC"); e && std::string(e) == "0")     // test hook: no guesses
             HIP_OK(hipMemsetAsync(guess, 0, nb * sizeof(BlockParam), s));
         SpecArgs sa;
         sa.guess = guess;
         sa.smin = smin; sa.smax = smax; sa.sflag = sflag;
         sa.TB = TB;
+        sa.prio = (int)env_int("CC_SPEC_PRIO", 0);
         auto seams = [&](hipStream_t q, int64_t t0, int64_t t1) {
             launch_on(c, q, "k_seams", [&] {
                 k_seams<0><<<(unsigned)((t1 - t0 + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, q>>>(
@@ -666,7 +666,7 @@ static void rid_unions(cc_ctx* c) {
     }
     if (!st.local_only && !st.identity_lut) {
         launch(c, "k_inter_union", [&] {
-            k_inter_union<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(g, c->ipairs.as<u64>(), c->ipc.as<u32>(), c->P.as<u32>(), c->KR.as<u64>());
+            k_inter_union<<<(unsigned)((nt + 4 * IU_TILES - 1) / (4 * IU_TILES)), 256, 0, s>>>(g, c->ipairs.as<u64>(), c->ipc.as<u32>(), c->P.as<u32>(), c->KR.as<u64>());
         });
         // tiles whose block-face pairs overflowed their list (and every tile under CC_DEBUG_GLOBAL_STITCH);
         // the one-read-back schedule launches it unread (it checks the flag itself): a smaller grid
@@ -867,14 +867,13 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
             if (sd) { sa.all = sd->all; sa.world = sd->world; sa.cap = sd->cap; }
         }
         launch(c, "k_lut_all", [&] {
-            // grid-stride over the ids (their count scalars[0] + 1 is on the device); the last
-            // workgroup writes the run's status (one-read-back schedule)
-            // (the one-read-back schedule sizes lut_cap by the root capacity, not the count: a
-            // smaller grid -- every workgroup takes part in the last-workgroup count)
-            k_lut_all<<<std::min<unsigned>(grid1d(lut_cap), st.fast ? 256 : 2048), 256, 0, s>>>(
+            // one workgroup per block (the id count scalars[0] + 1 stays on the device)
+            k_lut_all<<<(unsigned)std::min<int64_t>(nb, 1024), 256, 0, s>>>(
                 lut_cap, nb, base, st.base_dev ? st.sums : nullptr, st.rank, offsets, c->values.as<u64>(), c->seg.as<u32>(),
-                c->vals2.as<u32>(), (u64)nr, P, KR, U, V, m, hm, lut, scalars, sa);
+                c->vals2.as<u32>(), (u64)nr, P, KR, U, V, m, hm, lut, scalars);
         });
+        if (sa.out)
+            launch(c, "k_status", [&] { k_status<<<1, 256, 0, s>>>(sa, scalars, st.base_dev ? st.sums : nullptr, st.rank); });
         c->lut_valid = true;
     }
     // the fused path resolves each tile component's final label inside k_pass2 (no k_finalize)
@@ -899,7 +898,7 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
     uint64_t total = 0;
     if (st.fast) {
         // the one read-back of the run: flags, counts and the block values / offsets, gathered by
-        // k_lut_all's last workgroup into one buffer, one copy
+        // k_status into one buffer, one copy
         const size_t nst = 16 + 2 * (size_t)nb;
         u64* stat = c->status.as<u64>();
         std::vector<u64> h(nst);
