@@ -904,16 +904,12 @@ struct SpecArgs {
     u32* smin; u32* smax; u32* sflag;
     u32* TB;                  // 4 per tile (see above)
     int64_t t0;               // first tile of this launch (the front runs in z-layer chunks)
-    int prio = 0;             // A/B (CC_SPEC_PRIO): wave priority raised during the load phase
 };
 
 // SIDES: bounds of the guessed interval that can move (1 lower: 'greater', 2 upper: 'less', 3 both)
 // ABL (kernel ablation harness tools/ablate.hip only; 0 in the library): 99 stop once the bit rows
 // are in LDS (loads, ballots, statistics), else as pass1_finish's ABL
-// INFL: float4 loads in flight per wave on full tiles -- 1 for volumes of many tile rounds (HBM
-// bound: more in flight measured slower), 4 for small volumes (a few rounds of
-// resident tiles in lockstep: each tile's sixteen dependent load round trips were the kernel)
-template <bool HAS_MASK, int SIDES, int ABL = 0, int INFL = 1>
+template <bool HAS_MASK, int SIDES, int ABL = 0>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_spec(
     Geom g, SpecArgs sa, const float* __restrict__ in, const u8* __restrict__ mask, u64* BITS, face_t* FACES,
     u32* COUNT, u32* P, u64* KEY) {
@@ -928,7 +924,6 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
     const int tid = cc_tid(), lane = tid & 63, wave = wave_id();
     const u32 lo = p.lo, hi = p.hi;
-    if (sa.prio) __builtin_amdgcn_s_setprio(3);     // loads first: the CCL phase of other tiles waits
     // Statistics: ordered min / max of every voxel, and the nearest values around the guessed
     // bounds as the min / max of the wrapped distances k1 = o - lo and k2 = hi - o (mod 2^32) over
     // the used voxels: o - lo puts every voxel at or above lo below every voxel under it, so
@@ -998,21 +993,15 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
                 v[a] = *reinterpret_cast<const float4*>(pz + (z0 + a) * sz);
                 if (HAS_MASK) mk[a] = *reinterpret_cast<const uchar4*>(mz + (z0 + a) * sz);
             };
-            if (INFL > 1) {
 #pragma unroll
-                for (int a = 0; a < RZ4; ++a) ld(a);
-#pragma unroll
-                for (int a = 0; a < RZ4; ++a) plane_bits(z0 + a, v[a], HAS_MASK ? mk[a] : uchar4{});
-            } else {
-#pragma unroll
-                for (int a = 0; a < RZ4; ++a) {
-                    // each load issued right before its use, one in flight per wave (an empty asm
-                    // with a memory clobber keeps the next load below the previous processing;
-                    // two or four in flight measured slower on large volumes)
-                    asm volatile("" ::: "memory");
-                    ld(a);
-                    plane_bits(z0 + a, v[a], HAS_MASK ? mk[a] : uchar4{});
-                }
+            for (int a = 0; a < RZ4; ++a) {
+                // each load issued right before its use, one in flight per wave (an empty asm
+                // with a memory clobber keeps the next load below the previous processing; two or
+                // four in flight measured slower on large volumes, and four gained only 2 % at C2:
+                // DESIGN.md §3)
+                asm volatile("" ::: "memory");
+                ld(a);
+                plane_bits(z0 + a, v[a], HAS_MASK ? mk[a] : uchar4{});
             }
         }
         // row m = 4 z + q: bits 16 q .. 16 q + 15 of ballot j are voxels x = 4 i + j, i = 0..15
@@ -1073,7 +1062,6 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         u32* tb = sa.TB + 4 * t;
         tb[0] = A; tb[1] = B; tb[2] = C; tb[3] = D;
     }
-    if (sa.prio) __builtin_amdgcn_s_setprio(0);
     if (ABL == 99) return;
     pass1_finish<ABL % 99>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, true);
 }
@@ -1111,26 +1099,6 @@ __global__ void k_params_verify(Geom g, const BlockParam* guess, const u32* smin
     }
 }
 
-// pass 1 with the exact parameters for the listed tiles, one workgroup per tile (the host reads
-// the count first: a fixed grid walking the list hoisted the tile set-up out of the loop and
-// spilled; a grid over all tiles paid ~2 us of dependent loads per returning workgroup)
-// fchg[t] = 1 when the tile's faces changed; tiles k_spec only read for statistics (no guess)
-// hold no faces from this run and are always flagged.
-template <bool HAS_MASK>
-__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_fix(
-    Geom g, const u32* FIX, const BlockParam* bp, const BlockParam* guess, const float* __restrict__ in,
-    const u8* __restrict__ mask, float thr, int mode, u64* BITS, face_t* FACES, u32* COUNT, u32* P, u64* KEY,
-    u8* fchg) {
-    __shared__ Pass1LDS L;
-    const int64_t t = __builtin_amdgcn_readfirstlane(FIX[1 + blockIdx.x]);
-    const TileInfo ti = uniform_ti(tile_info(g, t));
-    const BlockParam p = uniform_bp(bp[ti.block]);
-    const bool fresh = __builtin_amdgcn_readfirstlane(guess[ti.block].kind) == BP_INTERVAL;
-    if (!fresh && cc_tid() == 0) fchg[t] = 1;
-    pass1_tile<HAS_MASK>(g, t, ti, p, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L, true,
-                         fresh ? fchg : nullptr);
-}
-
 // the 14 tiles whose seams read the faces of tile f (f itself and the 13 that have it as a
 // lex-negative neighbour): d = 0 .. 13, each marked once (flag) and listed in LIST[1 .. LIST[0]]
 __device__ __forceinline__ void mark_seam(const Geom& g, u32 f, u32 d, u32* flag, u32* LIST) {
@@ -1148,10 +1116,13 @@ __device__ __forceinline__ void mark_seam(const Geom& g, u32 f, u32 d, u32* flag
     if (atomicExch(&flag[t], 1u) == 0u) LIST[1 + atomicAdd(LIST, 1u)] = t;
 }
 
-// k_fix without a host read of the count (the one-read-back schedule): a fixed grid walks
-// FIX[1 .. FIX[0]], and a tile whose faces changed marks the seams to redo right away (what
-// k_mark_seams does after the host-gated k_fix).  fchg, flag and LIST[0] were cleared by
-// k_clear_front.  With nothing to fix every workgroup reads one word and leaves.
+// k_fix: pass 1 with the exact parameters for the tiles listed in FIX[1 .. FIX[0]] (k_params_verify),
+// and a tile whose faces changed marks the seams to redo (flag / LIST for k_seams).  fchg[t] = 1
+// when the tile's faces changed; tiles k_spec only read for statistics (no guess) hold no faces
+// from this run and are always flagged.  The grid walks the list: the one-read-back schedule
+// launches a fixed grid without reading the count (with nothing to fix every workgroup reads one
+// word and leaves), the host-synchronised one a workgroup per listed tile.  fchg, flag and
+// LIST[0] are cleared before (k_clear_front / memsets).
 // (no waves-per-EU bound: under the 64-VGPR bound of k_fix the loop spilled; this kernel sees
 // ~1 % of the tiles on continuous input and none on quantized input)
 template <bool HAS_MASK>
@@ -1899,18 +1870,6 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams_list(Geom g, const face
         const int64_t t = valid ? (int64_t)__builtin_amdgcn_readfirstlane(list[1 + idx]) : 0;
         seams_tile<0>(g, FACES, PAIRS, PC, big, IPAIRS, IPC, iovf, t, valid, LS);
         __syncthreads();
-    }
-}
-
-// Tiles whose seams read the faces of a relabelled tile whose faces changed (FIX[1 .. FIX[0]],
-// k_fix, fchg): the tile itself and the 13 tiles that have it as a lex-negative neighbour.  Each marked once (flag), listed in
-// LIST[1 .. LIST[0]] for k_seams.
-__global__ void k_mark_seams(Geom g, const u32* FIX, const u8* fchg, u32* flag, u32* LIST) {
-    const u32 n = FIX[0];
-    for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < 14 * n; i += gridDim.x * blockDim.x) {
-        const u32 f = FIX[1 + i / 14], d = i % 14;
-        if (!fchg[f]) continue;                    // same faces: every seam list still holds
-        mark_seam(g, f, d, flag, LIST);
     }
 }
 
@@ -3222,10 +3181,6 @@ __global__ __launch_bounds__(NTHREADS) void k_thr_fix(Geom g, const u32* FIX, co
     template __global__ void k_spec<M, S>(Geom, SpecArgs, const float*, const u8*, u64*, face_t*, u32*, u32*, u64*);
 CC_SPEC(false, 1) CC_SPEC(false, 2) CC_SPEC(false, 3) CC_SPEC(true, 1) CC_SPEC(true, 2) CC_SPEC(true, 3)
 #undef CC_SPEC
-template __global__ void k_fix<false>(Geom, const u32*, const BlockParam*, const BlockParam*, const float*, const u8*,
-                                      float, int, u64*, face_t*, u32*, u32*, u64*, u8*);
-template __global__ void k_fix<true>(Geom, const u32*, const BlockParam*, const BlockParam*, const float*, const u8*,
-                                     float, int, u64*, face_t*, u32*, u32*, u64*, u8*);
 template __global__ void k_seams<0>(Geom, const face_t*, u64*, u32*, u8*, u64*, u32*, u8*, int64_t, int64_t, const u32*);
 template __global__ void k_stitch<false>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_stitch<true>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);

@@ -133,10 +133,6 @@ struct cc_ctx {
     void* run = nullptr;     // RunState of the current labelling run
 };
 
-// k_spec launches of at most this many tiles take the four-loads-in-flight variant (8 rounds of
-// the 1024 tiles resident at 4 per CU on 256 CUs)
-constexpr int64_t SPEC_SMALL_TILES = 8 * 1024;
-
 // the context's stream: the caller's (cc_set_stream), else the null stream -- which is torch's
 // default stream too.  No stream of its own: creating one costs a hardware queue (10 ms in the
 // C1 cold-call trace, profiles/r03_c1_trace_*), paid by every one-shot job.
@@ -383,7 +379,6 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         sa.guess = guess;
         sa.smin = smin; sa.smax = smax; sa.sflag = sflag;
         sa.TB = TB;
-        sa.prio = (int)env_int("CC_SPEC_PRIO", 0);
         auto seams = [&](hipStream_t q, int64_t t0, int64_t t1) {
             launch_on(c, q, "k_seams", [&] {
                 k_seams<0><<<(unsigned)((t1 - t0 + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, q>>>(
@@ -404,13 +399,8 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             const int64_t t0 = g.nt[0] * ci / n_chunks * layer, t1 = g.nt[0] * (ci + 1) / n_chunks * layer;
             sa.t0 = t0;
             const unsigned ng = (unsigned)(t1 - t0);
-            // small volumes (<= SPEC_SMALL_TILES tiles: a few rounds of resident tiles): four loads in
-            // flight per wave (CC_SPEC_INFL = 1 / 4 forces one, A/B only)
-            int infl = (int64_t)ng <= SPEC_SMALL_TILES ? 4 : 1;
-            if (const char* e = std::getenv("CC_SPEC_INFL"); e && *e) infl = std::atoi(e) > 1 ? 4 : 1;
             launch(c, "k_spec", [&] {
-#define CC_SPEC_LAUNCH(M, S) (infl > 1 ? k_spec<M, S, 0, 4><<<ng, NTHREADS, spad, s>>>(g, sa, in, mask, BITS, FACES, COUNT, P, KR) \
-                                         : k_spec<M, S, 0, 1><<<ng, NTHREADS, spad, s>>>(g, sa, in, mask, BITS, FACES, COUNT, P, KR))
+#define CC_SPEC_LAUNCH(M, S) k_spec<M, S><<<ng, NTHREADS, spad, s>>>(g, sa, in, mask, BITS, FACES, COUNT, P, KR)
                 const unsigned spad = (unsigned)env_int("CC_LDS_PAD_SPEC", 0);   // A/B only, as CC_LDS_PAD_P2
                 if (mask) {
                     if (mode == MODE_GREATER) CC_SPEC_LAUNCH(true, 1);
@@ -457,17 +447,18 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         st.n_fix = nfix;
         if (lds_seams && ss != s) stream_wait(c, ss, s);
         if (nfix) {
+            // one workgroup per listed tile (the same kernel as the device-gated launch, whose
+            // loop then runs once); it marks the seams of the tiles whose faces changed
             HIP_OK(hipMemsetAsync(fchg, 0, nt, s));
+            HIP_OK(hipMemsetAsync(flag, 0, (nt + 1) * sizeof(u32), s));
             launch(c, "k_fix", [&] {
-                if (mask) k_fix<true><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, mask, thr, mode, BITS, FACES, COUNT, P, KR, fchg);
-                else k_fix<false><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR, fchg);
+                if (mask) k_fix_dev<true><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, mask, thr, mode, BITS, FACES, COUNT, P, KR, fchg, flag, list);
+                else k_fix_dev<false><<<nfix, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR, fchg, flag, list);
             });
             if (lds_seams) {
                 // relabelled faces: the seams of the relabelled tiles and of the tiles above /
                 // beside them again (their lists are overwritten; stale overflow flags only send
                 // work to the global fallback, which reads the current faces)
-                HIP_OK(hipMemsetAsync(flag, 0, (nt + 1) * sizeof(u32), s));
-                launch(c, "k_mark_seams", [&] { k_mark_seams<<<grid1d(14 * (int64_t)nfix), 256, 0, s>>>(g, FIX, fchg, flag, list); });
                 const int64_t nl = std::min<int64_t>(nt, 14 * (int64_t)nfix);
                 launch(c, "k_seams", [&] {
                     k_seams<0><<<(unsigned)((nl + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(

@@ -15,8 +15,7 @@
 #   evidence       rocprof summaries of the secondary kernels (threshold, stage path, 8-slab seams,
 #                  Gaussian prefilter, watershed);  prof_c4  C3 + mask with the --narrow correction
 #   roof / ablate  the box's streaming ceilings (tools/roof) and the k_spec ablation (tools/ablate)
-#   ab_fast / ab_infl / ab_infl_slabs   same-box round-robin A/B: one-read-back vs synchronised
-#                  schedule (C3); k_spec loads in flight 4 vs 1 (C2, C1; the 8-slab schedule)
+#   ab_fast        same-box round-robin A/B: one-read-back vs host-synchronised schedule (C3)
 set -e -o pipefail
 TAG=$1; shift
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -53,9 +52,6 @@ for step in "$@"; do
                 NO_PMC=1 $P ${TAG}_watershed tools/bench_watershed.py ;;
     prof_c4)    CC_NVOX=4294967296 tools/profile.sh "${TAG}_c4" --workload c4 --steps 10 --warmup 3 --mask ;;
     ab_fast)    ROUNDS=3 timeout -k 10 600 tools/gpu_ab.sh "CC_FAST=1" "CC_FAST=0" > $O/ab_fast_$TAG.txt 2>&1; cat $O/ab_fast_$TAG.txt ;;
-    ab_prio)    ROUNDS=3 timeout -k 10 600 tools/gpu_ab.sh "CC_SPEC_PRIO=1" "CC_SPEC_PRIO=0" > $O/ab_prio_$TAG.txt 2>&1; cat $O/ab_prio_$TAG.txt ;;
-    ab_infl)    for w in c2 c1; do ROUNDS=2 timeout -k 10 400 tools/gpu_ab.sh "CC_SPEC_INFL=4" "CC_SPEC_INFL=1" -- --workload $w --steps 30 > $O/ab_infl_${w}_$TAG.txt 2>&1; cat $O/ab_infl_${w}_$TAG.txt; done ;;
-    ab_infl_slabs) for v in 4 1; do CC_SPEC_INFL=$v timeout -k 10 300 python -u tools/bench_sharded_slabs.py 8 c3 10 > $O/slabs8_infl${v}_$TAG.json 2>&1; tail -c 600 $O/slabs8_infl${v}_$TAG.json; echo; done ;;
     roof)       timeout -k 10 300 tools/roof 1024 2048 2048 5 > $O/roof_$TAG.txt 2>&1; tail -40 $O/roof_$TAG.txt ;;
     ablate)     timeout -k 10 300 tools/ablate 1024 2048 2048 64 512 512 0 10 > $O/ablate_$TAG.txt 2>&1; tail -5 $O/ablate_$TAG.txt ;;
     trace_slabs8) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
