@@ -1902,17 +1902,16 @@ __global__ __launch_bounds__(256) void k_block_face_flags(Geom g, const face_t* 
 // lists as one flat sequence, one pair per lane (a wave per tile left most lanes idle and paid
 // a dependent-load chain per tile); node pairs -> current roots (both finds together),
 // duplicate root pairs dropped per wave, union keyed by rid (the smaller rid becomes the root).
-// IU_TILES tiles per wave (lanes >= IU_TILES count no pairs): fewer than 64 puts more waves on the
-// dependent finds of small volumes / slabs (a C3 slab: 256 waves of 64 tiles on 256 CUs)
-constexpr int IU_TILES = 16;
+// tpw tiles per wave (lanes >= tpw count no pairs): 64 for large volumes; 16 for small ones puts
+// more waves on the dependent finds (C2 0.023 -> 0.016 ms; at C3 16 measured 0.060 vs 0.044 ms)
 __global__ __launch_bounds__(256) void k_inter_union(Geom g, const u64* __restrict__ IPAIRS,
                                                      const u32* __restrict__ IPC, u32* P,
-                                                     const u64* __restrict__ K) {
+                                                     const u64* __restrict__ K, int tpw) {
     const int lane = threadIdx.x & 63;
-    const int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * IU_TILES;
+    const int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * tpw;
     if (t0 >= g.n_tiles) return;
     const int64_t tl = t0 + lane;
-    const u32 cnt = (lane < IU_TILES && tl < g.n_tiles) ? IPC[tl] : 0u;
+    const u32 cnt = (lane < tpw && tl < g.n_tiles) ? IPC[tl] : 0u;
     u32 incl = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {

@@ -657,7 +657,9 @@ static void rid_unions(cc_ctx* c) {
     }
     if (!st.local_only && !st.identity_lut) {
         launch(c, "k_inter_union", [&] {
-            k_inter_union<<<(unsigned)((nt + 4 * IU_TILES - 1) / (4 * IU_TILES)), 256, 0, s>>>(g, c->ipairs.as<u64>(), c->ipc.as<u32>(), c->P.as<u32>(), c->KR.as<u64>());
+            const int tpw = nt >= 65536 ? 64 : 16;
+            k_inter_union<<<(unsigned)((nt + 4 * tpw - 1) / (4 * tpw)), 256, 0, s>>>(g, c->ipairs.as<u64>(), c->ipc.as<u32>(), c->P.as<u32>(),
+                                                                                    c->KR.as<u64>(), tpw);
         });
         // tiles whose block-face pairs overflowed their list (and every tile under CC_DEBUG_GLOBAL_STITCH);
         // the one-read-back schedule launches it unread (it checks the flag itself): a smaller grid

@@ -30,6 +30,7 @@ for step in "$@"; do
     bench_full) timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench_full_$TAG.json 2> $O/bench_full_$TAG.err; cat $O/bench_full_$TAG.json ;;
     bench_c4)   timeout -k 10 240 python -u bench.py --no-cpu-baseline --workload c4 --steps 20 --warmup 5 > $O/bench_c4_$TAG.json 2> $O/bench_c4_$TAG.err; cat $O/bench_c4_$TAG.json ;;
     bench_c4_sync) CC_FAST=0 timeout -k 10 240 python -u bench.py --no-cpu-baseline --workload c4 --steps 20 --warmup 5 > $O/bench_c4_sync_$TAG.json 2> $O/bench_c4_sync_$TAG.err; cat $O/bench_c4_sync_$TAG.json ;;
+    bench_c1_sync) CC_FAST=0 timeout -k 10 240 python -u bench.py --no-cpu-baseline --workload c1 --steps 50 --warmup 10 > $O/bench_c1_sync_$TAG.json 2> $O/bench_c1_sync_$TAG.err; cat $O/bench_c1_sync_$TAG.json ;;
     bench_c2)   timeout -k 10 240 python -u bench.py --no-cpu-baseline --workload c2 --steps 50 --warmup 10 > $O/bench_c2_$TAG.json 2> $O/bench_c2_$TAG.err; cat $O/bench_c2_$TAG.json ;;
     bench_c1)   timeout -k 10 240 python -u bench.py --no-cpu-baseline --workload c1 --steps 50 --warmup 10 > $O/bench_c1_$TAG.json 2> $O/bench_c1_$TAG.err; cat $O/bench_c1_$TAG.json ;;
     bench_cont) timeout -k 10 240 python -u bench.py --no-cpu-baseline --dither --steps 20 --warmup 5 > $O/bench_cont_$TAG.json 2> $O/bench_cont_$TAG.err; cat $O/bench_cont_$TAG.json ;;
