@@ -174,6 +174,8 @@ def cold_start(args, x, block_shape):
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     if r.returncode != 0:
         raise RuntimeError('cold-start child failed (%d): %s' % (r.returncode, r.stderr[-2000:]))
+    if os.environ.get('CC_ALLOC_LOG'):
+        sys.stderr.write(r.stderr)
     res = json.loads(r.stdout.strip().splitlines()[-1])
     res['how'] = ('fresh process: torch up and the input in HBM, then timed: cc_create + the first '
                   'cc_label_volume (code-object load, workspace allocation, kernels) to completion; '

@@ -18,6 +18,7 @@ OUT = os.path.join(HERE, 'lib', 'libcc_mi355x.so')
 OUT_N5 = os.path.join(HERE, 'lib', 'libcc_n5.so')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = os.environ.get('CC_OFFLOAD_ARCH', 'gfx950')
+UNITS = ('cc_lib', 'cc_aux')      # translation units of libcc_mi355x.so
 
 
 def sources():
@@ -53,13 +54,29 @@ def build(force=False, verbose=True):
     h = '-DCC_SRC_HASH="%s"' % source_hash()
     cmd_n5 = [os.environ.get('CXX', 'g++'), '-O3', '-std=c++17', '-fPIC', '-shared', '-Wall', h,
               '-o', OUT_N5 + '.tmp', os.path.join(CSRC, 'cc_n5.cpp'), '-lz', '-pthread']
-    cmd = [HIPCC, '--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-shared',
-           '-Wall', '-Wno-unused-function', h, '-o', OUT + '.tmp', os.path.join(CSRC, 'cc_lib.hip')]
-    for c, out in ((cmd_n5, OUT_N5), (cmd, OUT)):
+    # two translation units, two code objects (cc_aux.hip says why), compiled side by side
+    flags = [HIPCC, '--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-Wall', '-Wno-unused-function', h]
+    objs = [OUT + '.%s.o' % u for u in UNITS]
+    cmds = [flags + ['-c', os.path.join(CSRC, u + '.hip'), '-o', o] for u, o in zip(UNITS, objs)]
+    if verbose:
+        print(' '.join(cmd_n5), file=sys.stderr)
+    subprocess.run(cmd_n5, check=True)
+    os.replace(OUT_N5 + '.tmp', OUT_N5)
+    procs = []
+    for c in cmds:
         if verbose:
             print(' '.join(c), file=sys.stderr)
-        subprocess.run(c, check=True)
-        os.replace(out + '.tmp', out)
+        procs.append(subprocess.Popen(c))
+    rcs = [p.wait() for p in procs]
+    if any(rcs):
+        raise subprocess.CalledProcessError(max(rcs), cmds[rcs.index(max(rcs))])
+    link = [HIPCC, '--offload-arch=%s' % ARCH, '-shared', '-o', OUT + '.tmp'] + objs
+    if verbose:
+        print(' '.join(link), file=sys.stderr)
+    subprocess.run(link, check=True)
+    for o in objs:
+        os.remove(o)
+    os.replace(OUT + '.tmp', OUT)
     return OUT
 
 

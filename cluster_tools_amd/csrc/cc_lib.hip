@@ -1,297 +1,22 @@
-// cc_lib.hip -- host orchestration and the C ABI (include/cc_mi355x.h).
-// One translation unit: kernels (cc_kernels.hip, cc_stage_kernels.hip, cc_generate.hip) and the
-// library's own scan / sort / select (cc_prims.hip; no hipcub: see there why).
+// cc_lib.hip -- the labelling path: host orchestration and its C ABI (include/cc_mi355x.h).
+// First of the library's two translation units (the second, cc_aux.hip, holds evaluation,
+// relabelling, prefilter and watershed, so that this unit's code object -- loaded whole at the
+// first launch of a one-shot job -- carries only the labelling path's kernels).  Kernels:
+// cc_kernels.hip, cc_stage_kernels.hip, cc_generate.hip, cc_mask.hip, and the library's own
+// scan / sort / select (cc_prims.hip; no hipcub: see there why).
 
-#include <algorithm>
-#include <atomic>
-#include <chrono>
-#include <cmath>
-#include <cstdlib>
-#include <cstdio>
-#include <cstring>
-#include <map>
-#include <string>
-#include <vector>
-
-#include "../../include/cc_mi355x.h"
 #include "cc_kernels.hip"
 #include "cc_stage_kernels.hip"
 #include "cc_generate.hip"
 #include "cc_mask.hip"
 
-using namespace cc;
-
-static thread_local std::string g_err;
-
-#include "cc_host.hpp"
-
-// integer from the environment (A/B knobs), read per call
-static inline long env_int(const char* name, long dflt) {
-    const char* e = std::getenv(name);
-    return (e && *e) ? std::atol(e) : dflt;
-}
-
-// host time spent in device allocations (instrumentation of the cold, first-call cost: reported by
-// cc_get_profile as the pseudo-kernel "host_alloc" -- count = hipMalloc calls, ms = their time)
-static std::atomic<int64_t> g_alloc_count{0}, g_alloc_ns{0};
-// host synchronisations of the library's streams (reported as "host_sync": count, host ms waited)
-static std::atomic<int64_t> g_sync_count{0}, g_sync_ns{0};
-
-struct DevBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    template <class T>
-    T* as() const { return (T*)p; }
-    void ensure(size_t need) {
-        if (need <= bytes && p) return;
-        const auto t0 = std::chrono::steady_clock::now();
-        if (p) HIP_OK(hipFree(p));
-        p = nullptr;
-        size_t nb = std::max<size_t>(need + need / 8, 256);
-        HIP_OK(hipMalloc(&p, nb));
-        bytes = nb;
-        g_alloc_count += 1;
-        g_alloc_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
-    }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-};
-
+#include "cc_ctx.hpp"
 #include "cc_prims.hip"
-
-// pinned host memory for the pipeline's small read-backs: a copy into pageable memory went
-// through the runtime's staging path (25-80 us of idle GPU per read in the C3 trace)
-struct HostPin {
-    void* p = nullptr;
-    size_t bytes = 0;
-    void* ensure(size_t n) {
-        if (n > bytes) {
-            if (p) HIP_OK(hipHostFree(p));
-            p = nullptr;
-            const size_t nb = std::max<size_t>(n, 64 << 10);
-            HIP_OK(hipHostMalloc(&p, nb, hipHostMallocDefault));
-            bytes = nb;
-        }
-        return p;
-    }
-    void release() {
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-};
-
-struct ProfEntry {
-    int64_t count = 0;
-    double ms = 0;
-};
-
-struct cc_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;      // k_seams of finished front chunks, concurrent with the next chunk
-    // workspace
-    DevBuf tiles, bstat, bparam, bits, faces, count, rc, roff, rl, rcb, P, KR, FIN, keys, keys2, vals, vals2, seg,
-        values, offsets, lut, cub_tmp, scalars, scalars2, counter, in_tmp, mask_tmp, out_tmp, pairs, pairs2,
-        flags, map_ids, map_ids2, map_vals, map_par, big, pairsl, pc, ipairs, ipc, iovf, spec, mark, bflag,
-        ev_main, ev_z, ev_seg, ev_gt, ev_flag, ev_part,   // evaluation (cc_eval.hip)
-        rl_wg,                                            // relabel: per-workgroup id lists
-        gs1, gs2, gs_tab,                                 // Gaussian prefilter temporaries (cc_prefilter.hip)
-        mask_xmap,                                        // resized masks (cc_mask.hip)
-        seam_hash,                                        // seam pair hash set (k_seam_pairs)
-        ws_tab, ws_buf;                                   // seeded watershed (cc_watershed.hip)
-    int64_t ev_cap = 0;      // entries per evaluation hash table of the last cc_evaluate
-    int64_t rl_cap = 0;      // id-set slots of the last cc_relabel_consecutive
-    // last run
-    int64_t n_blocks = 0;
-    uint64_t n_labels = 0;
-    std::vector<uint64_t> h_values, h_offsets;
-    std::vector<int32_t> h_tab;
-    std::vector<int32_t> h_gs;   // Gaussian segment tables (cc_prefilter.hip AxSeg), alive until copied
-    HostPin pin;             // small read-backs (see HostPin)
-    bool lut_valid = false;
-    // profiling
-    int prof = 0;          // 0 off, 1 every launch, 2 the volume-sized kernels only (cc_set_profiling)
-    int debug = 0;         // CC_DEBUG_* test hooks
-    int front_chunks = 1;  // z-layer chunks of the speculative front (CC_FRONT_CHUNKS)
-    int64_t quirk_jobs = 0;  // CC_OPT_EMPTY_JOB_QUIRK: emulate the reference's empty-job branch for max_jobs
-    // one-read-back schedule (see run_pipeline): capacity of the root arrays sized before the count
-    // is known (grown after a run that exceeded it), and whether the last volume of this geometry
-    // needed the global-stitch fallback (then the host-synchronised schedule runs directly)
-    bool ws_prenormalized = false;   // CC_OPT_WS_PRENORMALIZED
-    uint64_t root_cap = 0;
-    bool fast_big = false;
-    std::vector<int32_t> fast_big_tab;
-    DevBuf status, hmap_keys, hmap_par;
-    uint64_t hm_slots = 0;   // slots of the seam map (shards): cleared by the next k_clear_front
-    std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
-    std::vector<hipEvent_t> event_pool;
-    std::map<std::string, ProfEntry> prof_acc;
-    void* run = nullptr;     // RunState of the current labelling run
-};
-
-// the context's stream: the caller's (cc_set_stream), else the null stream -- which is torch's
-// default stream too.  No stream of its own: creating one costs a hardware queue (10 ms in the
-// C1 cold-call trace, profiles/r03_c1_trace_*), paid by every one-shot job.
-static hipStream_t cstream(cc_ctx* c) { return c->stream; }
-// the side stream (k_seams of finished front chunks), created on first use
-static hipStream_t side_stream(cc_ctx* c) {
-    if (!c->side) HIP_OK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-    return c->side;
-}
-
-// ------------------------------------------------------------------------------------------
-// helpers
-// ------------------------------------------------------------------------------------------
-static hipEvent_t pool_event(cc_ctx* c) {
-    if (!c->event_pool.empty()) {
-        hipEvent_t e = c->event_pool.back();
-        c->event_pool.pop_back();
-        return e;
-    }
-    hipEvent_t e;
-    HIP_OK(hipEventCreate(&e));
-    return e;
-}
-
-template <class F>
-static void launch_on(cc_ctx* c, hipStream_t s, const char* name, F&& f) {
-    hipEvent_t a = nullptr, b = nullptr;
-    const bool timed = c->prof == 1 || (c->prof == 2 && (!std::strcmp(name, "k_spec") || !std::strcmp(name, "k_pass2")));
-    if (timed) {
-        a = pool_event(c);
-        b = pool_event(c);
-        HIP_OK(hipEventRecord(a, s));
-    }
-    f();
-    HIP_OK(hipGetLastError());
-    if (timed) {
-        HIP_OK(hipEventRecord(b, s));
-        c->pending.push_back({name, {a, b}});
-    }
-}
-
-template <class F>
-static void launch(cc_ctx* c, const char* name, F&& f) { launch_on(c, cstream(c), name, static_cast<F&&>(f)); }
-
-// stream `waiter` waits for the work enqueued so far on `from`
-static void stream_wait(cc_ctx* c, hipStream_t from, hipStream_t waiter) {
-    hipEvent_t e;
-    HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIP_OK(hipEventRecord(e, from));
-    HIP_OK(hipStreamWaitEvent(waiter, e, 0));
-    HIP_OK(hipEventDestroy(e));
-}
-
-static void resolve_profile(cc_ctx* c) {
-    for (auto& pe : c->pending) {
-        float ms = 0;
-        HIP_OK(hipEventElapsedTime(&ms, pe.second.first, pe.second.second));
-        auto& acc = c->prof_acc[pe.first];
-        acc.count += 1;
-        acc.ms += ms;
-        c->event_pool.push_back(pe.second.first);
-        c->event_pool.push_back(pe.second.second);
-    }
-    c->pending.clear();
-}
-
-static void stream_sync(hipStream_t st) {
-    const auto t0 = std::chrono::steady_clock::now();
-    HIP_OK(hipStreamSynchronize(st));
-    g_sync_count += 1;
-    g_sync_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
-}
-
-static void sync(cc_ctx* c) {
-    stream_sync(cstream(c));
-    if (c->prof) resolve_profile(c);
-}
-
-// read-backs through the pinned buffer: enqueue (device src, bytes) pieces at increasing offsets,
-// one synchronisation, then copy out on the host.  Nothing else may use c->pin meanwhile.
-struct Readback {
-    cc_ctx* c;
-    size_t off = 0;
-    std::vector<std::pair<void*, std::pair<size_t, size_t>>> outs;   // (host dst, (offset, bytes))
-    Readback(cc_ctx* c_, size_t total) : c(c_) { c->pin.ensure(total); }
-    void add(void* dst, const void* src, size_t bytes) {
-        off = (off + 15) & ~size_t(15);
-        if (bytes) HIP_OK(hipMemcpyAsync((char*)c->pin.p + off, src, bytes, hipMemcpyDeviceToHost, cstream(c)));
-        outs.push_back({dst, {off, bytes}});
-        off += bytes;
-    }
-    // resolve = false: the side stream may still run timed kernels (the k_fix count is read
-    // while k_seams runs), so the stream is synchronised without resolving the profile events
-    void wait(bool resolve = true) {
-        if (resolve) sync(c);
-        else stream_sync(cstream(c));
-        for (auto& o : outs) if (o.second.second) std::memcpy(o.first, (char*)c->pin.p + o.second.first, o.second.second);
-    }
-};
-
-// 1-D grid; element kernels index one element per thread, so n must stay below 2^32 threads
-// (volume-sized kernels use CC_FOR with the grid capped by grid_stride()).
-static inline unsigned grid1d(int64_t n, int bs = 256) {
-    CC_REQUIRE(n < (1LL << 32) - bs, "1-D launch larger than 2^32 threads");
-    return (unsigned)std::max<int64_t>(1, (n + bs - 1) / bs);
-}
-static inline unsigned grid_stride(int64_t n, int bs = 256) { return (unsigned)std::min<int64_t>(1 << 20, std::max<int64_t>(1, (n + bs - 1) / bs)); }
-
-static void upload_geom(cc_ctx* c, HostGeom& hg) {
-    // the tables of the last upload are still on the device when the geometry repeats (the
-    // common case: one volume shape per context); otherwise upload (h_tab stays alive in the ctx
-    // until the stream has consumed it)
-    const size_t bytes = hg.tab.size() * sizeof(int32_t);
-    const size_t cap_before = c->tiles.bytes;      // ensure() only reallocates to a larger size
-    c->tiles.ensure(bytes);
-    if (!(c->tiles.bytes == cap_before && c->h_tab == hg.tab)) {
-        c->h_tab = hg.tab;
-        HIP_OK(hipMemcpyAsync(c->tiles.p, c->h_tab.data(), bytes, hipMemcpyHostToDevice, cstream(c)));
-    }
-    bind_geom_tables(hg, c->tiles.as<int32_t>());
-}
-
-static int to_mode(int mode) {
-    CC_REQUIRE(mode >= 0 && mode <= 2, "mode must be 0 (greater), 1 (less) or 2 (equal)");
-    return mode;
-}
 
 // ------------------------------------------------------------------------------------------
 // the device pipeline, in phases (single GPU: local -> rid(0) -> final; z-slab shards:
 // local -> [allgather of sums] -> rid(base) -> planes -> [seam exchange] -> map -> final)
 // ------------------------------------------------------------------------------------------
-struct RunState {
-    HostGeom hg;
-    float thr = 0.f;
-    int mode = 0;
-    int64_t nr = 0;            // block-local roots
-    uint64_t sum_v = 0;        // sum of block values of this volume / slab
-    uint64_t base = 0;         // global id base of this slab
-    int64_t n_map = 0;         // seam mapping size
-    bool local_only = false;
-    int64_t bs[3] = {0, 0, 0};  // block_shape
-    uint64_t n_fix = 0;        // tiles relabelled by k_fix
-    bool identity_lut = false; // the empty-job emulation dropped every block-face merge
-    int stage = 0;             // 1 local done, 2 rid done, 3 final done
-    bool rid0 = false;         // k_emit_roots already wrote the roots' ids for base 0
-    bool sum_known = false;    // sum_v already read back (phase_local's fast path)
-    bool any_iovf = true;      // some tile's block-face pair list overflowed (or not read back)
-    bool fast = false;         // the one-read-back schedule: counts stay on the device
-    bool base_dev = false;     // ids of this slab stay base 0; kernels add the allgathered sums below it
-    uint64_t redo = 0;         // RF_* flags read back by phase_final (fast schedule): run again synchronised
-    uint64_t n_pairs_max = 0;  // largest seam-pair count of a slab (shards of the fast schedule)
-    const uint64_t* sums = nullptr;   // the allgathered sums (shards of the fast schedule)
-    int rank = 0;
-};
-
-static RunState& state(cc_ctx* c) {
-    if (!c->run) c->run = new RunState();
-    return *(RunState*)c->run;
-}
 
 // stats -> params -> pass1 -> intra-block stitch -> roots -> sort -> offsets (local)
 // fast: the one-read-back schedule -- no host read-back in this phase (the k_fix count, the root
@@ -973,18 +698,6 @@ static void run_pipeline(cc_ctx* c, const float* in, const uint8_t* mask, const 
 // ------------------------------------------------------------------------------------------
 // C ABI
 // ------------------------------------------------------------------------------------------
-#define CC_TRY(...)                                                                            \
-    try {                                                                                      \
-        __VA_ARGS__;                                                                           \
-        return 0;                                                                              \
-    } catch (const CCError& e) {                                                               \
-        g_err = e.msg;                                                                         \
-        return -1;                                                                             \
-    } catch (const std::exception& e) {                                                        \
-        g_err = e.what();                                                                      \
-        return -2;                                                                             \
-    }
-
 extern "C" {
 
 #ifndef CC_SRC_HASH
@@ -1286,7 +999,3 @@ int cc_get_profile(cc_ctx* c, char* names, int names_cap, int64_t* counts, doubl
 }  // extern "C"
 
 #include "cc_stage_host.hip"
-#include "cc_eval.hip"
-#include "cc_relabel.hip"
-#include "cc_prefilter.hip"
-#include "cc_watershed.hip"

@@ -19,6 +19,12 @@
 // each tile rescanned with its carry.
 namespace cc {
 namespace prims {
+// one copy of the primitives per translation unit of the library (cc_lib.hip, cc_aux.hip): the
+// inline namespace keeps their kernels' symbols apart
+#ifndef CC_PRIMS_NS
+#define CC_PRIMS_NS core
+#endif
+inline namespace CC_PRIMS_NS {
 
 constexpr int PT = 256;                 // threads per workgroup
 constexpr int PW = PT / 64;             // waves
@@ -500,5 +506,6 @@ void scan_excl(const T* in, T* out, int64_t n, DevBuf& tmpbuf, hipStream_t s) {
     scan_excl<T>(in, out, n, (char*)tmpbuf.p, s);
 }
 
+}  // namespace CC_PRIMS_NS
 }  // namespace prims
 }  // namespace cc
