@@ -237,15 +237,49 @@ __device__ __forceinline__ void gunion_roots(u32* P, const u64* K, u32 a, u32 b)
     }
 }
 
+// ---- wave-level scan and reductions by DPP (row shifts / row broadcasts of the VALU operand):
+// no LDS round trip per step, where a shuffle (ds_bpermute) costs an LDS instruction and its
+// latency at each of the six steps.  All 64 lanes must be active.
+// dpp<CTRL, ROW, BANK>(old, x): x of the lane CTRL names; `old` where that lane is outside the
+// row or the lane is masked off by the row / bank masks.
+template <int CTRL, int ROW = 0xf, int BANK = 0xf>
+__device__ __forceinline__ u32 dpp(u32 old, u32 x) {
+    return (u32)__builtin_amdgcn_update_dpp((int)old, (int)x, CTRL, ROW, BANK, false);
+}
+constexpr int DPP_SHR1 = 0x111, DPP_SHR2 = 0x112, DPP_SHR3 = 0x113, DPP_SHR4 = 0x114, DPP_SHR8 = 0x118,
+              DPP_BCAST15 = 0x142, DPP_BCAST31 = 0x143;
+
+// sum of x over lanes 0..lane
+__device__ __forceinline__ u32 wave_incl_sum(u32 x) {
+    u32 y = x + dpp<DPP_SHR1>(0u, x);
+    y += dpp<DPP_SHR2>(0u, x);
+    y += dpp<DPP_SHR3>(0u, x);                 // lane: x over its 4-lane window of the row
+    y += dpp<DPP_SHR4, 0xf, 0xe>(0u, y);       // lanes 4..15 of each row: 8-lane windows
+    y += dpp<DPP_SHR8, 0xf, 0xc>(0u, y);       // lanes 8..15: the row's prefix
+    y += dpp<DPP_BCAST15, 0xa>(0u, y);         // rows 1, 3: + the previous row's total
+    y += dpp<DPP_BCAST31, 0xc>(0u, y);         // rows 2, 3: + the total of rows 0, 1
+    return y;
+}
+// min (MAX = false) / max of x over the wave, in lane 63 (other lanes: partial results)
+template <bool MAX>
+__device__ __forceinline__ u32 wave_minmax_last(u32 x) {
+    constexpr u32 id = MAX ? 0u : ~0u;
+    auto op = [](u32 a, u32 b) { return MAX ? (a > b ? a : b) : (a < b ? a : b); };
+    x = op(x, dpp<DPP_SHR1>(id, x));
+    x = op(x, dpp<DPP_SHR2>(id, x));
+    x = op(x, dpp<DPP_SHR4>(id, x));
+    x = op(x, dpp<DPP_SHR8>(id, x));            // lane 15 of each row: the row's
+    x = op(x, dpp<DPP_BCAST15, 0xa>(id, x));
+    x = op(x, dpp<DPP_BCAST31, 0xc>(id, x));
+    return x;
+}
+__device__ __forceinline__ u32 wave_min(u32 x) { return (u32)__builtin_amdgcn_readlane((int)wave_minmax_last<false>(x), 63); }
+__device__ __forceinline__ u32 wave_max(u32 x) { return (u32)__builtin_amdgcn_readlane((int)wave_minmax_last<true>(x), 63); }
+
 // ---- block-wide exclusive scan (NTHREADS threads) ----
 __device__ __forceinline__ u32 block_excl_scan(u32 v, u32* scratch, u32* total) {
     const int tid = cc_tid(), lane = tid & 63, wave = tid >> 6;
-    u32 x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        u32 y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
+    const u32 x = wave_incl_sum(v);
     if (lane == 63) scratch[wave] = x;
     __syncthreads();
     u32 base = 0, tot = 0;

@@ -108,8 +108,8 @@ struct TileCCL {
     u32 B[NCROW];          // run starts of each cube row (bit cx)
     u32 E[NCROW];          // x-links: bit cx iff cube cx is 26-linked to cube cx + 1
     u32 roff[NCROW];       // run id of each cube row's first run
-    u32 par[NRUN];         // union-find over run ids, then root | k << 16
     u32 scratch[8];
+    u32 par[NRUN];         // union-find over run ids, then root | k << 16
 };
 
 __device__ __forceinline__ void load_row4(const u64* rows, int row, u64 a[4]) {
@@ -657,18 +657,18 @@ __device__ __forceinline__ BlockParam widen(BlockParam p, int mode) {
     return p;
 }
 
-// block-wide reduction of one value per thread (red: NTHREADS / 64 words); result in every thread
-template <class Op>
-__device__ __forceinline__ u32 block_reduce(u32 v, u32* red, Op op) {
+// block-wide min (MAX = false) / max of one value per thread (red: NTHREADS / 64 words); result
+// in every thread
+template <bool MAX>
+__device__ __forceinline__ u32 block_minmax(u32 v, u32* red) {
     const int tid = cc_tid();
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o, 64));
+    v = wave_minmax_last<MAX>(v);
     __syncthreads();
-    if ((tid & 63) == 0) red[tid >> 6] = v;
+    if ((tid & 63) == 63) red[tid >> 6] = v;
     __syncthreads();
     v = red[0];
 #pragma unroll
-    for (int w = 1; w < NTHREADS / 64; ++w) v = op(v, red[w]);
+    for (int w = 1; w < NTHREADS / 64; ++w) v = MAX ? max(v, red[w]) : min(v, red[w]);
     return v;
 }
 
@@ -734,8 +734,8 @@ __global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __rest
     } else {
         sweep(f);
     }
-    mn = block_reduce(mn, red, [](u32 a, u32 c) { return min(a, c); });
-    mx = block_reduce(mx, red, [](u32 a, u32 c) { return max(a, c); });
+    mn = block_minmax<false>(mn, red);
+    mx = block_minmax<true>(mx, red);
     if (tid == 0) {
         u32* q = part + 4 * blockIdx.x;
         q[0] = mn; q[1] = 0; q[2] = mx; q[3] = 0;
@@ -880,9 +880,10 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
 #pragma unroll
             for (int a = 0; a < RZ4; ++a) {
                 // each load issued right before its use, one in flight per wave (an empty asm
-                // with a memory clobber keeps the next load below the previous processing; two or
-                // four in flight measured slower on large volumes, and four gained only 2 % at C2:
-                // DESIGN.md §3)
+                // with a memory clobber keeps the next load below the previous processing).  More
+                // in flight measured slower on large volumes -- two or four register loads, and a
+                // ring of four 1-KB LDS-DMA slots per wave (C3 k_spec 3.69 -> 3.87 ms, C4 masked
+                // 4.89 -> 5.27 ms; only C2 gained, 0.179 -> 0.172 ms): DESIGN.md §3
                 asm volatile("" ::: "memory");
                 ld(a);
                 plane_bits(z0 + a, v[a], HAS_MASK ? mk[a] : uchar4{});
@@ -912,13 +913,10 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         const int r = slot_row(lane, wave);
         if (r / TY < ti.lz && r % TY < ti.ly) L.rows[r] = split_row(((u64)mhi << 32) | mlo);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        mn = min(mn, (u32)__shfl_xor(mn, o, 64));
-        mx = max(mx, (u32)__shfl_xor(mx, o, 64));
-        if (SIDES & 1) { K1N = min(K1N, (u32)__shfl_xor(K1N, o, 64)); K1X = max(K1X, (u32)__shfl_xor(K1X, o, 64)); }
-        if (SIDES & 2) { K2N = min(K2N, (u32)__shfl_xor(K2N, o, 64)); K2X = max(K2X, (u32)__shfl_xor(K2X, o, 64)); }
-    }
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    if (SIDES & 1) { K1N = wave_min(K1N); K1X = wave_max(K1X); }
+    if (SIDES & 2) { K2N = wave_min(K2N); K2X = wave_max(K2X); }
     if (lane == 0) {
         red[0][wave] = mn; red[1][wave] = mx; red[2][wave] = K1N; red[3][wave] = K1X; red[4][wave] = K2N;
         red[5][wave] = K2X;
@@ -2905,13 +2903,10 @@ __device__ __forceinline__ void thr_spec_tile(const Geom& g, const SpecArgs& sa,
             out[o] = voxel(in[o]);
         }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        mn = min(mn, (u32)__shfl_xor(mn, o, 64));
-        mx = max(mx, (u32)__shfl_xor(mx, o, 64));
-        if (SIDES & 1) { K1N = min(K1N, (u32)__shfl_xor(K1N, o, 64)); K1X = max(K1X, (u32)__shfl_xor(K1X, o, 64)); }
-        if (SIDES & 2) { K2N = min(K2N, (u32)__shfl_xor(K2N, o, 64)); K2X = max(K2X, (u32)__shfl_xor(K2X, o, 64)); }
-    }
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    if (SIDES & 1) { K1N = wave_min(K1N); K1X = wave_max(K1X); }
+    if (SIDES & 2) { K2N = wave_min(K2N); K2X = wave_max(K2X); }
     if (lane == 0) {
         red[0][wave] = mn; red[1][wave] = mx; red[2][wave] = K1N; red[3][wave] = K1X; red[4][wave] = K2N;
         red[5][wave] = K2X;

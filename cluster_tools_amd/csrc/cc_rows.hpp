@@ -102,12 +102,8 @@ __device__ __forceinline__ void stats_tile(const Geom& g, const TileInfo& ti, co
         mn = o < mn ? o : mn;
         mx = o > mx ? o : mx;
     });
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const u32 a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
-        mn = a < mn ? a : mn;
-        mx = b > mx ? b : mx;
-    }
+    mn = wave_min(mn);
+    mx = wave_max(mx);
     const bool anynan = mx > 0xFF800000u || mn < 0x007FFFFFu;      // > ord(+inf) or < ord(-inf)
     if (lane == 0) { red[0][wave] = mn; red[1][wave] = mx; red[2][wave] = anynan; }
     __syncthreads();
