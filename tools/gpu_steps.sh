@@ -6,7 +6,7 @@
 #   bench_full     default bench line with the CPU baseline                 -> bench_full_TAG.json
 #   bench_c4 / bench_c2 / bench_c1 / bench_cont   other workloads on one GPU
 #   slabs8_c3 / slabs8_c4   the 8-slab strong-scaling schedule in one process (tools/bench_sharded_slabs.py)
-#   n2gloo         bench.py --gpus 2 --workload c4 self-launched, gloo on one GPU
+#   n2gloo / n4gloo  bench.py --gpus 2 --workload c4 / --gpus 4 --workload c3 self-launched, gloo on one GPU
 #   tests          the whole -m gpu suite                                   -> tests_TAG.log
 #   tests_sharded  tests/test_gpu_sharded.py only;  tests_parity  parity + watershed + workflow files
 #   bench_sync / bench_c2_sync   the host-synchronised schedule (CC_FAST=0), same-box A/B
@@ -39,6 +39,7 @@ for step in "$@"; do
     tests_parity) timeout -k 10 900 $PYT tests/test_gpu_parity.py tests/test_watershed.py tests/test_gpu_workflow.py > $O/tests_parity_$TAG.log 2>&1 || { tail -40 $O/tests_parity_$TAG.log; exit 1; }; tail -3 $O/tests_parity_$TAG.log ;;
     slabs8_c3)  timeout -k 10 300 python -u tools/bench_sharded_slabs.py 8 c3 10 > $O/slabs8_c3_$TAG.json 2> $O/slabs8_c3_$TAG.err; cat $O/slabs8_c3_$TAG.json ;;
     slabs8_c4)  timeout -k 10 300 python -u tools/bench_sharded_slabs.py 8 c4 10 > $O/slabs8_c4_$TAG.json 2> $O/slabs8_c4_$TAG.err; cat $O/slabs8_c4_$TAG.json ;;
+    n4gloo)     CC_DIST_BACKEND=gloo timeout -k 10 400 python -u bench.py --gpus 4 --workload c3 --steps 5 --warmup 2 --no-cpu-baseline > $O/n4gloo_$TAG.json 2> $O/n4gloo_$TAG.err; cat $O/n4gloo_$TAG.json ;;
     n2gloo)     CC_DIST_BACKEND=gloo timeout -k 10 300 python -u bench.py --gpus 2 --workload c4 --steps 5 --warmup 2 --no-cpu-baseline > $O/n2gloo_$TAG.json 2> $O/n2gloo_$TAG.err; cat $O/n2gloo_$TAG.json ;;
     tests)      timeout -k 10 1000 $PYT tests -m gpu > $O/tests_$TAG.log 2>&1 || { tail -40 $O/tests_$TAG.log; exit 1; }; tail -3 $O/tests_$TAG.log ;;
     tests_sharded) timeout -k 10 900 $PYT tests/test_gpu_sharded.py > $O/tests_sharded_$TAG.log 2>&1 || { tail -40 $O/tests_sharded_$TAG.log; exit 1; }; tail -3 $O/tests_sharded_$TAG.log ;;
