@@ -14,6 +14,7 @@
 #   trace_slabs8   rocprofv3 kernel trace of the 8-slab schedule
 #   evidence       rocprof summaries of the secondary kernels (threshold, stage path, 8-slab seams,
 #                  Gaussian prefilter, watershed);  prof_c4  C3 + mask with the --narrow correction
+#   clock          effective GPU clock per kernel of the C3 step (tools/pmc_clock.sh)
 #   roof / ablate  the box's streaming ceilings (tools/roof) and the k_spec ablation (tools/ablate)
 #   ab_fast        same-box round-robin A/B: one-read-back vs host-synchronised schedule (C3)
 set -e -o pipefail
@@ -54,6 +55,7 @@ for step in "$@"; do
                 NO_PMC=1 $P ${TAG}_watershed tools/bench_watershed.py ;;
     prof_c4)    CC_NVOX=4294967296 tools/profile.sh "${TAG}_c4" --workload c4 --steps 10 --warmup 3 --mask ;;
     ab_fast)    ROUNDS=3 timeout -k 10 600 tools/gpu_ab.sh "CC_FAST=1" "CC_FAST=0" > $O/ab_fast_$TAG.txt 2>&1; cat $O/ab_fast_$TAG.txt ;;
+    clock)      tools/pmc_clock.sh "$TAG" ;;
     roof)       timeout -k 10 300 tools/roof 1024 2048 2048 5 > $O/roof_$TAG.txt 2>&1; tail -40 $O/roof_$TAG.txt ;;
     ablate)     timeout -k 10 300 tools/ablate 1024 2048 2048 64 512 512 0 10 > $O/ablate_$TAG.txt 2>&1; tail -5 $O/ablate_$TAG.txt ;;
     trace_slabs8) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
