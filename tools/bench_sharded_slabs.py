@@ -7,7 +7,7 @@ synchronisations, launch gaps -- is measured without rank contention.  Workloads
   c3  the same without the mask
 The single-volume step of the same volume (cc_label_volume) is timed beside it: the target is
 per-slab time <= 1.15 x (single-volume step / N).  Prints one JSON line.
-Usage: python tools/bench_sharded_slabs.py [N] [c4|c3] [steps]"""
+Usage: python tools/bench_sharded_slabs.py [N] [c4|c3] [steps] [sync]"""
 import json
 import os
 import sys
@@ -26,6 +26,7 @@ def main():
     n = int(a[0]) if a else 8
     wl = a[1] if len(a) > 1 else 'c4'
     steps = int(a[2]) if len(a) > 2 else 5
+    sched = a[3] if len(a) > 3 else None        # 'sync': the host-synchronised schedule (evidence of its kernels)
     shape, bs = (1024, 2048, 2048), (64, 512, 512)
     dev = torch.device('cuda', 0)
     ctxs = [_lib.Context(0) for _ in range(n)]
@@ -47,12 +48,12 @@ def main():
     del out
     torch.cuda.empty_cache()
     for _ in range(2):
-        label_slabs_single_process(ctxs, x, bs, 0.5, 'greater', mask=mask)
+        label_slabs_single_process(ctxs, x, bs, 0.5, 'greater', mask=mask, schedule=sched)
     torch.cuda.synchronize()
     ctxs[0].reset_profile()                  # host_* counters are library-wide
     t0 = time.perf_counter()
     for _ in range(steps):
-        o, res, sums, luts = label_slabs_single_process(ctxs, x, bs, 0.5, 'greater', mask=mask)
+        o, res, sums, luts = label_slabs_single_process(ctxs, x, bs, 0.5, 'greater', mask=mask, schedule=sched)
         del o
     torch.cuda.synchronize()
     slabs_ms = (time.perf_counter() - t0) / steps * 1e3
@@ -62,7 +63,7 @@ def main():
     for c in ctxs:
         c.set_profiling(1)
         c.reset_profile()
-    o, res, sums, luts = label_slabs_single_process(ctxs, x, bs, 0.5, 'greater', mask=mask)
+    o, res, sums, luts = label_slabs_single_process(ctxs, x, bs, 0.5, 'greater', mask=mask, schedule=sched)
     torch.cuda.synchronize()
     per = []
     for c in ctxs:
@@ -73,6 +74,7 @@ def main():
     mid = per[n // 2]
     print(json.dumps({
         'workload': '%s %s block %s as %d z-slabs in one process' % (wl, shape, bs, n),
+        'schedule': sched or 'default',
         'single_volume_step_ms': round(single_ms, 3), 'all_slabs_ms': round(slabs_ms, 3),
         'per_slab_ms': round(slabs_ms / n, 3), 'target_per_slab_ms': round(1.15 * single_ms / n, 3),
         'ratio_to_ideal': round(slabs_ms / single_ms, 4),

@@ -12,8 +12,8 @@
 #   bench_sync / bench_c2_sync   the host-synchronised schedule (CC_FAST=0), same-box A/B
 #   prof_c3 / prof_c3_mask   rocprofv3 trace + FETCH/WRITE passes (tools/profile.sh)
 #   trace_slabs8   rocprofv3 kernel trace of the 8-slab schedule
-#   evidence       rocprof summaries of the secondary kernels (threshold, stage path, 8-slab seams,
-#                  Gaussian prefilter, watershed);  prof_c4  C3 + mask with the --narrow correction
+#   evidence       rocprof summaries of the secondary kernels (threshold, stage path, 8-slab seams of
+#                  both schedules, Gaussian prefilter, resized mask + 4-D normalize, watershed);  prof_c4  C3 + mask with the --narrow correction
 #   clock          effective GPU clock per kernel of the C3 step (tools/pmc_clock.sh)
 #   roof / ablate  the box's streaming ceilings (tools/roof) and the k_spec ablation (tools/ablate)
 #   ab_fast        same-box round-robin A/B: one-read-back vs host-synchronised schedule (C3)
@@ -52,7 +52,9 @@ for step in "$@"; do
                 $P ${TAG}_stage tools/bench_stage.py
                 $P ${TAG}_slabs8 tools/bench_sharded_slabs.py 8 c3 3
                 $P ${TAG}_prefilter tools/bench_prefilter.py --steps 3
-                NO_PMC=1 $P ${TAG}_watershed tools/bench_watershed.py ;;
+                NARROW=k_mask_resize=536870912 $P ${TAG}_misc tools/bench_misc.py
+                $P ${TAG}_slabs8sync tools/bench_sharded_slabs.py 8 c3 2 sync
+                $P ${TAG}_watershed tools/bench_watershed.py ;;
     prof_c4)    CC_NVOX=4294967296 tools/profile.sh "${TAG}_c4" --workload c4 --steps 10 --warmup 3 --mask ;;
     ab_fast)    ROUNDS=3 timeout -k 10 600 tools/gpu_ab.sh "CC_FAST=1" "CC_FAST=0" > $O/ab_fast_$TAG.txt 2>&1; cat $O/ab_fast_$TAG.txt ;;
     clock)      tools/pmc_clock.sh "$TAG" ;;
