@@ -909,13 +909,28 @@ int cc_resize_mask_nearest(cc_ctx* c, const uint8_t* mask, const int64_t mshape[
         HIP_OK(hipSetDevice(c->device));
         if (nz == 0) return 0;
         hipStream_t s = cstream(c);
-        c->mask_xmap.ensure(shape[2] * sizeof(int32_t));
-        launch(c, "k_mask_xmap", [&] { k_mask_xmap<<<grid_stride(shape[2]), 256, 0, s>>>(shape[2], mshape[2], c->mask_xmap.as<int32_t>()); });
-        const dim3 grid((unsigned)((shape[2] + 1023) / 1024), (unsigned)(nz * shape[1]));
-        launch(c, "k_mask_resize", [&] {
-            k_mask_resize<<<grid, 256, 0, s>>>(mask, mshape[0], mshape[1], mshape[2], shape[0], shape[1], shape[2], z0,
-                                               c->mask_xmap.as<int32_t>(), out);
-        });
+        // 16 bytes per thread when the rows allow 16-B stores (X % 16 == 0, out 16-B aligned)
+        const bool w16 = shape[2] % 16 == 0 && ((uintptr_t)out & 15) == 0 && nz * shape[1] < (1LL << 32);
+        if (w16) {
+            c->mask_xmap.ensure((shape[0] + shape[1] + shape[2]) * sizeof(int32_t));
+            int32_t* map = c->mask_xmap.as<int32_t>();
+            launch(c, "k_mask_xmap", [&] {
+                k_mask_maps<<<grid_stride(shape[0] + shape[1] + shape[2]), 256, 0, s>>>(shape[2], shape[1], shape[0], mshape[2],
+                                                                                   mshape[1], mshape[0], map);
+            });
+            launch(c, "k_mask_resize", [&] {
+                k_mask_resize16<<<grid_stride(nz * shape[1] * (shape[2] / 16)), 256, 0, s>>>(
+                    mask, mshape[1], mshape[2], shape[1], shape[2], z0, nz * shape[1], map, out);
+            });
+        } else {
+            c->mask_xmap.ensure(shape[2] * sizeof(int32_t));
+            launch(c, "k_mask_xmap", [&] { k_mask_xmap<<<grid_stride(shape[2]), 256, 0, s>>>(shape[2], mshape[2], c->mask_xmap.as<int32_t>()); });
+            const dim3 grid((unsigned)((shape[2] + 1023) / 1024), (unsigned)(nz * shape[1]));
+            launch(c, "k_mask_resize", [&] {
+                k_mask_resize<<<grid, 256, 0, s>>>(mask, mshape[0], mshape[1], mshape[2], shape[0], shape[1], shape[2], z0,
+                                                   c->mask_xmap.as<int32_t>(), out);
+            });
+        }
         sync(c);
     })
 }

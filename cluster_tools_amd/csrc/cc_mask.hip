@@ -41,4 +41,39 @@ __global__ __launch_bounds__(256) void k_mask_resize(const u8* __restrict__ mask
     }
 }
 
+// per-axis source tables: map[0 .. X) x, map[X .. X + Y) y, map[X + Y .. X + Y + Z) z
+__global__ void k_mask_maps(int64_t X, int64_t Y, int64_t Z, int64_t mX, int64_t mY, int64_t mZ, int32_t* map) {
+    CC_FOR(i, X + Y + Z) {
+        if (i < X) map[i] = (int32_t)nn_src(i, mX, X);
+        else if (i < X + Y) map[i] = (int32_t)nn_src(i - X, mY, Y);
+        else map[i] = (int32_t)nn_src(i - X - Y, mZ, Z);
+    }
+}
+
+// rows of X % 16 == 0 (the common case): a thread makes 16 consecutive bytes of one row -- the
+// x sources as four int4 of the table, one 16-B store -- walking (row, 16-byte unit) with a grid
+// stride; the row's source offset comes from the y / z tables (no 64-bit division per thread).
+// The one-workgroup-per-row form left half of each 256-thread workgroup idle at X = 2048 and
+// launched a workgroup per row (4.6 ms for a C3 volume from a half-size mask; this: DESIGN.md §1).
+__global__ __launch_bounds__(256) void k_mask_resize16(const u8* __restrict__ mask, int64_t mY, int64_t mX, int64_t Y,
+                                                       int64_t X, int64_t z0, int64_t rows /* nz * Y */,
+                                                       const int32_t* __restrict__ map, u8* __restrict__ out) {
+    const u32 upr = (u32)(X / 16), yy = (u32)Y;
+    const int64_t n = rows * upr;
+    CC_FOR(u, n) {
+        const u32 row = (u32)(u / upr), xc = (u32)(u - (int64_t)row * upr);
+        const u32 zl = row / yy, y = row - zl * yy;
+        const u8* src = mask + ((int64_t)map[X + Y + z0 + zl] * mY + map[X + y]) * mX;
+        const int4* xm = reinterpret_cast<const int4*>(map + 16 * (int64_t)xc);
+        u32 w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int4 s4 = xm[q];
+            w[q] = (u32)(src[s4.x] != 0) | ((u32)(src[s4.y] != 0) << 8) | ((u32)(src[s4.z] != 0) << 16) |
+                   ((u32)(src[s4.w] != 0) << 24);
+        }
+        *reinterpret_cast<uint4*>(out + (int64_t)row * X + 16 * (int64_t)xc) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
 }  // namespace cc

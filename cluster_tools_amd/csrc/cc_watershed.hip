@@ -319,6 +319,43 @@ __global__ void k_norm_agg(const float* __restrict__ in, int nc, int64_t Z, int6
     }
 }
 
+// The same per voxel row: one workgroup per (z, y) row, float4 per lane (X and the block's x
+// extent multiples of 4, so a float4 never straddles two blocks); the block lookup per float4 and
+// no per-voxel 64-bit index arithmetic (the element kernel above spent its time there: 21.8 ms
+// for three C3 channels = 3.2 TB/s, profiles/r04_misc_summary.txt).
+template <int AGG>
+__global__ __launch_bounds__(256) void k_norm_agg4(const float* __restrict__ in, int nc, int64_t Y, int64_t X,
+                                                   int64_t Bz, int64_t By, int Bx, int nby, int nbx,
+                                                   const float2* __restrict__ nm, float* __restrict__ out, int64_t n) {
+    const int64_t r = blockIdx.x;                    // row z * Y + y
+    const int64_t z = r / Y, y = r - z * Y;
+    const int64_t brow = ((z / Bz) * nby + y / By) * nbx;
+    const int x4n = (int)(X / 4);
+    for (int x4 = threadIdx.x; x4 < x4n; x4 += 256) {
+        const float2 p = nm[brow + (4 * x4) / Bx];
+        const int64_t i = r * X + 4 * x4;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int c = 0; c < nc; ++c) {
+            const float4 u = *reinterpret_cast<const float4*>(in + (int64_t)c * n + i);
+            float v[4] = {__fsub_rn(u.x, p.x), __fsub_rn(u.y, p.x), __fsub_rn(u.z, p.x), __fsub_rn(u.w, p.x)};
+            float* a = &acc.x;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (p.y > 0.0f) v[e] = __fdiv_rn(v[e], p.y);
+                if (c == 0) a[e] = v[e];
+                else if (AGG == 0) a[e] = __fadd_rn(a[e], v[e]);
+                else if (AGG == 1) a[e] = (a[e] >= v[e] || isnan(a[e])) ? a[e] : v[e];
+                else a[e] = (a[e] <= v[e] || isnan(a[e])) ? a[e] : v[e];
+            }
+        }
+        if (AGG == 0) {
+            const float d = (float)nc;
+            acc = make_float4(__fdiv_rn(acc.x, d), __fdiv_rn(acc.y, d), __fdiv_rn(acc.z, d), __fdiv_rn(acc.w, d));
+        }
+        *reinterpret_cast<float4*>(out + i) = acc;
+    }
+}
+
 }  // namespace cc
 
 extern "C" int cc_normalize_channels(cc_ctx* c, const float* in, int64_t n_channels, const int64_t shape[3],
@@ -348,12 +385,22 @@ extern "C" int cc_normalize_channels(cc_ctx* c, const float* in, int64_t n_chann
         float2* nm = c->gs_tab.as<float2>();
         launch(c, "k_norm_params", [&] { k_norm_params<<<grid1d(nb), 256, 0, s>>>(nb, smin, smax, sflag, nm); });
         const int nby = gg.nb[1], nbx = gg.nb[2];
+        const bool rows4 = shape[2] % 4 == 0 && block_shape[2] % 4 == 0 && block_shape[2] < (1LL << 31) &&
+                           ((uintptr_t)in | (uintptr_t)out) % 16 == 0 && shape[0] * shape[1] < (1LL << 31);
         launch(c, "k_norm_agg", [&] {
             auto run = [&](auto kern) {
                 kern<<<grid_stride(n), 256, 0, s>>>(in, (int)n_channels, shape[0], shape[1], shape[2], block_shape[0],
                                                    block_shape[1], block_shape[2], nby, nbx, nm, out);
             };
-            if (agg == 0) run(k_norm_agg<0>);
+            auto run4 = [&](auto kern) {
+                kern<<<(unsigned)(shape[0] * shape[1]), 256, 0, s>>>(in, (int)n_channels, shape[1], shape[2], block_shape[0],
+                                                                    block_shape[1], (int)block_shape[2], nby, nbx, nm, out, n);
+            };
+            if (rows4) {
+                if (agg == 0) run4(k_norm_agg4<0>);
+                else if (agg == 1) run4(k_norm_agg4<1>);
+                else run4(k_norm_agg4<2>);
+            } else if (agg == 0) run(k_norm_agg<0>);
             else if (agg == 1) run(k_norm_agg<1>);
             else run(k_norm_agg<2>);
         });

@@ -395,7 +395,9 @@ def test_pass2_tile_order_vs_oracle(ctx, monkeypatch, shape, bs, mode, order):
 
 
 @pytest.mark.parametrize('mshape,shape', [((20, 36, 44), (40, 72, 88)), ((40, 72, 88), (40, 72, 88)),
-                                          ((13, 50, 17), (40, 72, 88)), ((80, 30, 200), (40, 72, 89))])
+                                          ((13, 50, 17), (40, 72, 88)), ((80, 30, 200), (40, 72, 89)),
+                                          # X % 16 == 0: the 16-byte-per-thread kernel
+                                          ((20, 36, 48), (40, 72, 96)), ((13, 50, 1000), (24, 40, 2048))])
 def test_resized_mask_device_vs_oracle(ctx, mshape, shape):
     """cc_resize_mask_nearest (elf ResizedVolume(order=0) stand-in, volume_utils.py:174-184) against
     the oracle's rule, whole volume and z-slabs; then the labelling with it (parity with elf

@@ -147,6 +147,28 @@ def test_gpu_normalize_channels_golden(ctx, name, meta):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('shape,bs', [((10, 20, 44), (4, 8, 20)),      # rows of float4 (k_norm_agg4)
+                                      ((10, 20, 45), (4, 8, 20)),      # X % 4 != 0: the element kernel
+                                      ((10, 20, 44), (4, 8, 22))],     # block x % 4 != 0: the element kernel
+                         ids=['rows4', 'odd_x', 'odd_block_x'])
+@pytest.mark.parametrize('agg', ['mean', 'max', 'min'])
+def test_gpu_normalize_channels_paths_vs_oracle(ctx, shape, bs, agg):
+    """Both device kernels of cc_normalize_channels against oracle.watershed.read_data (NaN-aware,
+    bit for bit), random channels of different scales with a NaN, an inf and a constant block."""
+    import torch
+    rng = np.random.default_rng(11)
+    x4 = np.stack([rng.random(shape, dtype=np.float32) * np.float32(s) for s in (1.0, 1e3, 3e-3)])
+    x4[1, 1, 2, 3] = np.nan
+    x4[2, 9, 19, 40] = np.inf
+    x4[:, 4:8, 8:16, :bs[2]] = np.float32(0.5)
+    want = W.read_data(x4, bs, 0, None, agg)
+    got = ctx.normalize_channels(torch.from_numpy(x4).cuda(), bs, agg).cpu().numpy()
+    nan = np.isnan(want)
+    np.testing.assert_array_equal(np.isnan(got), nan)
+    np.testing.assert_array_equal(got.view(np.uint32)[~nan], want.view(np.uint32)[~nan])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('agg', ['mean', 'max', 'min'])
 def test_gpu_watershed_4d_vs_oracle(ctx, agg):
     """4-D input end to end: normalize_channels, then the watershed on those values as given
