@@ -209,7 +209,7 @@ struct cc_ctx {
     bool fast_big = false;
     std::vector<int32_t> fast_big_tab;
     DevBuf status, hmap_keys, hmap_par;
-    uint64_t hm_slots = 0;   // slots of the seam map (shards): cleared by the next k_clear_front
+    uint64_t hm_slots = 0;   // slots of the seam map (shards): cleared by the next front clear (k_sample)
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, ProfEntry> prof_acc;

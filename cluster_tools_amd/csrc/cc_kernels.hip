@@ -679,8 +679,42 @@ constexpr int SAMPLE_PARTS = 8;
 // (the guess stays a launch of its own, k_guess: folding it in by a last-part-of-the-block count
 // needed an agent-scope fence per workgroup -- an L2 write-back on gfx950 -- and measured k_sample
 // 0.11 -> 0.25 ms at C3)
-__global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __restrict__ in, u32* part) {
+// The front's initial state, written by k_sample's threads before they sample (it replaced nine
+// memsets of ~4 us each, then a launch of its own): ordered block min = ~0, max / NaN flag = 0,
+// scalars, the k_fix count, seam overflow flags (+ their "any" flags at big[nb] / iovf[nt];
+// fill = 1 sends everything to the global stitch), the inter-pair counts, the root segments and
+// the scan's extra element.
+// mflag / fchg (nullable, the device-gated k_fix of the one-read-back schedule): the seam marks
+// and their list count (mflag[nt]) and the changed-faces flags, which the host-synchronised
+// schedule clears only when the k_fix count it read back is non-zero.
+// htab / hkeys + hpar (nullable, shards of the one-read-back schedule): the seam pair set and the
+// seam map of the previous step cleared for this one (n_clear = the longest of all the ranges)
+struct FrontClear {
+    int64_t nb, nt;
+    u32* smin; u32* smax_flag; u64* scalars; u32* FIX; u8* big; u8* iovf; u32* ipc; u32* seg; u32* rc_end;
+    u8 fill;
+    u32* mflag; u8* fchg;
+    u64* htab; int64_t htab_n; u64* hkeys; u32* hpar; int64_t hm_n;
+    int64_t n_clear;      // the longest of the ranges (0: nothing to clear)
+};
+__device__ __forceinline__ void clear_front(const FrontClear& f, int64_t i) {
+    if (f.htab && i < f.htab_n) f.htab[i] = ~0ull;
+    if (f.hkeys && i < f.hm_n) { f.hkeys[i] = ~0ull; f.hpar[i] = (u32)i; }
+    if (i < f.nb) f.smin[i] = 0xFFFFFFFFu;
+    if (i < 2 * f.nb) { f.smax_flag[i] = 0u; f.seg[i] = 0u; }
+    if (i <= f.nb) f.big[i] = f.fill;
+    if (i <= f.nt) f.iovf[i] = f.fill;
+    if (i < f.nt) f.ipc[i] = 0u;
+    if (i < SCALARS) f.scalars[i] = 0ull;
+    if (i == 0) { f.FIX[0] = 0u; f.rc_end[0] = 0u; }
+    if (f.mflag && i <= f.nt) f.mflag[i] = 0u;
+    if (f.fchg && i < f.nt) f.fchg[i] = 0;
+}
+
+__global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __restrict__ in, u32* part, FrontClear fc) {
     __shared__ u32 red[NTHREADS / 64];
+    for (int64_t i = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; i < fc.n_clear; i += (int64_t)gridDim.x * NTHREADS)
+        clear_front(fc, i);
     const int64_t b = blockIdx.x / SAMPLE_PARTS;
     const int pt = blockIdx.x % SAMPLE_PARTS;
     const int tid = cc_tid();
@@ -752,35 +786,6 @@ __global__ void k_guess(int64_t nb, const u32* part, float thr, int mode, BlockP
     // On continuous data the sampled extremes are not the block's, so the guessed bound misses
     // the exact one by a little: only tiles holding a voxel between the two are relabelled.
     guess[b] = widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
-}
-
-// One launch for the front's initial state (it replaced nine memsets of ~4 us each): ordered
-// block min = ~0, max / NaN flag = 0, scalars, the k_fix count, seam overflow flags (+ their
-// "any" flags at big[nb] / iovf[nt]; fill = 1 sends everything to the global stitch), the
-// inter-pair counts, the root segments and the scan's extra element.
-// mflag / fchg (nullable, the device-gated k_fix of the one-read-back schedule): the seam marks
-// and their list count (mflag[nt]) and the changed-faces flags, which the host-synchronised
-// schedule clears only when the k_fix count it read back is non-zero.
-// htab / hkeys + hpar (nullable, shards of the one-read-back schedule): the seam pair set and the
-// seam map of the previous step cleared for this one (n_clear = the longest of all the ranges)
-__global__ __launch_bounds__(256) void k_clear_front(int64_t nb, int64_t nt, u32* smin, u32* smax_flag,
-                                                     u64* scalars, u32* FIX, u8* big, u8* iovf, u32* ipc,
-                                                     u32* seg, u32* rc_end, u8 fill, u32* mflag, u8* fchg,
-                                                     u64* htab, int64_t htab_n, u64* hkeys, u32* hpar, int64_t hm_n,
-                                                     int64_t n_clear) {
-    CC_FOR(i, n_clear) {
-        if (htab && i < htab_n) htab[i] = ~0ull;
-        if (hkeys && i < hm_n) { hkeys[i] = ~0ull; hpar[i] = (u32)i; }
-        if (i < nb) smin[i] = 0xFFFFFFFFu;
-        if (i < 2 * nb) { smax_flag[i] = 0u; seg[i] = 0u; }
-        if (i <= nb) big[i] = fill;
-        if (i <= nt) iovf[i] = fill;
-        if (i < nt) ipc[i] = 0u;
-        if (i < SCALARS) scalars[i] = 0ull;
-        if (i == 0) { FIX[0] = 0u; rc_end[0] = 0u; }
-        if (mflag && i <= nt) mflag[i] = 0u;
-        if (fchg && i < nt) fchg[i] = 0;
-    }
 }
 
 struct SpecArgs {
@@ -1004,7 +1009,7 @@ __device__ __forceinline__ void mark_seam(const Geom& g, u32 f, u32 d, u32* flag
 // from this run and are always flagged.  The grid walks the list: the one-read-back schedule
 // launches a fixed grid without reading the count (with nothing to fix every workgroup reads one
 // word and leaves), the host-synchronised one a workgroup per listed tile.  fchg, flag and
-// LIST[0] are cleared before (k_clear_front / memsets).
+// LIST[0] are cleared before (the front clear in k_sample / memsets).
 // (no waves-per-EU bound: under the 64-VGPR bound of k_fix the loop spilled; this kernel sees
 // ~1 % of the tiles on continuous input and none on quantized input)
 template <bool HAS_MASK>
@@ -1938,14 +1943,9 @@ __global__ __launch_bounds__(SB_THREADS) void k_block_uf(Geom g, const u32* __re
         for (int c0 = 0; c0 < ntb; c0 += 64) {
             const int lt = c0 + lane;
             const u32 v = lt < ntb ? arr[lt] : 0;
-            u32 x = v;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const u32 y = __shfl_up(x, o, 64);
-                if (lane >= o) x += y;
-            }
+            const u32 x = wave_incl_sum(v);
             if (lt < ntb) arr[lt] = run + x - v;
-            run += __shfl(x, 63, 64);
+            run += (u32)__builtin_amdgcn_readlane((int)x, 63);
         }
         if (lane == 0) arr[ntb] = run;
     }
@@ -1955,18 +1955,45 @@ __global__ __launch_bounds__(SB_THREADS) void k_block_uf(Geom g, const u32* __re
         if (tid == 0) { big[b] = 1; big[g.n_blocks] = 1; if (RCB) RCB[b] = 0; }
         return;
     }
-    for (u32 i = tid; i < N; i += SB_THREADS) {
-        const int lt = flat_tile(noff, ntb, i);
-        lpar[i] = i;
-        lkey[i] = KEY[(u64)tile_of(lt) * g.cap + (i - noff[lt])];
+    // the key and pair loads of UF_ILP iterations are issued together (the block's few workgroups
+    // leave most CUs idle here: the phases are latency-bound, one global round trip per iteration)
+    constexpr int UF_ILP = 4;
+    for (u32 i0 = tid; i0 < N; i0 += UF_ILP * SB_THREADS) {
+        u64 kv[UF_ILP];
+#pragma unroll
+        for (int j = 0; j < UF_ILP; ++j) {
+            const u32 i = i0 + j * SB_THREADS;
+            if (i < N) {
+                const int lt = flat_tile(noff, ntb, i);
+                kv[j] = KEY[(u64)tile_of(lt) * g.cap + (i - noff[lt])];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < UF_ILP; ++j) {
+            const u32 i = i0 + j * SB_THREADS;
+            if (i < N) { lpar[i] = i; lkey[i] = kv[j]; }
+        }
     }
     __syncthreads();
     lds_u32* par = as_lds(lpar);
-    for (u32 i = tid; i < M; i += SB_THREADS) {
-        const int lt = flat_tile(poff, ntb, i);
-        const u64 pr = PAIRS[tile_of(lt) * TPC + (i - poff[lt])];
-        const u32 a = (u32)(pr >> 32), c = (u32)pr;
-        lunion_key(par, lkey, noff[a >> 12] + (a & 0xFFFu), noff[c >> 12] + (c & 0xFFFu));
+    for (u32 i0 = tid; i0 < M; i0 += UF_ILP * SB_THREADS) {
+        u64 pv[UF_ILP];
+#pragma unroll
+        for (int j = 0; j < UF_ILP; ++j) {
+            const u32 i = i0 + j * SB_THREADS;
+            if (i < M) {
+                const int lt = flat_tile(poff, ntb, i);
+                pv[j] = PAIRS[tile_of(lt) * TPC + (i - poff[lt])];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < UF_ILP; ++j) {
+            const u32 i = i0 + j * SB_THREADS;
+            if (i < M) {
+                const u32 a = (u32)(pv[j] >> 32), c = (u32)pv[j];
+                lunion_key(par, lkey, noff[a >> 12] + (a & 0xFFFu), noff[c >> 12] + (c & 0xFFFu));
+            }
+        }
     }
     __syncthreads();
     for (u32 i = tid; i < N; i += SB_THREADS) {
@@ -2585,7 +2612,7 @@ __global__ __launch_bounds__(NTHREADS) void k_top_cubes(Geom g, const face_t* __
 // appended anyway: the replicated union-find takes duplicates), after a per-workgroup LDS set
 // (the membrane component's pair recurs in every tile).  Ids: KR holds this slab's own ids
 // (base 0); the global ones add the sums of the slabs below.  out = [cap + 1][2]: row 0 = (count,
-// redo flags), written by k_seam_hdr from scalars[5] (the count; zeroed by k_clear_front), then
+// redo flags), written by k_seam_hdr from scalars[5] (the count; zeroed by the front clear in k_sample), then
 // the pairs.  One workgroup per bottom-layer tile.
 __global__ __launch_bounds__(NTHREADS) void k_seam_cube_pairs(Geom g, const face_t* __restrict__ FACES, u32* P,
                                                               const u64* __restrict__ KR, const u32* __restrict__ upper,

@@ -86,17 +86,21 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         const bool shard = fast && sum_out != nullptr;
         if (shard) c->seam_hash.ensure(SEAM_SET * sizeof(u64));
         const int64_t hs_n = shard ? SEAM_SET : 0, hm_n = shard ? (int64_t)c->hm_slots : 0;
-        launch(c, "k_clear_front", [&] {
-            u32* mflag = fast ? c->mark.as<u32>() : nullptr;
-            u8* mchg = fast ? (u8*)(c->mark.as<u32>() + 2 * nt + 1) : nullptr;
-            const int64_t n_clear = std::max<int64_t>({nt + 1, 2 * nb + 1, hs_n, hm_n});
-            k_clear_front<<<grid1d(n_clear), 256, 0, s>>>(
-                nb, nt, smin, smax, c->scalars.as<u64>(), FIX, c->big.as<u8>(), c->iovf.as<u8>(), c->ipc.as<u32>(),
-                c->seg.as<u32>(), c->rc.as<u32>() + nt, lds_seams ? 0 : 1, mflag, mchg,
-                shard ? c->seam_hash.as<u64>() : nullptr, hs_n, hm_n ? c->hmap_keys.as<u64>() : nullptr,
-                hm_n ? c->hmap_par.as<u32>() : nullptr, hm_n, n_clear);
-        });
-        launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART); });
+        // k_sample's threads first write the front's initial state (FrontClear), then sample
+        FrontClear fc;
+        {
+            fc.nb = nb; fc.nt = nt;
+            fc.smin = smin; fc.smax_flag = smax; fc.scalars = c->scalars.as<u64>(); fc.FIX = FIX;
+            fc.big = c->big.as<u8>(); fc.iovf = c->iovf.as<u8>(); fc.ipc = c->ipc.as<u32>(); fc.seg = c->seg.as<u32>();
+            fc.rc_end = c->rc.as<u32>() + nt; fc.fill = lds_seams ? 0 : 1;
+            fc.mflag = fast ? c->mark.as<u32>() : nullptr;
+            fc.fchg = fast ? (u8*)(c->mark.as<u32>() + 2 * nt + 1) : nullptr;
+            fc.htab = shard ? c->seam_hash.as<u64>() : nullptr; fc.htab_n = hs_n;
+            fc.hkeys = hm_n ? c->hmap_keys.as<u64>() : nullptr; fc.hpar = hm_n ? c->hmap_par.as<u32>() : nullptr;
+            fc.hm_n = hm_n;
+            fc.n_clear = std::max<int64_t>({nt + 1, 2 * nb + 1, hs_n, hm_n});
+        }
+        launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART, fc); });
         launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, mode, guess); });
         if (const char* e = std::getenv("CC_SPEC"); e && std::string(e) == "0")     // test hook: no guesses
             HIP_OK(hipMemsetAsync(guess, 0, nb * sizeof(BlockParam), s));
@@ -152,7 +156,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         u32 nfix = 0;
         if (fast) {
             // device-gated: a fixed grid walks the k_fix list (usually empty) and marks the seams
-            // of changed tiles; k_seams_list redoes the marked ones (k_clear_front cleared both)
+            // of changed tiles; k_seams_list redoes the marked ones (k_sample's front clear zeroed both)
             launch(c, "k_fix", [&] {
                 const unsigned grid = (unsigned)std::min<int64_t>(nt, 512);
                 if (mask) k_fix_dev<true><<<grid, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, mask, thr, mode, BITS, FACES, COUNT, P, KR, fchg, flag, list);
@@ -547,7 +551,7 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
     HashMap hm;
     if (sd) {
         // seam map over every slab's pairs: slots for all their ids at <= 1/4 load (cleared by this
-        // step's k_clear_front unless its size changed)
+        // step's front clear (k_sample) unless its size changed)
         CC_REQUIRE(st.fast && st.base_dev, "phase order: the device seam map follows cc_shard_dev_assign");
         uint64_t hc = 1024;
         while (hc < 8 * (uint64_t)sd->world * sd->cap) hc <<= 1;
@@ -869,7 +873,8 @@ int cc_threshold(cc_ctx* c, const float* in, const int64_t shape[3], const int64
             HIP_OK(hipMemsetAsync(smin, 0xFF, nb * sizeof(u32), s));
             HIP_OK(hipMemsetAsync(smax, 0x00, 2 * nb * sizeof(u32), s));
             HIP_OK(hipMemsetAsync(FIX, 0, sizeof(u32), s));
-            launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART); });
+            FrontClear none{};
+            launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART, none); });
             launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, md, guess); });
             if (const char* e = std::getenv("CC_SPEC"); e && std::string(e) == "0")     // test hook: no guesses
                 HIP_OK(hipMemsetAsync(guess, 0, nb * sizeof(BlockParam), s));

@@ -410,7 +410,7 @@ int cc_shard_dev_seam_pairs(cc_ctx* c, const uint32_t* upper_cubes_dev, const ui
         }
         for (int a = 1; a < 3; ++a)
             CC_REQUIRE(g.nb[a] == 1 || st.bs[a] % 2 == 0, "cube form needs even tile origins (even block_shape[1:])");
-        // the seam pair hash set (see k_seam_cube_pairs) was cleared by this step's k_clear_front
+        // the seam pair hash set (see k_seam_cube_pairs) was cleared by this step's front clear (k_sample)
         const unsigned nlayer = (unsigned)((int64_t)g.nt[1] * g.nt[2]);
         launch(c, "k_seam_cube_pairs", [&] {
             k_seam_cube_pairs<<<nlayer, NTHREADS, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(),

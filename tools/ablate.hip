@@ -131,7 +131,7 @@ int main(int argc, char** argv) {
             HIP_OK(hipMalloc(&TB, nt * 16));
             HIP_OK(hipMalloc(&guess, nb * sizeof(BlockParam)));
             r.push_back({"k_sample_guess", time_ms(s, iters, [&] {
-                k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, part);
+                k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, part, FrontClear{});
                 k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, part, thr, mode, guess);
             })});
             std::vector<BlockParam> hb(nb);

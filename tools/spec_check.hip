@@ -59,7 +59,7 @@ int main(int argc, char** argv) {
         k_pass1<false, 0><<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, nullptr, bp, thr, mode, BITS[0], FACES, COUNT[0], P, KEY);
         u32* part;
         HIP_OK(hipMalloc(&part, nb * SAMPLE_PARTS * 16));
-        k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, part);
+        k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, part, FrontClear{});
         k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, part, thr, mode, guess);
         HIP_OK(hipDeviceSynchronize());
         std::vector<BlockParam> hb(nb), hgs(nb);

@@ -3,8 +3,8 @@ gpu_steps.sh trace_slabs8: tools/bench_sharded_slabs.py under --kernel-trace).
 
     python tools/trace_gaps.py TRACE_DIR_OR_CSV [n_slabs]
 
-The last step starts at the n_slabs-th last k_clear_front (one per slab; the slabs of a step run
-phase by phase).  For every kernel: launches, summed duration, and the idle time between the
+The last step starts at the n_slabs-th last k_sample (k_clear_front in builds before it was folded
+into k_sample; one per slab, the slabs of a step run phase by phase).  For every kernel: launches, summed duration, and the idle time between the
 previous kernel's end and its start ("gap-before": host synchronisations, launch latency).
 """
 import collections
@@ -21,7 +21,8 @@ def main():
     nsl = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r['Start_Timestamp']))
     name = [r['Kernel_Name'].split('(')[0].replace('void ', '').replace('cc::', '') for r in rows]
-    first = [i for i, n in enumerate(name) if n.startswith('k_clear_front')][-nsl]
+    mark = 'k_clear_front' if any(n.startswith('k_clear_front') for n in name) else 'k_sample'
+    first = [i for i, n in enumerate(name) if n.startswith(mark)][-nsl]
     seg = list(zip(name[first:], rows[first:]))
     t0 = int(seg[0][1]['Start_Timestamp'])
     t1 = max(int(r['End_Timestamp']) for _, r in seg)
