@@ -30,7 +30,7 @@ EXPORTS = (
     'cc_shard_dev_seam_pairs', 'cc_shard_dev_finish', 'cc_normalize_channels',
 )
 # redo flags of the one-read-back schedule (RF_* in csrc/cc_kernels.hip)
-RF_BIG, RF_ROOTS, RF_CUBES, RF_PAIRS = 1, 2, 4, 8
+RF_BIG, RF_ROOTS, RF_CUBES, RF_PAIRS, RF_IOVF = 1, 2, 4, 8, 16
 CC_ERR_ID_RANGE = -3          # cc_evaluate: ids beyond the key packing (include/cc_mi355x.h)
 # CC_DTYPE_* of include/cc_mi355x.h (cc_channel_mean)
 DTYPES = {'float32': 0, 'float64': 1, 'uint8': 2, 'int8': 3, 'uint16': 4, 'int16': 5, 'uint32': 6,

@@ -79,6 +79,8 @@ constexpr u64 RF_BIG = 1;       // some block needs the global-memory stitch fal
 constexpr u64 RF_ROOTS = 2;     // more block-local roots than the root arrays hold
 constexpr u64 RF_CUBES = 4;     // the slab's ids do not fit the 28-bit cube form of its top plane
 constexpr u64 RF_PAIRS = 8;     // more seam pairs than the pair buffer holds
+constexpr u64 RF_IOVF = 16;     // some tile's block-face pair list overflowed (the global-memory
+                                // inter stitch, k_stitch<true>, runs in the synchronised schedule)
 
 // the run's device scalars: [0] sum of block values, [1] components owned, [2] block-local roots,
 // [3] redo flags, [5] seam pairs appended
@@ -1791,10 +1793,14 @@ __global__ __launch_bounds__(256) void k_block_face_flags(Geom g, const face_t* 
 // duplicate root pairs dropped per wave, union keyed by rid (the smaller rid becomes the root).
 // tpw tiles per wave (lanes >= tpw count no pairs): 64 for large volumes; 16 for small ones puts
 // more waves on the dependent finds (C2 0.023 -> 0.016 ms; at C3 16 measured 0.060 vs 0.044 ms)
+// iovf_any / scalars (nullable; the one-read-back schedule): an overflowed tile list raises
+// RF_IOVF instead of a launch of the global-memory fallback (the run is redone synchronised)
 __global__ __launch_bounds__(256) void k_inter_union(Geom g, const u64* __restrict__ IPAIRS,
                                                      const u32* __restrict__ IPC, u32* P,
-                                                     const u64* __restrict__ K, int tpw) {
+                                                     const u64* __restrict__ K, int tpw, const u8* iovf_any,
+                                                     u64* scalars) {
     const int lane = threadIdx.x & 63;
+    if (iovf_any && blockIdx.x == 0 && threadIdx.x == 0 && *iovf_any) atomicOr(scalars + 3, RF_IOVF);
     const int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * tpw;
     if (t0 >= g.n_tiles) return;
     const int64_t tl = t0 + lane;

@@ -387,13 +387,18 @@ static void rid_unions(cc_ctx* c) {
     if (!st.local_only && !st.identity_lut) {
         launch(c, "k_inter_union", [&] {
             const int tpw = nt >= 65536 ? 64 : 16;
-            k_inter_union<<<(unsigned)((nt + 4 * tpw - 1) / (4 * tpw)), 256, 0, s>>>(g, c->ipairs.as<u64>(), c->ipc.as<u32>(), c->P.as<u32>(),
-                                                                                    c->KR.as<u64>(), tpw);
+            k_inter_union<<<(unsigned)((nt + 4 * tpw - 1) / (4 * tpw)), 256, 0, s>>>(
+                g, c->ipairs.as<u64>(), c->ipc.as<u32>(), c->P.as<u32>(), c->KR.as<u64>(), tpw,
+                st.fast ? c->iovf.as<u8>() + nt : nullptr, c->scalars.as<u64>());
         });
-        // tiles whose block-face pairs overflowed their list (and every tile under CC_DEBUG_GLOBAL_STITCH);
-        // the one-read-back schedule launches it unread (it checks the flag itself): a smaller grid
-        const unsigned stitch_grid = (unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, st.fast ? 256 : 2048);
-        if (st.any_iovf) launch(c, "k_stitch_inter", [&] { k_stitch<true><<<stitch_grid, SP_WAVES * 64, 0, s>>>(g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), c->big.as<u8>(), c->iovf.as<u8>()); });
+        // tiles whose block-face pairs overflowed their list (and every tile under CC_DEBUG_GLOBAL_STITCH):
+        // the global-memory fallback, in the synchronised schedule only (the one-read-back schedule
+        // raises RF_IOVF in k_inter_union and the run is redone)
+        if (!st.fast && st.any_iovf)
+            launch(c, "k_stitch_inter", [&] {
+                k_stitch<true><<<(unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, 2048), SP_WAVES * 64, 0, s>>>(
+                    g, c->faces.as<face_t>(), c->P.as<u32>(), c->KR.as<u64>(), c->big.as<u8>(), c->iovf.as<u8>());
+            });
     }
     st.n_map = 0;
     st.stage = 2;
@@ -548,6 +553,7 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
     const int64_t m = st.n_map;
     u64* FIN = KR;
     const uint64_t lut_cap = (uint64_t)nr + (uint64_t)nb + 1;
+    StatusArgs sa;           // the one read-back's status (k_status)
     HashMap hm;
     if (sd) {
         // seam map over every slab's pairs: slots for all their ids at <= 1/4 load (cleared by this
@@ -578,7 +584,6 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
         c->lut.ensure(lut_cap * sizeof(u64));
         u64* lut = c->lut.as<u64>();
         const u64 base = st.base;
-        StatusArgs sa;
         if (st.fast) {
             c->status.ensure((16 + 2 * (size_t)nb) * sizeof(u64));
             sa.out = c->status.as<u64>();
@@ -594,6 +599,8 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
                 lut_cap, nb, base, st.base_dev ? st.sums : nullptr, st.rank, offsets, c->values.as<u64>(), c->seg.as<u32>(),
                 c->vals2.as<u32>(), (u64)nr, P, KR, U, V, m, hm, lut, scalars);
         });
+        // (the status stays a launch of its own: folded into k_pass2's last workgroup it made
+        // k_pass2 0.11 ms slower at C3, profiles/r04_ab_kspec.txt)
         if (sa.out)
             launch(c, "k_status", [&] { k_status<<<1, 256, 0, s>>>(sa, scalars, st.base_dev ? st.sums : nullptr, st.rank); });
         c->lut_valid = true;
