@@ -241,7 +241,8 @@ int64_t cc_seam_pairs_cubes32(cc_ctx* ctx, const uint32_t* upper_cubes_dev, uint
  *                           headers and sums) mean an optimistic bound did not hold -- more seam
  *                           pairs than cap (8), ids beyond the 28-bit cube form (4), more roots than
  *                           the context's root arrays (2), a block needing the global-stitch
- *                           fallback (1) -- and the caller relabels this step with the schedule
+ *                           fallback (1), a tile's block-face pair list overflowing (16) -- and the
+ *                           caller relabels this step with the schedule
  *                           above (cc_shard_begin ...), which sizes everything from read-backs. */
 int cc_shard_dev_begin(cc_ctx* ctx, const float* in_dev, const uint8_t* mask_dev, const int64_t slab_shape[3],
                        const int64_t block_shape[3], double threshold, int mode, int64_t z_offset,
