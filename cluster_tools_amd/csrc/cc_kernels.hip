@@ -797,6 +797,17 @@ struct SpecArgs {
     int64_t t0;               // first tile of this launch (the front runs in z-layer chunks)
 };
 
+// workgroup b of n -> tile: the (b / 8)-th of the contiguous range of XCD b % 8 (workgroups are
+// dealt to the 8 XCDs round-robin), so that x-neighbour tiles run on one XCD and a cache line
+// they share (rows not 128-B aligned) meets in one L2 instead of being read / written by two.
+// A bijection on [0, n).  Used when the rows are not line-aligned: C1 (X = 1250) k_spec 0.273 ->
+// 0.257 ms, k_pass2 0.476 -> 0.437 ms (profiles/r04_ab_kspec.txt); on aligned rows the linear
+// order stays (no gain there, round 3).
+__device__ __forceinline__ int64_t xcd_contig(int64_t b, int64_t n) {
+    const int64_t k = b & 7, i = b >> 3, q = n >> 3, r = n & 7;
+    return k * q + (k < r ? k : r) + i;
+}
+
 // SIDES: bounds of the guessed interval that can move (1 lower: 'greater', 2 upper: 'less', 3 both)
 // ABL (kernel ablation harness tools/ablate.hip only; 0 in the library): 99 stop once the bit rows
 // are in LDS (loads, ballots, statistics), else as pass1_finish's ABL
@@ -806,7 +817,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     u32* COUNT, u32* P, u64* KEY) {
     __shared__ Pass1LDS L;
     __shared__ u32 red[6][NTHREADS / 64];
-    const int64_t t = sa.t0 + blockIdx.x;
+    const int64_t t = sa.t0 + ((g.X & 31) ? xcd_contig(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x);
     const TileInfo ti = tile_info(g, t);
     const BlockParam p = uniform_bp(sa.guess[ti.block]);
     if (p.kind != BP_INTERVAL) {                   // no guess: statistics only, k_fix labels the tile
@@ -2779,11 +2790,14 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
     __shared__ u64 lab[LABCAP];
     // tile order: 0 linear (x fastest), 1 z fastest (the host picks 1 for rows of >= 4096 voxels:
     // writing the 4096-wide C5 slabs in x-fastest order took 6.09-6.14 ms, z-fastest 5.36 ms;
-    // C3's 2048-wide volume is the other way round, 5.60 vs 5.84 ms)
+    // C3's 2048-wide volume is the other way round, 5.60 vs 5.84 ms), 2 XCD-contiguous (rows of
+    // labels not 128-B aligned, X % 16 != 0: see xcd_contig)
     int64_t t = blockIdx.x;
     if (order == 1) {
         const int64_t n0 = g.nt[0];
         t = (t % n0) * ((int64_t)g.nt[1] * g.nt[2]) + t / n0;
+    } else if (order == 2) {
+        t = xcd_contig(t, gridDim.x);
     }
     const TileInfo ti = tile_info(g, t);
     const int tid = threadIdx.x;

@@ -607,10 +607,11 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
     }
     // the fused path resolves each tile component's final label inside k_pass2 (no k_finalize)
     launch(c, "k_pass2", [&] {
-        // tile order of the write pass (see k_pass2): z fastest for rows of >= 4096 voxels
-        // (CC_PASS2_ORDER = 0 / 1 forces one, A/B only)
-        int order = g.X >= 4096 ? 1 : 0;
-        if (const char* e = std::getenv("CC_PASS2_ORDER"); e && *e) order = std::atoi(e) ? 1 : 0;
+        // tile order of the write pass (see k_pass2): z fastest for rows of >= 4096 voxels,
+        // XCD-contiguous for label rows that are not 128-B aligned (CC_PASS2_ORDER = 0 / 1 / 2
+        // forces one, A/B only)
+        int order = g.X >= 4096 ? 1 : (g.X & 15) ? 2 : 0;
+        if (const char* e = std::getenv("CC_PASS2_ORDER"); e && *e) order = std::min(std::max(std::atoi(e), 0), 2);
         // CC_LDS_PAD_P2 (A/B only): extra dynamic LDS per workgroup, i.e. fewer tiles per CU
         const unsigned pad = (unsigned)env_int("CC_LDS_PAD_P2", 0);
         // with a seam map every label goes through the slab's LUT (m = 1)
