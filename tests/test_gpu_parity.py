@@ -382,15 +382,38 @@ PASS2_ORDER_CASES = [
 ]
 
 
-@pytest.mark.parametrize('order', ['0', '1'])
+@pytest.mark.parametrize('order', ['0', '1', '2'])
 @pytest.mark.parametrize('shape,bs,mode', PASS2_ORDER_CASES)
 def test_pass2_tile_order_vs_oracle(ctx, monkeypatch, shape, bs, mode, order):
-    """Both k_pass2 tile orders (x fastest / z fastest; CC_PASS2_ORDER, read on every call) on the
-    fused path give the oracle's labels (order 1 was only reached by X >= 4096)."""
+    """Every k_pass2 tile order (x fastest / z fastest / XCD-contiguous; CC_PASS2_ORDER, read on
+    every call) on the fused path gives the oracle's labels (order 1 was only reached
+    by X >= 4096; order 2 otherwise only by rows that are not 128-B aligned)."""
     monkeypatch.setenv('CC_PASS2_ORDER', order)
     inp = O.boundary_map(shape, origin=(5, 9, 2))
     _check_against_oracle(ctx, inp, bs, 0.5, mode)
     inp = O.boundary_map(shape, origin=(5, 9, 2), dither=True)
+    _check_against_oracle(ctx, inp, bs, 0.41, mode)
+
+
+UNALIGNED_CASES = [
+    ((40, 72, 258), (32, 64, 130)),      # X = 2 mod 4
+    ((36, 70, 322), (36, 70, 322)),
+    ((33, 66, 195), (33, 66, 195)),      # odd X
+]
+
+
+@pytest.mark.parametrize('mode', ['greater', 'less'])
+@pytest.mark.parametrize('shape,bs', UNALIGNED_CASES)
+def test_unaligned_rows_vs_oracle(ctx, shape, bs, mode):
+    """Rows that are not 16-B aligned (X % 4 != 0, as C1's 1250): k_spec's lane = x path on full
+    tiles and the XCD-contiguous tile order of k_spec / k_pass2; quantized, masked and continuous
+    input."""
+    rng = np.random.default_rng(11)
+    inp = O.boundary_map(shape, origin=(3, 7, 1))
+    _check_against_oracle(ctx, inp, bs, 0.5, mode)
+    mask = (rng.random(shape) < 0.9).astype(np.uint8)
+    _check_against_oracle(ctx, inp, bs, 0.5, mode, mask)
+    inp = O.boundary_map(shape, origin=(3, 7, 1), dither=True)
     _check_against_oracle(ctx, inp, bs, 0.41, mode)
 
 
