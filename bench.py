@@ -183,6 +183,23 @@ def cold_start(args, x, block_shape):
     return res
 
 
+def load_traffic(path, kernel, lib_src):
+    """Per-launch HBM bytes of `kernel` from a tools/prof_summary.py file (PMC passes, corrected as
+    MI355X_MICROARCH.md §HBM says) -> (bytes or None, the file's lib_src).  The figure is used only
+    when the file is stamped with the source hash of the library being benched: a stale figure
+    never reaches the line."""
+    if not os.path.exists(path):
+        return None, None
+    tdat = json.load(open(path))
+    src = tdat.get('_meta', {}).get('lib_src')
+    if src is None or src != lib_src:
+        return None, src
+    for k, v in tdat.items():
+        if k.split('<')[0] == kernel and 'traffic' in v:
+            return int(v['traffic']), src
+    return None, src
+
+
 def main():
     args = parse()
     if args.cold_child:
@@ -204,6 +221,9 @@ def main():
     # CC_DIST_BACKEND=gloo: rehearsal of the N > 1 schedule with several ranks on one GPU (RCCL
     # refuses two ranks on one device); collectives staged through host memory
     backend = os.environ.get('CC_DIST_BACKEND', 'nccl')
+    if world > 1:
+        from cluster_tools_amd.distributed import check_rccl_ranks
+        check_rccl_ranks(backend, local_rank, int(os.environ.get('LOCAL_WORLD_SIZE', world)))
     gpu = local_rank if backend == 'nccl' else local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(gpu)
     dev = torch.device('cuda', gpu)
@@ -309,19 +329,15 @@ def main():
     kb = KERNEL_BYTES.get(dom)
     if dom == 'k_spec' and masked:
         kb += 1.0
-    traffic = None
     tj = args.traffic_json or os.path.join(ROOT, 'profiles', 'traffic_%s.json' % tag)
-    if os.path.exists(tj):
-        # per-launch HBM bytes of the same kernel on the same workload (PMC passes, corrected as
-        # MI355X_MICROARCH.md §HBM says; tools/prof_summary.py)
-        for k, v in json.load(open(tj)).items():
-            if k.split('<')[0] == dom and 'traffic' in v:
-                traffic = int(v['traffic'])
+    traffic, traffic_src = load_traffic(tj, dom, lib_src)
     roofline = None
     if kb is not None:
         achieved = kb * nvox_rank / (step_ms * 1e-3) / 1e9
         roofline = {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                     'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
+                    'traffic_file': {'path': os.path.relpath(tj, ROOT), 'lib_src': traffic_src,
+                                     'used': traffic is not None} if os.path.exists(tj) else None,
                     'alg_bytes_per_voxel': kb, 'avg_launch_ms': round(avg_ms, 4),
                     'launches_per_step': kern[dom]['count'] / args.steps}
     e2e_gbs = b_alg * nvox_all * args.steps / dt / 1e9 / world

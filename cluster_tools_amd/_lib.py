@@ -27,7 +27,7 @@ EXPORTS = (
     'cc_evaluate', 'cc_get_overlaps', 'cc_relabel_consecutive', 'cc_set_option', 'cc_channel_mean',
     'cc_gaussian_smooth_blocks', 'cc_gaussian_taps', 'cc_result_size', 'cc_resize_mask_nearest',
     'cc_watershed_from_seeds', 'cc_shard_dev_begin', 'cc_shard_dev_assign', 'cc_shard_dev_top_cubes',
-    'cc_shard_dev_seam_pairs', 'cc_shard_dev_finish', 'cc_normalize_channels',
+    'cc_shard_dev_seam_pairs', 'cc_shard_dev_finish', 'cc_normalize_channels', 'cc_shard_dev_ok',
 )
 # redo flags of the one-read-back schedule (RF_* in csrc/cc_kernels.hip)
 RF_BIG, RF_ROOTS, RF_CUBES, RF_PAIRS, RF_IOVF = 1, 2, 4, 8, 16
@@ -114,6 +114,7 @@ def load():
         'cc_shard_planes': (I, [P, P, P]),
         'cc_seam_pairs': (i64, [P, P, P, i64, P, i64]),
         'cc_shard_finish': (I, [P, P, i64, P, ctypes.POINTER(CCResult)]),
+        'cc_shard_dev_ok': (I, [P]),
         'cc_shard_dev_begin': (I, [P, P, P, P, P, ctypes.c_double, I, i64, P]),
         'cc_shard_dev_assign': (I, [P, P, I, I]),
         'cc_shard_dev_top_cubes': (I, [P, P]),
@@ -623,6 +624,10 @@ class Context:
         return res.as_dict()
 
     # ---- z-slab shards, one-read-back schedule (distributed.py's default) ----
+    def shard_dev_ok(self):
+        """Whether this context can run the one-read-back shard schedule (cc_shard_dev_ok)."""
+        return bool(load().cc_shard_dev_ok(self._h))
+
     def shard_dev_begin(self, x_dev, block_shape, threshold, mode, z_offset, sum_dev, mask_dev=None):
         """Local stages of the slab; its sum of block values goes to sum_dev (uint64 on the device)."""
         shape, bs = _i64(x_dev.shape), _i64(block_shape)

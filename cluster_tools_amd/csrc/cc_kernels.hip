@@ -808,6 +808,13 @@ __device__ __forceinline__ int64_t xcd_contig(int64_t b, int64_t n) {
     return k * q + (k < r ? k : r) + i;
 }
 
+// timing probe of the clock tool (tools/clock_probe.hip defines it: per-workgroup core / wall
+// clock stamps in k_spec and k_pass2); empty in the library
+#ifndef CC_KERNEL_PROBE
+#define CC_KERNEL_PROBE
+#define CC_KERNEL_PROBE_END
+#endif
+
 // SIDES: bounds of the guessed interval that can move (1 lower: 'greater', 2 upper: 'less', 3 both)
 // ABL (kernel ablation harness tools/ablate.hip only; 0 in the library): 99 stop once the bit rows
 // are in LDS (loads, ballots, statistics), else as pass1_finish's ABL
@@ -815,6 +822,7 @@ template <bool HAS_MASK, int SIDES, int ABL = 0>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_spec(
     Geom g, SpecArgs sa, const float* __restrict__ in, const u8* __restrict__ mask, u64* BITS, face_t* FACES,
     u32* COUNT, u32* P, u64* KEY) {
+    CC_KERNEL_PROBE
     __shared__ Pass1LDS L;
     __shared__ u32 red[6][NTHREADS / 64];
     const int64_t t = sa.t0 + ((g.X & 31) ? xcd_contig(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x);
@@ -964,6 +972,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
     if (ABL == 99) return;
     pass1_finish<ABL % 99>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, true);
+    CC_KERNEL_PROBE_END
 }
 
 // are the bits computed with the guess G those of the exact parameters T? (see above)
@@ -2784,7 +2793,8 @@ template <bool UF>
 __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restrict__ BITS, const u32* COUNT,
                                                     const u64* __restrict__ FIN, u32* P, const u64* lut, u64 id_base,
                                                     int64_t m, u64* __restrict__ out, int order,
-                                                    const u64* id_base_dev, const u64* lut_last) {
+                                                    const u64* id_base_dev, const u64* lut_last, u64 lut_n = ~0ull) {
+    CC_KERNEL_PROBE
     __shared__ u64 rows[NROWS];             // split bit rows (see tile_ccl)
     __shared__ TileCCL T;
     __shared__ u64 lab[LABCAP];
@@ -2821,8 +2831,10 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
     const u32 base = (u32)(t * g.cap);
     if (UF && id_base_dev) id_base = __builtin_amdgcn_readfirstlane(*id_base_dev);
     // lut_last (nullable): the LUT's last index on the device (the one-read-back shard schedule,
-    // whose ids are only checked after the run: a run to be redone must not read past the LUT)
-    const u64 lmax = (UF && lut_last) ? *lut_last : ~0ull;
+    // whose ids are only checked after the run: a run to be redone must not read past the LUT);
+    // lut_n: the LUT's allocated entries -- on a run flagged RF_ROOTS the slab's sum of block values
+    // exceeds them and roots past the root capacity keep their raw keys, so both bounds apply
+    const u64 lmax = (UF && lut_last) ? min(*lut_last, lut_n - 1) : lut_n - 1;
     auto label = [&](u32 node) -> u64 {
         if (!UF) return FIN[node];
         const u64 v = FIN[gfind(P, node)];
@@ -2867,6 +2879,7 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
             }
         }
     }
+    CC_KERNEL_PROBE_END
 }
 
 // ------------------------------------------------------------------------------------------

@@ -618,7 +618,7 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
         const int64_t mm = sd ? 1 : m;
         if (st.local_only) k_pass2<false><<<(unsigned)nt, NTHREADS, pad, s>>>(g, c->bits.as<u64>(), COUNT, FIN, nullptr, nullptr, 0, 0, out, order, nullptr, nullptr);
         else k_pass2<true><<<(unsigned)nt, NTHREADS, pad, s>>>(g, c->bits.as<u64>(), COUNT, KR, P, c->lut.as<u64>(), st.base, mm, out, order,
-                                                               nullptr, sd ? scalars : nullptr);
+                                                               nullptr, sd ? scalars : nullptr, lut_cap);
     });
 
     u64 sc[4] = {0, 0, 0, 0};
@@ -696,7 +696,9 @@ static void run_pipeline(cc_ctx* c, const float* in, const uint8_t* mask, const 
                 c->fast_big = false;
                 return;
             }
-            c->fast_big = (redo & RF_BIG) != 0;
+            // a block needing the global stitch or a tile's overflowed block-face pair list are
+            // properties of the input: the next volume of this geometry goes synchronised directly
+            c->fast_big = (redo & (RF_BIG | RF_IOVF)) != 0;
             if (c->fast_big) c->fast_big_tab = hg.tab;
         }
     }

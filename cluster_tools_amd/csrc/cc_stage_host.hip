@@ -355,6 +355,8 @@ int cc_shard_finish(cc_ctx* c, const uint64_t* pairs, int64_t n_pairs, uint64_t*
 // ---------------------------------------------------------------------------------------------
 extern "C" {
 
+int cc_shard_dev_ok(cc_ctx* c) { return c && fast_ok(c) ? 1 : 0; }
+
 int cc_shard_dev_begin(cc_ctx* c, const float* in, const uint8_t* mask, const int64_t slab_shape[3],
                        const int64_t block_shape[3], double threshold, int mode, int64_t z_offset,
                        uint64_t* sum_dev) {

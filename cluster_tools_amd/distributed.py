@@ -28,10 +28,29 @@ a fixed capacity (row 0 of each = (count, redo flags)).  The status is computed 
 allgathered headers and sums, so every rank reaches the same verdict; when an optimistic bound did
 not hold (more pairs than the capacity, ids beyond the cube form, a block needing the global
 stitch fallback, more roots than the context holds) every rank relabels the step with the
-host-synchronised schedule above, and the bound that failed is raised (pair capacity) or the
-schedule is left for good (the others).
+host-synchronised schedule above.  The pair capacity is raised; a block needing the global-stitch
+fallback (RF_BIG), ids beyond the cube form (RF_CUBES) or an overflowed block-face pair list
+(RF_IOVF) leave the schedule for good (properties of the input, they would recur every step); more
+roots than the context holds (RF_ROOTS) grows its root arrays and the next step is optimistic
+again.  A context that cannot run the schedule at all (CC_FAST=0, CC_FRONT_CHUNKS > 1, debug flags,
+the empty-job quirk: cc_shard_dev_ok) uses the synchronised one from the start, decided as the
+minimum over the ranks so every rank runs the same collectives.
 """
 import numpy as np
+
+
+def check_rccl_ranks(backend, local_rank, local_world):
+    """Fail fast, before any GPU call, when RCCL cannot give every rank of this node its own GPU
+    (RCCL refuses two ranks on one device, and a rank past the visible devices would die later
+    in set_device with a less telling error).  gloo may share GPUs (rehearsals)."""
+    if backend != 'nccl':
+        return
+    import torch
+    n = torch.cuda.device_count()          # does not initialise the GPU on this image
+    if local_world > n or local_rank >= n:
+        raise RuntimeError('RCCL (backend "nccl") needs one GPU per rank: %d rank(s) on this node, %d visible '
+                           'GPU(s); launch at most %d ranks per node, or use the gloo backend to rehearse several '
+                           'ranks on one GPU' % (local_world, n, n))
 
 
 class TorchComm:
@@ -196,8 +215,11 @@ class ShardedLabeler:
         self._sums = None
         self.form = None
         self.force_form = force_form          # tests: a wider seam-plane form than the ids need
-        # one-read-back schedule (cubes32 seam planes): device-resident sums and pair buffers
+        # one-read-back schedule (cubes32 seam planes): device-resident sums and pair buffers; every
+        # rank must run the same schedule, so the contexts' verdicts are combined over the ranks
         self.fast = self.cubes_ok and force_form is None
+        if self.fast:
+            self.fast = min(self.comm.allgather_int(1 if ctx.shard_dev_ok() else 0)) == 1
         self.pair_cap = PAIR_CAP
         self.redo_steps = 0                   # steps relabelled by the host-synchronised schedule
         self._dev = None
@@ -278,7 +300,7 @@ class ShardedLabeler:
             from cluster_tools_amd import _lib
             if redo & _lib.RF_PAIRS:          # every rank sees the same largest count
                 self.pair_cap = next_pow2(2 * max_pairs)
-            if redo & (_lib.RF_BIG | _lib.RF_CUBES):
+            if redo & (_lib.RF_BIG | _lib.RF_CUBES | _lib.RF_IOVF):
                 self.fast = False             # a property of the input / id range: stay synchronised
             return None
         self.form = 'cubes32'
@@ -370,14 +392,19 @@ def label_slabs_single_process(ctxs, x, block_shape, threshold, mode='greater', 
     ctxs: one _lib.Context per slab.  form: the seam-plane form ('cubes32', 'voxel32', 'voxel64';
     default: what ShardedLabeler picks).  schedule: None (the one-read-back schedule when the
     cube form applies, else -- or when its status asks for it -- the synchronised one), 'sync',
-    'fast' (the one-read-back schedule or an error).  Returns (labels, per-slab results, sums, luts)."""
+    'fast' (the one-read-back schedule or an error).  Contexts that cannot run the one-read-back
+    schedule (cc_shard_dev_ok) get the synchronised one.  Returns (labels, per-slab results, sums,
+    luts)."""
     import torch
     Z, Y, X = x.shape
     bounds = bounds or slab_bounds(Z, block_shape[0], len(ctxs))
     out = torch.empty(tuple(x.shape), dtype=torch.int64, device=x.device)
     nby, nbx = -(-Y // block_shape[1]), -(-X // block_shape[2])
     cubes_ok = (nby == 1 or block_shape[1] % 2 == 0) and (nbx == 1 or block_shape[2] % 2 == 0)
-    if schedule != 'sync' and form in (None, 'cubes32') and cubes_ok:
+    dev_ok = all(ctx.shard_dev_ok() for ctx in ctxs)
+    if schedule == 'fast' and not dev_ok:
+        raise ValueError('the one-read-back schedule is off on these contexts (CC_FAST=0, CC_FRONT_CHUNKS, debug flags or options)')
+    if schedule != 'sync' and form in (None, 'cubes32') and cubes_ok and dev_ok:
         r = _slabs_fast(ctxs, x, block_shape, threshold, mode, mask, bounds, out, pair_cap or PAIR_CAP)
         if r is not None:
             return r

@@ -31,6 +31,8 @@ def main(config_path, out_dir):
     rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
     local_rank = int(os.environ.get('LOCAL_RANK', rank))
     backend = config.get('dist_backend', 'nccl')
+    from cluster_tools_amd.distributed import check_rccl_ranks
+    check_rccl_ranks(backend, local_rank, int(os.environ.get('LOCAL_WORLD_SIZE', world)))
     gpu = local_rank if backend == 'nccl' else local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(gpu)
     dev = torch.device('cuda', gpu)

@@ -244,6 +244,11 @@ int64_t cc_seam_pairs_cubes32(cc_ctx* ctx, const uint32_t* upper_cubes_dev, uint
  *                           fallback (1), a tile's block-face pair list overflowing (16) -- and the
  *                           caller relabels this step with the schedule
  *                           above (cc_shard_begin ...), which sizes everything from read-backs. */
+/* 1 when this context can run the schedule above, 0 when it must use the host-synchronised one:
+ * CC_FAST=0 in the environment, CC_FRONT_CHUNKS > 1, CC_DEBUG_GLOBAL_STITCH or the empty-job quirk
+ * option (cc_shard_dev_begin fails on such a context).  Callers decide the schedule from it on
+ * every rank alike (distributed.py takes the minimum over the ranks). */
+int cc_shard_dev_ok(cc_ctx* ctx);
 int cc_shard_dev_begin(cc_ctx* ctx, const float* in_dev, const uint8_t* mask_dev, const int64_t slab_shape[3],
                        const int64_t block_shape[3], double threshold, int mode, int64_t z_offset,
                        uint64_t* sum_dev);

@@ -75,3 +75,19 @@ def test_self_launch_relays_rank0_line(tmp_path, n):
 def test_self_launch_fails_when_a_rank_fails(tmp_path):
     r = _run_launcher(_fake_rank_script(tmp_path, fail_rank=1), 2)
     assert r.returncode != 0
+
+
+def test_traffic_file_provenance(tmp_path):
+    """roofline.traffic comes only from a traffic file stamped with the benched library's source
+    hash (tools/prof_summary.py --bench-json); unstamped or stale files give None."""
+    import json
+    p = tmp_path / 't.json'
+    body = {'k_pass2<true>': {'traffic': 34940478334}, 'k_spec<false, 1, 0>': {'traffic': 18212456067}}
+    p.write_text(json.dumps(body))
+    assert bench.load_traffic(str(p), 'k_pass2', 'abc') == (None, None)          # unstamped
+    p.write_text(json.dumps(dict({'_meta': {'lib_src': 'old'}}, **body)))
+    assert bench.load_traffic(str(p), 'k_pass2', 'abc') == (None, 'old')         # another build
+    p.write_text(json.dumps(dict({'_meta': {'lib_src': 'abc'}}, **body)))
+    assert bench.load_traffic(str(p), 'k_pass2', 'abc') == (34940478334, 'abc')
+    assert bench.load_traffic(str(p), 'k_spec', 'abc') == (18212456067, 'abc')
+    assert bench.load_traffic(str(tmp_path / 'none.json'), 'k_pass2', 'abc') == (None, None)

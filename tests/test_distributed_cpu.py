@@ -17,6 +17,12 @@ from oracle import oracle as O
 
 
 class FakeShardCtx:
+    def __init__(self, dev_ok=True):
+        self.dev_ok = dev_ok
+
+    def shard_dev_ok(self):
+        return self.dev_ok
+
     def shard_begin(self, x, block_shape, threshold, mode, z0, mask=None):
         r = O.label_volume(x.numpy(), block_shape, threshold, mode,
                            None if mask is None else mask.numpy())
@@ -137,15 +143,35 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, shape, block_shape, thr, mode, result_dir, form=None, pair_cap=None):
+def _worker(rank, world, port, shape, block_shape, thr, mode, result_dir, form=None, pair_cap=None,
+            no_dev_ranks=()):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     from cluster_tools_amd.distributed import ShardedLabeler, TorchComm, slab_bounds
+
+    class CountingComm(TorchComm):
+        """The production communicator itself (no override of what it sends), with a call log."""
+        calls = []
+
+        def allgather_into(self, out, inp):
+            self.calls.append('allgather_into')
+            return TorchComm.allgather_into(self, out, inp)
+
+        def shift_up(self, send, recv):
+            self.calls.append('shift_up')
+            return TorchComm.shift_up(self, send, recv)
+
+        def allgather_int(self, v):
+            self.calls.append('allgather_int')
+            return TorchComm.allgather_int(self, v)
+
     x = O.boundary_map(shape, n_threads=1)
     z0, zs = slab_bounds(shape[0], block_shape[0], world)[rank]
-    lab = ShardedLabeler(FakeShardCtx(), shape, block_shape, z0, zs, device=None,
-                         comm=TorchComm(device=None), force_form=form)
+    comm = CountingComm(device=None)
+    lab = ShardedLabeler(FakeShardCtx(dev_ok=rank not in no_dev_ranks), shape, block_shape, z0, zs, device=None,
+                         comm=comm, force_form=form)
+    CountingComm.calls.clear()
     if pair_cap is not None:
         lab.pair_cap = pair_cap
     out = torch.empty((zs,) + tuple(shape[1:]), dtype=torch.int64)
@@ -158,6 +184,8 @@ def _worker(rank, world, port, shape, block_shape, thr, mode, result_dir, form=N
     np.save(os.path.join(result_dir, 'nl_%d.npy' % rank), np.array([res['n_labels'], res['id_base']]))
     with open(os.path.join(result_dir, 'sched_%d.txt' % rank), 'w') as f:
         f.write(' '.join(sched) + ' %d' % lab.pair_cap)
+    with open(os.path.join(result_dir, 'calls_%d.txt' % rank), 'w') as f:
+        f.write(' '.join(CountingComm.calls))
     dist.destroy_process_group()
 
 
@@ -182,8 +210,44 @@ def test_gloo_sharded_schedule_matches_oracle(tmp_path, world, shape, block_shap
         assert int(np.load(str(tmp_path / ('nl_%d.npy' % r)))[0]) == ref['n_labels']
         sched = open(str(tmp_path / ('sched_%d.txt' % r))).read().split()
         # even y/x blocks and no forced form: the one-read-back schedule, else the synchronised one
-        assert sched[0] == ('one-read-back' if form is None and block_shape[1] % 2 == 0 and
-                            block_shape[2] % 2 == 0 else 'synchronised')
+        fast = form is None and block_shape[1] % 2 == 0 and block_shape[2] % 2 == 0
+        assert sched[0] == ('one-read-back' if fast else 'synchronised')
+        calls = open(str(tmp_path / ('calls_%d.txt' % r))).read().split()
+        if fast:
+            # the production communicator's stream-ordered collectives ran at world > 1: the sums'
+            # allgather, the seam plane's point-to-point shift, the pair buffers' allgather
+            assert calls == ['allgather_into', 'shift_up', 'allgather_into']
+        else:
+            assert 'shift_up' in calls and 'allgather_into' not in calls
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_gloo_schedule_agreed_over_ranks(tmp_path, world):
+    """One rank's context cannot run the one-read-back schedule (cc_shard_dev_ok = 0: CC_FAST=0,
+    CC_FRONT_CHUNKS > 1, debug flags or the quirk option): every rank takes the synchronised one,
+    so the collectives match, and the labels equal the oracle."""
+    shape, block_shape = (40, 64, 64), (8, 32, 32)
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, shape, block_shape, 0.5, 'greater', str(tmp_path), None, None, (world - 1,)),
+             nprocs=world, join=True)
+    got = np.concatenate([np.load(str(tmp_path / ('slab_%d.npy' % r))) for r in range(world)]).astype(np.uint64)
+    ref = O.label_volume(O.boundary_map(shape, n_threads=1), block_shape, 0.5, 'greater')
+    np.testing.assert_array_equal(got, ref['labels'])
+    for r in range(world):
+        assert open(str(tmp_path / ('sched_%d.txt' % r))).read().split()[0] == 'synchronised'
+
+
+def test_check_rccl_ranks():
+    """bench.py / sharded_job.py fail fast when RCCL cannot give every local rank a GPU."""
+    from cluster_tools_amd.distributed import check_rccl_ranks
+    n = torch.cuda.device_count()
+    check_rccl_ranks('gloo', 5, n + 8)             # gloo may share GPUs
+    with pytest.raises(RuntimeError, match='one GPU per rank'):
+        check_rccl_ranks('nccl', 0, n + 1)
+    with pytest.raises(RuntimeError, match='one GPU per rank'):
+        check_rccl_ranks('nccl', n, n + 1)
+    if n:
+        check_rccl_ranks('nccl', n - 1, n)
 
 
 @pytest.mark.parametrize('world', [2, 3])

@@ -229,3 +229,58 @@ def test_sharded_pair_capacity_redo():
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.parametrize('env', [{'CC_FAST': '0'}, {'CC_FRONT_CHUNKS': '2'}])
+def test_sharded_contexts_without_fast_schedule(monkeypatch, env):
+    """Contexts that cannot run the one-read-back schedule (CC_FAST=0 forces the synchronised
+    schedule; CC_FRONT_CHUNKS > 1 chunks the front): the sharded run asks cc_shard_dev_ok and
+    takes the synchronised schedule instead of failing in cc_shard_dev_begin; schedule='fast' is
+    refused with a clear error."""
+    import torch
+    from cluster_tools_amd import _lib
+    from cluster_tools_amd.distributed import label_slabs_single_process, assemble_lut
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    shape, bs = (64, 150, 200), (16, 64, 64)
+    x = O.boundary_map(shape, origin=(2, 1, 4))
+    ctxs = [_lib.Context(0) for _ in range(3)]          # CC_FRONT_CHUNKS is read by cc_create
+    try:
+        assert not any(c.shard_dev_ok() for c in ctxs)
+        xd = torch.from_numpy(x).cuda()
+        lab, res, sums, luts = label_slabs_single_process(ctxs, xd, bs, 0.5, 'greater')
+        assert {r['schedule'] for r in res} == {'synchronised'}
+        ref = O.label_volume(x, bs, 0.5, 'greater', n_threads=8)
+        np.testing.assert_array_equal(lab.cpu().numpy().view(np.uint64), ref['labels'])
+        np.testing.assert_array_equal(assemble_lut(luts, sums), ref['lut'])
+        with pytest.raises(ValueError, match='one-read-back'):
+            label_slabs_single_process(ctxs, xd, bs, 0.5, 'greater', schedule='fast')
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def test_sharded_root_capacity_redo(monkeypatch):
+    """More block-local roots than the contexts' root arrays hold (CC_ROOT_CAP=8) in the sharded
+    one-read-back step: k_pass2 runs before the status is read, with slab sums beyond the LUT's
+    allocation -- its LUT reads stay inside the allocation (lut_n) -- then RF_ROOTS sends the step
+    to the synchronised schedule (same labels), and the grown capacity lets the next step run the
+    one-read-back schedule."""
+    import torch
+    from cluster_tools_amd import _lib
+    from cluster_tools_amd.distributed import label_slabs_single_process, assemble_lut
+    monkeypatch.setenv('CC_ROOT_CAP', '8')
+    shape, bs = (96, 160, 192), (16, 64, 64)
+    x = O.boundary_map(shape, origin=(5, 2, 1))
+    ref = O.label_volume(x, bs, 0.5, 'less', n_threads=8)
+    ctxs = [_lib.Context(0) for _ in range(3)]
+    try:
+        xd = torch.from_numpy(x).cuda()
+        for want in ('synchronised', 'one-read-back'):
+            lab, res, sums, luts = label_slabs_single_process(ctxs, xd, bs, 0.5, 'less')
+            assert {r['schedule'] for r in res} == {want}
+            np.testing.assert_array_equal(lab.cpu().numpy().view(np.uint64), ref['labels'])
+            np.testing.assert_array_equal(assemble_lut(luts, sums), ref['lut'])
+    finally:
+        for c in ctxs:
+            c.close()

@@ -1,0 +1,194 @@
+// tools/clock_probe.hip -- the core clock each kernel of the C3 step actually runs at (timing
+// tool, not part of the library).
+//
+// Every workgroup of k_spec / k_pass2 stamps the core clock counter (clock64) and the constant-
+// rate wall counter (wall_clock64, hipDeviceAttributeWallClockRate) when it starts and ends (the
+// CC_KERNEL_PROBE hook of cc_kernels.hip, empty in the library), plus its XCC id.  From the
+// stamps: the effective core clock = sum of core cycles / sum of wall time over workgroups, per
+// XCD and overall; the mean workgroup lifetime; the mean number of workgroups resident per CU
+// (sum of lifetimes / kernel span / 256).  A VALU-only spin kernel over the whole chip gives
+// the clock at light power for comparison.  Box-to-box differences of k_spec at equal memory
+// roofs either show here as a lower clock or not.
+// Build: make -C tools clock_probe   Run: tools/clock_probe [Z Y X bz by bx] [iters]
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+struct ProbeRec {
+    unsigned long long c0, c1, w0, w1;
+    unsigned xcc, pad;
+};
+__device__ ProbeRec* g_probe;
+
+// (no branch on the lane: every wave stores its own stamps to the workgroup's record, the last
+// store wins -- a branch here turned k_spec's writelane region divergent)
+__device__ __forceinline__ void probe_begin() {
+    ProbeRec& r = g_probe[blockIdx.x];
+    r.w0 = wall_clock64();
+    r.c0 = clock64();
+    r.xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);     // HW_REG_XCC_ID[3:0]
+}
+__device__ __forceinline__ void probe_end() {
+    ProbeRec& r = g_probe[blockIdx.x];
+    r.c1 = clock64();
+    r.w1 = wall_clock64();
+}
+// stamps at the start and at the normal end of the kernel (early-return workgroups, e.g. k_pass2's
+// empty tiles, leave c1 = 0 and are skipped)
+#define CC_KERNEL_PROBE probe_begin();
+#define CC_KERNEL_PROBE_END probe_end();
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../cluster_tools_amd/csrc/cc_kernels.hip"
+#include "../cluster_tools_amd/csrc/cc_generate.hip"
+#include "../cluster_tools_amd/csrc/cc_host.hpp"
+
+using namespace cc;
+
+__global__ __launch_bounds__(512) void k_spin(int iters, float* out) {
+    probe_begin();
+    float a = threadIdx.x * 1e-3f, b = 1.0001f;
+    for (int i = 0; i < iters; ++i) {
+        a = __builtin_fmaf(a, b, 0.5f);
+        b = __builtin_fmaf(b, a, -0.25f);
+    }
+    if (a == 1234.5f) out[0] = b;
+    probe_end();
+}
+
+struct Summary {
+    double mhz, life_us, resident_per_cu, span_ms;
+    double xcc_mhz[8];
+};
+
+static Summary summarize(const std::vector<ProbeRec>& v, double wall_khz) {
+    Summary s{};
+    double cyc = 0, wall = 0, xc[8] = {0}, xw[8] = {0};
+    unsigned long long t0 = ~0ull, t1 = 0;
+    size_t n = 0;
+    for (const auto& r : v) {
+        if (r.c1 <= r.c0 || r.w1 <= r.w0) continue;
+        ++n;
+        const double dc = (double)(r.c1 - r.c0), dw = (double)(r.w1 - r.w0);
+        cyc += dc; wall += dw;
+        xc[r.xcc & 7] += dc; xw[r.xcc & 7] += dw;
+        if (r.w0 < t0) t0 = r.w0;
+        if (r.w1 > t1) t1 = r.w1;
+    }
+    const double tick_us = 1e3 / wall_khz;
+    s.mhz = cyc / wall * wall_khz / 1e3;
+    for (int k = 0; k < 8; ++k) s.xcc_mhz[k] = xw[k] > 0 ? xc[k] / xw[k] * wall_khz / 1e3 : 0;
+    s.life_us = n ? wall / n * tick_us : 0;
+    s.span_ms = (double)(t1 - t0) * tick_us / 1e3;
+    s.resident_per_cu = wall / (double)(t1 - t0) / 256.0;
+    return s;
+}
+
+static void print(const char* name, double ms, const Summary& s) {
+    std::printf("{\"kernel\": \"%s\", \"event_ms\": %.4f, \"span_ms\": %.4f, \"core_mhz\": %.0f, \"wg_life_us\": %.2f, "
+                "\"wg_resident_per_cu\": %.2f, \"xcd_mhz\": [", name, ms, s.span_ms, s.mhz, s.life_us, s.resident_per_cu);
+    for (int k = 0; k < 8; ++k) std::printf("%s%.0f", k ? ", " : "", s.xcc_mhz[k]);
+    std::printf("]}\n");
+    std::fflush(stdout);
+}
+
+int main(int argc, char** argv) {
+    try {
+        const int64_t shape[3] = {argc > 3 ? atoll(argv[1]) : 1024, argc > 3 ? atoll(argv[2]) : 2048, argc > 3 ? atoll(argv[3]) : 2048};
+        const int64_t bs[3] = {argc > 6 ? atoll(argv[4]) : 64, argc > 6 ? atoll(argv[5]) : 512, argc > 6 ? atoll(argv[6]) : 512};
+        const int iters = argc > 7 ? atoi(argv[7]) : 5;
+        int dev = 0, wall_khz = 0;
+        HIP_OK(hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, dev));
+        HostGeom hg = make_geom(shape, bs, 0);
+        Geom& g = hg.g;
+        const int64_t nt = g.n_tiles, nb = g.n_blocks, nvox = hg.nvox;
+        const uint64_t nodes = (uint64_t)nt * g.cap;
+        hipStream_t s;
+        HIP_OK(hipStreamCreate(&s));
+        int32_t* tab;
+        HIP_OK(hipMalloc(&tab, hg.tab.size() * 4));
+        HIP_OK(hipMemcpy(tab, hg.tab.data(), hg.tab.size() * 4, hipMemcpyHostToDevice));
+        bind_geom_tables(hg, tab);
+        ProbeRec* rec;
+        const int64_t nrec = nt > 1 << 20 ? nt : 1 << 20;
+        HIP_OK(hipMalloc(&rec, nrec * sizeof(ProbeRec)));
+        HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_probe), &rec, sizeof(rec)));
+        float *in, *dummy;
+        u64* out;
+        HIP_OK(hipMalloc(&in, nvox * 4));
+        HIP_OK(hipMalloc(&out, nvox * 8));
+        HIP_OK(hipMalloc(&dummy, 64));
+        {
+            const int64_t nxb = (shape[2] + 255) / 256;
+            k_generate<<<dim3((unsigned)(shape[1] * nxb), (unsigned)shape[0]), 256, 0, s>>>(in, shape[0], shape[1], shape[2], 0, 0, 0, 0x5EED, 0);
+        }
+        u32 *st, *COUNT, *P, *fst, *TB;
+        face_t* FACES;
+        u64 *BITS, *KEY, *FIN;
+        BlockParam *bp, *guess;
+        HIP_OK(hipMalloc(&st, nb * 12));
+        HIP_OK(hipMalloc(&fst, nb * 12));
+        HIP_OK(hipMalloc(&bp, nb * sizeof(BlockParam)));
+        HIP_OK(hipMalloc(&guess, nb * sizeof(BlockParam)));
+        HIP_OK(hipMalloc(&TB, nt * 16));
+        HIP_OK(hipMalloc(&BITS, nt * NROWS * 8));
+        HIP_OK(hipMalloc(&FACES, nt * FACE_STRIDE * 4));
+        HIP_OK(hipMalloc(&COUNT, nt * 4));
+        HIP_OK(hipMalloc(&P, nodes * 4));
+        HIP_OK(hipMalloc(&KEY, nodes * 8));
+        HIP_OK(hipMalloc(&FIN, nodes * 8));
+        HIP_OK(hipMemset(FIN, 0, nodes * 8));
+        u32 *smin = st, *smax = st + nb, *sflag = st + 2 * nb;
+        const float thr = 0.5f;
+        HIP_OK(hipMemsetAsync(smin, 0xFF, nb * 4, s));
+        HIP_OK(hipMemsetAsync(smax, 0, 2 * nb * 4, s));
+        k_block_stats<<<(unsigned)nt, NTHREADS, 0, s>>>(g, in, smin, smax, sflag);
+        k_block_params<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, smin, smax, sflag, thr, 0, bp);
+        HIP_OK(hipStreamSynchronize(s));
+        std::vector<BlockParam> hb(nb);
+        HIP_OK(hipMemcpy(hb.data(), bp, nb * sizeof(BlockParam), hipMemcpyDeviceToHost));
+        for (auto& q : hb)
+            if (q.kind == BP_INTERVAL) q.hi = 0xFFFFFFFFu;
+        HIP_OK(hipMemcpy(guess, hb.data(), nb * sizeof(BlockParam), hipMemcpyHostToDevice));
+        SpecArgs sa;
+        sa.guess = guess; sa.smin = fst; sa.smax = fst + nb; sa.sflag = fst + 2 * nb; sa.TB = TB; sa.t0 = 0;
+
+        hipEvent_t e0, e1;
+        HIP_OK(hipEventCreate(&e0));
+        HIP_OK(hipEventCreate(&e1));
+        auto run = [&](const char* name, int64_t nwg, auto&& launch) {
+            for (int i = 0; i < iters; ++i) {
+                HIP_OK(hipMemsetAsync(rec, 0, nwg * sizeof(ProbeRec), s));
+                HIP_OK(hipEventRecord(e0, s));
+                launch();
+                HIP_OK(hipEventRecord(e1, s));
+                HIP_OK(hipEventSynchronize(e1));
+                HIP_OK(hipGetLastError());
+                float ms = 0;
+                HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+                std::vector<ProbeRec> v(nwg);
+                HIP_OK(hipMemcpy(v.data(), rec, nwg * sizeof(ProbeRec), hipMemcpyDeviceToHost));
+                if (i == 0) continue;      // first launch: cold
+                print(name, ms, summarize(v, wall_khz));
+            }
+        };
+        run("k_spin_valu", 2048, [&] { k_spin<<<2048, 512, 0, s>>>(200000, dummy); });
+        run("k_spec", nt, [&] {
+            HIP_OK(hipMemsetAsync(fst, 0xFF, nb * 4, s));
+            HIP_OK(hipMemsetAsync(fst + nb, 0, 2 * nb * 4, s));
+            k_spec<false, 1><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS, FACES, COUNT, P, KEY);
+        });
+        run("k_pass2", nt, [&] {
+            k_pass2<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, BITS, COUNT, FIN, nullptr, nullptr, 0, 0, out, 0, nullptr, nullptr);
+        });
+        run("k_spin_valu_after", 2048, [&] { k_spin<<<2048, 512, 0, s>>>(200000, dummy); });
+        std::printf("# wall clock rate %d kHz, %lld tiles\n", wall_khz, (long long)nt);
+    } catch (const CCError& e) {
+        std::fprintf(stderr, "error: %s\n", e.msg.c_str());
+        return 1;
+    }
+    return 0;
+}

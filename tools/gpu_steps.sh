@@ -17,6 +17,8 @@
 #   clock          effective GPU clock per kernel of the C3 step (tools/pmc_clock.sh)
 #   roof / ablate  the box's streaming ceilings (tools/roof) and the k_spec ablation (tools/ablate)
 #   ab_fast        same-box round-robin A/B: one-read-back vs host-synchronised schedule (C3)
+#   boxinfo        the lease's static / current SMI info (product, VBIOS, power cap, clocks, memory)
+#   clockprobe     core clock per kernel from in-kernel clock stamps (tools/clock_probe)
 set -e -o pipefail
 TAG=$1; shift
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -63,6 +65,11 @@ for step in "$@"; do
     trace_slabs8) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
                     -d "$ROOT/$O/trace_slabs8_$TAG" -o run -- python3 "$ROOT/tools/bench_sharded_slabs.py" 8 c3 3 \
                     > "$ROOT/$O/trace_slabs8_$TAG.json" 2> "$ROOT/$O/trace_slabs8_$TAG.err") ;;
+    boxinfo)    { timeout -k 5 60 rocm-smi --showproductname --showvbios --showdriverversion --showpower --showmaxpower \
+                    --showclocks --showmemvendor --showmeminfo vram --showcomputepartition --showmemorypartition 2>&1 || true;
+                  timeout -k 5 60 amd-smi static -g 0 2>&1 || true; timeout -k 5 60 amd-smi metric -g 0 2>&1 || true; } > $O/boxinfo_$TAG.txt
+                grep -iE "vbios|power cap|max.*power|sclk|mclk|fclk|partition|Card Series|Market" $O/boxinfo_$TAG.txt | head -40 || true ;;
+    clockprobe) timeout -k 10 120 tools/clock_probe 1024 2048 2048 64 512 512 4 > $O/clockprobe_$TAG.txt 2>&1; cat $O/clockprobe_$TAG.txt ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -70,6 +70,10 @@ def main():
     p.add_argument('-o', '--out', required=True)
     p.add_argument('--narrow', action='append', default=[],
                    help='KERNEL_PREFIX=BYTES: per-dispatch bytes of byte-wide reads (counted exactly)')
+    p.add_argument('--bench-json', default=None,
+                   help="the bench line of the profiled run: its lib.src (the library's source hash) and "
+                        "workload are stamped into the summary's '_meta', so bench.py uses the traffic "
+                        "figures only for the library they were measured on")
     a = p.parse_args()
     narrow = {k: float(v) for k, v in (n.split('=') for n in a.narrow)}
     res = trace_stats(a.trace)
@@ -90,9 +94,22 @@ def main():
             v['traffic'] = v['fetch_bytes'] + v['write_bytes']
             v['traffic_gbs'] = v['traffic'] / (v['avg_ms'] * 1e-3) / 1e9
     res = dict(sorted(res.items(), key=lambda kv: -kv[1]['total_ms']))
+    if a.bench_json:
+        line = None
+        for ln in open(a.bench_json).read().splitlines():
+            if ln.strip().startswith('{'):
+                line = json.loads(ln)
+        if line is None:
+            raise SystemExit('no bench line in %s' % a.bench_json)
+        res = dict({'_meta': {'lib_src': line['lib']['src'], 'workload': line['config'].get('workload_id'),
+                              'mask': line['config'].get('mask'), 'continuous': line['config'].get('continuous')}},
+                   **res)
     with open(a.out, 'w') as f:
         json.dump(res, f, indent=1)
     for k, v in res.items():
+        if k == '_meta':
+            print('# lib.src %s workload %s' % (v['lib_src'], v['workload']))
+            continue
         print('%-40s n=%4d avg %.4f ms total %.3f ms%s' % (
             k[:40], v['count'], v['avg_ms'], v['total_ms'],
             ('  traffic %.3f GB' % (v['traffic'] / 1e9)) if 'traffic' in v else ''))

@@ -19,5 +19,5 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/writ
 NARROW=()
 case " $* " in *" --mask "*) NARROW=(--narrow "k_spec<true=${CC_NVOX:-4294967296}");; esac
 python3 "$ROOT/tools/prof_summary.py" --trace "$OUT/trace" --fetch "$OUT/fetch" --write "$OUT/write" \
-    "${NARROW[@]}" -o "$OUT/summary.json" > "$OUT/summary.txt"
+    "${NARROW[@]}" --bench-json "$OUT/bench_trace.json" -o "$OUT/summary.json" > "$OUT/summary.txt"
 cat "$OUT/summary.txt"
