@@ -28,6 +28,7 @@ EXPORTS = (
     'cc_gaussian_smooth_blocks', 'cc_gaussian_taps', 'cc_result_size', 'cc_resize_mask_nearest',
     'cc_watershed_from_seeds', 'cc_shard_dev_begin', 'cc_shard_dev_assign', 'cc_shard_dev_top_cubes',
     'cc_shard_dev_seam_pairs', 'cc_shard_dev_finish', 'cc_normalize_channels', 'cc_shard_dev_ok',
+    'cc_comm_unique_id', 'cc_comm_create', 'cc_comm_destroy', 'cc_label_volume_sharded',
 )
 # redo flags of the one-read-back schedule (RF_* in csrc/cc_kernels.hip)
 RF_BIG, RF_ROOTS, RF_CUBES, RF_PAIRS, RF_IOVF = 1, 2, 4, 8, 16
@@ -115,6 +116,10 @@ def load():
         'cc_seam_pairs': (i64, [P, P, P, i64, P, i64]),
         'cc_shard_finish': (I, [P, P, i64, P, ctypes.POINTER(CCResult)]),
         'cc_shard_dev_ok': (I, [P]),
+        'cc_comm_unique_id': (I, [P, i64]),
+        'cc_comm_create': (I, [P, I, I, I, ctypes.POINTER(P)]),
+        'cc_comm_destroy': (None, [P]),
+        'cc_label_volume_sharded': (I, [P, P, P, P, P, i64, i64, P, ctypes.c_double, I, P, ctypes.POINTER(CCResult)]),
         'cc_shard_dev_begin': (I, [P, P, P, P, P, ctypes.c_double, I, i64, P]),
         'cc_shard_dev_assign': (I, [P, P, I, I]),
         'cc_shard_dev_top_cubes': (I, [P, P]),
@@ -221,6 +226,35 @@ def mode_id(mode):
     return MODES[mode]
 
 
+def comm_unique_id():
+    """The RCCL bootstrap id (128 bytes) for Comm: made on one rank, handed to every rank."""
+    buf = ctypes.create_string_buffer(128)
+    _check(load().cc_comm_unique_id(buf, 128))
+    return buf.raw
+
+
+class Comm:
+    """One rank's RCCL communicator owned by the library (cc_comm_create): z-slab sharding from a
+    plain C / ctypes caller, no torch.distributed (Context.label_volume_sharded)."""
+
+    def __init__(self, unique_id, world, rank, device=0):
+        h = ctypes.c_void_p()
+        uid = ctypes.create_string_buffer(bytes(unique_id), 128)
+        _check(load().cc_comm_create(uid, int(world), int(rank), int(device), ctypes.byref(h)))
+        self._h, self.world, self.rank, self.device = h, world, rank, device
+
+    def close(self):
+        if self._h:
+            load().cc_comm_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
 class Context:
     """One cc_ctx (one GPU).  Not thread-safe."""
 
@@ -281,6 +315,26 @@ class Context:
                 out = np.empty(inp.shape, dtype=np.uint64)
             _check(L.cc_label_volume_host(self._h, _ptr(inp), _ptr(mask), _ptr(shape), _ptr(bs),
                                           float(threshold), mode_id(mode), _ptr(out), ctypes.byref(res)))
+        return out, res.as_dict()
+
+    def label_volume_sharded(self, comm, slab, global_shape, z_offset, block_shape, threshold, mode='greater',
+                             mask=None, out=None):
+        """This rank's z-slab [z_offset, z_offset + len(slab)) of a volume sharded over comm's ranks
+        (cc_label_volume_sharded: the schedule with RCCL inside the library).  `slab` / `mask`:
+        CUDA tensors of the slab.  Returns (labels of the slab, result dict with the global
+        n_labels)."""
+        import torch
+        assert slab.is_cuda and slab.dtype == torch.float32 and slab.is_contiguous() and slab.dim() == 3
+        if mask is not None:
+            assert mask.is_cuda and mask.dtype == torch.uint8 and mask.shape == slab.shape
+            mask = mask.contiguous()
+        if out is None:
+            out = torch.empty(tuple(slab.shape), dtype=torch.int64, device=slab.device)
+        gs, bs = _i64(global_shape), _i64(block_shape)
+        res = CCResult()
+        _check(load().cc_label_volume_sharded(self._h, comm._h, _ptr(slab), _ptr(mask), _ptr(gs), int(z_offset),
+                                              int(slab.shape[0]), _ptr(bs), float(threshold), mode_id(mode), _ptr(out),
+                                              ctypes.byref(res)))
         return out, res.as_dict()
 
     def torch_device(self):

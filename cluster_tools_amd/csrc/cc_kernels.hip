@@ -741,8 +741,12 @@ __global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __rest
                 for (int u = 0; u < SAMPLE_U; ++u) f(f2ord(__float_as_uint(v[u])));
             }
     };
-    u32 mn = 0xFFFFFFFFu, mx = 0u;
+    // extremes and how often each occurs in the sample (k_guess: quantized data repeats its
+    // extremes, continuous data does not)
+    u32 mn = 0xFFFFFFFFu, mx = 0u, cmn = 0u, cmx = 0u;
     auto f = [&](u32 o) {
+        cmn = o < mn ? 1u : cmn + (o == mn ? 1u : 0u);
+        cmx = o > mx ? 1u : cmx + (o == mx ? 1u : 0u);
         mn = min(mn, o);
         mx = max(mx, o);
     };
@@ -770,24 +774,45 @@ __global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __rest
     } else {
         sweep(f);
     }
+    const u32 tmn = mn, tmx = mx;
     mn = block_minmax<false>(mn, red);
     mx = block_minmax<true>(mx, red);
+    // (a thread's count of a value repeated by the clamped row index is counted again: harmless,
+    // the count only steers the choice of k_spec's statistics, never a result)
+    u32 nmn = 0, nmx = 0;
+    block_excl_scan(tmn == mn ? cmn : 0u, red, &nmn);
+    block_excl_scan(tmx == mx ? cmx : 0u, red, &nmx);
     if (tid == 0) {
         u32* q = part + 4 * blockIdx.x;
-        q[0] = mn; q[1] = 0; q[2] = mx; q[3] = 0;
+        q[0] = mn; q[1] = nmn; q[2] = mx; q[3] = nmx;
     }
 }
 
-__global__ void k_guess(int64_t nb, const u32* part, float thr, int mode, BlockParam* guess) {
+// guess.pad (GUESS_TB): 1 = k_spec records each tile's TB (the nearest values around the guessed
+// bounds) and k_params_verify keeps every tile whose bits the exact interval would not change;
+// 0 = the sampled extremes each occurred at least twice (quantized data: the block's extremes
+// are almost surely in the sample), k_spec skips TB (a quarter of its load-loop VALU) and the
+// guess holds only if it equals the exact parameters (else every tile of the block goes to
+// k_fix).  Results never depend on the choice; the k_fix work does.
+constexpr u32 GUESS_TB = 1;
+
+__global__ void k_guess(int64_t nb, const u32* part, float thr, int mode, BlockParam* guess, int tb_free) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     const u32* q = part + 4 * SAMPLE_PARTS * b;
     u32 mn = 0xFFFFFFFFu, mx = 0u;
     for (int p = 0; p < SAMPLE_PARTS; ++p) { mn = min(mn, q[4 * p]); mx = max(mx, q[4 * p + 2]); }
+    u32 nmn = 0, nmx = 0;
+    for (int p = 0; p < SAMPLE_PARTS; ++p) {
+        nmn += q[4 * p] == mn ? q[4 * p + 1] : 0u;
+        nmx += q[4 * p + 2] == mx ? q[4 * p + 3] : 0u;
+    }
     const bool nan = mx > 0xFF800000u || mn < 0x007FFFFFu;
     // On continuous data the sampled extremes are not the block's, so the guessed bound misses
     // the exact one by a little: only tiles holding a voxel between the two are relabelled.
-    guess[b] = widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
+    BlockParam p = widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
+    p.pad = (tb_free && nmn >= 2 && nmx >= 2) ? 0u : GUESS_TB;
+    guess[b] = p;
 }
 
 struct SpecArgs {
@@ -795,6 +820,8 @@ struct SpecArgs {
     u32* smin; u32* smax; u32* sflag;
     u32* TB;                  // 4 per tile (see above)
     int64_t t0;               // first tile of this launch (the front runs in z-layer chunks)
+    u32* TS = nullptr;        // k_spec: per-tile (ordered min, max) for k_block_verify instead of
+                              // the per-block atomics (nullptr: atomics, as k_thr_spec)
 };
 
 // workgroup b of n -> tile: the (b / 8)-th of the contiguous range of XCD b % 8 (workgroups are
@@ -808,32 +835,25 @@ __device__ __forceinline__ int64_t xcd_contig(int64_t b, int64_t n) {
     return k * q + (k < r ? k : r) + i;
 }
 
-// timing probe of the clock tool (tools/clock_probe.hip defines it: per-workgroup core / wall
-// clock stamps in k_spec and k_pass2); empty in the library
-#ifndef CC_KERNEL_PROBE
-#define CC_KERNEL_PROBE
-#define CC_KERNEL_PROBE_END
+#ifndef CC_MASK_STAGE
+#define CC_MASK_STAGE 0
 #endif
 
-// SIDES: bounds of the guessed interval that can move (1 lower: 'greater', 2 upper: 'less', 3 both)
-// ABL (kernel ablation harness tools/ablate.hip only; 0 in the library): 99 stop once the bit rows
-// are in LDS (loads, ballots, statistics), else as pass1_finish's ABL
-template <bool HAS_MASK, int SIDES, int ABL = 0>
-__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_spec(
-    Geom g, SpecArgs sa, const float* __restrict__ in, const u8* __restrict__ mask, u64* BITS, face_t* FACES,
-    u32* COUNT, u32* P, u64* KEY) {
-    CC_KERNEL_PROBE
-    __shared__ Pass1LDS L;
-    __shared__ u32 red[6][NTHREADS / 64];
-    const int64_t t = sa.t0 + ((g.X & 31) ? xcd_contig(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x);
-    const TileInfo ti = tile_info(g, t);
-    const BlockParam p = uniform_bp(sa.guess[ti.block]);
-    if (p.kind != BP_INTERVAL) {                   // no guess: statistics only, k_fix labels the tile
-        stats_tile(g, ti, in, sa.smin, sa.smax, sa.sflag, red);
-        return;
-    }
+// The front of k_spec for tile t: the tile's voxels in one read -> exact statistics (red, then
+// the block's atomics or the per-tile TS words), the bit rows under the guessed interval
+// [lo, hi] into L.rows, and (TBR) the tile's TB words.  TBR: this tile records TB, the nearest
+// values around the guessed bounds -- not when k_guess found the sampled extremes repeated
+// (GUESS_TB clear: the guess must equal the exact parameters, spec_valid); k_spec branches once,
+// uniformly, between the two instantiations.
+// F4: the tile is full and 16-B aligned (float4 loads); partial tiles (F4 = false, rare: block
+// and volume ends) always record TB -- harmless for a TB-free block, whose guess is checked by
+// equality -- so only the float4 path has two instantiations (one of each path per kernel: three
+// copies of the whole front left the compiler a private frame it never used).
+template <bool HAS_MASK, int SIDES, bool F4, bool tbr>
+__device__ __forceinline__ void spec_front(Geom g, SpecArgs sa, int64_t t, TileInfo ti,
+                                           const float* __restrict__ in, const u8* __restrict__ mask, u32 lo,
+                                           u32 hi, Pass1LDS& L, u32 (*red)[NTHREADS / 64]) {
     const int tid = cc_tid(), lane = tid & 63, wave = wave_id();
-    const u32 lo = p.lo, hi = p.hi;
     // Statistics: ordered min / max of every voxel, and the nearest values around the guessed
     // bounds as the min / max of the wrapped distances k1 = o - lo and k2 = hi - o (mod 2^32) over
     // the used voxels: o - lo puts every voxel at or above lo below every voxel under it, so
@@ -850,31 +870,30 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         const u32 o = f2ord(__float_as_uint(x));
         mn = min(mn, o);
         mx = max(mx, o);
-        if (SIDES & 1) { const u32 k = o - lo; K1N = min(K1N, k); K1X = max(K1X, k); }
-        if (SIDES & 2) { const u32 k = hi - o; K2N = min(K2N, k); K2X = max(K2X, k); }
+        if ((SIDES & 1) && tbr) { const u32 k = o - lo; K1N = min(K1N, k); K1X = max(K1X, k); }
+        if ((SIDES & 2) && tbr) { const u32 k = hi - o; K2N = min(K2N, k); K2X = max(K2X, k); }
         return (!HAS_MASK || mk != 0) && fgp(o);
     };
     // four voxels of one float4 (full tiles): the same, min / max folded three operands at a time
-    auto quad = [&](float4 v, uchar4 mk, bool fg[4]) {
+    auto quad = [&](float4 v, uchar4 mk, bool& f0, bool& f1, bool& f2, bool& f3) {
         const u32 o0 = f2ord(__float_as_uint(v.x)), o1 = f2ord(__float_as_uint(v.y));
         const u32 o2 = f2ord(__float_as_uint(v.z)), o3 = f2ord(__float_as_uint(v.w));
         mn = min(min(min(min(mn, o0), o1), o2), o3);
         mx = max(max(max(max(mx, o0), o1), o2), o3);
-        if (SIDES & 1) {
+        if ((SIDES & 1) && tbr) {
             const u32 k0 = o0 - lo, k1 = o1 - lo, k2 = o2 - lo, k3 = o3 - lo;
             K1N = min(min(min(min(K1N, k0), k1), k2), k3);
             K1X = max(max(max(max(K1X, k0), k1), k2), k3);
         }
-        if (SIDES & 2) {
+        if ((SIDES & 2) && tbr) {
             const u32 k0 = hi - o0, k1 = hi - o1, k2 = hi - o2, k3 = hi - o3;
             K2N = min(min(min(min(K2N, k0), k1), k2), k3);
             K2X = max(max(max(max(K2X, k0), k1), k2), k3);
         }
         const bool u0 = !HAS_MASK || mk.x, u1 = !HAS_MASK || mk.y, u2 = !HAS_MASK || mk.z, u3 = !HAS_MASK || mk.w;
-        fg[0] = u0 && fgp(o0); fg[1] = u1 && fgp(o1); fg[2] = u2 && fgp(o2); fg[3] = u3 && fgp(o3);
+        f0 = u0 && fgp(o0); f1 = u1 && fgp(o1); f2 = u2 && fgp(o2); f3 = u3 && fgp(o3);
     };
-    const bool f4 = ti.lz == TZ && ti.ly == TY && ti.lx == TX && ((ti.x0 | (int)(g.X & 3)) & 3) == 0;
-    if (f4) {
+    if constexpr (F4) {
         // Full, 16-B aligned tile: float4 per lane (4 rows of 64 voxels per load instruction, a
         // quarter of the load instructions of the lane = x walk).  Wave w owns rows y = 4w .. 4w+3
         // of every plane; lane l holds x = 4 (l % 16) .. + 3 of row 4w + l / 16.  The four
@@ -884,12 +903,22 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         const int64_t sz = g.Y * g.X;
         const float* pz = in + ((int64_t)ti.z0 * g.Y + ti.y0 + 4 * wave + (lane >> 4)) * g.X + ti.x0 + i4;
         const u8* mz = HAS_MASK ? mask + (pz - in) : nullptr;
+#if CC_MASK_STAGE
+        // mask bytes 16 per lane (A/B, CC_MASK_STAGE=1): per group of 4 planes lane L loads 16 B of
+        // plane z0 + L / 16, row 4w + (L / 4) % 4, x = 16 (L % 4) and stages them in the wave's
+        // 1 KB of LDS (L.key, unused until the tile CCL), where lane m finds its 4 bytes of plane a
+        // at word a * 64 + m (one 16-B load instead of four 4-B loads per lane and group)
+        const u8* mz16 = HAS_MASK ? mask + ((int64_t)ti.z0 * g.Y + ti.y0 + 4 * wave + ((lane >> 2) & 3)) * g.X + ti.x0 +
+                                        16 * (lane & 3) + (int64_t)(lane >> 4) * sz
+                                  : nullptr;
+        u32* mstage = L.key + wave * 256;
+#endif
         constexpr int RZ4 = 4;
         u32 R[8] = {0, 0, 0, 0, 0, 0, 0, 0};      // lane z: ballots (lo, hi) of values 0..3 of plane z
         auto plane_bits = [&](int z, float4 v, uchar4 mk) {
-            bool fg[4];
-            quad(v, mk, fg);
-            const u64 b0 = __ballot(fg[0]), b1 = __ballot(fg[1]), b2 = __ballot(fg[2]), b3 = __ballot(fg[3]);
+            bool f0, f1, f2, f3;
+            quad(v, mk, f0, f1, f2, f3);
+            const u64 b0 = __ballot(f0), b1 = __ballot(f1), b2 = __ballot(f2), b3 = __ballot(f3);
             CC_WRITELANE2(R[0], R[1], (u32)b0, (u32)(b0 >> 32), z);
             CC_WRITELANE2(R[2], R[3], (u32)b1, (u32)(b1 >> 32), z);
             CC_WRITELANE2(R[4], R[5], (u32)b2, (u32)(b2 >> 32), z);
@@ -899,10 +928,18 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         for (int z0 = 0; z0 < TZ; z0 += RZ4) {
             float4 v[RZ4];
             uchar4 mk[RZ4];
+#if CC_MASK_STAGE
+            if (HAS_MASK) reinterpret_cast<uint4*>(mstage)[lane] = *reinterpret_cast<const uint4*>(mz16 + z0 * sz);
+            auto ld = [&](int a) {
+                v[a] = *reinterpret_cast<const float4*>(pz + (z0 + a) * sz);
+                if (HAS_MASK) mk[a] = __builtin_bit_cast(uchar4, mstage[a * 64 + lane]);
+            };
+#else
             auto ld = [&](int a) {
                 v[a] = *reinterpret_cast<const float4*>(pz + (z0 + a) * sz);
                 if (HAS_MASK) mk[a] = *reinterpret_cast<const uchar4*>(mz + (z0 + a) * sz);
             };
+#endif
 #pragma unroll
             for (int a = 0; a < RZ4; ++a) {
                 // each load issued right before its use, one in flight per wave (an empty asm
@@ -927,6 +964,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         const u32 even = spread2(seg[0]) | (spread2(seg[2]) << 1), odd = spread2(seg[1]) | (spread2(seg[3]) << 1);
         L.rows[zz * TY + 4 * wave + qq] = ((u64)odd << 32) | even;
     } else {
+        static_assert(F4 || tbr, "partial tiles always record TB");
         for (int i = tid; i < NROWS; i += NTHREADS) L.rows[i] = 0;
         __syncthreads();
         const u64 lanes = ti.lx >= 64 ? ~0ull : ((1ull << ti.lx) - 1);
@@ -941,8 +979,8 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
     mn = wave_min(mn);
     mx = wave_max(mx);
-    if (SIDES & 1) { K1N = wave_min(K1N); K1X = wave_max(K1X); }
-    if (SIDES & 2) { K2N = wave_min(K2N); K2X = wave_max(K2X); }
+    if ((SIDES & 1) && tbr) { K1N = wave_min(K1N); K1X = wave_max(K1X); }
+    if ((SIDES & 2) && tbr) { K2N = wave_min(K2N); K2X = wave_max(K2X); }
     if (lane == 0) {
         red[0][wave] = mn; red[1][wave] = mx; red[2][wave] = K1N; red[3][wave] = K1X; red[4][wave] = K2N;
         red[5][wave] = K2X;
@@ -953,23 +991,60 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
             mn = min(mn, red[0][w]); mx = max(mx, red[1][w]);
             K1N = min(K1N, red[2][w]); K1X = max(K1X, red[3][w]); K2N = min(K2N, red[4][w]); K2X = max(K2X, red[5][w]);
         }
-        atomicMin(sa.smin + ti.block, mn);
-        atomicMax(sa.smax + ti.block, mx);
-        if (mx > 0xFF800000u || mn < 0x007FFFFFu) atomicOr(sa.sflag + ti.block, 1u);    // NaN
+        if (sa.TS) {                    // per-tile statistics, reduced per block by k_block_verify
+            sa.TS[2 * t] = mn;
+            sa.TS[2 * t + 1] = mx;
+        } else {
+            atomicMin(sa.smin + ti.block, mn);
+            atomicMax(sa.smax + ti.block, mx);
+            if (mx > 0xFF800000u || mn < 0x007FFFFFu) atomicOr(sa.sflag + ti.block, 1u);    // NaN
+        }
         // TB from the wrapped distances: A = max used o < lo, B = min used o >= lo, C = max used
         // o <= hi, D = min used o > hi (0 / ~0 when there is none)
-        u32 A = 0u, B = 0xFFFFFFFFu, C = 0u, D = 0xFFFFFFFFu;
-        if (SIDES & 1) {
-            if ((u64)K1N + lo < (1ull << 32)) B = K1N + lo;
-            if ((u64)K1X + lo >= (1ull << 32)) A = K1X + lo;
+        if (tbr) {
+            u32 A = 0u, B = 0xFFFFFFFFu, C = 0u, D = 0xFFFFFFFFu;
+            if (SIDES & 1) {
+                if ((u64)K1N + lo < (1ull << 32)) B = K1N + lo;
+                if ((u64)K1X + lo >= (1ull << 32)) A = K1X + lo;
+            }
+            if (SIDES & 2) {
+                if (K2N <= hi) C = hi - K2N;
+                if (K2X > hi) D = hi - K2X;
+            }
+            u32* tb = sa.TB + 4 * t;
+            tb[0] = A; tb[1] = B; tb[2] = C; tb[3] = D;
         }
-        if (SIDES & 2) {
-            if (K2N <= hi) C = hi - K2N;
-            if (K2X > hi) D = hi - K2X;
-        }
-        u32* tb = sa.TB + 4 * t;
-        tb[0] = A; tb[1] = B; tb[2] = C; tb[3] = D;
     }
+}
+
+// timing probe of the clock tool (tools/clock_probe.hip defines it: per-workgroup core / wall
+// clock stamps in k_spec and k_pass2); empty in the library
+#ifndef CC_KERNEL_PROBE
+#define CC_KERNEL_PROBE
+#define CC_KERNEL_PROBE_END
+#endif
+
+// SIDES: bounds of the guessed interval that can move (1 lower: 'greater', 2 upper: 'less', 3 both)
+// ABL (kernel ablation harness tools/ablate.hip only; 0 in the library): 99 stop once the bit rows
+// are in LDS (loads, ballots, statistics), else as pass1_finish's ABL
+template <bool HAS_MASK, int SIDES, int ABL = 0>
+__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_spec(
+    Geom g, SpecArgs sa, const float* __restrict__ in, const u8* __restrict__ mask, u64* BITS, face_t* FACES,
+    u32* COUNT, u32* P, u64* KEY) {
+    CC_KERNEL_PROBE
+    __shared__ Pass1LDS L;
+    __shared__ u32 red[6][NTHREADS / 64];
+    const int64_t t = sa.t0 + ((g.X & 31) ? xcd_contig(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x);
+    const TileInfo ti = tile_info(g, t);
+    const BlockParam p = uniform_bp(sa.guess[ti.block]);
+    if (p.kind != BP_INTERVAL) {                   // no guess: statistics only, k_fix labels the tile
+        stats_tile(g, ti, in, sa.smin, sa.smax, sa.sflag, red, sa.TS, t);
+        return;
+    }
+    const bool f4 = ti.lz == TZ && ti.ly == TY && ti.lx == TX && ((ti.x0 | (int)(g.X & 3)) & 3) == 0;
+    if (!f4) spec_front<HAS_MASK, SIDES, false, true>(g, sa, t, ti, in, mask, p.lo, p.hi, L, red);
+    else if (p.pad & GUESS_TB) spec_front<HAS_MASK, SIDES, true, true>(g, sa, t, ti, in, mask, p.lo, p.hi, L, red);
+    else spec_front<HAS_MASK, SIDES, true, false>(g, sa, t, ti, in, mask, p.lo, p.hi, L, red);
     if (ABL == 99) return;
     pass1_finish<ABL % 99>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, true);
     CC_KERNEL_PROBE_END
@@ -979,6 +1054,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
 __device__ __forceinline__ bool spec_valid(const BlockParam& G, BlockParam T, const u32* tb, int mode) {
     if (G.kind != BP_INTERVAL || T.kind != BP_INTERVAL) return false;
     T = widen(T, mode);
+    if (!(G.pad & GUESS_TB)) return T.lo == G.lo && T.hi == G.hi;      // no TB recorded (k_guess)
     if (T.lo != G.lo && (T.lo > G.lo ? tb[1] < T.lo : tb[0] >= T.lo)) return false;
     if (T.hi != G.hi && (T.hi < G.hi ? tb[2] > T.hi : tb[3] <= T.hi)) return false;
     return true;
@@ -1005,6 +1081,45 @@ __global__ void k_params_verify(Geom g, const BlockParam* guess, const u32* smin
                            (ti.ix == 0 || g.tblk[2][ti.ix - 1] != g.tblk[2][ti.ix]);
         if (first) bp[b] = T;
         if (!spec_valid(guess[b], T, TB + 4 * t, mode)) FIX[1 + atomicAdd(FIX, 1u)] = (u32)t;
+    }
+}
+
+// k_params_verify for per-tile statistics (SpecArgs::TS): one workgroup per block reduces its
+// tiles' (min, max) -- the NaN flag read off the extremes as in stats_tile --, derives the exact
+// parameters (bp, and the block statistics for the status), then verifies its tiles.  Replaces
+// the three device-scope atomics per tile on one word per block that k_spec issued otherwise.
+__global__ __launch_bounds__(256) void k_block_verify(Geom g, const BlockParam* guess, const u32* __restrict__ TS,
+                                                      float thr, int mode, BlockParam* bp, u32* smin, u32* smax,
+                                                      u32* sflag, const u32* TB, u32* FIX) {
+    __shared__ u32 red[2][4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int64_t b = blockIdx.x; b < g.n_blocks; b += gridDim.x) {
+        const int bx = (int)(b % g.nb[2]), by = (int)((b / g.nb[2]) % g.nb[1]), bz = (int)(b / ((int64_t)g.nb[2] * g.nb[1]));
+        const int n = g.btn[0][bz] * g.btn[1][by] * g.btn[2][bx];
+        u32 mn = 0xFFFFFFFFu, mx = 0u;
+        for (int lt = tid; lt < n; lt += 256) {
+            const int64_t t = block_tile(g, b, lt);
+            mn = min(mn, TS[2 * t]);
+            mx = max(mx, TS[2 * t + 1]);
+        }
+        mn = wave_min(mn);
+        mx = wave_max(mx);
+        if (lane == 0) { red[0][wave] = mn; red[1][wave] = mx; }
+        __syncthreads();
+        mn = min(min(red[0][0], red[0][1]), min(red[0][2], red[0][3]));
+        mx = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
+        __syncthreads();
+        const u32 nan = (mx > 0xFF800000u || mn < 0x007FFFFFu) ? 1u : 0u;
+        const BlockParam T = block_param(mn, mx, nan, thr, mode);
+        const BlockParam G = guess[b];
+        if (tid == 0) {
+            bp[b] = T;
+            smin[b] = mn; smax[b] = mx; sflag[b] = nan;
+        }
+        for (int lt = tid; lt < n; lt += 256) {
+            const int64_t t = block_tile(g, b, lt);
+            if (!spec_valid(G, T, TB + 4 * t, mode)) FIX[1 + atomicAdd(FIX, 1u)] = (u32)t;
+        }
     }
 }
 
@@ -2114,6 +2229,56 @@ __global__ __launch_bounds__(SB_THREADS) void k_block_scan(int64_t nb, const u32
         scalars[2] = carry_r;
         scalars[3] = (big[nb] ? RF_BIG : 0ull) | (carry_r > root_cap ? RF_ROOTS : 0ull);
         if (sum_out) *sum_out = carry_v;                // the slab's sum for the allgather
+    }
+}
+
+// k_block_scan and k_emit_roots in one launch for up to SCAN_EMIT_MAXB blocks (the one-read-back
+// schedule): every workgroup b reads all the blocks' root counts (8 KB at most, from L2) and forms
+// its own exclusive prefixes of the root counts and of the block values, then emits its roots as
+// k_emit_roots; workgroup 0 writes the totals and flags as k_block_scan (one launch and its ~6 us
+// of boundary fewer per volume / slab)
+constexpr int64_t SCAN_EMIT_MAXB = 2048;
+__global__ __launch_bounds__(256) void k_scan_emit(int64_t nb, const u32* __restrict__ RL, const u32* __restrict__ RCB,
+                                                   u32* ROFFB, u64* values, u64* offsets, const u8* big, u64* scalars,
+                                                   u64 root_cap, u64* sum_out, u64* KEY, u64* keys2, u32* vals2,
+                                                   u32* seg_start, u32* seg_end) {
+    __shared__ u64 red[4][4];
+    const int64_t b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    u64 s[4] = {0, 0, 0, 0};                 // prefix roots, prefix values, total roots, total values
+    for (int64_t i = tid; i < nb; i += 256) {
+        const u64 r = RCB[i], v = r ? r + 1 : 0ull;
+        if (i < b) { s[0] += r; s[1] += v; }
+        s[2] += r; s[3] += v;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s[k] += __shfl_down(s[k], o, 64);
+        if (lane == 0) red[k][wave] = s[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s[k] = red[k][0] + red[k][1] + red[k][2] + red[k][3];
+    const u32 R = RCB[b], off = (u32)s[0];
+    if (tid == 0) {
+        ROFFB[b] = off;
+        values[b] = R ? (u64)R + 1 : 0ull;
+        offsets[b] = s[1];
+        seg_start[b] = off;
+        seg_end[b] = off + R;
+        if (b == 0) {
+            scalars[0] = s[3];
+            scalars[2] = s[2];
+            scalars[3] = (big[nb] ? RF_BIG : 0ull) | (s[2] > root_cap ? RF_ROOTS : 0ull);
+            if (sum_out) *sum_out = s[3];
+        }
+    }
+    for (u32 r = tid; r < R && off + (u64)r < root_cap; r += 256) {
+        const u32 node = RL[(u64)b * SB_LCAP + r];
+        keys2[off + r] = ((u64)b << KEY_BITS) | KEY[node];
+        vals2[off + r] = node;
+        KEY[node] = s[1] + r + 1;                          // its reference id (k_assign_rid with base 0)
     }
 }
 

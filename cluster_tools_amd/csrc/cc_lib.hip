@@ -67,10 +67,14 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         // speculative front: sample -> one read for statistics + pass 1 -> exact parameters ->
         // relabel the tiles whose guessed interval was not exact (see k_spec)
         BlockParam* guess = bp + nb;
-        c->spec.ensure((4 * nt + 4 * SAMPLE_PARTS * nb + nt + 1) * sizeof(u32));
+        // per-tile statistics (CC_SPEC_TILESTATS, default on): k_spec stores each tile's (min, max),
+        // k_block_verify reduces them per block; 0: per-block atomics in k_spec, k_params_verify
+        const bool tilestats = env_int("CC_SPEC_TILESTATS", 1) != 0;
+        c->spec.ensure((4 * nt + 4 * SAMPLE_PARTS * nb + nt + 1 + 2 * nt) * sizeof(u32));
         u32* TB = c->spec.as<u32>();
         u32* SPART = TB + 4 * nt;
         u32* FIX = SPART + 4 * SAMPLE_PARTS * nb;
+        u32* TS = FIX + nt + 1;
         // seam outputs and flags (big[nb] / iovf[nt]: "any" flags of the global-stitch fallback)
         c->big.ensure(nb + 1);
         c->pairsl.ensure((size_t)nt * TPC * sizeof(u64));
@@ -101,13 +105,16 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             fc.n_clear = std::max<int64_t>({nt + 1, 2 * nb + 1, hs_n, hm_n});
         }
         launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART, fc); });
-        launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, mode, guess); });
+        // CC_SPEC_TBFREE (default 1): blocks whose sampled extremes repeat skip TB (see k_guess)
+        const int tb_free = (int)env_int("CC_SPEC_TBFREE", 1);
+        launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, mode, guess, tb_free); });
         if (const char* e = std::getenv("CC_SPEC"); e && std::string(e) == "0")     // test hook: no guesses
             HIP_OK(hipMemsetAsync(guess, 0, nb * sizeof(BlockParam), s));
         SpecArgs sa;
         sa.guess = guess;
         sa.smin = smin; sa.smax = smax; sa.sflag = sflag;
         sa.TB = TB;
+        sa.TS = tilestats ? TS : nullptr;
         auto seams = [&](hipStream_t q, int64_t t0, int64_t t1) {
             launch_on(c, q, "k_seams", [&] {
                 k_seams<0><<<(unsigned)((t1 - t0 + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, q>>>(
@@ -148,7 +155,11 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             }
         }
         launch(c, "k_params_verify", [&] {
-            k_params_verify<<<grid_stride(nt), 256, 0, s>>>(g, guess, smin, smax, sflag, thr, mode, bp, TB, FIX);
+            if (tilestats)
+                k_block_verify<<<(unsigned)std::min<int64_t>(nb, 65535), 256, 0, s>>>(g, guess, TS, thr, mode, bp, smin, smax,
+                                                                                       sflag, TB, FIX);
+            else
+                k_params_verify<<<grid_stride(nt), 256, 0, s>>>(g, guess, smin, smax, sflag, thr, mode, bp, TB, FIX);
         });
         u32* flag = c->mark.as<u32>();
         u32* list = flag + nt;
@@ -235,13 +246,20 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         // (CC_ROOT_CAP: test hook, a context's first capacity)
         if (c->root_cap == 0) c->root_cap = (uint64_t)env_int("CC_ROOT_CAP", std::max<int64_t>(1 << 16, 4 * nt));
         const uint64_t cap = c->root_cap;
-        launch(c, "k_block_scan", [&] { k_block_scan<<<1, SB_THREADS, 0, s>>>(nb, RCB, ROFFB, values, offsets, big, scalars, cap, sum_out); });
         st.nr = (int64_t)cap;
         ensure_roots((int64_t)cap);
-        launch(c, "k_emit_roots", [&] {
-            k_emit_roots<<<(unsigned)nb, 256, 0, s>>>(RL, RCB, ROFFB, KR, offsets, c->keys2.as<u64>(), c->vals2.as<u32>(),
-                                                      seg_start, seg_end, cap);
-        });
+        if (nb <= SCAN_EMIT_MAXB) {
+            launch(c, "k_scan_emit", [&] {
+                k_scan_emit<<<(unsigned)nb, 256, 0, s>>>(nb, RL, RCB, ROFFB, values, offsets, big, scalars, cap, sum_out, KR,
+                                                         c->keys2.as<u64>(), c->vals2.as<u32>(), seg_start, seg_end);
+            });
+        } else {
+            launch(c, "k_block_scan", [&] { k_block_scan<<<1, SB_THREADS, 0, s>>>(nb, RCB, ROFFB, values, offsets, big, scalars, cap, sum_out); });
+            launch(c, "k_emit_roots", [&] {
+                k_emit_roots<<<(unsigned)nb, 256, 0, s>>>(RL, RCB, ROFFB, KR, offsets, c->keys2.as<u64>(), c->vals2.as<u32>(),
+                                                          seg_start, seg_end, cap);
+            });
+        }
         st.rid0 = true;
         st.stage = 1;
         return;
@@ -885,7 +903,7 @@ int cc_threshold(cc_ctx* c, const float* in, const int64_t shape[3], const int64
             HIP_OK(hipMemsetAsync(FIX, 0, sizeof(u32), s));
             FrontClear none{};
             launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART, none); });
-            launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, md, guess); });
+            launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, md, guess, 0); });
             if (const char* e = std::getenv("CC_SPEC"); e && std::string(e) == "0")     // test hook: no guesses
                 HIP_OK(hipMemsetAsync(guess, 0, nb * sizeof(BlockParam), s));
             SpecArgs sa;
@@ -1029,3 +1047,4 @@ int cc_get_profile(cc_ctx* c, char* names, int names_cap, int64_t* counts, doubl
 }  // extern "C"
 
 #include "cc_stage_host.hip"
+#include "cc_comm.hip"

@@ -259,6 +259,28 @@ int cc_shard_dev_seam_pairs(cc_ctx* ctx, const uint32_t* upper_cubes_dev, const 
 int cc_shard_dev_finish(cc_ctx* ctx, const uint64_t* all_dev, int world, int64_t cap, const uint64_t* sums_dev,
                         uint64_t* labels_dev, cc_result* res, uint64_t* status_host);
 
+/* --- z-slab sharding with RCCL inside the library (cc_comm.hip) ----------------------------
+ * Replaces the reference's job pool for this path (cluster_tools/cluster_tasks.py:529-551: the
+ * block_components / block_faces / write jobs of a ProcessPool exchanging offsets and face
+ * assignments through files) for a plain C / ctypes caller: one process (or thread) per GPU,
+ * each owning the z-slab [z_offset, z_offset + slab_depth) of the volume (slab boundaries on
+ * block faces); the one-read-back schedule above with its three exchanges as RCCL collectives
+ * on the context's stream (the communicator's own stream when the context has none), and the
+ * host-synchronised schedule (uint64 seam planes) when a step's status asks for it.  Results are
+ * those of cc_label_volume on the whole volume (labels of this slab; res->n_labels global).
+ *   cc_comm_unique_id   the RCCL bootstrap id (128 bytes), made on one rank and handed to all
+ *   cc_comm_create      one rank's communicator (ncclCommInitRank: collective over the ranks)
+ * RCCL is opened on first use (an RCCL already in the process, e.g. torch's, is reused;
+ * CC_RCCL_PATH overrides). */
+typedef struct cc_comm cc_comm;
+int  cc_comm_unique_id(void* id_out, int64_t cap);
+int  cc_comm_create(const void* id, int world, int rank, int device, cc_comm** out);
+void cc_comm_destroy(cc_comm* comm);
+int  cc_label_volume_sharded(cc_ctx* ctx, cc_comm* comm, const float* slab_dev, const uint8_t* mask_dev,
+                             const int64_t global_shape[3], int64_t z_offset, int64_t slab_depth,
+                             const int64_t block_shape[3], double threshold, int mode,
+                             uint64_t* labels_dev, cc_result* res);
+
 /* --- synthetic benchmark input (oracle/synth.py is its restatement) ---
  * dither = 0: q / 256 (quantized); dither = 1: (q * 2^16 + 16-bit hash dither) / 2^24, the
  * continuous variant (block extremes and threshold crossings no longer on a 2^-8 grid). */

@@ -138,6 +138,22 @@ def test_synthetic_vs_oracle(ctx, shape, bs, mode):
     _check_against_oracle(ctx, inp, bs, 0.5, mode)
 
 
+@pytest.mark.parametrize('tilestats,tbfree', [('0', '0'), ('1', '0'), ('0', '1'), ('1', '1')])
+@pytest.mark.parametrize('shape,bs,mode', SYNTH[:3])
+def test_front_variants_vs_oracle(ctx, monkeypatch, shape, bs, mode, tilestats, tbfree):
+    """The front's statistics variants: per-block atomics in k_spec + k_params_verify, or per-tile
+    statistics + k_block_verify (CC_SPEC_TILESTATS); TB recorded for every block, or TB-free for
+    blocks whose sampled extremes repeat (CC_SPEC_TBFREE) -- on quantized, continuous and
+    outlier-carrying inputs, bit-exact with the oracle."""
+    monkeypatch.setenv('CC_SPEC_TILESTATS', tilestats)
+    monkeypatch.setenv('CC_SPEC_TBFREE', tbfree)
+    inp = O.boundary_map(shape, origin=(7, 3, 1))
+    _check_against_oracle(ctx, inp, bs, 0.5, mode)
+    _check_against_oracle(ctx, O.boundary_map(shape, origin=(7, 3, 1), dither=True), bs, 0.41, mode)
+    inp[shape[0] // 2 + 1, 3, 5] = -0.5                  # an extreme off the sampled rows
+    _check_against_oracle(ctx, inp, bs, 0.5, mode)
+
+
 @pytest.mark.parametrize('shape,bs,mode', SYNTH[:4])
 def test_continuous_synthetic_vs_oracle(ctx, shape, bs, mode):
     """Continuous (dithered) input: the speculated intervals miss the exact ones."""
@@ -168,12 +184,17 @@ def test_max_runs_per_tile(ctx):
     _check_against_oracle(ctx, inp, (48, 96, 192), 0.5, 'less')
 
 
+@pytest.mark.parametrize('tbfree', ['0', '1'])
 @pytest.mark.parametrize('outlier', [-1.0, -1.0 / 32, 3.0, 1.0 + 1.0 / 64])
 @pytest.mark.parametrize('mode,thr', [('greater', 0.5), ('less', 0.5), ('equal', 0.5), ('greater', 0.3)])
-def test_speculated_interval_corrected(ctx, mode, thr, outlier):
+def test_speculated_interval_corrected(ctx, monkeypatch, mode, thr, outlier, tbfree):
     """Quantized data whose block extremes the sample misses (one outlier voxel off the sampled
-    rows): the guessed interval is wrong; tiles with voxels between the guessed and the exact
-    bounds must be relabelled (large outliers), the others kept (small outliers)."""
+    rows): the guessed interval is wrong.  With TB recorded (CC_SPEC_TBFREE=0) tiles with voxels
+    between the guessed and the exact bounds must be relabelled (large outliers), the others kept
+    (small outliers); TB-free (the default for blocks whose sampled extremes repeat, as here) the
+    guess is checked by equality and every tile of a block whose extremes the sample missed is
+    relabelled.  Same labels either way."""
+    monkeypatch.setenv('CC_SPEC_TBFREE', tbfree)
     rng = np.random.default_rng(3)
     inp = (rng.integers(0, 17, (64, 128, 192)) / np.float32(16)).astype(np.float32)
     inp[1, 1, 5] = outlier               # block (0, 0, 0); sample rows are z = 8 mod 16, y = 16 mod 32
@@ -183,7 +204,10 @@ def test_speculated_interval_corrected(ctx, mode, thr, outlier):
         if mode != 'equal' and outlier in (-1.0, 3.0):
             assert res['n_relabelled_tiles'] > 0        # the guess moved past quantization levels
         if (mode, thr, outlier) == ('greater', 0.3, -1.0 / 32):
-            assert res['n_relabelled_tiles'] == 0       # guess != exact, but no voxel in between
+            if tbfree == '0':
+                assert res['n_relabelled_tiles'] == 0   # guess != exact, but no voxel in between
+            else:
+                assert res['n_relabelled_tiles'] > 0    # guess != exact: the blocks are relabelled
     mask = (rng.random(inp.shape) < 0.9).astype(np.uint8)
     _check_against_oracle(ctx, inp, (32, 64, 96), thr, mode, mask)
 
@@ -449,7 +473,7 @@ def test_both_schedules_vs_oracle(ctx, monkeypatch, fast, shape, bs, mode):
 
 def test_root_capacity_redo(monkeypatch):
     """More block-local roots than a context's root arrays hold (CC_ROOT_CAP: the first capacity):
-    the one read-back carries RF_ROOTS, the run is redone host-synchronised (k_block_scan twice)
+    the one read-back carries RF_ROOTS, the run is redone host-synchronised (two block scans)
     with the oracle's result, and the capacity is raised so the next run needs one pass."""
     from cluster_tools_amd import _lib
     monkeypatch.setenv('CC_ROOT_CAP', '8')
@@ -460,4 +484,5 @@ def test_root_capacity_redo(monkeypatch):
         for passes in (2, 1):
             c.reset_profile()
             _check_against_oracle(c, x, bs, 0.5, 'less')
-            assert c.profile()['k_block_scan']['count'] == passes
+            prof = c.profile()         # the one-read-back pass scans in k_scan_emit, the redo in k_block_scan
+            assert sum(prof.get(k, {}).get('count', 0) for k in ('k_block_scan', 'k_scan_emit')) == passes

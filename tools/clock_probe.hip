@@ -150,11 +150,22 @@ int main(int argc, char** argv) {
         HIP_OK(hipStreamSynchronize(s));
         std::vector<BlockParam> hb(nb);
         HIP_OK(hipMemcpy(hb.data(), bp, nb * sizeof(BlockParam), hipMemcpyDeviceToHost));
-        for (auto& q : hb)
+        for (auto& q : hb) {
             if (q.kind == BP_INTERVAL) q.hi = 0xFFFFFFFFu;
+            q.pad = GUESS_TB;
+        }
         HIP_OK(hipMemcpy(guess, hb.data(), nb * sizeof(BlockParam), hipMemcpyHostToDevice));
+        BlockParam* guess_free;
+        HIP_OK(hipMalloc(&guess_free, nb * sizeof(BlockParam)));
+        for (auto& q : hb) q.pad = 0;
+        HIP_OK(hipMemcpy(guess_free, hb.data(), nb * sizeof(BlockParam), hipMemcpyHostToDevice));
+        u32* TSd;
+        HIP_OK(hipMalloc(&TSd, nt * 8));
         SpecArgs sa;
         sa.guess = guess; sa.smin = fst; sa.smax = fst + nb; sa.sflag = fst + 2 * nb; sa.TB = TB; sa.t0 = 0;
+        SpecArgs sf = sa;
+        sf.guess = guess_free;
+        sf.TS = TSd;
 
         hipEvent_t e0, e1;
         HIP_OK(hipEventCreate(&e0));
@@ -180,6 +191,9 @@ int main(int argc, char** argv) {
             HIP_OK(hipMemsetAsync(fst, 0xFF, nb * 4, s));
             HIP_OK(hipMemsetAsync(fst + nb, 0, 2 * nb * 4, s));
             k_spec<false, 1><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS, FACES, COUNT, P, KEY);
+        });
+        run("k_spec_tbfree_tilestats", nt, [&] {
+            k_spec<false, 1><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sf, in, nullptr, BITS, FACES, COUNT, P, KEY);
         });
         run("k_pass2", nt, [&] {
             k_pass2<false><<<(unsigned)nt, NTHREADS, 0, s>>>(g, BITS, COUNT, FIN, nullptr, nullptr, 0, 0, out, 0, nullptr, nullptr);
