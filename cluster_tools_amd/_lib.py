@@ -137,7 +137,12 @@ def load():
         'cc_normalize_channels': (I, [P, P, i64, P, P, I, P]),
     }
     for name, (res, args) in sig.items():
-        fn = getattr(L, name)
+        try:
+            fn = getattr(L, name)
+        except AttributeError:
+            if os.environ.get('CC_LIB_PATH'):   # an older build for same-box A/B timing: newer entries absent
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     _lib = L

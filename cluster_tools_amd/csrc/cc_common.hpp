@@ -59,7 +59,7 @@ __device__ __forceinline__ BlockParam uniform_bp(const BlockParam& q) {
     p.lo = __builtin_amdgcn_readfirstlane(q.lo);
     p.hi = __builtin_amdgcn_readfirstlane(q.hi);
     p.kind = __builtin_amdgcn_readfirstlane(q.kind);
-    p.pad = __builtin_amdgcn_readfirstlane(q.pad);      // flags of a guess (k_guess), else 0
+    p.pad = 0;
     return p;
 }
 

@@ -555,10 +555,12 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
     TileCCL& T = L.T;
     u32* key = L.key;
     const int tid = cc_tid();
-    if (write)
+    // (ABL 20 / 21 / 22: the whole pass without the BITS / FACES / both stores -- the store-volume
+    // ablation of tools/ablate.hip)
+    if (write && ABL != 20 && ABL != 22)
         for (int i = tid; i < NROWS; i += NTHREADS) BITS[t * NROWS + i] = rows[i];
     if (ABL == 1) return;
-    if (ABL >= 10) { tile_ccl<ABL - 10>(rows, T, key, key); return; }
+    if constexpr (ABL >= 10 && ABL < 20) { tile_ccl<ABL - 10>(rows, T, key, key); return; }
     const u32 R = tile_ccl(rows, T, key, key);      // key[k] = first voxel of component k
     if (ABL == 2) { if (tid == 0) COUNT[t] = R; return; }
     if (tid == 0 && write) COUNT[t] = R;
@@ -579,6 +581,10 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
     if (fchg) {
         const bool diff = FW[tid] != w0 || (two && FW[NTHREADS + tid] != w1);
         if (__syncthreads_or(diff) && tid == 0) fchg[t] = 1;
+    }
+    if (ABL == 21 || ABL == 22) {          // ablation: faces computed, not stored
+        if (__syncthreads_or(w0 == 0x12345678u && w1 == 0x9ABCDEF0u) && tid == 0) COUNT[t] = R + 1;
+        return;
     }
     FW[tid] = w0;
     if (two) FW[NTHREADS + tid] = w1;
@@ -741,12 +747,8 @@ __global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __rest
                 for (int u = 0; u < SAMPLE_U; ++u) f(f2ord(__float_as_uint(v[u])));
             }
     };
-    // extremes and how often each occurs in the sample (k_guess: quantized data repeats its
-    // extremes, continuous data does not)
-    u32 mn = 0xFFFFFFFFu, mx = 0u, cmn = 0u, cmx = 0u;
+    u32 mn = 0xFFFFFFFFu, mx = 0u;
     auto f = [&](u32 o) {
-        cmn = o < mn ? 1u : cmn + (o == mn ? 1u : 0u);
-        cmx = o > mx ? 1u : cmx + (o == mx ? 1u : 0u);
         mn = min(mn, o);
         mx = max(mx, o);
     };
@@ -774,45 +776,24 @@ __global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __rest
     } else {
         sweep(f);
     }
-    const u32 tmn = mn, tmx = mx;
     mn = block_minmax<false>(mn, red);
     mx = block_minmax<true>(mx, red);
-    // (a thread's count of a value repeated by the clamped row index is counted again: harmless,
-    // the count only steers the choice of k_spec's statistics, never a result)
-    u32 nmn = 0, nmx = 0;
-    block_excl_scan(tmn == mn ? cmn : 0u, red, &nmn);
-    block_excl_scan(tmx == mx ? cmx : 0u, red, &nmx);
     if (tid == 0) {
         u32* q = part + 4 * blockIdx.x;
-        q[0] = mn; q[1] = nmn; q[2] = mx; q[3] = nmx;
+        q[0] = mn; q[1] = 0; q[2] = mx; q[3] = 0;
     }
 }
 
-// guess.pad (GUESS_TB): 1 = k_spec records each tile's TB (the nearest values around the guessed
-// bounds) and k_params_verify keeps every tile whose bits the exact interval would not change;
-// 0 = the sampled extremes each occurred at least twice (quantized data: the block's extremes
-// are almost surely in the sample), k_spec skips TB (a quarter of its load-loop VALU) and the
-// guess holds only if it equals the exact parameters (else every tile of the block goes to
-// k_fix).  Results never depend on the choice; the k_fix work does.
-constexpr u32 GUESS_TB = 1;
-
-__global__ void k_guess(int64_t nb, const u32* part, float thr, int mode, BlockParam* guess, int tb_free) {
+__global__ void k_guess(int64_t nb, const u32* part, float thr, int mode, BlockParam* guess) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     const u32* q = part + 4 * SAMPLE_PARTS * b;
     u32 mn = 0xFFFFFFFFu, mx = 0u;
     for (int p = 0; p < SAMPLE_PARTS; ++p) { mn = min(mn, q[4 * p]); mx = max(mx, q[4 * p + 2]); }
-    u32 nmn = 0, nmx = 0;
-    for (int p = 0; p < SAMPLE_PARTS; ++p) {
-        nmn += q[4 * p] == mn ? q[4 * p + 1] : 0u;
-        nmx += q[4 * p + 2] == mx ? q[4 * p + 3] : 0u;
-    }
     const bool nan = mx > 0xFF800000u || mn < 0x007FFFFFu;
     // On continuous data the sampled extremes are not the block's, so the guessed bound misses
     // the exact one by a little: only tiles holding a voxel between the two are relabelled.
-    BlockParam p = widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
-    p.pad = (tb_free && nmn >= 2 && nmx >= 2) ? 0u : GUESS_TB;
-    guess[b] = p;
+    guess[b] = widen(block_param(mn, mx, nan ? 1u : 0u, thr, mode), mode);
 }
 
 struct SpecArgs {
@@ -820,8 +801,6 @@ struct SpecArgs {
     u32* smin; u32* smax; u32* sflag;
     u32* TB;                  // 4 per tile (see above)
     int64_t t0;               // first tile of this launch (the front runs in z-layer chunks)
-    u32* TS = nullptr;        // k_spec: per-tile (ordered min, max) for k_block_verify instead of
-                              // the per-block atomics (nullptr: atomics, as k_thr_spec)
 };
 
 // workgroup b of n -> tile: the (b / 8)-th of the contiguous range of XCD b % 8 (workgroups are
@@ -835,22 +814,17 @@ __device__ __forceinline__ int64_t xcd_contig(int64_t b, int64_t n) {
     return k * q + (k < r ? k : r) + i;
 }
 
+// mask bytes 16 per lane through LDS (default; CC_MASK_STAGE=0: 4-B mask loads per plane, A/B
+// only): C4 k_spec<true> 4.90-4.95 -> 4.72-4.76 ms on a slow box (profiles/r05_ab_mstage.txt)
 #ifndef CC_MASK_STAGE
-#define CC_MASK_STAGE 0
+#define CC_MASK_STAGE 1
 #endif
 
-// The front of k_spec for tile t: the tile's voxels in one read -> exact statistics (red, then
-// the block's atomics or the per-tile TS words), the bit rows under the guessed interval
-// [lo, hi] into L.rows, and (TBR) the tile's TB words.  TBR: this tile records TB, the nearest
-// values around the guessed bounds -- not when k_guess found the sampled extremes repeated
-// (GUESS_TB clear: the guess must equal the exact parameters, spec_valid); k_spec branches once,
-// uniformly, between the two instantiations.
-// F4: the tile is full and 16-B aligned (float4 loads); partial tiles (F4 = false, rare: block
-// and volume ends) always record TB -- harmless for a TB-free block, whose guess is checked by
-// equality -- so only the float4 path has two instantiations (one of each path per kernel: three
-// copies of the whole front left the compiler a private frame it never used).
-template <bool HAS_MASK, int SIDES, bool F4, bool tbr>
-__device__ __forceinline__ void spec_front(Geom g, SpecArgs sa, int64_t t, TileInfo ti,
+// The front of k_spec for tile t: the tile's voxels in one read -> exact statistics (the
+// block's atomics), the bit rows under the guessed interval [lo, hi] into L.rows, the tile's TB
+// words.
+template <bool HAS_MASK, int SIDES>
+__device__ __forceinline__ void spec_front(const Geom& g, const SpecArgs& sa, int64_t t, const TileInfo& ti,
                                            const float* __restrict__ in, const u8* __restrict__ mask, u32 lo,
                                            u32 hi, Pass1LDS& L, u32 (*red)[NTHREADS / 64]) {
     const int tid = cc_tid(), lane = tid & 63, wave = wave_id();
@@ -870,30 +844,37 @@ __device__ __forceinline__ void spec_front(Geom g, SpecArgs sa, int64_t t, TileI
         const u32 o = f2ord(__float_as_uint(x));
         mn = min(mn, o);
         mx = max(mx, o);
-        if ((SIDES & 1) && tbr) { const u32 k = o - lo; K1N = min(K1N, k); K1X = max(K1X, k); }
-        if ((SIDES & 2) && tbr) { const u32 k = hi - o; K2N = min(K2N, k); K2X = max(K2X, k); }
+        if (SIDES & 1) { const u32 k = o - lo; K1N = min(K1N, k); K1X = max(K1X, k); }
+        if (SIDES & 2) { const u32 k = hi - o; K2N = min(K2N, k); K2X = max(K2X, k); }
         return (!HAS_MASK || mk != 0) && fgp(o);
     };
     // four voxels of one float4 (full tiles): the same, min / max folded three operands at a time
-    auto quad = [&](float4 v, uchar4 mk, bool& f0, bool& f1, bool& f2, bool& f3) {
+    // (returns the four ballots: the interval test and the mask test ballot separately and are
+    // ANDed as lane masks -- a ballot of their combined bool went through a VGPR select and a
+    // compare per value, 8 VALU per plane with a mask)
+    auto quad = [&](float4 v, uchar4 mk, u64& b0, u64& b1, u64& b2, u64& b3) {
         const u32 o0 = f2ord(__float_as_uint(v.x)), o1 = f2ord(__float_as_uint(v.y));
         const u32 o2 = f2ord(__float_as_uint(v.z)), o3 = f2ord(__float_as_uint(v.w));
         mn = min(min(min(min(mn, o0), o1), o2), o3);
         mx = max(max(max(max(mx, o0), o1), o2), o3);
-        if ((SIDES & 1) && tbr) {
+        if (SIDES & 1) {
             const u32 k0 = o0 - lo, k1 = o1 - lo, k2 = o2 - lo, k3 = o3 - lo;
             K1N = min(min(min(min(K1N, k0), k1), k2), k3);
             K1X = max(max(max(max(K1X, k0), k1), k2), k3);
         }
-        if ((SIDES & 2) && tbr) {
+        if (SIDES & 2) {
             const u32 k0 = hi - o0, k1 = hi - o1, k2 = hi - o2, k3 = hi - o3;
             K2N = min(min(min(min(K2N, k0), k1), k2), k3);
             K2X = max(max(max(max(K2X, k0), k1), k2), k3);
         }
-        const bool u0 = !HAS_MASK || mk.x, u1 = !HAS_MASK || mk.y, u2 = !HAS_MASK || mk.z, u3 = !HAS_MASK || mk.w;
-        f0 = u0 && fgp(o0); f1 = u1 && fgp(o1); f2 = u2 && fgp(o2); f3 = u3 && fgp(o3);
+        b0 = __ballot(fgp(o0)); b1 = __ballot(fgp(o1)); b2 = __ballot(fgp(o2)); b3 = __ballot(fgp(o3));
+        if (HAS_MASK) {
+            b0 &= __ballot(mk.x != 0); b1 &= __ballot(mk.y != 0);
+            b2 &= __ballot(mk.z != 0); b3 &= __ballot(mk.w != 0);
+        }
     };
-    if constexpr (F4) {
+    const bool f4 = ti.lz == TZ && ti.ly == TY && ti.lx == TX && ((ti.x0 | (int)(g.X & 3)) & 3) == 0;
+    if (f4) {
         // Full, 16-B aligned tile: float4 per lane (4 rows of 64 voxels per load instruction, a
         // quarter of the load instructions of the lane = x walk).  Wave w owns rows y = 4w .. 4w+3
         // of every plane; lane l holds x = 4 (l % 16) .. + 3 of row 4w + l / 16.  The four
@@ -902,9 +883,10 @@ __device__ __forceinline__ void spec_front(Geom g, SpecArgs sa, int64_t t, TileI
         const int i4 = 4 * (lane & 15);
         const int64_t sz = g.Y * g.X;
         const float* pz = in + ((int64_t)ti.z0 * g.Y + ti.y0 + 4 * wave + (lane >> 4)) * g.X + ti.x0 + i4;
+#if !CC_MASK_STAGE
         const u8* mz = HAS_MASK ? mask + (pz - in) : nullptr;
-#if CC_MASK_STAGE
-        // mask bytes 16 per lane (A/B, CC_MASK_STAGE=1): per group of 4 planes lane L loads 16 B of
+#else
+        // mask bytes 16 per lane: per group of 4 planes lane L loads 16 B of
         // plane z0 + L / 16, row 4w + (L / 4) % 4, x = 16 (L % 4) and stages them in the wave's
         // 1 KB of LDS (L.key, unused until the tile CCL), where lane m finds its 4 bytes of plane a
         // at word a * 64 + m (one 16-B load instead of four 4-B loads per lane and group)
@@ -916,9 +898,8 @@ __device__ __forceinline__ void spec_front(Geom g, SpecArgs sa, int64_t t, TileI
         constexpr int RZ4 = 4;
         u32 R[8] = {0, 0, 0, 0, 0, 0, 0, 0};      // lane z: ballots (lo, hi) of values 0..3 of plane z
         auto plane_bits = [&](int z, float4 v, uchar4 mk) {
-            bool f0, f1, f2, f3;
-            quad(v, mk, f0, f1, f2, f3);
-            const u64 b0 = __ballot(f0), b1 = __ballot(f1), b2 = __ballot(f2), b3 = __ballot(f3);
+            u64 b0, b1, b2, b3;
+            quad(v, mk, b0, b1, b2, b3);
             CC_WRITELANE2(R[0], R[1], (u32)b0, (u32)(b0 >> 32), z);
             CC_WRITELANE2(R[2], R[3], (u32)b1, (u32)(b1 >> 32), z);
             CC_WRITELANE2(R[4], R[5], (u32)b2, (u32)(b2 >> 32), z);
@@ -964,7 +945,6 @@ __device__ __forceinline__ void spec_front(Geom g, SpecArgs sa, int64_t t, TileI
         const u32 even = spread2(seg[0]) | (spread2(seg[2]) << 1), odd = spread2(seg[1]) | (spread2(seg[3]) << 1);
         L.rows[zz * TY + 4 * wave + qq] = ((u64)odd << 32) | even;
     } else {
-        static_assert(F4 || tbr, "partial tiles always record TB");
         for (int i = tid; i < NROWS; i += NTHREADS) L.rows[i] = 0;
         __syncthreads();
         const u64 lanes = ti.lx >= 64 ? ~0ull : ((1ull << ti.lx) - 1);
@@ -979,8 +959,8 @@ __device__ __forceinline__ void spec_front(Geom g, SpecArgs sa, int64_t t, TileI
     }
     mn = wave_min(mn);
     mx = wave_max(mx);
-    if ((SIDES & 1) && tbr) { K1N = wave_min(K1N); K1X = wave_max(K1X); }
-    if ((SIDES & 2) && tbr) { K2N = wave_min(K2N); K2X = wave_max(K2X); }
+    if (SIDES & 1) { K1N = wave_min(K1N); K1X = wave_max(K1X); }
+    if (SIDES & 2) { K2N = wave_min(K2N); K2X = wave_max(K2X); }
     if (lane == 0) {
         red[0][wave] = mn; red[1][wave] = mx; red[2][wave] = K1N; red[3][wave] = K1X; red[4][wave] = K2N;
         red[5][wave] = K2X;
@@ -991,17 +971,12 @@ __device__ __forceinline__ void spec_front(Geom g, SpecArgs sa, int64_t t, TileI
             mn = min(mn, red[0][w]); mx = max(mx, red[1][w]);
             K1N = min(K1N, red[2][w]); K1X = max(K1X, red[3][w]); K2N = min(K2N, red[4][w]); K2X = max(K2X, red[5][w]);
         }
-        if (sa.TS) {                    // per-tile statistics, reduced per block by k_block_verify
-            sa.TS[2 * t] = mn;
-            sa.TS[2 * t + 1] = mx;
-        } else {
-            atomicMin(sa.smin + ti.block, mn);
-            atomicMax(sa.smax + ti.block, mx);
-            if (mx > 0xFF800000u || mn < 0x007FFFFFu) atomicOr(sa.sflag + ti.block, 1u);    // NaN
-        }
+        atomicMin(sa.smin + ti.block, mn);
+        atomicMax(sa.smax + ti.block, mx);
+        if (mx > 0xFF800000u || mn < 0x007FFFFFu) atomicOr(sa.sflag + ti.block, 1u);    // NaN
         // TB from the wrapped distances: A = max used o < lo, B = min used o >= lo, C = max used
         // o <= hi, D = min used o > hi (0 / ~0 when there is none)
-        if (tbr) {
+        {
             u32 A = 0u, B = 0xFFFFFFFFu, C = 0u, D = 0xFFFFFFFFu;
             if (SIDES & 1) {
                 if ((u64)K1N + lo < (1ull << 32)) B = K1N + lo;
@@ -1038,13 +1013,10 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     const TileInfo ti = tile_info(g, t);
     const BlockParam p = uniform_bp(sa.guess[ti.block]);
     if (p.kind != BP_INTERVAL) {                   // no guess: statistics only, k_fix labels the tile
-        stats_tile(g, ti, in, sa.smin, sa.smax, sa.sflag, red, sa.TS, t);
+        stats_tile(g, ti, in, sa.smin, sa.smax, sa.sflag, red);
         return;
     }
-    const bool f4 = ti.lz == TZ && ti.ly == TY && ti.lx == TX && ((ti.x0 | (int)(g.X & 3)) & 3) == 0;
-    if (!f4) spec_front<HAS_MASK, SIDES, false, true>(g, sa, t, ti, in, mask, p.lo, p.hi, L, red);
-    else if (p.pad & GUESS_TB) spec_front<HAS_MASK, SIDES, true, true>(g, sa, t, ti, in, mask, p.lo, p.hi, L, red);
-    else spec_front<HAS_MASK, SIDES, true, false>(g, sa, t, ti, in, mask, p.lo, p.hi, L, red);
+    spec_front<HAS_MASK, SIDES>(g, sa, t, ti, in, mask, p.lo, p.hi, L, red);
     if (ABL == 99) return;
     pass1_finish<ABL % 99>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, true);
     CC_KERNEL_PROBE_END
@@ -1054,7 +1026,6 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
 __device__ __forceinline__ bool spec_valid(const BlockParam& G, BlockParam T, const u32* tb, int mode) {
     if (G.kind != BP_INTERVAL || T.kind != BP_INTERVAL) return false;
     T = widen(T, mode);
-    if (!(G.pad & GUESS_TB)) return T.lo == G.lo && T.hi == G.hi;      // no TB recorded (k_guess)
     if (T.lo != G.lo && (T.lo > G.lo ? tb[1] < T.lo : tb[0] >= T.lo)) return false;
     if (T.hi != G.hi && (T.hi < G.hi ? tb[2] > T.hi : tb[3] <= T.hi)) return false;
     return true;
@@ -1084,45 +1055,6 @@ __global__ void k_params_verify(Geom g, const BlockParam* guess, const u32* smin
     }
 }
 
-// k_params_verify for per-tile statistics (SpecArgs::TS): one workgroup per block reduces its
-// tiles' (min, max) -- the NaN flag read off the extremes as in stats_tile --, derives the exact
-// parameters (bp, and the block statistics for the status), then verifies its tiles.  Replaces
-// the three device-scope atomics per tile on one word per block that k_spec issued otherwise.
-__global__ __launch_bounds__(256) void k_block_verify(Geom g, const BlockParam* guess, const u32* __restrict__ TS,
-                                                      float thr, int mode, BlockParam* bp, u32* smin, u32* smax,
-                                                      u32* sflag, const u32* TB, u32* FIX) {
-    __shared__ u32 red[2][4];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int64_t b = blockIdx.x; b < g.n_blocks; b += gridDim.x) {
-        const int bx = (int)(b % g.nb[2]), by = (int)((b / g.nb[2]) % g.nb[1]), bz = (int)(b / ((int64_t)g.nb[2] * g.nb[1]));
-        const int n = g.btn[0][bz] * g.btn[1][by] * g.btn[2][bx];
-        u32 mn = 0xFFFFFFFFu, mx = 0u;
-        for (int lt = tid; lt < n; lt += 256) {
-            const int64_t t = block_tile(g, b, lt);
-            mn = min(mn, TS[2 * t]);
-            mx = max(mx, TS[2 * t + 1]);
-        }
-        mn = wave_min(mn);
-        mx = wave_max(mx);
-        if (lane == 0) { red[0][wave] = mn; red[1][wave] = mx; }
-        __syncthreads();
-        mn = min(min(red[0][0], red[0][1]), min(red[0][2], red[0][3]));
-        mx = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
-        __syncthreads();
-        const u32 nan = (mx > 0xFF800000u || mn < 0x007FFFFFu) ? 1u : 0u;
-        const BlockParam T = block_param(mn, mx, nan, thr, mode);
-        const BlockParam G = guess[b];
-        if (tid == 0) {
-            bp[b] = T;
-            smin[b] = mn; smax[b] = mx; sflag[b] = nan;
-        }
-        for (int lt = tid; lt < n; lt += 256) {
-            const int64_t t = block_tile(g, b, lt);
-            if (!spec_valid(G, T, TB + 4 * t, mode)) FIX[1 + atomicAdd(FIX, 1u)] = (u32)t;
-        }
-    }
-}
-
 // the 14 tiles whose seams read the faces of tile f (f itself and the 13 that have it as a
 // lex-negative neighbour): d = 0 .. 13, each marked once (flag) and listed in LIST[1 .. LIST[0]]
 __device__ __forceinline__ void mark_seam(const Geom& g, u32 f, u32 d, u32* flag, u32* LIST) {
@@ -1146,7 +1078,8 @@ __device__ __forceinline__ void mark_seam(const Geom& g, u32 f, u32 d, u32* flag
 // from this run and are always flagged.  The grid walks the list: the one-read-back schedule
 // launches a fixed grid without reading the count (with nothing to fix every workgroup reads one
 // word and leaves), the host-synchronised one a workgroup per listed tile.  fchg, flag and
-// LIST[0] are cleared before (the front clear in k_sample / memsets).
+// LIST[0] are cleared before (the front clear in k_sample / memsets).  fchg = flag = nullptr: no
+// seams to mark (the one-read-back schedule runs k_seams after k_fix).
 // (no waves-per-EU bound: under the 64-VGPR bound of k_fix the loop spilled; this kernel sees
 // ~1 % of the tiles on continuous input and none on quantized input)
 template <bool HAS_MASK>
@@ -1162,11 +1095,11 @@ __global__ __launch_bounds__(NTHREADS) void k_fix_dev(
         const TileInfo ti = uniform_ti(tile_info(g, t));
         const BlockParam p = uniform_bp(bp[ti.block]);
         const bool fresh = __builtin_amdgcn_readfirstlane(guess[ti.block].kind) == BP_INTERVAL;
-        if (!fresh && cc_tid() == 0) fchg[t] = 1;
+        if (fchg && !fresh && cc_tid() == 0) fchg[t] = 1;
         pass1_tile<HAS_MASK>(g, t, ti, p, in, mask, thr, mode, BITS, FACES, COUNT, P, KEY, L, true,
                              fresh ? fchg : nullptr);
         __syncthreads();                              // fchg[t] (thread 0) visible to the workgroup
-        if (cc_tid() < 14 && fchg[t]) mark_seam(g, (u32)t, (u32)cc_tid(), flag, LIST);
+        if (flag && cc_tid() < 14 && fchg[t]) mark_seam(g, (u32)t, (u32)cc_tid(), flag, LIST);
         __syncthreads();                              // L is reused by the next tile
     }
 }

@@ -67,14 +67,10 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         // speculative front: sample -> one read for statistics + pass 1 -> exact parameters ->
         // relabel the tiles whose guessed interval was not exact (see k_spec)
         BlockParam* guess = bp + nb;
-        // per-tile statistics (CC_SPEC_TILESTATS, default on): k_spec stores each tile's (min, max),
-        // k_block_verify reduces them per block; 0: per-block atomics in k_spec, k_params_verify
-        const bool tilestats = env_int("CC_SPEC_TILESTATS", 1) != 0;
-        c->spec.ensure((4 * nt + 4 * SAMPLE_PARTS * nb + nt + 1 + 2 * nt) * sizeof(u32));
+        c->spec.ensure((4 * nt + 4 * SAMPLE_PARTS * nb + nt + 1) * sizeof(u32));
         u32* TB = c->spec.as<u32>();
         u32* SPART = TB + 4 * nt;
         u32* FIX = SPART + 4 * SAMPLE_PARTS * nb;
-        u32* TS = FIX + nt + 1;
         // seam outputs and flags (big[nb] / iovf[nt]: "any" flags of the global-stitch fallback)
         c->big.ensure(nb + 1);
         c->pairsl.ensure((size_t)nt * TPC * sizeof(u64));
@@ -105,16 +101,13 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             fc.n_clear = std::max<int64_t>({nt + 1, 2 * nb + 1, hs_n, hm_n});
         }
         launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART, fc); });
-        // CC_SPEC_TBFREE (default 1): blocks whose sampled extremes repeat skip TB (see k_guess)
-        const int tb_free = (int)env_int("CC_SPEC_TBFREE", 1);
-        launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, mode, guess, tb_free); });
+        launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, mode, guess); });
         if (const char* e = std::getenv("CC_SPEC"); e && std::string(e) == "0")     // test hook: no guesses
             HIP_OK(hipMemsetAsync(guess, 0, nb * sizeof(BlockParam), s));
         SpecArgs sa;
         sa.guess = guess;
         sa.smin = smin; sa.smax = smax; sa.sflag = sflag;
         sa.TB = TB;
-        sa.TS = tilestats ? TS : nullptr;
         auto seams = [&](hipStream_t q, int64_t t0, int64_t t1) {
             launch_on(c, q, "k_seams", [&] {
                 k_seams<0><<<(unsigned)((t1 - t0 + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, q>>>(
@@ -130,6 +123,9 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         const int64_t n_chunks = lds_seams ? std::min<int64_t>(g.nt[0], c->front_chunks) : 1;
         // one chunk (the default): the seams follow on the same stream, no side stream needed
         const hipStream_t ss = n_chunks > 1 ? side_stream(c) : s;
+        // the one-read-back schedule with one chunk runs the seams once, after k_fix (whose
+        // relabelled tiles then need no second seam pass: k_seams_list and its launch are gone)
+        const bool seams_after_fix = fast && n_chunks == 1 && lds_seams;
         if (lds_seams && ss != s) stream_wait(c, s, ss);
         for (int64_t ci = 0; ci < n_chunks; ++ci) {
             const int64_t t0 = g.nt[0] * ci / n_chunks * layer, t1 = g.nt[0] * (ci + 1) / n_chunks * layer;
@@ -149,31 +145,32 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
                 }
 #undef CC_SPEC_LAUNCH
             });
-            if (lds_seams) {
+            if (lds_seams && !seams_after_fix) {
                 if (ss != s) stream_wait(c, s, ss);
                 seams(ss, t0, t1);
             }
         }
         launch(c, "k_params_verify", [&] {
-            if (tilestats)
-                k_block_verify<<<(unsigned)std::min<int64_t>(nb, 65535), 256, 0, s>>>(g, guess, TS, thr, mode, bp, smin, smax,
-                                                                                       sflag, TB, FIX);
-            else
-                k_params_verify<<<grid_stride(nt), 256, 0, s>>>(g, guess, smin, smax, sflag, thr, mode, bp, TB, FIX);
+            k_params_verify<<<grid_stride(nt), 256, 0, s>>>(g, guess, smin, smax, sflag, thr, mode, bp, TB, FIX);
         });
         u32* flag = c->mark.as<u32>();
         u32* list = flag + nt;
         u8* fchg = (u8*)(list + nt + 1);
         u32 nfix = 0;
         if (fast) {
-            // device-gated: a fixed grid walks the k_fix list (usually empty) and marks the seams
-            // of changed tiles; k_seams_list redoes the marked ones (k_sample's front clear zeroed both)
+            // device-gated: a fixed grid walks the k_fix list (usually empty); with the seams
+            // after it nothing is marked, else it marks the seams of changed tiles and
+            // k_seams_list redoes the marked ones (k_sample's front clear zeroed both)
+            u8* fc_ = seams_after_fix ? nullptr : fchg;
+            u32* fl_ = seams_after_fix ? nullptr : flag;
             launch(c, "k_fix", [&] {
                 const unsigned grid = (unsigned)std::min<int64_t>(nt, 512);
-                if (mask) k_fix_dev<true><<<grid, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, mask, thr, mode, BITS, FACES, COUNT, P, KR, fchg, flag, list);
-                else k_fix_dev<false><<<grid, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR, fchg, flag, list);
+                if (mask) k_fix_dev<true><<<grid, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, mask, thr, mode, BITS, FACES, COUNT, P, KR, fc_, fl_, list);
+                else k_fix_dev<false><<<grid, NTHREADS, 0, s>>>(g, FIX, bp, guess, in, nullptr, thr, mode, BITS, FACES, COUNT, P, KR, fc_, fl_, list);
             });
-            if (lds_seams)
+            if (seams_after_fix)
+                seams(s, 0, nt);
+            else if (lds_seams)
                 launch(c, "k_seams", [&] {
                     const unsigned grid = (unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, 512);
                     k_seams_list<<<grid, SP_WAVES * 64, 0, s>>>(g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), c->big.as<u8>(),
@@ -903,7 +900,7 @@ int cc_threshold(cc_ctx* c, const float* in, const int64_t shape[3], const int64
             HIP_OK(hipMemsetAsync(FIX, 0, sizeof(u32), s));
             FrontClear none{};
             launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART, none); });
-            launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, md, guess, 0); });
+            launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, md, guess); });
             if (const char* e = std::getenv("CC_SPEC"); e && std::string(e) == "0")     // test hook: no guesses
                 HIP_OK(hipMemsetAsync(guess, 0, nb * sizeof(BlockParam), s));
             SpecArgs sa;

@@ -91,11 +91,8 @@ __device__ __forceinline__ int slot_row(int j, int wave) { return (j / RY) * TY 
 // k_block_stats: per-block ordered min / max and NaN flag.  One workgroup per tile.
 // ------------------------------------------------------------------------------------------
 // Stats of one tile folded into its block's (smin, smax, sflag); red = LDS scratch [3][WAVES].
-// ts (nullable): store the tile's (min, max) at ts[2 t] instead (k_block_verify reduces them; the NaN
-// flag is read off the extremes there)
 __device__ __forceinline__ void stats_tile(const Geom& g, const TileInfo& ti, const float* __restrict__ in,
-                                           u32* smin, u32* smax, u32* sflag, u32 (*red)[NTHREADS / 64],
-                                           u32* ts = nullptr, int64_t t = 0) {
+                                           u32* smin, u32* smax, u32* sflag, u32 (*red)[NTHREADS / 64]) {
     const int tid_ = cc_tid(), lane = tid_ & 63, wave = tid_ >> 6;
     u32 mn = 0xFFFFFFFFu, mx = 0u;
     // ordered min / max over all values; a NaN orders above +inf or below -inf, so the NaN flag
@@ -116,11 +113,6 @@ __device__ __forceinline__ void stats_tile(const Geom& g, const TileInfo& ti, co
             a = red[0][w] < a ? red[0][w] : a;
             b = red[1][w] > b ? red[1][w] : b;
             f |= red[2][w];
-        }
-        if (ts) {
-            ts[2 * t] = a;
-            ts[2 * t + 1] = b;
-            return;
         }
         // returning atomics: the caller waits for them before it hands the block on
         const u32 o1 = atomicMin(smin + ti.block, a);

@@ -138,22 +138,6 @@ def test_synthetic_vs_oracle(ctx, shape, bs, mode):
     _check_against_oracle(ctx, inp, bs, 0.5, mode)
 
 
-@pytest.mark.parametrize('tilestats,tbfree', [('0', '0'), ('1', '0'), ('0', '1'), ('1', '1')])
-@pytest.mark.parametrize('shape,bs,mode', SYNTH[:3])
-def test_front_variants_vs_oracle(ctx, monkeypatch, shape, bs, mode, tilestats, tbfree):
-    """The front's statistics variants: per-block atomics in k_spec + k_params_verify, or per-tile
-    statistics + k_block_verify (CC_SPEC_TILESTATS); TB recorded for every block, or TB-free for
-    blocks whose sampled extremes repeat (CC_SPEC_TBFREE) -- on quantized, continuous and
-    outlier-carrying inputs, bit-exact with the oracle."""
-    monkeypatch.setenv('CC_SPEC_TILESTATS', tilestats)
-    monkeypatch.setenv('CC_SPEC_TBFREE', tbfree)
-    inp = O.boundary_map(shape, origin=(7, 3, 1))
-    _check_against_oracle(ctx, inp, bs, 0.5, mode)
-    _check_against_oracle(ctx, O.boundary_map(shape, origin=(7, 3, 1), dither=True), bs, 0.41, mode)
-    inp[shape[0] // 2 + 1, 3, 5] = -0.5                  # an extreme off the sampled rows
-    _check_against_oracle(ctx, inp, bs, 0.5, mode)
-
-
 @pytest.mark.parametrize('shape,bs,mode', SYNTH[:4])
 def test_continuous_synthetic_vs_oracle(ctx, shape, bs, mode):
     """Continuous (dithered) input: the speculated intervals miss the exact ones."""
@@ -184,17 +168,12 @@ def test_max_runs_per_tile(ctx):
     _check_against_oracle(ctx, inp, (48, 96, 192), 0.5, 'less')
 
 
-@pytest.mark.parametrize('tbfree', ['0', '1'])
 @pytest.mark.parametrize('outlier', [-1.0, -1.0 / 32, 3.0, 1.0 + 1.0 / 64])
 @pytest.mark.parametrize('mode,thr', [('greater', 0.5), ('less', 0.5), ('equal', 0.5), ('greater', 0.3)])
-def test_speculated_interval_corrected(ctx, monkeypatch, mode, thr, outlier, tbfree):
+def test_speculated_interval_corrected(ctx, mode, thr, outlier):
     """Quantized data whose block extremes the sample misses (one outlier voxel off the sampled
-    rows): the guessed interval is wrong.  With TB recorded (CC_SPEC_TBFREE=0) tiles with voxels
-    between the guessed and the exact bounds must be relabelled (large outliers), the others kept
-    (small outliers); TB-free (the default for blocks whose sampled extremes repeat, as here) the
-    guess is checked by equality and every tile of a block whose extremes the sample missed is
-    relabelled.  Same labels either way."""
-    monkeypatch.setenv('CC_SPEC_TBFREE', tbfree)
+    rows): the guessed interval is wrong; tiles with voxels between the guessed and the exact
+    bounds must be relabelled (large outliers), the others kept (small outliers)."""
     rng = np.random.default_rng(3)
     inp = (rng.integers(0, 17, (64, 128, 192)) / np.float32(16)).astype(np.float32)
     inp[1, 1, 5] = outlier               # block (0, 0, 0); sample rows are z = 8 mod 16, y = 16 mod 32
@@ -204,10 +183,7 @@ def test_speculated_interval_corrected(ctx, monkeypatch, mode, thr, outlier, tbf
         if mode != 'equal' and outlier in (-1.0, 3.0):
             assert res['n_relabelled_tiles'] > 0        # the guess moved past quantization levels
         if (mode, thr, outlier) == ('greater', 0.3, -1.0 / 32):
-            if tbfree == '0':
-                assert res['n_relabelled_tiles'] == 0   # guess != exact, but no voxel in between
-            else:
-                assert res['n_relabelled_tiles'] > 0    # guess != exact: the blocks are relabelled
+            assert res['n_relabelled_tiles'] == 0       # guess != exact, but no voxel in between
     mask = (rng.random(inp.shape) < 0.9).astype(np.uint8)
     _check_against_oracle(ctx, inp, (32, 64, 96), thr, mode, mask)
 

@@ -132,22 +132,13 @@ int main(int argc, char** argv) {
             HIP_OK(hipMalloc(&guess, nb * sizeof(BlockParam)));
             r.push_back({"k_sample_guess", time_ms(s, iters, [&] {
                 k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, part, FrontClear{});
-                k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, part, thr, mode, guess, 1);
+                k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, part, thr, mode, guess);
             })});
             std::vector<BlockParam> hb(nb);
             HIP_OK(hipMemcpy(hb.data(), bp, nb * sizeof(BlockParam), hipMemcpyDeviceToHost));
-            for (auto& q : hb) {
+            for (auto& q : hb)
                 if (q.kind == BP_INTERVAL) { if (mode == 0) q.hi = 0xFFFFFFFFu; else if (mode == 1) q.lo = 0; }
-                q.pad = GUESS_TB;             // the TB-recording front (k_spec_tbfree below: without)
-            }
             HIP_OK(hipMemcpy(guess, hb.data(), nb * sizeof(BlockParam), hipMemcpyHostToDevice));
-            BlockParam* guess_free;
-            HIP_OK(hipMalloc(&guess_free, nb * sizeof(BlockParam)));
-            {
-                std::vector<BlockParam> hf = hb;
-                for (auto& q : hf) q.pad = 0;
-                HIP_OK(hipMemcpy(guess_free, hf.data(), nb * sizeof(BlockParam), hipMemcpyHostToDevice));
-            }
             SpecArgs sa;
             sa.guess = guess; sa.smin = fst; sa.smax = fst + nb; sa.sflag = fst + 2 * nb; sa.TB = TB; sa.t0 = 0;
             r.push_back({"k_spec", time_ms(s, iters, [&] {
@@ -157,22 +148,10 @@ int main(int argc, char** argv) {
                 else if (mode == 1) k_spec<false, 2><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS, FACES, COUNT, P, KEY);
                 else k_spec<false, 3><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS, FACES, COUNT, P, KEY);
             })});
-            {
-                SpecArgs sf = sa;
-                sf.guess = guess_free;
-                r.push_back({"k_spec_tbfree", time_ms(s, iters, [&] {
-                    HIP_OK(hipMemsetAsync(fst, 0xFF, nb * 4, s));
-                    HIP_OK(hipMemsetAsync(fst + nb, 0, 2 * nb * 4, s));
-                    k_spec<false, 1><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sf, in, nullptr, BITS, FACES, COUNT, P, KEY);
-                })});
-                u32* TSd;
-                HIP_OK(hipMalloc(&TSd, nt * 8));
-                sf.TS = TSd;
-                r.push_back({"k_spec_tbfree_tilestats", time_ms(s, iters, [&] {
-                    k_spec<false, 1><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sf, in, nullptr, BITS, FACES, COUNT, P, KEY);
-                })});
-            }
 #define SPS(A) k_spec<false, 1, A><<<(unsigned)nt, NTHREADS, 0, s>>>(g, sa, in, nullptr, BITS, FACES, COUNT, P, KEY)
+            r.push_back({"k_spec_nobits", time_ms(s, iters, [&] { SPS(20); })});
+            r.push_back({"k_spec_nofaces", time_ms(s, iters, [&] { SPS(21); })});
+            r.push_back({"k_spec_nostores", time_ms(s, iters, [&] { SPS(22); })});
             r.push_back({"k_spec_rows", time_ms(s, iters, [&] { SPS(99); })});
             r.push_back({"k_spec_bits", time_ms(s, iters, [&] { SPS(1); })});
             r.push_back({"k_spec_ph2", time_ms(s, iters, [&] { SPS(12); })});
@@ -198,12 +177,7 @@ int main(int argc, char** argv) {
             HIP_OK(hipMalloc(&fst, 3 * nb * 4));
             HIP_OK(hipMalloc(&TB, nt * 16));
             HIP_OK(hipMalloc(&guess, nb * sizeof(BlockParam)));
-            {
-                std::vector<BlockParam> hb(nb);
-                HIP_OK(hipMemcpy(hb.data(), bp, nb * sizeof(BlockParam), hipMemcpyDeviceToHost));
-                for (auto& q : hb) q.pad = GUESS_TB;
-                HIP_OK(hipMemcpy(guess, hb.data(), nb * sizeof(BlockParam), hipMemcpyHostToDevice));
-            }
+            HIP_OK(hipMemcpy(guess, bp, nb * sizeof(BlockParam), hipMemcpyDeviceToDevice));
             SpecArgs sa;
             sa.guess = guess; sa.smin = fst; sa.smax = fst + nb; sa.sflag = fst + 2 * nb; sa.TB = TB; sa.t0 = 0;
             r.push_back({"k_spec_cached", time_ms(s, iters, [&] {

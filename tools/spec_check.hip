@@ -60,7 +60,7 @@ int main(int argc, char** argv) {
         u32* part;
         HIP_OK(hipMalloc(&part, nb * SAMPLE_PARTS * 16));
         k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, part, FrontClear{});
-        k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, part, thr, mode, guess, 1);
+        k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, part, thr, mode, guess);
         HIP_OK(hipDeviceSynchronize());
         std::vector<BlockParam> hb(nb), hgs(nb);
         HIP_OK(hipMemcpy(hb.data(), bp, nb * sizeof(BlockParam), hipMemcpyDeviceToHost));
