@@ -41,9 +41,15 @@ inline std::atomic<int64_t> g_sync_count{0}, g_sync_ns{0};
 // Device memory of every context comes from per-device chunks of at least 1 GiB, handed out
 // first-fit in 256-B pieces.  In a fresh process each large hipMalloc / hipFree measured ~0.2 ms
 // after a pageable upload (the one-shot job's first call made six of them, 1.0 ms, and as many
-// frees at cc_destroy: profiles/r04_cold_*); a chunk pays that once.  A piece is only handed out
-// again after a device synchronisation (as hipFree implies), so work still queued on any stream
-// never sees its buffer reused; a chunk is returned to HIP when its last piece is released.
+// frees at cc_destroy: profiles/r04_cold_*); a chunk pays that once.  Requests of LARGE bytes or
+// more (volume-sized buffers of big inputs) get a chunk of their own, of their exact size, so the
+// arena never holds gigabytes beside them.  A released piece is reused only once the work queued
+// before its release has finished: release() records an event on the owner's stream (the
+// context's stream, which its side stream has joined) and the piece waits in `pending` until the
+// event completes -- no device-wide synchronisation, so RCCL collectives and other streams in
+// flight are not waited for.  A piece released without an owner stream (the communicator's
+// buffers) falls back to a device synchronisation.  A chunk is returned to HIP when its last piece
+// is free and no pending piece refers to it.
 struct Arena {
     struct Chunk {
         int dev;
@@ -51,9 +57,16 @@ struct Arena {
         size_t size, live;
         std::map<size_t, size_t> free;   // offset -> bytes
     };
-    static constexpr size_t ALIGN = 256, MIN_CHUNK = size_t(1) << 30, GROW_CAP = size_t(8) << 30;
+    struct Pending {
+        Chunk* ch;
+        size_t off, nb;
+        hipEvent_t ev;
+    };
+    static constexpr size_t ALIGN = 256, MIN_CHUNK = size_t(1) << 30, GROW_CAP = size_t(2) << 30,
+                            LARGE = size_t(256) << 20;
     std::mutex mu;
     std::vector<Chunk*> chunks;
+    std::vector<Pending> pending;
     std::map<char*, std::pair<Chunk*, size_t>> owner;      // piece -> (chunk, bytes)
 
     void* take(Chunk* ch, std::map<size_t, size_t>::iterator it, size_t nb) {
@@ -64,25 +77,72 @@ struct Arena {
         owner[ch->base + off] = {ch, nb};
         return ch->base + off;
     }
+    // back into its chunk's free list (coalesced); the chunk is freed when nothing of it is live
+    // or pending
+    void put_back(Chunk* ch, size_t off, size_t nb) {
+        auto nx = ch->free.lower_bound(off);
+        if (nx != ch->free.end() && off + nb == nx->first) { nb += nx->second; nx = ch->free.erase(nx); }
+        if (nx != ch->free.begin()) {
+            auto pv = std::prev(nx);
+            if (pv->first + pv->second == off) { off = pv->first; nb += pv->second; ch->free.erase(pv); }
+        }
+        ch->free[off] = nb;
+        if (--ch->live == 0 && std::none_of(pending.begin(), pending.end(), [&](const Pending& q) { return q.ch == ch; })) {
+            (void)hipFree(ch->base);
+            chunks.erase(std::find(chunks.begin(), chunks.end(), ch));
+            delete ch;
+        }
+    }
+    // pending pieces whose event has completed (wait = true: all of them, waiting)
+    void reap(bool wait) {
+        for (size_t i = 0; i < pending.size();) {
+            Pending q = pending[i];
+            const hipError_t r = wait ? hipEventSynchronize(q.ev) : hipEventQuery(q.ev);
+            if (r == hipErrorNotReady) { ++i; continue; }
+            (void)hipGetLastError();
+            (void)hipEventDestroy(q.ev);
+            pending.erase(pending.begin() + i);
+            q.ch->live += 1;              // put_back's accounting: the piece was counted live until now
+            put_back(q.ch, q.off, q.nb);
+        }
+    }
+    void* find_free(int dev, size_t nb, size_t* total) {
+        for (Chunk* ch : chunks) {
+            if (ch->dev != dev) continue;
+            if (total) *total += ch->size;
+            for (auto it = ch->free.begin(); it != ch->free.end(); ++it)
+                if (it->second >= nb) return take(ch, it, nb);
+        }
+        return nullptr;
+    }
     void* alloc(size_t need) {
         const size_t nb = (need + ALIGN - 1) & ~(ALIGN - 1);
         int dev = 0;
         HIP_OK(hipGetDevice(&dev));
         std::lock_guard<std::mutex> g(mu);
+        reap(false);
         size_t total = 0;
-        for (Chunk* ch : chunks) {
-            if (ch->dev != dev) continue;
-            total += ch->size;
-            for (auto it = ch->free.begin(); it != ch->free.end(); ++it)
-                if (it->second >= nb) return take(ch, it, nb);
+        if (nb < LARGE) {
+            if (void* p = find_free(dev, nb, &total)) return p;
+            // pieces still in use by queued work: wait for them before growing the arena
+            bool mine = false;
+            for (const Pending& q : pending) mine |= q.ch->dev == dev;
+            if (mine) {
+                reap(true);
+                if (void* p = find_free(dev, nb, nullptr)) return p;
+            }
         }
-        // a new chunk: at least 1 GiB, growing with what the device already holds (up to 8 GiB
-        // beyond the request); the exact size when that much is not available
-        size_t cs = std::max(nb, std::max(MIN_CHUNK, std::min(total, GROW_CAP)));
+        // a new chunk: a large request gets its own of its size; otherwise at least 1 GiB, growing
+        // with what the device already holds (at most GROW_CAP beyond the request); the exact size
+        // when that much is not available
+        size_t cs = nb >= LARGE ? nb : std::max(nb, std::max(MIN_CHUNK, std::min(total, GROW_CAP)));
         cs = (cs + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
         char* base = nullptr;
         if (hipMalloc(&base, cs) != hipSuccess) {
             (void)hipGetLastError();
+            reap(true);
+            if (nb < LARGE)
+                if (void* p = find_free(dev, nb, nullptr)) return p;
             cs = nb;
             HIP_OK(hipMalloc(&base, cs));
         }
@@ -91,26 +151,38 @@ struct Arena {
         chunks.push_back(ch);
         return take(ch, ch->free.begin(), nb);
     }
-    void release(void* p) {
+    // stream (nullable): the owner's stream; the piece is reusable once the work queued on it
+    // so far has finished.  nullptr: a device synchronisation first (reusable at once).
+    // the pieces whose event has completed back into the free lists (chunks freed when empty)
+    void trim() {
+        std::lock_guard<std::mutex> g(mu);
+        reap(false);
+    }
+    void release(void* p, hipStream_t* stream = nullptr) {
         if (!p) return;
-        (void)hipDeviceSynchronize();
+        hipEvent_t ev = nullptr;
+        if (stream) {
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess || hipEventRecord(ev, *stream) != hipSuccess) {
+                (void)hipGetLastError();
+                if (ev) (void)hipEventDestroy(ev);
+                ev = nullptr;
+            }
+        }
+        if (!ev) (void)hipDeviceSynchronize();
         std::lock_guard<std::mutex> g(mu);
         auto o = owner.find((char*)p);
-        if (o == owner.end()) return;
-        Chunk* ch = o->second.first;
-        size_t off = (char*)p - ch->base, nb = o->second.second;
-        owner.erase(o);
-        auto nx = ch->free.lower_bound(off);
-        if (nx != ch->free.end() && off + nb == nx->first) { nb += nx->second; nx = ch->free.erase(nx); }
-        if (nx != ch->free.begin()) {
-            auto pv = std::prev(nx);
-            if (pv->first + pv->second == off) { off = pv->first; nb += pv->second; ch->free.erase(pv); }
+        if (o == owner.end()) {
+            if (ev) (void)hipEventDestroy(ev);
+            return;
         }
-        ch->free[off] = nb;
-        if (--ch->live == 0) {
-            (void)hipFree(ch->base);
-            chunks.erase(std::find(chunks.begin(), chunks.end(), ch));
-            delete ch;
+        Chunk* ch = o->second.first;
+        const size_t off = (char*)p - ch->base, nb = o->second.second;
+        owner.erase(o);
+        if (ev) {
+            ch->live -= 1;                 // counted again when reaped
+            pending.push_back({ch, off, nb, ev});
+        } else {
+            put_back(ch, off, nb);
         }
     }
 };
@@ -119,13 +191,14 @@ inline Arena g_arena;
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    hipStream_t* stream = nullptr;       // the owner's stream (deferred reuse on release), if bound
     template <class T>
     T* as() const { return (T*)p; }
     void ensure(size_t need) {
         if (need <= bytes && p) return;
         const auto t0 = std::chrono::steady_clock::now();
         const size_t before = g_arena.chunks.size();
-        g_arena.release(p);
+        g_arena.release(p, stream);
         p = nullptr;
         bytes = 0;
         size_t nb = std::max<size_t>(need + need / 8, 256);
@@ -139,7 +212,7 @@ struct DevBuf {
         if (log) std::fprintf(stderr, "cc_alloc %zu B %.1f us chunks %zu\n", nb, ns * 1e-3, g_arena.chunks.size());
     }
     void release() {
-        g_arena.release(p);
+        g_arena.release(p, stream);
         p = nullptr;
         bytes = 0;
     }
@@ -215,6 +288,17 @@ struct cc_ctx {
     std::map<std::string, ProfEntry> prof_acc;
     void* run = nullptr;     // RunState of the current labelling run
 };
+
+// every device buffer of a context (bound to its stream at creation, released at destruction)
+static inline std::vector<DevBuf*> ctx_bufs(cc_ctx* c) {
+    return {&c->tiles, &c->bstat, &c->bparam, &c->bits, &c->faces, &c->count, &c->rc, &c->roff, &c->rl, &c->rcb, &c->P,
+            &c->KR, &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets, &c->lut,
+            &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp, &c->out_tmp, &c->pairs, &c->pairs2,
+            &c->scalars2, &c->flags, &c->map_ids, &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc,
+            &c->ipairs, &c->ipc, &c->iovf, &c->spec, &c->mark, &c->bflag, &c->ev_main, &c->ev_z, &c->ev_seg, &c->ev_gt,
+            &c->ev_flag, &c->ev_part, &c->rl_wg, &c->gs1, &c->gs2, &c->gs_tab, &c->mask_xmap, &c->seam_hash, &c->ws_tab,
+            &c->ws_buf, &c->status, &c->hmap_keys, &c->hmap_par};
+}
 
 // the context's stream: the caller's (cc_set_stream), else the null stream -- which is torch's
 // default stream too.  No stream of its own: creating one costs a hardware queue (10 ms in the

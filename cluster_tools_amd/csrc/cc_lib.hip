@@ -749,6 +749,7 @@ int cc_create(int device, cc_ctx** out) {
         cc_ctx* c = new cc_ctx();
         c->device = device;
         if (const char* e = std::getenv("CC_FRONT_CHUNKS")) c->front_chunks = std::max(1, atoi(e));
+        for (DevBuf* b : ctx_bufs(c)) b->stream = &c->stream;   // released pieces wait for this stream's work
         *out = c;
     })
 }
@@ -758,16 +759,9 @@ void cc_destroy(cc_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     if (c->side) (void)hipStreamSynchronize(c->side);
-    DevBuf* bufs[] = {&c->tiles, &c->bstat, &c->bparam, &c->bits, &c->faces, &c->count, &c->rc, &c->roff, &c->rl, &c->rcb, &c->P, &c->KR,
-                      &c->FIN, &c->keys, &c->keys2, &c->vals, &c->vals2, &c->seg, &c->values, &c->offsets,
-                      &c->lut, &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp,
-                      &c->out_tmp, &c->pairs, &c->pairs2, &c->scalars2, &c->flags, &c->map_ids,
-                      &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc, &c->ipairs, &c->ipc, &c->iovf, &c->spec, &c->mark, &c->bflag,
-                      &c->ev_main, &c->ev_z, &c->ev_seg, &c->ev_gt, &c->ev_flag, &c->ev_part, &c->rl_wg,
-                      &c->gs1, &c->gs2, &c->gs_tab, &c->mask_xmap, &c->seam_hash, &c->ws_tab, &c->ws_buf,
-                      &c->status, &c->hmap_keys, &c->hmap_par};
-    for (DevBuf* b : bufs) b->release();
+    for (DevBuf* b : ctx_bufs(c)) b->release();
     c->pin.release();
+    g_arena.trim();             // the stream has drained: the context's pieces are free again
     for (auto& pe : c->pending) { (void)hipEventDestroy(pe.second.first); (void)hipEventDestroy(pe.second.second); }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     if (c->side) (void)hipStreamDestroy(c->side);
@@ -778,6 +772,13 @@ void cc_destroy(cc_ctx* c) {
 int cc_set_stream(cc_ctx* c, void* stream) {
     CC_TRY({
         CC_REQUIRE(c, "ctx is NULL");
+        // the context's buffers are released behind events on its stream: work still queued on
+        // the previous stream must be done before another stream takes over
+        if (c->stream != (hipStream_t)stream) {
+            HIP_OK(hipSetDevice(c->device));
+            HIP_OK(hipStreamSynchronize(c->stream));
+            if (c->side) HIP_OK(hipStreamSynchronize(c->side));
+        }
         c->stream = (hipStream_t)stream;
     })
 }

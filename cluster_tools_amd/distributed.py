@@ -357,7 +357,7 @@ def _slabs_fast(ctxs, x, block_shape, threshold, mode, mask, bounds, out, cap):
     Z, Y, X = x.shape
     stream = torch.cuda.current_stream(dev).cuda_stream
     for ctx in ctxs:
-        ctx.set_stream(stream)               # every slab's kernels in one stream order
+        ctx.set_stream(stream)               # every slab's kernels in one stream order (left bound: see docstring)
     sum_ts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(n)]
     for r, (ctx, (z0, zs)) in enumerate(zip(ctxs, bounds)):
         m = None if mask is None else mask[z0:z0 + zs]
@@ -393,7 +393,9 @@ def label_slabs_single_process(ctxs, x, block_shape, threshold, mode='greater', 
     default: what ShardedLabeler picks).  schedule: None (the one-read-back schedule when the
     cube form applies, else -- or when its status asks for it -- the synchronised one), 'sync',
     'fast' (the one-read-back schedule or an error).  Contexts that cannot run the one-read-back
-    schedule (cc_shard_dev_ok) get the synchronised one.  Returns (labels, per-slab results, sums,
+    schedule (cc_shard_dev_ok) get the synchronised one.  The one-read-back schedule binds every
+    context to torch's current stream of the input's device (ctx.set_stream) and leaves it bound:
+    later calls on these contexts run on that stream.  Returns (labels, per-slab results, sums,
     luts)."""
     import torch
     Z, Y, X = x.shape

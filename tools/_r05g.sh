@@ -1,7 +1,7 @@
 set -e -o pipefail
 mkdir -p gpurun_out
 T="python -u -m pytest -x -q --timeout 200 --timeout-method thread"
-timeout -k 10 600 $T tests/test_gpu_parity.py tests/test_gpu_sharded.py -k "mask or speculated or front_variants or c4_scale or fused_path_golden" > gpurun_out/t_r05g.log 2>&1 || { tail -40 gpurun_out/t_r05g.log; exit 1; }
+timeout -k 10 600 $T tests/test_gpu_parity.py tests/test_gpu_sharded.py -k "mask_vs_oracle or c3_mask or speculated or fused_path_golden or synthetic_vs_oracle or both_schedules" > gpurun_out/t_r05g.log 2>&1 || { tail -40 gpurun_out/t_r05g.log; exit 1; }
 tail -2 gpurun_out/t_r05g.log
 timeout -k 10 300 tools/ablate 1024 2048 2048 64 512 512 0 10 > gpurun_out/ablate_r05g.txt 2>&1
 python3 -c "
