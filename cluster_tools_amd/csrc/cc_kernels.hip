@@ -555,6 +555,22 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
     TileCCL& T = L.T;
     u32* key = L.key;
     const int tid = cc_tid();
+    // An empty tile (no foreground voxel: a masked-out or all-background region) stores no bit
+    // rows -- k_pass2 writes its zeros without them -- and skips the tile CCL; its faces are
+    // stored as zeros (their readers take them as they are).
+    static_assert(NROWS == NTHREADS, "one bit row per thread");
+    if (ABL == 0 && write && !__syncthreads_or(rows[tid] != 0)) {
+        if (tid == 0) COUNT[t] = 0;
+        u32* FW = (u32*)(FACES + t * FACE_STRIDE);
+        const bool two = NTHREADS + tid < FACE_STRIDE / 2;
+        if (fchg) {
+            const bool diff = FW[tid] != 0u || (two && FW[NTHREADS + tid] != 0u);
+            if (__syncthreads_or(diff) && tid == 0) fchg[t] = 1;
+        }
+        FW[tid] = 0u;
+        if (two) FW[NTHREADS + tid] = 0u;
+        return;
+    }
     // (ABL 20 / 21 / 22: the whole pass without the BITS / FACES / both stores -- the store-volume
     // ablation of tools/ablate.hip)
     if (write && ABL != 20 && ABL != 22)

@@ -462,3 +462,26 @@ def test_root_capacity_redo(monkeypatch):
             _check_against_oracle(c, x, bs, 0.5, 'less')
             prof = c.profile()         # the one-read-back pass scans in k_scan_emit, the redo in k_block_scan
             assert sum(prof.get(k, {}).get('count', 0) for k in ('k_block_scan', 'k_scan_emit')) == passes
+
+
+def test_empty_tiles_context_reuse(ctx):
+    """Tiles without foreground store no bit rows and zero faces: one context labels inputs whose
+    empty tiles move (non-empty -> empty -> non-empty), with and without a mask and through a
+    speculation miss (the k_fix path re-runs pass 1 of such tiles), always equal to the oracle --
+    nothing of an earlier run leaks through the skipped stores."""
+    shape, bs = (64, 160, 256), (32, 64, 128)
+    base = O.boundary_map(shape, origin=(2, 7, 3))
+    a = base.copy()
+    a[:, :, 128:] = 0.0                    # x half empty ('greater')
+    b = base.copy()
+    b[:, :80, :] = 0.0                     # y half empty instead
+    c = base.copy()
+    c[5, 9, 200] = -3.0                    # an extreme off the sampled rows: k_fix relabels tiles
+    c[:32] = 0.0
+    for inp in (base, a, b, a, c, base):
+        _check_against_oracle(ctx, inp, bs, 0.5, 'greater')
+        _check_against_oracle(ctx, inp, bs, 0.5, 'less')
+    from oracle.synth import ellipsoid_mask
+    m = ellipsoid_mask(shape)
+    for inp in (base, b, base):
+        _check_against_oracle(ctx, inp, bs, 0.5, 'greater', m)

@@ -1,0 +1,11 @@
+set -e -o pipefail
+mkdir -p gpurun_out
+T="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+timeout -k 10 700 $T tests/test_gpu_parity.py tests/test_gpu_sharded.py -k "empty_tiles or mask or speculated or c3_vs_oracle or synthetic_vs_oracle or fused_path_golden or max_runs or white_noise or single_gpu_vs_oracle" > gpurun_out/t_r05i.log 2>&1 || { tail -40 gpurun_out/t_r05i.log; exit 1; }
+tail -2 gpurun_out/t_r05i.log
+timeout -k 10 240 python -u bench.py --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/sd_r05i.json 2>/dev/null
+python3 -c "import json; d = json.loads(open('gpurun_out/sd_r05i.json').read().strip().splitlines()[-1]); print('bench', d['ms_per_step'], d['kernels_ms_per_step'])"
+ROUNDS=3 timeout -k 10 600 tools/gpu_ab.sh "CC_X=0" "CC_LIB_PATH=tools/ab/lib_f89f4ef.so" "CC_LIB_PATH=tools/ab/lib_mnostage.so" -- --workload c4 > gpurun_out/ab_c4_r05i.txt 2>&1
+cat gpurun_out/ab_c4_r05i.txt
+ROUNDS=3 timeout -k 10 600 tools/gpu_ab.sh "CC_X=0" "CC_LIB_PATH=tools/ab/lib_f89f4ef.so" > gpurun_out/ab_c3_r05i.txt 2>&1
+cat gpurun_out/ab_c3_r05i.txt
