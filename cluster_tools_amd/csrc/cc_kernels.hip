@@ -527,7 +527,7 @@ struct Pass1LDS {
 template <int ABL>
 __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const TileInfo& ti, u64* BITS, face_t* FACES,
                                              u32* COUNT, u32* P, u64* KEY, Pass1LDS& L, bool write,
-                                             u8* fchg = nullptr);
+                                             u8* fchg = nullptr, int empty = -1);
 
 // Pass 1 of tile t (block parameters p): bit rows -> BITS, tile CCL -> COUNT, nodes (P, KEY),
 // face planes.  ABL (kernel ablation harness tools/ablate.hip only; 0 in the library): stop
@@ -548,9 +548,12 @@ __device__ __forceinline__ void pass1_tile(const Geom& g, int64_t t, const TileI
 // Pass 1 after the bit rows are in L.rows (and a barrier): BITS, tile CCL, COUNT, nodes, faces.
 // fchg (k_fix): fchg[t] = 1 when the new face planes differ from the ones in FACES (the seams
 // that read them must be redone; unchanged faces leave every seam list as it was).
+// empty: whether the tile has no foreground voxel, if the caller knows (k_spec reads it off its
+// statistics barrier); -1: decided here (one more barrier)
 template <int ABL>
 __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const TileInfo& ti, u64* BITS, face_t* FACES,
-                                             u32* COUNT, u32* P, u64* KEY, Pass1LDS& L, bool write, u8* fchg) {
+                                             u32* COUNT, u32* P, u64* KEY, Pass1LDS& L, bool write, u8* fchg,
+                                             int empty) {
     u64* rows = L.rows;
     TileCCL& T = L.T;
     u32* key = L.key;
@@ -559,7 +562,7 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
     // rows -- k_pass2 writes its zeros without them -- and skips the tile CCL; its faces are
     // stored as zeros (their readers take them as they are).
     static_assert(NROWS == NTHREADS, "one bit row per thread");
-    if (ABL == 0 && write && !__syncthreads_or(rows[tid] != 0)) {
+    if (ABL == 0 && write && (empty >= 0 ? empty != 0 : !__syncthreads_or(rows[tid] != 0))) {
         if (tid == 0) COUNT[t] = 0;
         u32* FW = (u32*)(FACES + t * FACE_STRIDE);
         const bool two = NTHREADS + tid < FACE_STRIDE / 2;
@@ -839,8 +842,9 @@ __device__ __forceinline__ int64_t xcd_contig(int64_t b, int64_t n) {
 // The front of k_spec for tile t: the tile's voxels in one read -> exact statistics (the
 // block's atomics), the bit rows under the guessed interval [lo, hi] into L.rows, the tile's TB
 // words.
+// Returns whether the tile holds no foreground voxel (read off the statistics barrier).
 template <bool HAS_MASK, int SIDES>
-__device__ __forceinline__ void spec_front(const Geom& g, const SpecArgs& sa, int64_t t, const TileInfo& ti,
+__device__ __forceinline__ bool spec_front(const Geom& g, const SpecArgs& sa, int64_t t, const TileInfo& ti,
                                            const float* __restrict__ in, const u8* __restrict__ mask, u32 lo,
                                            u32 hi, Pass1LDS& L, u32 (*red)[NTHREADS / 64]) {
     const int tid = cc_tid(), lane = tid & 63, wave = wave_id();
@@ -854,6 +858,7 @@ __device__ __forceinline__ void spec_front(const Geom& g, const SpecArgs& sa, in
     // to k_fix (a masked voxel between the guessed and the exact bound), never fewer -- and the
     // masked kernel saves the per-voxel selects (8 per float4).
     u32 mn = 0xFFFFFFFFu, mx = 0u, K1N = 0xFFFFFFFFu, K1X = 0u, K2N = 0xFFFFFFFFu, K2X = 0u;
+    u64 myrow = 0;                                  // this thread's bit row (emptiness test)
     auto fgp = [&](u32 o) -> bool { return SIDES == 1 ? o >= lo : SIDES == 2 ? o <= hi : (o >= lo && o <= hi); };
     // one voxel (partial tiles)
     auto voxel = [&](float x, u32 mk) -> bool {
@@ -959,7 +964,8 @@ __device__ __forceinline__ void spec_front(const Geom& g, const SpecArgs& sa, in
         }
         // split form: even voxels x = 4i (j = 0), 4i + 2 (j = 2) -> bits 2i, 2i + 1 of the low half
         const u32 even = spread2(seg[0]) | (spread2(seg[2]) << 1), odd = spread2(seg[1]) | (spread2(seg[3]) << 1);
-        L.rows[zz * TY + 4 * wave + qq] = ((u64)odd << 32) | even;
+        myrow = ((u64)odd << 32) | even;
+        L.rows[zz * TY + 4 * wave + qq] = myrow;
     } else {
         for (int i = tid; i < NROWS; i += NTHREADS) L.rows[i] = 0;
         __syncthreads();
@@ -971,17 +977,24 @@ __device__ __forceinline__ void spec_front(const Geom& g, const SpecArgs& sa, in
             CC_WRITELANE2(mlo, mhi, blo, bhi, j);
         });
         const int r = slot_row(lane, wave);
-        if (r / TY < ti.lz && r % TY < ti.ly) L.rows[r] = split_row(((u64)mhi << 32) | mlo);
+        if (r / TY < ti.lz && r % TY < ti.ly) {
+            myrow = split_row(((u64)mhi << 32) | mlo);
+            L.rows[r] = myrow;
+        }
     }
+    const u32 nzw = __ballot(myrow != 0) ? 1u : 0u;
     mn = wave_min(mn);
     mx = wave_max(mx);
     if (SIDES & 1) { K1N = wave_min(K1N); K1X = wave_max(K1X); }
     if (SIDES & 2) { K2N = wave_min(K2N); K2X = wave_max(K2X); }
     if (lane == 0) {
         red[0][wave] = mn; red[1][wave] = mx; red[2][wave] = K1N; red[3][wave] = K1X; red[4][wave] = K2N;
-        red[5][wave] = K2X;
+        red[5][wave] = K2X; red[6][wave] = nzw;
     }
     __syncthreads();
+    u32 nz = 0;
+#pragma unroll
+    for (int w = 0; w < NTHREADS / 64; ++w) nz |= red[6][w];
     if (tid == 0) {
         for (int w = 1; w < NTHREADS / 64; ++w) {
             mn = min(mn, red[0][w]); mx = max(mx, red[1][w]);
@@ -1006,6 +1019,7 @@ __device__ __forceinline__ void spec_front(const Geom& g, const SpecArgs& sa, in
             tb[0] = A; tb[1] = B; tb[2] = C; tb[3] = D;
         }
     }
+    return nz == 0;
 }
 
 // timing probe of the clock tool (tools/clock_probe.hip defines it: per-workgroup core / wall
@@ -1024,7 +1038,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
     u32* COUNT, u32* P, u64* KEY) {
     CC_KERNEL_PROBE
     __shared__ Pass1LDS L;
-    __shared__ u32 red[6][NTHREADS / 64];
+    __shared__ u32 red[7][NTHREADS / 64];
     const int64_t t = sa.t0 + ((g.X & 31) ? xcd_contig(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x);
     const TileInfo ti = tile_info(g, t);
     const BlockParam p = uniform_bp(sa.guess[ti.block]);
@@ -1032,9 +1046,9 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8, 8))
         stats_tile(g, ti, in, sa.smin, sa.smax, sa.sflag, red);
         return;
     }
-    spec_front<HAS_MASK, SIDES>(g, sa, t, ti, in, mask, p.lo, p.hi, L, red);
+    const bool empty = spec_front<HAS_MASK, SIDES>(g, sa, t, ti, in, mask, p.lo, p.hi, L, red);
     if (ABL == 99) return;
-    pass1_finish<ABL % 99>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, true);
+    pass1_finish<ABL % 99>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, true, nullptr, empty ? 1 : 0);
     CC_KERNEL_PROBE_END
 }
 
