@@ -545,6 +545,17 @@ __device__ __forceinline__ void pass1_tile(const Geom& g, int64_t t, const TileI
     pass1_finish<ABL>(g, t, ti, BITS, FACES, COUNT, P, KEY, L, write, fchg);
 }
 
+// pass 1's BITS / FACES stores, non-temporal (CC_SPEC_NT=0 for A/B: plain stores; C3 on a fast box
+// k_spec 3.140-3.148 -> 3.113-3.122 ms, C4 unchanged: profiles/r05_ab_spec_nt.txt)
+#ifndef CC_SPEC_NT
+#define CC_SPEC_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ void spec_store(T* p, T v) {
+    if (CC_SPEC_NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // Pass 1 after the bit rows are in L.rows (and a barrier): BITS, tile CCL, COUNT, nodes, faces.
 // fchg (k_fix): fchg[t] = 1 when the new face planes differ from the ones in FACES (the seams
 // that read them must be redone; unchanged faces leave every seam list as it was).
@@ -577,7 +588,7 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
     // (ABL 20 / 21 / 22: the whole pass without the BITS / FACES / both stores -- the store-volume
     // ablation of tools/ablate.hip)
     if (write && ABL != 20 && ABL != 22)
-        for (int i = tid; i < NROWS; i += NTHREADS) BITS[t * NROWS + i] = rows[i];
+        for (int i = tid; i < NROWS; i += NTHREADS) spec_store(BITS + t * NROWS + i, rows[i]);
     if (ABL == 1) return;
     if constexpr (ABL >= 10 && ABL < 20) { tile_ccl<ABL - 10>(rows, T, key, key); return; }
     const u32 R = tile_ccl(rows, T, key, key);      // key[k] = first voxel of component k
@@ -605,8 +616,8 @@ __device__ __forceinline__ void pass1_finish(const Geom& g, int64_t t, const Til
         if (__syncthreads_or(w0 == 0x12345678u && w1 == 0x9ABCDEF0u) && tid == 0) COUNT[t] = R + 1;
         return;
     }
-    FW[tid] = w0;
-    if (two) FW[NTHREADS + tid] = w1;
+    spec_store(FW + tid, w0);
+    if (two) spec_store(FW + NTHREADS + tid, w1);
 }
 
 // k_pass1: one workgroup per tile, block parameters precomputed (ablation harness; the library
