@@ -58,3 +58,31 @@ def test_sharded_c_entry_errors():
         x = torch.zeros((20, 32, 32), dtype=torch.float32, device='cuda')
         with pytest.raises(RuntimeError, match='block faces'):
             ctx.label_volume_sharded(comm, x, (40, 32, 32), 5, (16, 32, 32), 0.5)
+
+
+def test_integration_comm_binding_runs_as_documented():
+    """INTEGRATION.md's torch-free sharded binding (cc_comm_* + cc_label_volume_sharded) executed
+    as written, one rank, against the oracle on the whole volume."""
+    import ctypes
+    import torch
+    from conftest import exec_integration_binding, integration_blocks
+    ns = exec_integration_binding()
+    for b in integration_blocks():
+        if 'def label_slab' in b:
+            exec(compile(b, 'INTEGRATION.md', 'exec'), ns)
+    shape, bs = (64, 150, 200), (16, 64, 64)
+    x = O.boundary_map(shape, origin=(4, 1, 2))
+    ref = O.label_volume(x, bs, 0.5, 'greater', None, n_threads=8)
+    L = ns['_L']
+    ctx = ctypes.c_void_p()
+    assert L.cc_create(0, ctypes.byref(ctx)) == 0
+    try:
+        xd = torch.from_numpy(x).cuda()
+        out = torch.empty(shape, dtype=torch.int64, device='cuda')
+        torch.cuda.synchronize()
+        res = ns['label_slab'](ctx, ns['rccl_id'](), 1, 0, 0, xd.data_ptr(), shape, 0, shape[0], bs, 0.5, 0,
+                               out.data_ptr())
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), ref['labels'])
+        assert res.n_labels == ref['n_labels'] and res.max_id == ref['n_labels'] - 1
+    finally:
+        L.cc_destroy(ctx)
