@@ -1516,19 +1516,23 @@ __device__ __forceinline__ void seam_rows3(const face_t* S, const int mode[3], i
     const u64 Am = r > 0 ? Am_ : 0ull, Ap = r + 1 < nr ? Ap_ : 0ull;
     if (!md || !A) return;
     const bool full26 = md == 1;
-    u32 la = NONE, lb = NONE;                                         // last pair emitted by this lane
     // bit x := bit x + dx
     auto sh = [](u64 v, int dx) { return dx > 0 ? v >> 1 : dx < 0 ? v << 1 : v; };
+    // the run starts of the nine contact directions j = (dr + 1) * 3 + dx + 1 first (unrolled,
+    // constant shifts), then ONE emit site walking them as a rolled loop over the directions
+    // that have a contact anywhere in the wave (nine inlined copies of the emit path made the
+    // kernel 19 k instructions with 1.7 k SGPR spill / reload sites)
+    u64 M[9];
+    u32 nzj = 0;
 #pragma unroll
     for (int dr = -1; dr <= 1; ++dr) {
-        if (dr && !full26) continue;
         const u64 B = dr < 0 ? Bm : dr > 0 ? Bp : B0;
-        if (!B) continue;
         const u64 Ad = dr < 0 ? Am : Ap;
-        const int rb = r + dr;
 #pragma unroll
         for (int dx = -1; dx <= 1; ++dx) {
-            if (dx && !full26) continue;
+            const int j = (dr + 1) * 3 + dx + 1;
+            M[j] = 0;
+            if ((dr || dx) && !full26) continue;
             // contact A_r[x] - B_{r+dr}[x+dx].  Voxels next to each other on one side of the seam
             // are one component of that tile, so the pair is also given by a contact of smaller
             // |dr| + |dx| when A_r[x+dx] or B_{r+dr}[x] is set (dx != 0: the (dr, 0) contact) or
@@ -1541,14 +1545,25 @@ __device__ __forceinline__ void seam_rows3(const face_t* S, const int mode[3], i
             // a (0, 0) run starting where the row before also had a (0, 0) contact repeats that
             // contact's pair (rows r - 1 and r are adjacent on both sides): only the topmost emits
             if (!dr && !dx) m0 &= ~(Am & Bm);
-            for (u64 m = m0; m; m &= m - 1) {
-                const int x = __builtin_ctzll(m);
-                const u32 ka = FA[(r >> 1) * stride + (x >> 1)] & FK_MASK;
-                const u32 kb = FB[(rb >> 1) * stride + ((x + dx) >> 1)] & FK_MASK;
-                if (ka == la && kb == lb) continue;             // cheap first filter
-                la = ka; lb = kb;
-                emit(seam, ka, kb);
-            }
+            M[j] = m0;
+            nzj |= m0 ? 1u << j : 0u;
+        }
+    }
+    u32 la = NONE, lb = NONE;                                         // last pair emitted by this lane
+#pragma unroll 1
+    for (u32 todo = nzj; todo; todo &= todo - 1) {
+        const int j = __builtin_ctz(todo);
+        u64 m = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) m = i == j ? M[i] : m;
+        const int dx = j % 3 - 1, rb = r + j / 3 - 1;
+        for (; m; m &= m - 1) {
+            const int x = __builtin_ctzll(m);
+            const u32 ka = FA[(r >> 1) * stride + (x >> 1)] & FK_MASK;
+            const u32 kb = FB[(rb >> 1) * stride + ((x + dx) >> 1)] & FK_MASK;
+            if (ka == la && kb == lb) continue;             // cheap first filter
+            la = ka; lb = kb;
+            emit(seam, ka, kb);
         }
     }
 }
@@ -1561,34 +1576,38 @@ __device__ __forceinline__ void seam_rows3(const face_t* S, const int mode[3], i
 //   [112,116) ZHI corner entries of (-1, s1, s2), index (s1 > 0) * 2 + (s2 > 0)
 constexpr int EDGE_N = 128;
 
+// Which of a tile's neighbours lie in its block (from the tile's block-local position; no table
+// loads).  A lower neighbour inside the block is a full tile (only a block's last tile along an
+// axis is truncated), so its facing row / column is row TY - 1 / column TX - 1.
+struct InBlock {
+    bool z, ym, yp, xm, xp;        // (-1, 0, 0), (0, -1, 0), (0, +1, 0), (0, 0, -1), (0, 0, +1)
+    __device__ __forceinline__ bool y(int s) const { return s < 0 ? ym : yp; }
+    __device__ __forceinline__ bool x(int s) const { return s < 0 ? xm : xp; }
+};
+
 __device__ __forceinline__ void stage_edges(const Geom& g, const face_t* __restrict__ FACES, int64_t t,
-                                            const TileInfo& ti, face_t* E, int lane) {
+                                            const InBlock& nb, face_t* E, int lane) {
     const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
-    const bool zok = ti.iz > 0 && g.tblk[0][ti.iz] == g.tblk[0][ti.iz - 1];
-    auto yok = [&](int s) { const int j = ti.iy + s; return j >= 0 && j < g.nt[1] && g.tblk[1][j] == g.tblk[1][ti.iy]; };
-    auto xok = [&](int s) { const int j = ti.ix + s; return j >= 0 && j < g.nt[2] && g.tblk[2][j] == g.tblk[2][ti.ix]; };
-    auto ylast = [&](int s) { return (g.tlen[1][ti.iy + s] - 1) / 2; };
-    auto xlast = [&](int s) { return (g.tlen[2][ti.ix + s] - 1) / 2; };
+    constexpr int YL = (TY - 1) / 2, XL = (TX - 1) / 2;          // facing cube row / column of a lower neighbour
 #pragma unroll
     for (int i = lane; i < EDGE_N; i += 64) {
         u32 v = 0;
         if (i < 32) {
-            if (zok && yok(-1)) v = FACES[(t - sz - sy) * FACE_STRIDE + F_ZHI + ylast(-1) * CX + i];
+            if (nb.z && nb.ym) v = FACES[(t - sz - sy) * FACE_STRIDE + F_ZHI + YL * CX + i];
         } else if (i < 64) {
-            if (zok && yok(1)) v = FACES[(t - sz + sy) * FACE_STRIDE + F_ZHI + (i - 32)];
+            if (nb.z && nb.yp) v = FACES[(t - sz + sy) * FACE_STRIDE + F_ZHI + (i - 32)];
         } else if (i < 80) {
-            if (zok && xok(-1)) v = FACES[(t - sz - 1) * FACE_STRIDE + F_ZHI + (i - 64) * CX + xlast(-1)];
+            if (nb.z && nb.xm) v = FACES[(t - sz - 1) * FACE_STRIDE + F_ZHI + (i - 64) * CX + XL];
         } else if (i < 96) {
-            if (zok && xok(1)) v = FACES[(t - sz + 1) * FACE_STRIDE + F_ZHI + (i - 80) * CX];
+            if (nb.z && nb.xp) v = FACES[(t - sz + 1) * FACE_STRIDE + F_ZHI + (i - 80) * CX];
         } else if (i < 104) {
-            if (ti.iy > 0 && yok(-1) && xok(-1)) v = FACES[(t - sy - 1) * FACE_STRIDE + F_YHI + (i - 96) * CX + xlast(-1)];
+            if (nb.ym && nb.xm) v = FACES[(t - sy - 1) * FACE_STRIDE + F_YHI + (i - 96) * CX + XL];
         } else if (i < 112) {
-            if (ti.iy > 0 && yok(-1) && xok(1)) v = FACES[(t - sy + 1) * FACE_STRIDE + F_YHI + (i - 104) * CX];
+            if (nb.ym && nb.xp) v = FACES[(t - sy + 1) * FACE_STRIDE + F_YHI + (i - 104) * CX];
         } else if (i < 116) {
             const int s1 = (i - 112) & 2 ? 1 : -1, s2 = (i - 112) & 1 ? 1 : -1;
-            if (zok && yok(s1) && xok(s2))
-                v = FACES[(t - sz + s1 * sy + s2) * FACE_STRIDE + F_ZHI + (s1 < 0 ? ylast(s1) : 0) * CX +
-                          (s2 < 0 ? xlast(s2) : 0)];
+            if (nb.z && nb.y(s1) && nb.x(s2))
+                v = FACES[(t - sz + s1 * sy + s2) * FACE_STRIDE + F_ZHI + (s1 < 0 ? YL : 0) * CX + (s2 < 0 ? XL : 0)];
         }
         E[i] = (face_t)v;
     }
@@ -1601,18 +1620,23 @@ __device__ __forceinline__ void stage_edges(const Geom& g, const face_t* __restr
 // EMIT(oz, oy, ox, ka, kb) once per run of contacts (26-connectivity along the edge), the
 // neighbour tile being t + oz sz + oy sy + ox.
 template <class EM>
-__device__ __forceinline__ void seam_edges_rows(const Geom& g, const face_t* S, const face_t* E, int64_t t,
-                                                const TileInfo& ti, int lane, EM&& emit) {
+__device__ __forceinline__ void seam_edges_rows(const face_t* S, const face_t* E, const TileInfo& ti,
+                                                const InBlock& nb, int lane, EM&& emit) {
     const int ncy = (ti.ly + 1) / 2, ncx = (ti.lx + 1) / 2;
-    const bool zok = ti.iz > 0 && g.tblk[0][ti.iz] == g.tblk[0][ti.iz - 1];
-    auto yok = [&](int s) { const int j = ti.iy + s; return j >= 0 && j < g.nt[1] && g.tblk[1][j] == g.tblk[1][ti.iy]; };
-    auto xok = [&](int s) { const int j = ti.ix + s; return j >= 0 && j < g.nt[2] && g.tblk[2][j] == g.tblk[2][ti.ix]; };
-    auto ypar = [&](int s) { return s < 0 ? (g.tlen[1][ti.iy + s] - 1) & 1 : 0; };   // neighbour's facing y parity
-    auto xpar = [&](int s) { return s < 0 ? (g.tlen[2][ti.ix + s] - 1) & 1 : 0; };
+    const bool zok = nb.z;
+    auto yok = [&](int s) { return nb.y(s); };
+    auto xok = [&](int s) { return nb.x(s); };
+    auto ypar = [&](int s) { return s < 0 ? (TY - 1) & 1 : 0; };   // neighbour's facing y parity
+    auto xpar = [&](int s) { return s < 0 ? (TX - 1) & 1 : 0; };
     const bool ok[6] = {zok && yok(-1), zok && yok(1), zok && xok(-1), zok && xok(1),
-                        ti.iy > 0 && yok(-1) && xok(-1), ti.iy > 0 && yok(-1) && xok(1)};
-    // own / neighbour rows of the six edges (ballots over the position p = lane)
-    u64 A[6], B[6];
+                        yok(-1) && xok(-1), yok(-1) && xok(1)};
+    // own / neighbour rows of the six edges (ballots over the position p = lane), and I: the
+    // voxels next to both ends of a contact in a lower face neighbour of this tile inside the
+    // block (staged in S) -- own (z, y, x) [edge voxel p] and the neighbour's voxel are both
+    // 26-adjacent to (z - 1, y, x) (z faces: t - sz's ZHI), (z, y - 1, x) (t - sy's YHI) or
+    // (z, y, x - 1) (t - 1's XHI), at position p or p + d; the face seams of this tile and of that
+    // neighbour connect the pair through it, so such an edge contact is dropped
+    u64 A[6], B[6], I[6];
     {
         const int p = lane;
 #pragma unroll
@@ -1621,6 +1645,9 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const face_t* S, 
             const u32 ea = ok[e] ? S[F_ZLO + cyo * CX + (p >> 1)] : 0u, eb = ok[e] ? E[(e ? 32 : 0) + (p >> 1)] : 0u;
             A[e] = __ballot((ea >> (FK_BITS + jo * 2 + (p & 1))) & 1u);
             B[e] = __ballot((eb >> (FK_BITS + ypar(s) * 2 + (p & 1))) & 1u);
+            const u32 iz = ok[e] ? S[F_ZHI + cyo * CX + (p >> 1)] : 0u;     // (z - 1, y_e, x)
+            const u32 iy = (ok[e] && s < 0) ? S[F_YHI + (p >> 1)] : 0u;      // (z, y_e - 1, x), plane z = 0
+            I[e] = __ballot(((iz >> (FK_BITS + jo * 2 + (p & 1))) | (iy >> (FK_BITS + (p & 1)))) & 1u);
         }
 #pragma unroll
         for (int e = 2; e < 4; ++e) {                      // bits y
@@ -1629,6 +1656,9 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const face_t* S, 
             const u32 ea = in ? S[F_ZLO + (p >> 1) * CX + cxo] : 0u, eb = in ? E[(e == 3 ? 80 : 64) + (p >> 1)] : 0u;
             A[e] = __ballot((ea >> (FK_BITS + (p & 1) * 2 + io)) & 1u);
             B[e] = __ballot((eb >> (FK_BITS + (p & 1) * 2 + xpar(s))) & 1u);
+            const u32 iz = in ? S[F_ZHI + (p >> 1) * CX + cxo] : 0u;          // (z - 1, y, x_e)
+            const u32 ix = (in && s < 0) ? S[F_XHI + (p >> 1)] : 0u;          // (z, y, x_e - 1), plane z = 0
+            I[e] = __ballot(((iz >> (FK_BITS + (p & 1) * 2 + io)) | (ix >> (FK_BITS + (p & 1)))) & 1u);
         }
 #pragma unroll
         for (int e = 4; e < 6; ++e) {                      // bits z
@@ -1637,18 +1667,21 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const face_t* S, 
             const u32 ea = in ? S[F_YLO + (p >> 1) * CX + cxo] : 0u, eb = in ? E[(e == 5 ? 104 : 96) + (p >> 1)] : 0u;
             A[e] = __ballot((ea >> (FK_BITS + (p & 1) * 2 + io)) & 1u);
             B[e] = __ballot((eb >> (FK_BITS + (p & 1) * 2 + xpar(s))) & 1u);
+            const u32 iy = in ? S[F_YHI + (p >> 1) * CX + cxo] : 0u;          // (z, y - 1, x_e)
+            const u32 ix = (in && s < 0) ? S[F_XHI + (p >> 1) * CY] : 0u;     // (z, y, x_e - 1), row y = 0
+            I[e] = __ballot(((iy >> (FK_BITS + (p & 1) * 2 + io)) | (ix >> (FK_BITS + (p & 1) * 2))) & 1u);
         }
     }
     // one candidate row pair per lane: the edges on lanes 0-5, the corners on lanes 6-9 (a single
     // bit each side); contact p of own row -> own entry S[ab + (p >> 1) as], neighbour entry
     // E[bb + (q >> 1)]; one emit site (the loops stay rolled: a copy of the emit path per
     // direction would blow the kernel past the instruction cache)
-    u64 a = 0, b = 0;
+    u64 a = 0, b = 0, im = 0;
     int ab = 0, as = 0, bb = 0, oz = 0, oy = 0, ox = 0;
     if (lane < 6) {
         const int e = lane;
 #pragma unroll
-        for (int i = 0; i < 6; ++i) if (i == e) { a = A[i]; b = B[i]; }
+        for (int i = 0; i < 6; ++i) if (i == e) { a = A[i]; b = B[i]; im = I[i]; }
         const int s = (e & 1) ? 1 : -1;
         // neighbour offset (oz, oy, ox): tn = t + oz sz + oy sy + ox
         oz = e < 4 ? -1 : 0; oy = e < 2 ? s : e < 4 ? 0 : -1; ox = e < 2 ? 0 : s;
@@ -1674,6 +1707,7 @@ __device__ __forceinline__ void seam_edges_rows(const Geom& g, const face_t* S, 
             // a diagonal contact a[p] - b[p + d] whose pair a (0) contact also gives (a[p + d] or
             // b[p] set: neighbours along the line are one component of their tile) is dropped
             if (d) C &= ~((d > 0 ? a >> 1 : a << 1) | b);
+            C &= ~(im | (d > 0 ? im >> 1 : d < 0 ? im << 1 : im));    // through a face neighbour
             for (u64 m = C & ~(C << 1); m; m &= m - 1) {
                 const int p = __builtin_ctzll(m), q = p + d;
                 const u32 ka = S[ab + (p >> 1) * as] & FK_MASK, kb = E[bb + (q >> 1)] & FK_MASK;
@@ -1710,20 +1744,25 @@ __device__ __forceinline__ void seams_tile(const Geom& g, const face_t* __restri
     u32* H = Hall[w];
     TileInfo ti;
     face_t* E = Eall[w];
+    // block-local position of the own tile and the tile strides inside its block (a neighbour in
+    // the same block at offset (oz, oy, ox) is lt_own + oz bny bnx + oy bnx + ox)
+    int lz = 0, ly = 0, lx = 0, bny = 0, bnx_ = 0;
+    InBlock nb{};
     if (valid) {
         ti = tile_info(g, t);
+        const int bz = g.tblk[0][ti.iz], by = g.tblk[1][ti.iy], bx = g.tblk[2][ti.ix];
+        lz = ti.iz - g.bt0[0][bz]; ly = ti.iy - g.bt0[1][by]; lx = ti.ix - g.bt0[2][bx];
+        bny = g.btn[1][by]; bnx_ = g.btn[2][bx];
+        nb.z = lz > 0; nb.ym = ly > 0; nb.yp = ly + 1 < bny; nb.xm = lx > 0; nb.xp = lx + 1 < bnx_;
         stage_faces(g, FACES, t, ti, S, lane, 64);
-        stage_edges(g, FACES, t, ti, E, lane);
+        stage_edges(g, FACES, t, nb, E, lane);
     }
     for (int i = lane; i < SEAM_HASH; i += 64) H[i] = NONE;
     if (lane < 2) cnt[w][lane] = 0;
     __syncthreads();
     if (!valid) return;
-    // block-local index of the own tile and the tile strides inside its block (a neighbour in
-    // the same block at offset (oz, oy, ox) is lt_own + oz bny bnx + oy bnx + ox)
-    const int bz = g.tblk[0][ti.iz], by = g.tblk[1][ti.iy], bx = g.tblk[2][ti.ix];
-    const u32 bnx = (u32)g.btn[2][bx], bnyx = (u32)g.btn[1][by] * bnx;
-    const u32 lt_own = (u32)(ti.iz - g.bt0[0][bz]) * bnyx + (u32)(ti.iy - g.bt0[1][by]) * bnx + (u32)(ti.ix - g.bt0[2][bx]);
+    const u32 bnx = (u32)bnx_, bnyx = (u32)bny * bnx;
+    const u32 lt_own = (u32)lz * bnyx + (u32)ly * bnx + (u32)lx;
     const u32 capu = (u32)g.cap;
     u64* out = PAIRS + t * TPC;
     u64* iout = IPAIRS + t * TPI;
@@ -1782,10 +1821,7 @@ __device__ __forceinline__ void seams_tile(const Geom& g, const face_t* __restri
     };
     const int64_t sz = (int64_t)g.nt[1] * g.nt[2], sy = g.nt[2];
     // the three lower seams: neighbour tile, mode (0 none, 1 intra 26-conn, 2 block face 6-conn)
-    int mode[3] = {0, 0, 0};
-    if (ti.iz > 0) mode[0] = g.tblk[0][ti.iz] == g.tblk[0][ti.iz - 1] ? 1 : 2;
-    if (ti.iy > 0) mode[1] = g.tblk[1][ti.iy] == g.tblk[1][ti.iy - 1] ? 1 : 2;
-    if (ti.ix > 0) mode[2] = g.tblk[2][ti.ix] == g.tblk[2][ti.ix - 1] ? 1 : 2;
+    const int mode[3] = {nb.z ? 1 : ti.iz > 0 ? 2 : 0, nb.ym ? 1 : ti.iy > 0 ? 2 : 0, nb.xm ? 1 : ti.ix > 0 ? 2 : 0};
     const int myseam = lane < 32 ? 0 : lane < 48 ? 1 : 2;
     const int64_t tn_l = t - (myseam == 0 ? sz : myseam == 1 ? sy : 1);
     const u32 code_l = myseam == 0 ? 13u : myseam == 1 ? 1u : 3u;    // (-1,0,0) / (0,-1,0) / (0,0,-1)
@@ -1798,7 +1834,7 @@ __device__ __forceinline__ void seams_tile(const Geom& g, const face_t* __restri
     });
     if (STOP != 4) {
         // edges and corners inside the block
-        seam_edges_rows(g, S, E, t, ti, lane, [&](int oz, int oy, int ox, u32 k1, u32 k2) {
+        seam_edges_rows(S, E, ti, nb, lane, [&](int oz, int oy, int ox, u32 k1, u32 k2) {
             const u32 code = (u32)(-oz * 9 + (oy + 1) * 3 + (ox + 1));
             if (!fresh(code, k1, k2)) return;
             const u32 lt_e = lt_own + (u32)(oz * (int)bnyx + oy * (int)bnx + ox);

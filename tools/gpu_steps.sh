@@ -10,7 +10,7 @@
 #   tests          the whole -m gpu suite                                   -> tests_TAG.log
 #   tests_sharded  tests/test_gpu_sharded.py only;  tests_parity  parity + watershed + workflow files
 #   bench_sync / bench_c2_sync   the host-synchronised schedule (CC_FAST=0), same-box A/B
-#   prof_c3 / prof_c3_mask   rocprofv3 trace + FETCH/WRITE passes (tools/profile.sh)
+#   prof_c3 / prof_c3_mask / prof_cont / prof_c2 / prof_c1   rocprofv3 trace + FETCH/WRITE passes (tools/profile.sh)
 #   trace_slabs8   rocprofv3 kernel trace of the 8-slab schedule
 #   evidence       rocprof summaries of the secondary kernels (threshold, stage path, 8-slab seams of
 #                  both schedules, Gaussian prefilter, resized mask + 4-D normalize, watershed);  prof_c4  C3 + mask with the --narrow correction
@@ -51,6 +51,9 @@ for step in "$@"; do
     tests_sharded) timeout -k 10 900 $PYT tests/test_gpu_sharded.py > $O/tests_sharded_$TAG.log 2>&1 || { tail -40 $O/tests_sharded_$TAG.log; exit 1; }; tail -3 $O/tests_sharded_$TAG.log ;;
     prof_c3)    tools/profile.sh "${TAG}_c3" --steps 10 --warmup 3 ;;
     prof_c3_mask) tools/profile.sh "${TAG}_c3_mask" --steps 10 --warmup 3 --mask ;;
+    prof_cont)  tools/profile.sh "${TAG}_c3_cont" --steps 10 --warmup 3 --dither ;;
+    prof_c2)    tools/profile.sh "${TAG}_c2" --workload c2 --steps 20 --warmup 5 ;;
+    prof_c1)    tools/profile.sh "${TAG}_c1" --workload c1 --steps 20 --warmup 5 ;;
     evidence)   # rocprof trace + FETCH / WRITE of the secondary kernels (tools/profile_cmd.sh)
                 P=tools/profile_cmd.sh
                 $P ${TAG}_threshold tools/bench_threshold.py
