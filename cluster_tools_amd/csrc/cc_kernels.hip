@@ -710,6 +710,59 @@ __device__ __forceinline__ u32 block_minmax(u32 v, u32* red) {
     return v;
 }
 
+// k_spec's float4 input loads, non-temporal (the input is read once): C3 k_spec 3.09-3.11 ->
+// 2.98-3.00 ms, C4 4.06 -> 3.97 ms on a fast-kind box (profiles/r05_ab_ntload.txt; CC_SPEC_NTLOAD=0
+// for A/B)
+#ifndef CC_SPEC_NTLOAD
+#define CC_SPEC_NTLOAD 1
+#endif
+__device__ __forceinline__ float4 ld_in4(const float* p) {
+#if CC_SPEC_NTLOAD
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+    return float4{v.x, v.y, v.z, v.w};
+#else
+    return *reinterpret_cast<const float4*>(p);
+#endif
+}
+
+// k_sample's rows, non-temporal too (C3 k_sample 0.114 -> 0.055 ms; CC_SAMPLE_NT=0 for A/B).  The
+// other read-once streams measured worse or equal that way (CC_RD_NT, A/B only: k_spec's mask
+// 4.40 -> 4.89 ms at C4, k_seams' face planes 0.272 -> 0.285 ms, k_pass2's bit rows equal), and so
+// did k_pass2's label stores (CC_P2_NTSTORE: 5.52 -> 5.80 ms): profiles/r05_ab_ntload.txt
+#ifndef CC_SAMPLE_NT
+#define CC_SAMPLE_NT 1
+#endif
+#ifndef CC_RD_NT
+#define CC_RD_NT 0
+#endif
+#ifndef CC_P2_NTSTORE
+#define CC_P2_NTSTORE 0
+#endif
+template <class T>
+__device__ __forceinline__ T ld_once(const T* p) {
+    if constexpr (CC_RD_NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+__device__ __forceinline__ float4 ld_sample4(const float* p) {
+#if CC_SAMPLE_NT
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+    return float4{v.x, v.y, v.z, v.w};
+#else
+    return *reinterpret_cast<const float4*>(p);
+#endif
+}
+__device__ __forceinline__ uint4 ld_once_u4(const void* p) {
+#if CC_RD_NT
+    typedef u32 v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    return uint4{v.x, v.y, v.z, v.w};
+#else
+    return *reinterpret_cast<const uint4*>(p);
+#endif
+}
+
 // k_sample: workgroup (b, part) reads every SAMPLE_PARTS-th sample row of block b and writes its
 // (min, 0, max, 0); k_guess combines the parts of each block.
 constexpr int SAMPLE_PARTS = 8;
@@ -795,7 +848,7 @@ __global__ __launch_bounds__(NTHREADS) void k_sample(Geom g, const float* __rest
                     const int j = min(j0 + 4 * u + slot, nj - 1);             // repeats are harmless
                     const int r = pt + SAMPLE_PARTS * j;
                     const int z = e0[0] + (r / nys) * SAMPLE_DZ + zo, y = e0[1] + (r % nys) * SAMPLE_DY + yo;
-                    v[u] = *reinterpret_cast<const float4*>(in + ((int64_t)z * g.Y + y) * g.X + e0[2] + x);
+                    v[u] = ld_sample4(in + ((int64_t)z * g.Y + y) * g.X + e0[2] + x);
                 }
 #pragma unroll
                 for (int u = 0; u < SAMPLE_U; ++u) {
@@ -942,14 +995,14 @@ __device__ __forceinline__ bool spec_front(const Geom& g, const SpecArgs& sa, in
             float4 v[RZ4];
             uchar4 mk[RZ4];
 #if CC_MASK_STAGE
-            if (HAS_MASK) reinterpret_cast<uint4*>(mstage)[lane] = *reinterpret_cast<const uint4*>(mz16 + z0 * sz);
+            if (HAS_MASK) reinterpret_cast<uint4*>(mstage)[lane] = ld_once_u4(mz16 + z0 * sz);
             auto ld = [&](int a) {
-                v[a] = *reinterpret_cast<const float4*>(pz + (z0 + a) * sz);
+                v[a] = ld_in4(pz + (z0 + a) * sz);
                 if (HAS_MASK) mk[a] = __builtin_bit_cast(uchar4, mstage[a * 64 + lane]);
             };
 #else
             auto ld = [&](int a) {
-                v[a] = *reinterpret_cast<const float4*>(pz + (z0 + a) * sz);
+                v[a] = ld_in4(pz + (z0 + a) * sz);
                 if (HAS_MASK) mk[a] = *reinterpret_cast<const uchar4*>(mz + (z0 + a) * sz);
             };
 #endif
@@ -1178,7 +1231,7 @@ __device__ __forceinline__ void stage_faces(const Geom& g, const face_t* __restr
         for (int j = 0; j < NJ; ++j) {
             const int w = tid + 64 * j;
             const int64_t ts = src(128 * j);
-            v[j] = (w < FACE_STRIDE / 2 && ts >= 0) ? FW[ts * (FACE_STRIDE / 2) + w] : 0u;
+            v[j] = (w < FACE_STRIDE / 2 && ts >= 0) ? ld_once(FW + ts * (FACE_STRIDE / 2) + w) : 0u;
         }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
@@ -2951,7 +3004,12 @@ constexpr int LABCAP = 2048;          // component labels cached in LDS
 // 5.50 ms at C3, same box)
 __device__ __forceinline__ void store2(u64* __restrict__ out, int64_t idx, u64 v0, u64 v1, bool two, bool vec) {
     if (two && vec) {
+#if CC_P2_NTSTORE
+        typedef u64 v2u __attribute__((ext_vector_type(2)));
+        __builtin_nontemporal_store(v2u{v0, v1}, reinterpret_cast<v2u*>(out + idx));
+#else
         *reinterpret_cast<ulonglong2*>(out + idx) = make_ulonglong2(v0, v1);
+#endif
     } else {
         out[idx] = v0;
         if (two) out[idx + 1] = v1;
@@ -3022,7 +3080,7 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
         const u32 k = tid + j * NTHREADS;
         lv[j] = k < R ? label(base + k) : 0ull;
     }
-    for (int i = tid; i < NROWS; i += NTHREADS) rows[i] = BITS[t * NROWS + i];
+    for (int i = tid; i < NROWS; i += NTHREADS) rows[i] = ld_once(BITS + t * NROWS + i);
     __syncthreads();
     tile_ccl(rows, T, (u32*)lab);
 #pragma unroll
@@ -3240,6 +3298,8 @@ __global__ __launch_bounds__(NTHREADS) void k_thr_spec(Geom g, SpecArgs sa, cons
 #pragma unroll 2
     for (int z = 0; z < TZ; ++z) {
         const float4* q = reinterpret_cast<const float4*>(pin + z * sz);
+        // (plain loads: non-temporal ones, as in k_spec, made this kernel 4.4 -> 5.7 ms,
+        // profiles/r05_ab_ntload.txt)
         const float4 v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3];
         uint4 r;
         r.x = quad(v0); r.y = quad(v1); r.z = quad(v2); r.w = quad(v3);
