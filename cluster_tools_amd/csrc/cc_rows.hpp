@@ -17,6 +17,15 @@ namespace cc {
 // x extent re-load the last column (duplicates: harmless to min / max; the bit rows are masked
 // by the caller) and rows past the extent are skipped (f is not called for them).
 constexpr int RZ = 4;                       // planes per round
+// the input's loads (CC_ROWS_NT, A/B only: non-temporal, as k_spec's float4 path -- C1 k_spec 0.258
+// -> 0.223 ms but k_pass2 0.433 -> 0.484 ms after it, profiles/r05_ab_ntload.txt)
+#ifndef CC_ROWS_NT
+#define CC_ROWS_NT 0
+#endif
+__device__ __forceinline__ float ld_row(const float* p) {
+    if constexpr (CC_ROWS_NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
 #ifndef CC_MASK_RZ
 #define CC_MASK_RZ 2
 #endif
@@ -45,7 +54,7 @@ __device__ __forceinline__ void for_tile_rows(const Geom& g, const TileInfo& ti,
             for (int a = 0; a < RZ_; ++a)
 #pragma unroll
                 for (int b = 0; b < RY; ++b) {
-                    v[a][b] = pz[a * sz + b * sy + lane];
+                    v[a][b] = ld_row(pz + a * sz + b * sy + lane);
                     if (HAS_MASK) mk[a][b] = mz[(z0 + a) * sz + b * sy + lane];
                 }
 #pragma unroll
@@ -70,7 +79,7 @@ __device__ __forceinline__ void for_tile_rows(const Geom& g, const TileInfo& ti,
                 mk[a][b] = 0;
                 if (lz < ti.lz && ly < ti.ly) {
                     const int64_t row = o0 + lz * sz + b * sy;
-                    v[a][b] = in[row + lx];
+                    v[a][b] = ld_row(in + row + lx);
                     if (HAS_MASK) mk[a][b] = mask[row + lx];
                 }
             }
