@@ -5,6 +5,7 @@
 //                 instruction, R planes x 4 rows = 4R loads in flight per lane, 512-thread tiles
 //   rd_tile4_rzR  the same tile walk with float4 per lane (16 lanes per 64-float row, 4 rows per
 //                 load instruction), R planes x 4 row groups in flight
+//   rd_tile4_nt_rzR  the same with non-temporal loads (k_spec's input loads)
 //   wr_u2_uU      16-B uint64 pair stores per lane, U per lane per iteration
 // Run: tools/roof Z Y X [iters]
 #include <hip/hip_runtime.h>
@@ -62,7 +63,7 @@ __global__ __launch_bounds__(512) void rd_tile(const float* __restrict__ in, int
 }
 
 // float4 lanes: lane l reads x = 4 (l % 16) .. + 3 of row group row 4 * (wave-slot) + l / 16
-template <int RZ>
+template <int RZ, bool NT = false>
 __global__ __launch_bounds__(512) void rd_tile4(const float* __restrict__ in, int64_t Y, int64_t X, int ntx, int nty,
                                                 float* out) {
     const int t = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -75,7 +76,15 @@ __global__ __launch_bounds__(512) void rd_tile4(const float* __restrict__ in, in
     for (int z0 = 0; z0 < 16; z0 += RZ) {
         float4 v[RZ];
 #pragma unroll
-        for (int a = 0; a < RZ; ++a) v[a] = *reinterpret_cast<const float4*>(p + (z0 + a) * sz);
+        for (int a = 0; a < RZ; ++a) {
+            if constexpr (NT) {          // non-temporal, as k_spec's input loads
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                const v4f w = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p + (z0 + a) * sz));
+                v[a] = float4{w.x, w.y, w.z, w.w};
+            } else {
+                v[a] = *reinterpret_cast<const float4*>(p + (z0 + a) * sz);
+            }
+        }
 #pragma unroll
         for (int a = 0; a < RZ; ++a) mx = fmaxf(mx, fmaxf(fmaxf(v[a].x, v[a].y), fmaxf(v[a].z, v[a].w)));
     }
@@ -211,6 +220,8 @@ int main(int argc, char** argv) {
     r.push_back({"rd_tile4_rz4", time_ms(s, iters, [&] { rd_tile4<4><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
     r.push_back({"rd_tile4_rz8", time_ms(s, iters, [&] { rd_tile4<8><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
     r.push_back({"rd_tile4_rz16", time_ms(s, iters, [&] { rd_tile4<16><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
+    r.push_back({"rd_tile4_nt_rz1", time_ms(s, iters, [&] { rd_tile4<1, true><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
+    r.push_back({"rd_tile4_nt_rz4", time_ms(s, iters, [&] { rd_tile4<4, true><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
     r.push_back({"wr_u2_u1", time_ms(s, iters, [&] { wr_u2<1><<<g * 8, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
     r.push_back({"wr_u2_u4", time_ms(s, iters, [&] { wr_u2<4><<<g * 2, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
     r.push_back({"wr_u2_u8", time_ms(s, iters, [&] { wr_u2<8><<<g, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
