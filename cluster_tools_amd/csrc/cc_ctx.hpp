@@ -438,6 +438,7 @@ struct RunState {
     uint64_t base = 0;         // global id base of this slab
     int64_t n_map = 0;         // seam mapping size
     bool local_only = false;
+    bool masked = false;       // a mask was given (k_pass2's tile order)
     int64_t bs[3] = {0, 0, 0};  // block_shape
     uint64_t n_fix = 0;        // tiles relabelled by k_fix
     bool identity_lut = false; // the empty-job emulation dropped every block-face merge

@@ -897,10 +897,13 @@ __device__ __forceinline__ int64_t xcd_contig(int64_t b, int64_t n) {
     return k * q + (k < r ? k : r) + i;
 }
 
-// mask bytes 16 per lane through LDS (default; CC_MASK_STAGE=0: 4-B mask loads per plane, A/B
-// only): C4 k_spec<true> 4.90-4.95 -> 4.72-4.76 ms on a slow box (profiles/r05_ab_mstage.txt)
+// mask bytes: 4 per lane and plane (default), or 16 per lane staged through LDS (CC_MASK_STAGE=1,
+// A/B only).  With plain input loads the staging won on the slow box kind (C4 k_spec<true>
+// 4.90-4.95 -> 4.72-4.76 ms) and lost on the fast one (profiles/r05_ab_mstage*.txt); with the
+// non-temporal input loads the 4-B loads win (fast kind 4.04-4.07 -> 3.96-3.97 ms:
+// profiles/r05_ab_c4_order_mask.txt)
 #ifndef CC_MASK_STAGE
-#define CC_MASK_STAGE 1
+#define CC_MASK_STAGE 0
 #endif
 
 // The front of k_spec for tile t: the tile's voxels in one read -> exact statistics (the

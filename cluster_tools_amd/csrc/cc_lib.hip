@@ -34,6 +34,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
     st.thr = (float)threshold;                // numpy: python float -> float32
     st.mode = mode;
     st.local_only = local_only;
+    st.masked = mask != nullptr;
     const int64_t nt = g.n_tiles, nb = g.n_blocks;
     const uint64_t nodes = (uint64_t)nt * g.cap;
     hipStream_t s = cstream(c);
@@ -625,7 +626,9 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
         // tile order of the write pass (see k_pass2): z fastest for rows of >= 4096 voxels,
         // XCD-contiguous for label rows that are not 128-B aligned (CC_PASS2_ORDER = 0 / 1 / 2
         // forces one, A/B only)
-        int order = g.X >= 4096 ? 1 : (g.X & 15) ? 2 : 0;
+        // (and XCD-contiguous for masked volumes: C4 k_pass2 5.68-5.74 -> 5.63 ms,
+        // profiles/r05_ab_c4_order_mask.txt; C3 unmasked is slower that way, 5.49-5.53 -> 5.70)
+        int order = g.X >= 4096 ? 1 : ((g.X & 15) || st.masked) ? 2 : 0;
         if (const char* e = std::getenv("CC_PASS2_ORDER"); e && *e) order = std::min(std::max(std::atoi(e), 0), 2);
         // CC_LDS_PAD_P2 (A/B only): extra dynamic LDS per workgroup, i.e. fewer tiles per CU
         const unsigned pad = (unsigned)env_int("CC_LDS_PAD_P2", 0);
