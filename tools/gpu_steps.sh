@@ -19,7 +19,7 @@
 #   ab_fast        same-box round-robin A/B: one-read-back vs host-synchronised schedule (C3)
 #   boxinfo        the lease's static / current SMI info (product, VBIOS, power cap, clocks, memory)
 #   clockprobe     core clock per kernel from in-kernel clock stamps (tools/clock_probe)
-#   slowdiag       a short bench first; only when k_spec runs slow (> 3.45 ms, the driver's slow box
+#   slowdiag       a short bench first; only when k_spec runs slow (> 3.3 ms, the driver's slow box
 #                  kind) the box's roof, the k_spec ablation, the clock probe and the PMC passes
 #                  (TCP latency / UTCL1, SQ instruction + wait counters) -> *_slow_TAG
 set -e -o pipefail
@@ -79,7 +79,7 @@ for step in "$@"; do
     slowdiag)   timeout -k 10 240 python -u bench.py --no-cpu-baseline --steps 10 --warmup 3 > $O/sd_bench_$TAG.json 2> $O/sd_bench_$TAG.err
                 KS=$(python3 -c "import json; d = json.loads(open('$O/sd_bench_$TAG.json').read().strip().splitlines()[-1]); print(d['kernels_ms_per_step']['k_spec'])")
                 echo "k_spec $KS ms"
-                if python3 -c "import sys; sys.exit(0 if $KS > 3.45 else 1)"; then
+                if python3 -c "import sys; sys.exit(0 if $KS > 3.3 else 1)"; then
                   echo "slow box kind: diagnostics"
                   timeout -k 10 300 tools/roof 1024 2048 2048 5 > $O/roof_slow_$TAG.txt 2>&1
                   timeout -k 10 300 tools/ablate 1024 2048 2048 64 512 512 0 10 > $O/ablate_slow_$TAG.txt 2>&1
