@@ -7,6 +7,7 @@
 //                 load instruction), R planes x 4 row groups in flight
 //   rd_tile4_nt_rzR  the same with non-temporal loads (k_spec's input loads)
 //   wr_u2_uU      16-B uint64 pair stores per lane, U per lane per iteration
+//   mix_wW_*      the non-temporal tile read plus W 4-B words stored per tile (k_spec: 1920)
 // Run: tools/roof Z Y X [iters]
 #include <hip/hip_runtime.h>
 
@@ -189,6 +190,32 @@ static double time_ms(hipStream_t s, int iters, F&& f) {
     return ms / iters;
 }
 
+// k_spec's memory pattern without its compute: the non-temporal tile read (rd_tile4_nt, one plane
+// in flight) plus W 4-byte words stored per tile after the read (BITS 1024 words + FACES 896 words
+// = 1920 in k_spec), non-temporally (NT) or plainly: how much a side stream of stores costs the read
+template <int W, bool NT>
+__global__ __launch_bounds__(512) void mix_tile(const float* __restrict__ in, int64_t Y, int64_t X, int ntx, int nty,
+                                                unsigned* __restrict__ side) {
+    const int t = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int tx = t % ntx, ty = (t / ntx) % nty, tz = t / (ntx * nty);
+    const float* p = in + (((int64_t)tz * 16) * Y + ty * 32 + 4 * wave + (lane >> 4)) * X + tx * 64 + 4 * (lane & 15);
+    const int64_t sz = Y * X;
+    float mx = -1e30f;
+#pragma unroll
+    for (int z = 0; z < 16; ++z) {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        asm volatile("" ::: "memory");
+        const v4f w = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p + z * sz));
+        mx = fmaxf(mx, fmaxf(fmaxf(w.x, w.y), fmaxf(w.z, w.w)));
+    }
+    const unsigned v = __float_as_uint(mx);
+    unsigned* q = side + (int64_t)t * W;
+    for (int i = threadIdx.x; i < W; i += 512) {
+        if (NT) __builtin_nontemporal_store(v + i, q + i);
+        else q[i] = v + i;
+    }
+}
+
 int main(int argc, char** argv) {
     const int64_t Z = argc > 1 ? atoll(argv[1]) : 1024, Y = argc > 2 ? atoll(argv[2]) : 2048,
                   X = argc > 3 ? atoll(argv[3]) : 2048;
@@ -222,6 +249,16 @@ int main(int argc, char** argv) {
     r.push_back({"rd_tile4_rz16", time_ms(s, iters, [&] { rd_tile4<16><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
     r.push_back({"rd_tile4_nt_rz1", time_ms(s, iters, [&] { rd_tile4<1, true><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
     r.push_back({"rd_tile4_nt_rz4", time_ms(s, iters, [&] { rd_tile4<4, true><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
+    // read + side stores per tile (the side buffer is the start of `out`: nt * 1920 words)
+#define MIX(W, NT, NAME) r.push_back({NAME, time_ms(s, iters, [&] { mix_tile<W, NT><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, (unsigned*)out); })});
+    MIX(128, true, "mix_w128_nt")
+    MIX(256, true, "mix_w256_nt")
+    MIX(512, true, "mix_w512_nt")
+    MIX(1024, true, "mix_w1024_nt")
+    MIX(1472, true, "mix_w1472_nt")
+    MIX(1920, true, "mix_w1920_nt")
+    MIX(1920, false, "mix_w1920_plain")
+#undef MIX
     r.push_back({"wr_u2_u1", time_ms(s, iters, [&] { wr_u2<1><<<g * 8, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
     r.push_back({"wr_u2_u4", time_ms(s, iters, [&] { wr_u2<4><<<g * 2, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
     r.push_back({"wr_u2_u8", time_ms(s, iters, [&] { wr_u2<8><<<g, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
