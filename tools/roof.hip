@@ -214,6 +214,14 @@ __global__ __launch_bounds__(512) void mix_tile(const float* __restrict__ in, in
         if (NT) __builtin_nontemporal_store(v + i, q + i);
         else q[i] = v + i;
     }
+    if ((int)threadIdx.x >= W && v == 0x12345678u) q[0] = v;  // keeps every thread's loads live
+}
+
+// The side stores alone (no reads): what the 1920 words/tile would cost in a phase of their own.
+template <int W>
+__global__ __launch_bounds__(512) void side_only(unsigned* __restrict__ side) {
+    unsigned* q = side + (int64_t)blockIdx.x * W;
+    for (int i = threadIdx.x; i < W; i += 512) __builtin_nontemporal_store((unsigned)(blockIdx.x + i), q + i);
 }
 
 int main(int argc, char** argv) {
@@ -251,6 +259,7 @@ int main(int argc, char** argv) {
     r.push_back({"rd_tile4_nt_rz4", time_ms(s, iters, [&] { rd_tile4<4, true><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, dummy); })});
     // read + side stores per tile (the side buffer is the start of `out`: nt * 1920 words)
 #define MIX(W, NT, NAME) r.push_back({NAME, time_ms(s, iters, [&] { mix_tile<W, NT><<<nt, 512, 0, s>>>(in, Y, X, ntx, nty, (unsigned*)out); })});
+    MIX(0, true, "mix_w0")
     MIX(128, true, "mix_w128_nt")
     MIX(256, true, "mix_w256_nt")
     MIX(512, true, "mix_w512_nt")
@@ -259,6 +268,8 @@ int main(int argc, char** argv) {
     MIX(1920, true, "mix_w1920_nt")
     MIX(1920, false, "mix_w1920_plain")
 #undef MIX
+    r.push_back({"side_only_w1920", time_ms(s, iters, [&] { side_only<1920><<<nt, 512, 0, s>>>((unsigned*)out); })});
+    r.push_back({"side_only_w1024", time_ms(s, iters, [&] { side_only<1024><<<nt, 512, 0, s>>>((unsigned*)out); })});
     r.push_back({"wr_u2_u1", time_ms(s, iters, [&] { wr_u2<1><<<g * 8, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
     r.push_back({"wr_u2_u4", time_ms(s, iters, [&] { wr_u2<4><<<g * 2, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
     r.push_back({"wr_u2_u8", time_ms(s, iters, [&] { wr_u2<8><<<g, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
