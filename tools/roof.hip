@@ -217,6 +217,98 @@ __global__ __launch_bounds__(512) void mix_tile(const float* __restrict__ in, in
     if ((int)threadIdx.x >= W && v == 0x12345678u) q[0] = v;  // keeps every thread's loads live
 }
 
+// Persistent form of mix_tile: G workgroups walk tiles t = k*G + g; each keeps the side words of
+// E consecutive tiles in LDS and stores them together, so the chip's stores come in bunches
+// between read stretches (no grid barrier: uniform work keeps the workgroups roughly in step).
+template <int W, int E>
+__global__ __launch_bounds__(512) void mix_epoch(const float* __restrict__ in, int64_t Y, int64_t X, int ntx, int nty,
+                                                 int ntiles, unsigned* __restrict__ side) {
+    __shared__ unsigned buf[E * W];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t sz = Y * X;
+    int e = 0, t0 = blockIdx.x;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int tx = t % ntx, ty = (t / ntx) % nty, tz = t / (ntx * nty);
+        const float* p = in + (((int64_t)tz * 16) * Y + ty * 32 + 4 * wave + (lane >> 4)) * X + tx * 64 + 4 * (lane & 15);
+        float mx = -1e30f;
+#pragma unroll
+        for (int z = 0; z < 16; ++z) {
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            asm volatile("" ::: "memory");
+            const v4f w = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p + z * sz));
+            mx = fmaxf(mx, fmaxf(fmaxf(w.x, w.y), fmaxf(w.z, w.w)));
+        }
+        const unsigned v = __float_as_uint(mx);
+        for (int i = threadIdx.x; i < W; i += 512) buf[e * W + i] = v + i;
+        if (++e == E || t + (int)gridDim.x >= ntiles) {
+            __syncthreads();
+            for (int k = 0; k < e; ++k) {
+                unsigned* q = side + (int64_t)(t0 + k * (int)gridDim.x) * W;
+                for (int i = threadIdx.x; i < W; i += 512) __builtin_nontemporal_store(buf[k * W + i], q + i);
+            }
+            __syncthreads();
+            e = 0;
+            t0 = t + gridDim.x;
+        }
+    }
+}
+
+// Bounded grid barrier (thread 0 of each workgroup arrives and spins; gives up after ~2^20 polls and
+// counts the give-up in tmo, so a non-resident grid skews a timing instead of hanging the device).
+__device__ inline void grid_sync(unsigned* ctr, unsigned target, unsigned* tmo) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        atomicAdd(ctr, 1u);
+        int spins = 0;
+        while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (++spins > (1 << 20)) {
+                atomicAdd(tmo, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+}
+
+// mix_epoch with chip-wide phases: every workgroup reads E tiles (side words into LDS), grid
+// barrier, every workgroup stores its E tiles' words, grid barrier — the stores no longer share
+// the memory with the read stream (G must be resident at once).
+template <int W, int E>
+__global__ __launch_bounds__(512) void mix_gbar(const float* __restrict__ in, int64_t Y, int64_t X, int ntx, int nty,
+                                                int ntiles, unsigned* __restrict__ side, unsigned* ctr, unsigned* tmo) {
+    __shared__ unsigned buf[E * W];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t sz = Y * X;
+    const int G = gridDim.x, tpw = ntiles / G;
+    unsigned nbar = 0;
+    for (int k0 = 0; k0 < tpw; k0 += E) {
+        const int ne = tpw - k0 < E ? tpw - k0 : E;
+        for (int e = 0; e < ne; ++e) {
+            const int t = (k0 + e) * G + blockIdx.x;
+            const int tx = t % ntx, ty = (t / ntx) % nty, tz = t / (ntx * nty);
+            const float* p = in + (((int64_t)tz * 16) * Y + ty * 32 + 4 * wave + (lane >> 4)) * X + tx * 64 + 4 * (lane & 15);
+            float mx = -1e30f;
+#pragma unroll
+            for (int z = 0; z < 16; ++z) {
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                asm volatile("" ::: "memory");
+                const v4f w = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p + z * sz));
+                mx = fmaxf(mx, fmaxf(fmaxf(w.x, w.y), fmaxf(w.z, w.w)));
+            }
+            const unsigned v = __float_as_uint(mx);
+            for (int i = threadIdx.x; i < W; i += 512) buf[e * W + i] = v + i;
+        }
+        grid_sync(ctr, ++nbar * G, tmo);
+        for (int e = 0; e < ne; ++e) {
+            unsigned* q = side + (int64_t)((k0 + e) * G + blockIdx.x) * W;
+            for (int i = threadIdx.x; i < W; i += 512) __builtin_nontemporal_store(buf[e * W + i], q + i);
+        }
+        grid_sync(ctr, ++nbar * G, tmo);
+    }
+}
+
 // The side stores alone (no reads): what the 1920 words/tile would cost in a phase of their own.
 template <int W>
 __global__ __launch_bounds__(512) void side_only(unsigned* __restrict__ side) {
@@ -268,6 +360,31 @@ int main(int argc, char** argv) {
     MIX(1920, true, "mix_w1920_nt")
     MIX(1920, false, "mix_w1920_plain")
 #undef MIX
+#define EP(E, G, NAME) r.push_back({NAME, time_ms(s, iters, [&] { mix_epoch<1920, E><<<G, 512, 0, s>>>(in, Y, X, ntx, nty, (int)nt, (unsigned*)out); })});
+    EP(1, 512, "epoch_e1_g512")
+    EP(4, 512, "epoch_e4_g512")
+    EP(8, 512, "epoch_e8_g512")
+    EP(4, 1024, "epoch_e4_g1024")
+    EP(8, 1024, "epoch_e8_g1024")
+#undef EP
+    unsigned* bar;
+    CHK(hipMalloc(&bar, 16));
+    CHK(hipMemset(bar, 0, 16));
+#define GB(E, G, NAME)                                                                                               \
+    {                                                                                                               \
+        r.push_back({NAME, time_ms(s, iters, [&] {                                                                  \
+                         CHK(hipMemsetAsync(bar, 0, 4, s));                                                         \
+                         mix_gbar<1920, E><<<G, 512, 0, s>>>(in, Y, X, ntx, nty, (int)nt, (unsigned*)out, bar, bar + 1); \
+                     })});                                                                                          \
+        unsigned h[2];                                                                                              \
+        CHK(hipMemcpy(h, bar, 8, hipMemcpyDeviceToHost));                                                           \
+        r.push_back({std::string(NAME) + "_tmo", (double)h[1]});                                                    \
+        CHK(hipMemset(bar, 0, 16));                                                                                 \
+    }
+    GB(8, 256, "gbar_e8_g256")
+    GB(16, 256, "gbar_e16_g256")
+    GB(8, 512, "gbar_e8_g512")
+#undef GB
     r.push_back({"side_only_w1920", time_ms(s, iters, [&] { side_only<1920><<<nt, 512, 0, s>>>((unsigned*)out); })});
     r.push_back({"side_only_w1024", time_ms(s, iters, [&] { side_only<1024><<<nt, 512, 0, s>>>((unsigned*)out); })});
     r.push_back({"wr_u2_u1", time_ms(s, iters, [&] { wr_u2<1><<<g * 8, 256, 0, s>>>((ulonglong2*)out, n / 2); })});
