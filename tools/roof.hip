@@ -217,6 +217,33 @@ __global__ __launch_bounds__(512) void mix_tile(const float* __restrict__ in, in
     if ((int)threadIdx.x >= W && v == 0x12345678u) q[0] = v;  // keeps every thread's loads live
 }
 
+// mix_tile with k_spec<mask>'s second input: a u8 mask read with plain 4-byte loads beside the
+// non-temporal float4 loads (the masked pass's memory pattern: 5 B per voxel in, W words out).
+template <int W>
+__global__ __launch_bounds__(512) void mix_mask(const float* __restrict__ in, const unsigned* __restrict__ mask, int64_t Y,
+                                                int64_t X, int ntx, int nty, unsigned* __restrict__ side) {
+    const int t = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int tx = t % ntx, ty = (t / ntx) % nty, tz = t / (ntx * nty);
+    const int64_t off = (((int64_t)tz * 16) * Y + ty * 32 + 4 * wave + (lane >> 4)) * X + tx * 64 + 4 * (lane & 15);
+    const float* p = in + off;
+    const unsigned* m = mask + off / 4;
+    const int64_t sz = Y * X;
+    float mx = -1e30f;
+    unsigned mm = 0;
+#pragma unroll
+    for (int z = 0; z < 16; ++z) {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        asm volatile("" ::: "memory");
+        const v4f w = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p + z * sz));
+        mm |= m[z * sz / 4];
+        mx = fmaxf(mx, fmaxf(fmaxf(w.x, w.y), fmaxf(w.z, w.w)));
+    }
+    const unsigned v = __float_as_uint(mx) ^ mm;
+    unsigned* q = side + (int64_t)t * W;
+    for (int i = threadIdx.x; i < W; i += 512) __builtin_nontemporal_store(v + i, q + i);
+    if ((int)threadIdx.x >= W && v == 0x12345678u) q[0] = v;
+}
+
 // Persistent form of mix_tile: G workgroups walk tiles t = k*G + g; each keeps the side words of
 // E consecutive tiles in LDS and stores them together, so the chip's stores come in bunches
 // between read stretches (no grid barrier: uniform work keeps the workgroups roughly in step).
@@ -367,6 +394,14 @@ int main(int argc, char** argv) {
     EP(4, 1024, "epoch_e4_g1024")
     EP(8, 1024, "epoch_e8_g1024")
 #undef EP
+    {
+        unsigned* mask;
+        CHK(hipMalloc(&mask, n));
+        CHK(hipMemset(mask, 1, n));
+        r.push_back({"mask_rd_w0", time_ms(s, iters, [&] { mix_mask<0><<<nt, 512, 0, s>>>(in, mask, Y, X, ntx, nty, (unsigned*)out); })});
+        r.push_back({"mask_mix_w1920", time_ms(s, iters, [&] { mix_mask<1920><<<nt, 512, 0, s>>>(in, mask, Y, X, ntx, nty, (unsigned*)out); })});
+        CHK(hipFree(mask));
+    }
     unsigned* bar;
     CHK(hipMalloc(&bar, 16));
     CHK(hipMemset(bar, 0, 16));
@@ -381,9 +416,11 @@ int main(int argc, char** argv) {
         r.push_back({std::string(NAME) + "_tmo", (double)h[1]});                                                    \
         CHK(hipMemset(bar, 0, 16));                                                                                 \
     }
-    GB(8, 256, "gbar_e8_g256")
-    GB(16, 256, "gbar_e16_g256")
-    GB(8, 512, "gbar_e8_g512")
+    if (std::getenv("ROOF_GBAR")) {  // measured in r05_roof_mix_gbar_fastbox.txt; 6-9 ms each
+        GB(8, 256, "gbar_e8_g256")
+        GB(16, 256, "gbar_e16_g256")
+        GB(8, 512, "gbar_e8_g512")
+    }
 #undef GB
     r.push_back({"side_only_w1920", time_ms(s, iters, [&] { side_only<1920><<<nt, 512, 0, s>>>((unsigned*)out); })});
     r.push_back({"side_only_w1024", time_ms(s, iters, [&] { side_only<1024><<<nt, 512, 0, s>>>((unsigned*)out); })});
