@@ -28,7 +28,7 @@ EXPORTS = (
     'cc_gaussian_smooth_blocks', 'cc_gaussian_taps', 'cc_result_size', 'cc_resize_mask_nearest',
     'cc_watershed_from_seeds', 'cc_shard_dev_begin', 'cc_shard_dev_assign', 'cc_shard_dev_top_cubes',
     'cc_shard_dev_seam_pairs', 'cc_shard_dev_finish', 'cc_normalize_channels', 'cc_shard_dev_ok',
-    'cc_comm_unique_id', 'cc_comm_create', 'cc_comm_destroy', 'cc_label_volume_sharded',
+    'cc_comm_unique_id', 'cc_comm_create', 'cc_comm_destroy', 'cc_label_volume_sharded', 'cc_comm_info',
 )
 # redo flags of the one-read-back schedule (RF_* in csrc/cc_kernels.hip)
 RF_BIG, RF_ROOTS, RF_CUBES, RF_PAIRS, RF_IOVF = 1, 2, 4, 8, 16
@@ -119,6 +119,7 @@ def load():
         'cc_comm_unique_id': (I, [P, i64]),
         'cc_comm_create': (I, [P, I, I, I, ctypes.POINTER(P)]),
         'cc_comm_destroy': (None, [P]),
+        'cc_comm_info': (I, [P, P]),
         'cc_label_volume_sharded': (I, [P, P, P, P, P, i64, i64, P, ctypes.c_double, I, P, ctypes.POINTER(CCResult)]),
         'cc_shard_dev_begin': (I, [P, P, P, P, P, ctypes.c_double, I, i64, P]),
         'cc_shard_dev_assign': (I, [P, P, I, I]),
@@ -248,6 +249,16 @@ class Comm:
         _check(load().cc_comm_create(uid, int(world), int(rank), int(device), ctypes.byref(h)))
         self._h, self.world, self.rank, self.device = h, world, rank, device
 
+    def info(self):
+        """cc_comm_info: world, rank, the last call's schedule ('one-read-back' / 'synchronised' /
+        None), its redo flags (RF_*), the seam-pair capacity, whether an error aborted the
+        communicator, and the number of calls."""
+        out = (ctypes.c_int64 * 8)()
+        _check(load().cc_comm_info(self._h, out))
+        return {'world': out[0], 'rank': out[1],
+                'schedule': {1: 'one-read-back', 0: 'synchronised'}.get(out[2]),
+                'redo': out[3], 'pair_cap': out[4], 'aborted': bool(out[5]), 'calls': out[6]}
+
     def close(self):
         if self._h:
             load().cc_comm_destroy(self._h)
@@ -289,6 +300,7 @@ class Context:
 
     def set_stream(self, stream_ptr):
         _check(load().cc_set_stream(self._h, ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+        self._stream = stream_ptr or None
 
     # ---- fused path ----
     def label_volume(self, inp, block_shape, threshold, mode='greater', mask=None, out=None):
@@ -327,7 +339,9 @@ class Context:
         """This rank's z-slab [z_offset, z_offset + len(slab)) of a volume sharded over comm's ranks
         (cc_label_volume_sharded: the schedule with RCCL inside the library).  `slab` / `mask`:
         CUDA tensors of the slab.  Returns (labels of the slab, result dict with the global
-        n_labels)."""
+        n_labels).  The call is collective (every rank of comm calls it); it is ordered on torch's
+        current stream: on the default (null) stream the library fences its own stream against it,
+        another current stream is bound to the context for the call."""
         import torch
         assert slab.is_cuda and slab.dtype == torch.float32 and slab.is_contiguous() and slab.dim() == 3
         if mask is not None:
@@ -337,9 +351,17 @@ class Context:
             out = torch.empty(tuple(slab.shape), dtype=torch.int64, device=slab.device)
         gs, bs = _i64(global_shape), _i64(block_shape)
         res = CCResult()
-        _check(load().cc_label_volume_sharded(self._h, comm._h, _ptr(slab), _ptr(mask), _ptr(gs), int(z_offset),
-                                              int(slab.shape[0]), _ptr(bs), float(threshold), mode_id(mode), _ptr(out),
-                                              ctypes.byref(res)))
+        prev = getattr(self, '_stream', None)
+        cur = prev or torch.cuda.current_stream(slab.device).cuda_stream or None
+        if cur != prev:
+            self.set_stream(cur)
+        try:
+            _check(load().cc_label_volume_sharded(self._h, comm._h, _ptr(slab), _ptr(mask), _ptr(gs), int(z_offset),
+                                                  int(slab.shape[0]), _ptr(bs), float(threshold), mode_id(mode),
+                                                  _ptr(out), ctypes.byref(res)))
+        finally:
+            if cur != prev:
+                self.set_stream(prev)
         return out, res.as_dict()
 
     def torch_device(self):

@@ -281,6 +281,9 @@ struct cc_ctx {
     uint64_t root_cap = 0;
     bool fast_big = false;
     std::vector<int32_t> fast_big_tab;
+    // the sharded C entry (cc_comm.hip): geometry key of the last z-slab step whose status left
+    // the one-read-back schedule for good (RF_BIG / RF_CUBES / RF_IOVF; 0 none)
+    uint64_t shard_slow_key = 0;
     DevBuf status, hmap_keys, hmap_par;
     uint64_t hm_slots = 0;   // slots of the seam map (shards): cleared by the next front clear (k_sample)
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -366,9 +369,19 @@ static void resolve_profile(cc_ctx* c) {
     c->pending.clear();
 }
 
+// While the sharded C entry runs (cc_comm.hip), host synchronisations go through its bounded
+// wait: it polls the stream with a deadline and the communicator's asynchronous error, so a peer
+// that failed between collectives ends this rank's wait with an error instead of a hang.
+struct SyncHook {
+    void (*wait)(void* arg, hipStream_t s);
+    void* arg;
+};
+static thread_local SyncHook* g_sync_hook = nullptr;
+
 static void stream_sync(hipStream_t st) {
     const auto t0 = std::chrono::steady_clock::now();
-    HIP_OK(hipStreamSynchronize(st));
+    if (g_sync_hook) g_sync_hook->wait(g_sync_hook->arg, st);
+    else HIP_OK(hipStreamSynchronize(st));
     g_sync_count += 1;
     g_sync_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
 }

@@ -270,11 +270,23 @@ int cc_shard_dev_finish(cc_ctx* ctx, const uint64_t* all_dev, int world, int64_t
  * those of cc_label_volume on the whole volume (labels of this slab; res->n_labels global).
  *   cc_comm_unique_id   the RCCL bootstrap id (128 bytes), made on one rank and handed to all
  *   cc_comm_create      one rank's communicator (ncclCommInitRank: collective over the ranks)
+ *   cc_comm_info        out[8]: world, rank, last schedule (1 one-read-back, 0 synchronised,
+ *                       -1 none), RF_* redo flags of the last one-read-back attempt, seam-pair
+ *                       capacity, aborted (0/1), calls, 0
+ * Every call of cc_label_volume_sharded is collective: it begins with an agreement over the ranks
+ * (arguments, volume, slab tiling in rank order), so a bad argument on ANY rank makes every rank
+ * return -1 and the communicator stays usable.  An error after the agreement aborts the
+ * communicator (ncclCommAbort) so peers blocked in a collective return too (every host wait is
+ * bounded by CC_COMM_TIMEOUT seconds, default 300); an aborted communicator refuses further calls
+ * and must be destroyed.  Ordering: with no stream set on the context the call runs on the
+ * communicator's stream, after the work queued on the null stream and before the null stream's
+ * later work.
  * RCCL is opened on first use (an RCCL already in the process, e.g. torch's, is reused;
  * CC_RCCL_PATH overrides). */
 typedef struct cc_comm cc_comm;
 int  cc_comm_unique_id(void* id_out, int64_t cap);
 int  cc_comm_create(const void* id, int world, int rank, int device, cc_comm** out);
+int  cc_comm_info(const cc_comm* comm, int64_t* out);
 void cc_comm_destroy(cc_comm* comm);
 int  cc_label_volume_sharded(cc_ctx* ctx, cc_comm* comm, const float* slab_dev, const uint8_t* mask_dev,
                              const int64_t global_shape[3], int64_t z_offset, int64_t slab_depth,
