@@ -8,6 +8,7 @@ torch CUDA tensors (ROCm) passed by data_ptr().
 """
 import ctypes
 import os
+import sys
 
 import numpy as np
 
@@ -65,22 +66,34 @@ class CCEvalResult(ctypes.Structure):
 
 
 _lib = None
+_host_only = False
 
 
-def load():
-    """Load the shared library and declare signatures (no GPU needed)."""
-    global _lib
+def load(host_only=False):
+    """Load the shared library and declare signatures (no GPU needed).
+
+    One HIP runtime per process: torch bundles its own libamdhip64 (SONAME libamdhip64.so.7), and
+    the library must bind to that one.  Loaded first, the library would pull /opt/rocm's copy and
+    torch would then load a second runtime beside it (the second to initialise sees no device), so
+    torch is imported first.  host_only=True is for processes that never touch torch (the drop-in's
+    job processes on numpy buffers: cc_label_volume_host, cc_merge_offsets): without torch already
+    imported, the library binds the system HIP runtime and the ~2 s torch import is skipped; a later
+    import of torch in such a process is refused here."""
+    global _lib, _host_only
     if _lib is not None:
+        if _host_only and not host_only and 'torch' in sys.modules:
+            raise RuntimeError('libcc_mi355x.so was loaded host-only (without torch) in this process; '
+                               'torch tensors cannot be used with it here')
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError('libcc_mi355x.so not built (%s): run __graft_entry__.build()' % LIB_PATH)
-    # One HIP runtime per process: torch bundles its own libamdhip64 (SONAME libamdhip64.so.7), and
-    # the library must bind to that one.  Loaded first, the library would pull /opt/rocm's copy and
-    # torch would then load a second runtime beside it (the second to initialise sees no device).
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    if host_only and 'torch' not in sys.modules:
+        _host_only = True
+    else:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     L = ctypes.CDLL(LIB_PATH)
     P, i64, u64, I = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int
     sig = {
@@ -777,12 +790,12 @@ class Context:
 
 
 def merge_offsets(values):
-    """merge_offsets.py:104-120 through the C ABI (host arithmetic)."""
+    """merge_offsets.py:104-120 through the C ABI (host arithmetic: no torch, no device)."""
     values = np.ascontiguousarray(values, dtype=np.uint64)
     offsets = np.empty_like(values)
     empty = np.empty(len(values), dtype=np.uint8)
     n_labels = np.zeros(1, dtype=np.uint64)
-    _check(load().cc_merge_offsets(_ptr(values), len(values), _ptr(offsets), _ptr(empty), _ptr(n_labels)))
+    _check(load(host_only=True).cc_merge_offsets(_ptr(values), len(values), _ptr(offsets), _ptr(empty), _ptr(n_labels)))
     return offsets, np.nonzero(empty)[0], int(n_labels[0])
 
 

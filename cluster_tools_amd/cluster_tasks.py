@@ -18,6 +18,7 @@ import shutil
 import stat
 import subprocess
 import sys
+import time
 from concurrent import futures
 from datetime import datetime
 from multiprocessing import cpu_count
@@ -192,8 +193,10 @@ class LocalTask(BaseClusterTask):
         err_file = os.path.join(self.tmp_folder, 'error_logs', '%s_%i.err' % (job_name, job_id))
         env = dict(os.environ)
         env['PYTHONPATH'] = _REPO + (os.pathsep + env['PYTHONPATH'] if env.get('PYTHONPATH') else '')
+        t0 = time.perf_counter()
         with open(log_file, 'w') as fo, open(err_file, 'w') as fe:
             subprocess.call([script, config_file], stdout=fo, stderr=fe, env=env)
+        self._write_log('job %s %i wall %.3f s' % (job_name, job_id, time.perf_counter() - t0))
 
     def submit_jobs(self, n_jobs, job_prefix=None):
         assert n_jobs <= self.max_local_jobs

@@ -217,17 +217,48 @@ def _write_fused_artefacts(tmp_folder, config, values, lut, res, timing):
     fu.log('timing (s): ' + ', '.join('%s %.3f' % (k, v) for k, v in timing.items() if k.endswith('_s')))
 
 
+def _fused_host(config, shape, nb, inp, mask, timing):
+    """The common case of the fused job -- 3-D float input, no resized mask, no prefilter -- with
+    no torch in the process: numpy buffers straight through cc_label_volume_host (H2D, the five
+    stages, D2H in one call on the system HIP runtime).  The torch import is most of a one-shot
+    job's wall time."""
+    from cluster_tools_amd import _lib
+    _lib.load(host_only=True)
+    device = int(os.environ.get('CC_DEVICE', '0'))
+    t = time.perf_counter()
+    with _lib.Context(device) as ctx:
+        timing['ctx_init_s'] = time.perf_counter() - t
+        ctx.set_empty_job_quirk(config.get('quirk_jobs', 0))
+        t = time.perf_counter()
+        labels, res = ctx.label_volume(inp, config['block_shape'], config['threshold'], config['threshold_mode'],
+                                       mask=mask)
+        timing['h2d_device_d2h_s'] = time.perf_counter() - t
+        values = ctx.block_values(nb)
+        lut = ctx.lut(res['n_labels'])
+    del inp, mask
+    t = time.perf_counter()
+    _write_output(config, labels, [(0, s) for s in shape])
+    timing['n5_write_s'] = time.perf_counter() - t
+    timing['torch_imported'] = 'torch' in sys.modules
+    if res.get('identity_lut'):
+        fu.log('a block_faces job has no pairs: no merge (reference empty-job branch)')
+    return values, lut, res, timing
+
+
 def _fused_single(config, shape, nb):
     """All five stages on one GPU, with the host side split out: N5 read, H2D, device, D2H, N5
     write (the PCIe-inclusive and codec-inclusive rates are reported beside the
     device-resident one)."""
-    import torch
-    from cluster_tools_amd import _lib
     timing = {'voxels': int(np.prod(shape)), 'gpus': 1}
     t = time.perf_counter()
     inp, chans = read_input(config)
     mask, resized = read_mask(config, shape)
     timing['n5_read_s'] = time.perf_counter() - t
+    sigma = float(config.get('sigma_prefilter', 0) or 0)
+    if chans is None and not resized and sigma <= 0 and not config.get('torch_path', False):
+        return _fused_host(config, shape, nb, inp, mask, timing)
+    import torch
+    from cluster_tools_amd import _lib
     device = int(os.environ.get('CC_DEVICE', '0'))
     dev = torch.device('cuda', device)
     torch.cuda.set_device(dev)

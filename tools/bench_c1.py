@@ -5,13 +5,14 @@
 Writes a CREMI-sized (125, 1250, 1250) float32 boundary map (synthetic: the CREMI sample is not
 available) as a gzip N5 dataset, runs ThresholdedComponentsWorkflow(target='local', threshold 0.5,
 block_shape [50, 512, 512] = the reference default, max_jobs 16) and prints one JSON line: the
-workflow wall time, the fused job's n5-read / H2D / device / D2H / n5-write split
-(<tmp>/cc_fused_timing.json), and the C restatement of the reference path (oracle/cc_oracle.c,
+workflow wall time, each stage job's process wall, the fused job's n5-read /
+H2D+device+D2H (cc_label_volume_host, no torch in the job) / n5-write split (<tmp>/cc_fused_timing.json), and the C restatement of the reference path (oracle/cc_oracle.c,
 in memory, no gzip) on the same voxels and the same host threads.  Run on the GPU box.
 """
 import argparse
 import json
 import os
+import re
 import shutil
 import sys
 import tempfile
@@ -63,8 +64,14 @@ def main():
         wall = time.perf_counter() - t
         with open(os.path.join(tmp, 'cc_fused_timing.json')) as f:
             timing = json.load(f)
-        runs.append({'workflow_wall_s': round(wall, 3), **{k: round(v, 4) if isinstance(v, float) else v
-                                                            for k, v in timing.items()}})
+        # per-stage job wall (cluster_tasks.LocalTask._submit logs each job process's wall time)
+        jobs = {}
+        for fn in sorted(os.listdir(tmp)):
+            if fn.endswith('.log'):
+                for m in re.finditer(r'job (\S+) (\d+) wall ([\d.]+) s', open(os.path.join(tmp, fn)).read()):
+                    jobs[m.group(1)] = float(m.group(3))
+        runs.append({'workflow_wall_s': round(wall, 3), 'job_wall_s': jobs,
+                     **{k: round(v, 4) if isinstance(v, float) else v for k, v in timing.items()}})
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
     t = time.perf_counter()
     ref = O.label_volume(x, bs, 0.5, a.mode, n_threads=threads, want_lut=False)
@@ -78,9 +85,8 @@ def main():
                     '(synthetic CREMI-sized boundary map), block [50, 512, 512], threshold 0.5 %s, '
                     "target 'local', max_jobs 16" % a.mode,
         'voxels': nvox, 'runs': runs,
-        'device_gvox_s': round(nvox / best['device_s'] / 1e9, 2),
-        'job_gvox_s': round(nvox / sum(best[k] for k in ('n5_read_s', 'h2d_s', 'device_s', 'd2h_s', 'n5_write_s'))
-                            / 1e9, 3),
+        'label_host_gvox_s': round(nvox / best['h2d_device_d2h_s'] / 1e9, 3),
+        'job_gvox_s': round(nvox / sum(best[k] for k in ('n5_read_s', 'h2d_device_d2h_s', 'n5_write_s')) / 1e9, 3),
         'workflow_gvox_s': round(nvox / best['workflow_wall_s'] / 1e9, 3),
         'input_n5_write_s': round(t_in, 3),
         'labels_equal_oracle': same,

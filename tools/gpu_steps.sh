@@ -8,6 +8,11 @@
 #   slabs8_c3 / slabs8_c4   the 8-slab strong-scaling schedule in one process (tools/bench_sharded_slabs.py)
 #   n2gloo / n4gloo  bench.py --gpus 2 --workload c4 / --gpus 4 --workload c3 self-launched, gloo on one GPU
 #   tests          the whole -m gpu suite                                   -> tests_TAG.log
+#   smoke          __graft_entry__.smoke()                                  -> smoke_TAG.log
+#   tests_comm     the sharded C entry: world 1 on RCCL, world 2 / 3 on the test-only stand-in
+#   bench_c5       one rank's C5 slab (256, 4096, 4096)
+#   c1_dropin      BASELINE C1 through ThresholdedComponentsWorkflow, per-stage job wall (tools/bench_c1.py)
+#   tests_workflow tests/test_gpu_workflow.py
 #   tests_sharded  tests/test_gpu_sharded.py only;  tests_parity  parity + watershed + workflow files
 #   bench_sync / bench_c2_sync   the host-synchronised schedule (CC_FAST=0), same-box A/B
 #   prof_c3 / prof_c3_mask / prof_cont / prof_c2 / prof_c1   rocprofv3 trace + FETCH/WRITE passes (tools/profile.sh)
@@ -48,6 +53,11 @@ for step in "$@"; do
     n4gloo)     CC_DIST_BACKEND=gloo timeout -k 10 400 python -u bench.py --gpus 4 --workload c3 --steps 5 --warmup 2 --no-cpu-baseline > $O/n4gloo_$TAG.json 2> $O/n4gloo_$TAG.err; cat $O/n4gloo_$TAG.json ;;
     n2gloo)     CC_DIST_BACKEND=gloo timeout -k 10 300 python -u bench.py --gpus 2 --workload c4 --steps 5 --warmup 2 --no-cpu-baseline > $O/n2gloo_$TAG.json 2> $O/n2gloo_$TAG.err; cat $O/n2gloo_$TAG.json ;;
     tests)      timeout -k 10 1000 $PYT tests -m gpu > $O/tests_$TAG.log 2>&1 || { tail -40 $O/tests_$TAG.log; exit 1; }; tail -3 $O/tests_$TAG.log ;;
+    smoke)      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$TAG.log 2>&1 || { tail -20 $O/smoke_$TAG.log; exit 1; }; tail -3 $O/smoke_$TAG.log ;;
+    tests_comm) timeout -k 10 600 $PYT tests/test_gpu_comm.py tests/test_gpu_comm_ranks.py > $O/tests_comm_$TAG.log 2>&1 || { tail -40 $O/tests_comm_$TAG.log; exit 1; }; tail -3 $O/tests_comm_$TAG.log ;;
+    bench_c5)   timeout -k 10 300 python -u bench.py --no-cpu-baseline --workload c5 --steps 20 --warmup 5 > $O/bench_c5_$TAG.json 2> $O/bench_c5_$TAG.err; cat $O/bench_c5_$TAG.json ;;
+    c1_dropin)  timeout -k 10 600 python -u tools/bench_c1.py --repeats 3 > $O/c1_dropin_$TAG.json 2> $O/c1_dropin_$TAG.err; cat $O/c1_dropin_$TAG.json ;;
+    tests_workflow) timeout -k 10 900 $PYT tests/test_gpu_workflow.py > $O/tests_workflow_$TAG.log 2>&1 || { tail -40 $O/tests_workflow_$TAG.log; exit 1; }; tail -3 $O/tests_workflow_$TAG.log ;;
     tests_sharded) timeout -k 10 900 $PYT tests/test_gpu_sharded.py > $O/tests_sharded_$TAG.log 2>&1 || { tail -40 $O/tests_sharded_$TAG.log; exit 1; }; tail -3 $O/tests_sharded_$TAG.log ;;
     prof_c3)    tools/profile.sh "${TAG}_c3" --steps 10 --warmup 3 ;;
     prof_c3_mask) tools/profile.sh "${TAG}_c3_mask" --steps 10 --warmup 3 --mask ;;
