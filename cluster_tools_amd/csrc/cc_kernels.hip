@@ -3038,10 +3038,16 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2(Geom g, const u64* __restric
     // writing the 4096-wide C5 slabs in x-fastest order took 6.09-6.14 ms, z-fastest 5.36 ms;
     // C3's 2048-wide volume is the other way round, 5.60 vs 5.84 ms), 2 XCD-contiguous (rows of
     // labels not 128-B aligned, X % 16 != 0: see xcd_contig)
+    // (3 y fastest, 4 / 5: z / y fastest over the XCD-contiguous order: A/B of the C5 slab's
+    // 4096-wide rows, CC_PASS2_ORDER)
     int64_t t = blockIdx.x;
-    if (order == 1) {
+    if (order >= 4) t = xcd_contig(t, gridDim.x);
+    if (order == 1 || order == 4) {
         const int64_t n0 = g.nt[0];
         t = (t % n0) * ((int64_t)g.nt[1] * g.nt[2]) + t / n0;
+    } else if (order == 3 || order == 5) {
+        const int64_t n1 = g.nt[1], n2 = g.nt[2], q = t / n1;
+        t = (q / n2) * n1 * n2 + (t % n1) * n2 + q % n2;
     } else if (order == 2) {
         t = xcd_contig(t, gridDim.x);
     }

@@ -629,7 +629,7 @@ static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev*
         // (and XCD-contiguous for masked volumes: C4 k_pass2 5.68-5.74 -> 5.63 ms,
         // profiles/r05_ab_c4_order_mask.txt; C3 unmasked is slower that way, 5.49-5.53 -> 5.70)
         int order = g.X >= 4096 ? 1 : ((g.X & 15) || st.masked) ? 2 : 0;
-        if (const char* e = std::getenv("CC_PASS2_ORDER"); e && *e) order = std::min(std::max(std::atoi(e), 0), 2);
+        if (const char* e = std::getenv("CC_PASS2_ORDER"); e && *e) order = std::min(std::max(std::atoi(e), 0), 5);
         // CC_LDS_PAD_P2 (A/B only): extra dynamic LDS per workgroup, i.e. fewer tiles per CU
         const unsigned pad = (unsigned)env_int("CC_LDS_PAD_P2", 0);
         // with a seam map every label goes through the slab's LUT (m = 1)

@@ -1,9 +1,11 @@
 """Worker of tests/test_gpu_comm_ranks.py: ONE rank of the library's own sharded C entry
 (cc_comm_create / cc_label_volume_sharded) on cuda:0, with the collectives served by the
-test-only RCCL stand-in (tests/fake_rccl, loaded through CC_RCCL_PATH by the parent) so that 2-3
+test-only RCCL stand-in (tests/fake_rccl, loaded through CC_RCCL_PATH by the parent) so that 2-8
 ranks can share the one GPU of a test box.
 
-argv[1]: JSON spec {out, rank, world, uid (hex), shape, origin, mode, mask, calls: [...]}; each
+argv[1]: JSON spec {out, rank, world, uid (hex), shape, origin, mode, mask, generate (the slab made
+on the device by cc_generate_boundary_map), hash_only (an xxh64 digest of the labels instead of
+the array), calls: [...]}; each
 call: {block_shape, z_shift (this rank's z_offset moved by this much: a bad slab), src ('host' |
 'kernel' | 'kernel_side': the slab written by a torch kernel queued behind a GPU sleep, on the
 default or a side stream, with no synchronisation before the call)}.
@@ -34,13 +36,16 @@ def main():
         for k, call in enumerate(spec['calls']):
             bs = tuple(call['block_shape'])
             z0, zs = slab_bounds(shape[0], bs[0], world)[rank]
-            x = O.boundary_map((zs,) + shape[1:], origin=(origin[0] + z0,) + origin[1:], n_threads=1)
+            if spec.get('generate'):          # full-size runs: the slab made on the device
+                x = ctx.generate_boundary_map((zs,) + shape[1:], origin=(origin[0] + z0,) + origin[1:])
+            else:
+                x = O.boundary_map((zs,) + shape[1:], origin=(origin[0] + z0,) + origin[1:], n_threads=1)
             m = None
             if spec.get('mask'):
                 from oracle.synth import ellipsoid_mask
                 m = torch.from_numpy(np.ascontiguousarray(ellipsoid_mask(shape)[z0:z0 + zs])).to(dev)
             src = call.get('src', 'host')
-            xh = torch.from_numpy(x).to(dev)
+            xh = x if spec.get('generate') else torch.from_numpy(x).to(dev)
             torch.cuda.synchronize()
             side = torch.cuda.Stream(dev) if src == 'kernel_side' else None
             with torch.cuda.stream(side) if side is not None else torch.cuda.stream(torch.cuda.default_stream(dev)):
@@ -58,8 +63,12 @@ def main():
                     lab, res = ctx.label_volume_sharded(comm, xd, shape, z0 + call.get('z_shift', 0), bs, 0.5,
                                                         spec['mode'], mask=m)
                     torch.cuda.current_stream(dev).synchronize()
-                    np.save(os.path.join(spec['out'], 'rank%d_call%d.npy' % (rank, k)), lab.cpu().numpy())
-                    entry = {'ok': True, 'res': res}
+                    entry = {'ok': True, 'res': res, 'label_seconds': time.time() - t0}
+                    if spec.get('hash_only'):     # full-size runs: a digest of the slab's labels
+                        import xxhash
+                        entry['xxh64'] = xxhash.xxh64(lab.cpu().numpy().data).hexdigest()
+                    else:
+                        np.save(os.path.join(spec['out'], 'rank%d_call%d.npy' % (rank, k)), lab.cpu().numpy())
                 except RuntimeError as e:
                     entry = {'ok': False, 'error': str(e)}
                 entry['seconds'] = time.time() - t0

@@ -30,7 +30,8 @@ def _unique_id():
     return buf.raw.hex()
 
 
-def _run(tmp_path, world, calls, mode='greater', mask=False, env_by_rank=None, env=None, calls_by_rank=None):
+def _run(tmp_path, world, calls, mode='greater', mask=False, env_by_rank=None, env=None, calls_by_rank=None,
+         shape=SHAPE, origin=ORIGIN, extra=None, timeout=240):
     """Start `world` worker processes (one rank each, all on cuda:0) and return their call logs."""
     uid = _unique_id()
     procs, outs = [], []
@@ -39,13 +40,13 @@ def _run(tmp_path, world, calls, mode='greater', mask=False, env_by_rank=None, e
                  CC_COMM_TIMEOUT='60')
         e.update(env or {})
         e.update((env_by_rank or {}).get(r, {}))
-        spec = dict(out=str(tmp_path), rank=r, world=world, uid=uid, shape=list(SHAPE), origin=list(ORIGIN),
-                    mode=mode, mask=mask, calls=(calls_by_rank or {}).get(r, calls))
+        spec = dict(out=str(tmp_path), rank=r, world=world, uid=uid, shape=list(shape), origin=list(origin),
+                    mode=mode, mask=mask, calls=(calls_by_rank or {}).get(r, calls), **(extra or {}))
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, 'tests', '_comm_worker.py'), json.dumps(spec)],
                                       env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     try:
         for p in procs:
-            outs.append(p.communicate(timeout=240)[0])
+            outs.append(p.communicate(timeout=timeout)[0])
     finally:
         for p in procs:
             if p.poll() is None:
@@ -158,3 +159,38 @@ def test_ranks_input_from_an_unsynchronised_kernel(tmp_path, src):
     bs = [16, 64, 64]
     logs = _run(tmp_path, 2, [dict(block_shape=bs, src=src)], mode='greater')
     _check_call(tmp_path, logs, 0, bs, 'greater', 'one-read-back')
+
+
+@pytest.mark.slow
+def test_ranks_world8_c3_full_size(tmp_path):
+    """The 8-GPU strong-scaling split of BASELINE C3 through the library's sharded C entry: eight
+    rank processes (all on cuda:0, collectives by the stand-in), each labelling its (128, 2048,
+    2048) z-slab generated on the device, block (64, 512, 512); every slab's labels bit-exact
+    (xxh64 of the raw uint64 labels) against the C oracle on the whole 1024 x 2048 x 2048 volume,
+    n_labels equal, the one-read-back schedule on every rank."""
+    import os as _os
+    import torch
+    import xxhash
+    from cluster_tools_amd import _lib
+    shape, bs = (1024, 2048, 2048), [64, 512, 512]
+    with _lib.Context(0) as ctx:
+        x = ctx.generate_boundary_map(shape)
+        inp = x.cpu().numpy()
+        del x
+    torch.cuda.empty_cache()
+    threads = max(1, min(16, len(_os.sched_getaffinity(0))))
+    ref = O.label_volume(inp, bs, 0.5, 'greater', n_threads=threads, want_lut=False)
+    del inp
+    labels = ref.pop('labels')
+    logs = _run(tmp_path, 8, [dict(block_shape=bs)], shape=shape, origin=(0, 0, 0),
+                extra=dict(generate=True, hash_only=True), env={'CC_FAKE_RCCL_TIMEOUT': '300', 'CC_COMM_TIMEOUT': '300'},
+                timeout=900)
+    for r in range(8):
+        e = logs[r][0]
+        assert e['ok'], (r, e.get('error'))
+        assert e['res']['n_labels'] == ref['n_labels'], (r, e['res'])
+        assert e['info']['schedule'] == 'one-read-back', (r, e['info'])
+        z0, zs = e['z0'], e['zs']
+        assert (z0, zs) == (128 * r, 128)
+        assert e['xxh64'] == xxhash.xxh64(labels[z0:z0 + zs].data).hexdigest(), 'rank %d labels differ' % r
+    print("world 8 C3 label seconds per rank:", [round(logs[r][0]["label_seconds"], 3) for r in range(8)])
