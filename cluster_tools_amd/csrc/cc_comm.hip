@@ -147,7 +147,9 @@ static void comm_wait(void* arg, hipStream_t s) {
                 throw CCError{"timed out after " + std::to_string((int)m->timeout_s) +
                               " s waiting for the z-slab exchange (a peer failed or stopped)"};
         }
-        if (spin > 256) usleep(20);
+        // busy-poll for the first 50 ms (a step's waits are shorter: no wake-up latency), then
+        // yield the core between polls
+        if (spin > 4096 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) usleep(50);
     }
 }
 
