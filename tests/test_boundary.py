@@ -131,3 +131,29 @@ def test_resized_mask_rule_and_loader(tmp_path):
     r = vu.load_mask(p, 'mask', (12, 16, 20))
     assert isinstance(r, vu.ResizedMask) and r.mask_shape == (6, 8, 10) and r.shape == (12, 16, 20)
     assert not isinstance(vu.load_mask(p, 'mask', (6, 8, 10)), vu.ResizedMask)
+
+
+def test_host_only_load_skips_torch_and_refuses_it_later():
+    """_lib.load(host_only=True) (the drop-in's one-shot job processes: cc_merge_offsets,
+    cc_label_volume_host) binds the library without importing torch; a torch import afterwards in
+    that process is refused on the next load() instead of running two HIP runtimes side by side."""
+    import subprocess
+    import sys
+    code = (
+        "import sys\n"
+        "from cluster_tools_amd import _lib\n"
+        "import numpy as np\n"
+        "offs, empty, n = _lib.merge_offsets(np.array([3, 0, 2], dtype=np.uint64))\n"
+        "assert 'torch' not in sys.modules, 'host-only load imported torch'\n"
+        "assert list(offs) == [0, 3, 3] and n == 6, (list(offs), n)\n"
+        "import torch\n"
+        "try:\n"
+        "    _lib.load()\n"
+        "except RuntimeError as e:\n"
+        "    assert 'host-only' in str(e)\n"
+        "else:\n"
+        "    raise SystemExit('torch after a host-only load was not refused')\n"
+        "print('ok')\n")
+    r = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=300,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and r.stdout.strip().endswith('ok'), r.stdout + r.stderr
