@@ -790,12 +790,12 @@ class Context:
 
 
 def merge_offsets(values):
-    """merge_offsets.py:104-120 through the C ABI (host arithmetic: no torch, no device)."""
+    """merge_offsets.py:104-120 through the C ABI (host arithmetic: no device call)."""
     values = np.ascontiguousarray(values, dtype=np.uint64)
     offsets = np.empty_like(values)
     empty = np.empty(len(values), dtype=np.uint8)
     n_labels = np.zeros(1, dtype=np.uint64)
-    _check(load(host_only=True).cc_merge_offsets(_ptr(values), len(values), _ptr(offsets), _ptr(empty), _ptr(n_labels)))
+    _check(load().cc_merge_offsets(_ptr(values), len(values), _ptr(offsets), _ptr(empty), _ptr(n_labels)))
     return offsets, np.nonzero(empty)[0], int(n_labels[0])
 
 

@@ -46,6 +46,7 @@ class MergeOffsetsLocal(MergeOffsetsBase, LocalTask):
 
 def merge_offsets(job_id, config_path):
     from cluster_tools_amd import _lib
+    _lib.load(host_only=True)         # a one-shot job process: host arithmetic only, no torch import
     fu.log('start processing job %i' % job_id)
     fu.log('reading config from %s' % config_path)
     with open(config_path) as f:

@@ -143,6 +143,7 @@ def test_host_only_load_skips_torch_and_refuses_it_later():
         "import sys\n"
         "from cluster_tools_amd import _lib\n"
         "import numpy as np\n"
+        "_lib.load(host_only=True)\n"
         "offs, empty, n = _lib.merge_offsets(np.array([3, 0, 2], dtype=np.uint64))\n"
         "assert 'torch' not in sys.modules, 'host-only load imported torch'\n"
         "assert list(offs) == [0, 3, 3] and n == 6, (list(offs), n)\n"
