@@ -41,7 +41,10 @@ def main():
             else:
                 x = O.boundary_map((zs,) + shape[1:], origin=(origin[0] + z0,) + origin[1:], n_threads=1)
             m = None
-            if spec.get('mask'):
+            if spec.get('mask') and spec.get('generate'):
+                from cluster_tools_amd.synthetic import ellipsoid_mask_device
+                m = ellipsoid_mask_device(shape, z0, zs, dev)
+            elif spec.get('mask'):
                 from oracle.synth import ellipsoid_mask
                 m = torch.from_numpy(np.ascontiguousarray(ellipsoid_mask(shape)[z0:z0 + zs])).to(dev)
             src = call.get('src', 'host')

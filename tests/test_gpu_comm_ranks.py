@@ -162,27 +162,31 @@ def test_ranks_input_from_an_unsynchronised_kernel(tmp_path, src):
 
 
 @pytest.mark.slow
-def test_ranks_world8_c3_full_size(tmp_path):
-    """The 8-GPU strong-scaling split of BASELINE C3 through the library's sharded C entry: eight
-    rank processes (all on cuda:0, collectives by the stand-in), each labelling its (128, 2048,
-    2048) z-slab generated on the device, block (64, 512, 512); every slab's labels bit-exact
-    (xxh64 of the raw uint64 labels) against the C oracle on the whole 1024 x 2048 x 2048 volume,
-    n_labels equal, the one-read-back schedule on every rank."""
+@pytest.mark.parametrize('masked', [False, True])
+def test_ranks_world8_c3_full_size(tmp_path, masked):
+    """The 8-GPU strong-scaling split of BASELINE C3 (and of C4 = C3 + the ellipsoid uint8 mask)
+    through the library's sharded C entry: eight rank processes (all on cuda:0, collectives by the
+    stand-in), each labelling its (128, 2048, 2048) z-slab generated on the device, block
+    (64, 512, 512); every slab's labels bit-exact (xxh64 of the raw uint64 labels) against the C
+    oracle on the whole 1024 x 2048 x 2048 volume, n_labels equal, the one-read-back schedule on
+    every rank."""
     import os as _os
     import torch
     import xxhash
     from cluster_tools_amd import _lib
+    from cluster_tools_amd.synthetic import ellipsoid_mask_device
     shape, bs = (1024, 2048, 2048), [64, 512, 512]
     with _lib.Context(0) as ctx:
         x = ctx.generate_boundary_map(shape)
         inp = x.cpu().numpy()
         del x
+        hmask = ellipsoid_mask_device(shape, 0, shape[0], torch.device('cuda', 0)).cpu().numpy() if masked else None
     torch.cuda.empty_cache()
     threads = max(1, min(16, len(_os.sched_getaffinity(0))))
-    ref = O.label_volume(inp, bs, 0.5, 'greater', n_threads=threads, want_lut=False)
-    del inp
+    ref = O.label_volume(inp, bs, 0.5, 'greater', hmask, n_threads=threads, want_lut=False)
+    del inp, hmask
     labels = ref.pop('labels')
-    logs = _run(tmp_path, 8, [dict(block_shape=bs)], shape=shape, origin=(0, 0, 0),
+    logs = _run(tmp_path, 8, [dict(block_shape=bs)], shape=shape, origin=(0, 0, 0), mask=masked,
                 extra=dict(generate=True, hash_only=True), env={'CC_FAKE_RCCL_TIMEOUT': '300', 'CC_COMM_TIMEOUT': '300'},
                 timeout=900)
     for r in range(8):
