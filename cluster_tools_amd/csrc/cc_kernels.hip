@@ -1788,9 +1788,9 @@ struct SeamsLDS {
 
 // the seams of tile t (valid) for wave w; every wave of the workgroup calls it (one barrier)
 template <int STOP = 0>
-__device__ __forceinline__ void seams_tile(const Geom& g, const face_t* __restrict__ FACES, u64* PAIRS, u32* PC,
-                                           u8* big, u64* IPAIRS, u32* IPC, u8* iovf, int64_t t, bool valid,
-                                           SeamsLDS& LS) {
+__device__ __forceinline__ void seams_tile(const Geom& g, const face_t* __restrict__ FACES, const u32* __restrict__ COUNT,
+                                           u64* PAIRS, u32* PC, u8* big, u64* IPAIRS, u32* IPC, u8* iovf, int64_t t,
+                                           bool valid, SeamsLDS& LS) {
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     auto& Sall = LS.S;
     auto& Hall = LS.H;
@@ -1804,7 +1804,10 @@ __device__ __forceinline__ void seams_tile(const Geom& g, const face_t* __restri
     // the same block at offset (oz, oy, ox) is lt_own + oz bny bnx + oy bnx + ox)
     int lz = 0, ly = 0, lx = 0, bny = 0, bnx_ = 0;
     InBlock nb{};
-    if (valid) {
+    // an empty tile (no foreground voxel: masked out or all background) touches nothing across
+    // its seams -- every contact needs an own foreground voxel -- so it skips the whole walk
+    const bool empty = valid && __builtin_amdgcn_readfirstlane(COUNT[t]) == 0;
+    if (valid && !empty) {
         ti = tile_info(g, t);
         const int bz = g.tblk[0][ti.iz], by = g.tblk[1][ti.iy], bx = g.tblk[2][ti.ix];
         lz = ti.iz - g.bt0[0][bz]; ly = ti.iy - g.bt0[1][by]; lx = ti.ix - g.bt0[2][bx];
@@ -1817,6 +1820,10 @@ __device__ __forceinline__ void seams_tile(const Geom& g, const face_t* __restri
     if (lane < 2) cnt[w][lane] = 0;
     __syncthreads();
     if (!valid) return;
+    if (empty) {
+        if (lane == 0) { PC[t] = 0; IPC[t] = 0; }
+        return;
+    }
     const u32 bnx = (u32)bnx_, bnyx = (u32)bny * bnx;
     const u32 lt_own = (u32)lz * bnyx + (u32)ly * bnx + (u32)lx;
     const u32 capu = (u32)g.cap;
@@ -1929,7 +1936,8 @@ __device__ __forceinline__ void seams_tile(const Geom& g, const face_t* __restri
 }
 
 template <int STOP = 0>
-__global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* __restrict__ FACES, u64* PAIRS, u32* PC,
+__global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* __restrict__ FACES,
+                                                         const u32* __restrict__ COUNT, u64* PAIRS, u32* PC,
                                                          u8* big, u64* IPAIRS, u32* IPC, u8* iovf,
                                                          int64_t t_begin, int64_t t_end, const u32* list) {
     __shared__ SeamsLDS LS;
@@ -1942,12 +1950,13 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams(Geom g, const face_t* _
         valid = idx < (int64_t)nl;
         t = valid ? (int64_t)__builtin_amdgcn_readfirstlane(list[1 + idx]) : 0;
     }
-    seams_tile<STOP>(g, FACES, PAIRS, PC, big, IPAIRS, IPC, iovf, t, valid, LS);
+    seams_tile<STOP>(g, FACES, COUNT, PAIRS, PC, big, IPAIRS, IPC, iovf, t, valid, LS);
 }
 
 // the listed tiles list[1 .. list[0]] with a fixed grid (the count stays on the device: the
 // one-read-back schedule); the loop's trip count is uniform per workgroup
-__global__ __launch_bounds__(SP_WAVES * 64) void k_seams_list(Geom g, const face_t* __restrict__ FACES, u64* PAIRS,
+__global__ __launch_bounds__(SP_WAVES * 64) void k_seams_list(Geom g, const face_t* __restrict__ FACES,
+                                                              const u32* __restrict__ COUNT, u64* PAIRS,
                                                               u32* PC, u8* big, u64* IPAIRS, u32* IPC, u8* iovf,
                                                               const u32* list) {
     __shared__ SeamsLDS LS;
@@ -1958,7 +1967,7 @@ __global__ __launch_bounds__(SP_WAVES * 64) void k_seams_list(Geom g, const face
         const int64_t idx = i0 + w;
         const bool valid = idx < (int64_t)nl;
         const int64_t t = valid ? (int64_t)__builtin_amdgcn_readfirstlane(list[1 + idx]) : 0;
-        seams_tile<0>(g, FACES, PAIRS, PC, big, IPAIRS, IPC, iovf, t, valid, LS);
+        seams_tile<0>(g, FACES, COUNT, PAIRS, PC, big, IPAIRS, IPC, iovf, t, valid, LS);
         __syncthreads();
     }
 }
@@ -3363,7 +3372,7 @@ __global__ __launch_bounds__(NTHREADS) void k_thr_fix(Geom g, const u32* FIX, co
     template __global__ void k_spec<M, S>(Geom, SpecArgs, const float*, const u8*, u64*, face_t*, u32*, u32*, u64*);
 CC_SPEC(false, 1) CC_SPEC(false, 2) CC_SPEC(false, 3) CC_SPEC(true, 1) CC_SPEC(true, 2) CC_SPEC(true, 3)
 #undef CC_SPEC
-template __global__ void k_seams<0>(Geom, const face_t*, u64*, u32*, u8*, u64*, u32*, u8*, int64_t, int64_t, const u32*);
+template __global__ void k_seams<0>(Geom, const face_t*, const u32*, u64*, u32*, u8*, u64*, u32*, u8*, int64_t, int64_t, const u32*);
 template __global__ void k_stitch<false>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_stitch<true>(Geom, const face_t*, u32*, const u64*, const u8*, const u8*);
 template __global__ void k_finalize<true>(Geom, const u32*, u32*, const u64*, const u64*, const u64*, const u64*, int64_t, u64*);

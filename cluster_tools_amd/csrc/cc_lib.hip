@@ -112,7 +112,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
         auto seams = [&](hipStream_t q, int64_t t0, int64_t t1) {
             launch_on(c, q, "k_seams", [&] {
                 k_seams<0><<<(unsigned)((t1 - t0 + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, q>>>(
-                    g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), c->big.as<u8>(), c->ipairs.as<u64>(),
+                    g, FACES, COUNT, c->pairsl.as<u64>(), c->pc.as<u32>(), c->big.as<u8>(), c->ipairs.as<u64>(),
                     c->ipc.as<u32>(), c->iovf.as<u8>(), t0, t1, nullptr);
             });
         };
@@ -174,7 +174,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             else if (lds_seams)
                 launch(c, "k_seams", [&] {
                     const unsigned grid = (unsigned)std::min<int64_t>((nt + SP_WAVES - 1) / SP_WAVES, 512);
-                    k_seams_list<<<grid, SP_WAVES * 64, 0, s>>>(g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), c->big.as<u8>(),
+                    k_seams_list<<<grid, SP_WAVES * 64, 0, s>>>(g, FACES, COUNT, c->pairsl.as<u64>(), c->pc.as<u32>(), c->big.as<u8>(),
                                                                c->ipairs.as<u64>(), c->ipc.as<u32>(), c->iovf.as<u8>(), list);
                 });
         } else {
@@ -200,7 +200,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
                 const int64_t nl = std::min<int64_t>(nt, 14 * (int64_t)nfix);
                 launch(c, "k_seams", [&] {
                     k_seams<0><<<(unsigned)((nl + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, s>>>(
-                        g, FACES, c->pairsl.as<u64>(), c->pc.as<u32>(), c->big.as<u8>(), c->ipairs.as<u64>(),
+                        g, FACES, COUNT, c->pairsl.as<u64>(), c->pc.as<u32>(), c->big.as<u8>(), c->ipairs.as<u64>(),
                         c->ipc.as<u32>(), c->iovf.as<u8>(), 0, 0, list);
                 });
             }

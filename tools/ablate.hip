@@ -219,7 +219,7 @@ int main(int argc, char** argv) {
             HIP_OK(hipMemset(big, 0, nb));
             HIP_OK(hipMemset(iovf, 0, nt));
             const unsigned sg = (unsigned)((nt + SP_WAVES - 1) / SP_WAVES);
-#define SEAMS(V) k_seams<V><<<sg, SP_WAVES * 64, 0, s>>>(g, FACES, pairs, pc, big, ipairs, ipc, iovf, 0, nt, nullptr)
+#define SEAMS(V) k_seams<V><<<sg, SP_WAVES * 64, 0, s>>>(g, FACES, COUNT, pairs, pc, big, ipairs, ipc, iovf, 0, nt, nullptr)
             r.push_back({"k_seams_stage", time_ms(s, iters, [&] { SEAMS(1); })});
             r.push_back({"k_seams_z", time_ms(s, iters, [&] { SEAMS(2); })});
             r.push_back({"k_seams_zy", time_ms(s, iters, [&] { SEAMS(3); })});
