@@ -257,6 +257,7 @@ struct cc_ctx {
         rl_wg,                                            // relabel: per-workgroup id lists
         gs1, gs2, gs_tab,                                 // Gaussian prefilter temporaries (cc_prefilter.hip)
         mask_xmap,                                        // resized masks (cc_mask.hip)
+        mlive,                                            // masked runs: blocks holding a mask voxel (k_mask_live)
         seam_hash,                                        // seam pair hash set (k_seam_pairs)
         ws_tab, ws_buf;                                   // seeded watershed (cc_watershed.hip)
     int64_t ev_cap = 0;      // entries per evaluation hash table of the last cc_evaluate
@@ -299,7 +300,7 @@ static inline std::vector<DevBuf*> ctx_bufs(cc_ctx* c) {
             &c->cub_tmp, &c->scalars, &c->counter, &c->in_tmp, &c->mask_tmp, &c->out_tmp, &c->pairs, &c->pairs2,
             &c->scalars2, &c->flags, &c->map_ids, &c->map_ids2, &c->map_vals, &c->map_par, &c->big, &c->pairsl, &c->pc,
             &c->ipairs, &c->ipc, &c->iovf, &c->spec, &c->mark, &c->bflag, &c->ev_main, &c->ev_z, &c->ev_seg, &c->ev_gt,
-            &c->ev_flag, &c->ev_part, &c->rl_wg, &c->gs1, &c->gs2, &c->gs_tab, &c->mask_xmap, &c->seam_hash, &c->ws_tab,
+            &c->ev_flag, &c->ev_part, &c->rl_wg, &c->gs1, &c->gs2, &c->gs_tab, &c->mask_xmap, &c->mlive, &c->seam_hash, &c->ws_tab,
             &c->ws_buf, &c->status, &c->hmap_keys, &c->hmap_par};
 }
 

@@ -24,6 +24,8 @@
 static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const int64_t shape[3],
                         const int64_t block_shape[3], double threshold, int mode, int64_t zoff,
                         bool local_only, bool fast = false, uint64_t* sum_out = nullptr) {
+    // the kernels' 16-B row loads assume 16-B aligned bases (any device allocation is)
+    CC_REQUIRE(((uintptr_t)in & 15) == 0 && ((uintptr_t)mask & 15) == 0, "input / mask not 16-byte aligned");
     RunState& st = state(c);
     st = RunState();
     st.fast = fast;
@@ -99,16 +101,27 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             fc.htab = shard ? c->seam_hash.as<u64>() : nullptr; fc.htab_n = hs_n;
             fc.hkeys = hm_n ? c->hmap_keys.as<u64>() : nullptr; fc.hpar = hm_n ? c->hmap_par.as<u32>() : nullptr;
             fc.hm_n = hm_n;
+            if (mask) c->mlive.ensure(nb * sizeof(u32));
+            fc.mlive = mask ? c->mlive.as<u32>() : nullptr;
             fc.n_clear = std::max<int64_t>({nt + 1, 2 * nb + 1, hs_n, hm_n});
         }
-        launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART, fc); });
-        launch(c, "k_guess", [&] { k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, mode, guess); });
+        launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART, fc, mask); });
+        launch(c, "k_guess", [&] {
+            k_guess<<<(unsigned)((nb + 255) / 256), 256, 0, s>>>(nb, SPART, thr, mode, guess, mask ? c->mlive.as<u32>() : nullptr);
+        });
         if (const char* e = std::getenv("CC_SPEC"); e && std::string(e) == "0")     // test hook: no guesses
             HIP_OK(hipMemsetAsync(guess, 0, nb * sizeof(BlockParam), s));
+        // masked runs: which blocks hold a mask voxel (the others are skipped, as the reference does)
+        const u32* live = mask ? c->mlive.as<u32>() : nullptr;
+        if (mask)
+            launch(c, "k_mask_live", [&] {
+                k_mask_live<<<(unsigned)(nb * LIVE_PARTS), LIVE_THREADS, 0, s>>>(g, mask, c->mlive.as<u32>());
+            });
         SpecArgs sa;
         sa.guess = guess;
         sa.smin = smin; sa.smax = smax; sa.sflag = sflag;
         sa.TB = TB;
+        sa.live = live;
         auto seams = [&](hipStream_t q, int64_t t0, int64_t t1) {
             launch_on(c, q, "k_seams", [&] {
                 k_seams<0><<<(unsigned)((t1 - t0 + SP_WAVES - 1) / SP_WAVES), SP_WAVES * 64, 0, q>>>(
@@ -152,7 +165,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             }
         }
         launch(c, "k_params_verify", [&] {
-            k_params_verify<<<grid_stride(nt), 256, 0, s>>>(g, guess, smin, smax, sflag, thr, mode, bp, TB, FIX);
+            k_params_verify<<<grid_stride(nt), 256, 0, s>>>(g, guess, smin, smax, sflag, thr, mode, bp, TB, FIX, live);
         });
         u32* flag = c->mark.as<u32>();
         u32* list = flag + nt;
@@ -553,6 +566,7 @@ struct SeamDev {
 
 // LUT, final label per node, bit rows -> uint64 labels; small artefacts to host
 static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev* sd = nullptr) {
+    CC_REQUIRE(((uintptr_t)out & 15) == 0, "labels not 16-byte aligned");
     RunState& st = state(c);
     CC_REQUIRE(st.stage == 2, "phase order: call assign first");
     Geom& g = st.hg.g;
@@ -919,7 +933,7 @@ int cc_threshold(cc_ctx* c, const float* in, const int64_t shape[3], const int64
                 else k_thr_spec<3><<<ng, NTHREADS, 0, s>>>(g, sa, in, out);
             });
             launch(c, "k_params_verify", [&] {
-                k_params_verify<<<grid_stride(nt), 256, 0, s>>>(g, guess, smin, smax, sflag, thr, md, bp, TB, FIX);
+                k_params_verify<<<grid_stride(nt), 256, 0, s>>>(g, guess, smin, smax, sflag, thr, md, bp, TB, FIX, nullptr);
             });
             launch(c, "k_thr_fix", [&] {
                 k_thr_fix<<<(unsigned)std::min<int64_t>(nt, 2048), NTHREADS, 0, s>>>(g, FIX, bp, in, thr, md, out);

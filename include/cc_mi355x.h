@@ -76,6 +76,8 @@ const char* cc_version(void);
  * mask_dev   uint8 [Z*Y*X] or NULL (nonzero = inside, block_components.py:194,225)
  * labels_dev uint64 [Z*Y*X] final labels (0 = background)
  * res        may be NULL
+ * The three device pointers must be 16-byte aligned (any hipMalloc / torch allocation is; a
+ * view at an odd element offset is refused with an error, as is the same in the sharded entry).
  */
 int cc_label_volume(cc_ctx* ctx, const float* in_dev, const uint8_t* mask_dev,
                     const int64_t shape[3], const int64_t block_shape[3],

@@ -58,6 +58,12 @@ def test_sharded_c_entry_errors():
         x = torch.zeros((20, 32, 32), dtype=torch.float32, device='cuda')
         with pytest.raises(RuntimeError, match='block faces'):
             ctx.label_volume_sharded(comm, x, (40, 32, 32), 5, (16, 32, 32), 0.5)
+        # a contiguous view one float into its storage: refused, not read with 16-B loads
+        xo = torch.zeros(20 * 32 * 32 + 1, dtype=torch.float32, device='cuda')[1:].view(20, 32, 32)
+        with pytest.raises(RuntimeError, match='16-byte aligned'):
+            ctx.label_volume_sharded(comm, xo, (20, 32, 32), 0, (16, 32, 32), 0.5)
+        lab, res = ctx.label_volume_sharded(comm, x, (20, 32, 32), 0, (16, 32, 32), 0.5)   # still usable
+        assert res['n_labels'] == 1
 
 
 def test_integration_comm_binding_runs_as_documented():
