@@ -63,7 +63,9 @@ def test_sharded_c_entry_errors():
         with pytest.raises(RuntimeError, match='16-byte aligned'):
             ctx.label_volume_sharded(comm, xo, (20, 32, 32), 0, (16, 32, 32), 0.5)
         lab, res = ctx.label_volume_sharded(comm, x, (20, 32, 32), 0, (16, 32, 32), 0.5)   # still usable
-        assert res['n_labels'] == 1
+        ref = O.label_volume(np.zeros((20, 32, 32), np.float32), (16, 32, 32), 0.5, 'greater', None, n_threads=1)
+        np.testing.assert_array_equal(lab.cpu().numpy().view(np.uint64), ref['labels'])
+        assert res['n_labels'] == ref['n_labels']
 
 
 def test_integration_comm_binding_runs_as_documented():
