@@ -103,7 +103,7 @@ static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const i
             fc.hm_n = hm_n;
             if (mask) c->mlive.ensure(nb * sizeof(u32));
             fc.mlive = mask ? c->mlive.as<u32>() : nullptr;
-            fc.n_clear = std::max<int64_t>({nt + 1, 2 * nb + 1, hs_n, hm_n});
+            fc.n_clear = std::max<int64_t>({nt + 1, 2 * nb + 1, hs_n, hm_n, (int64_t)SCALARS});   // every scalar, however small the volume
         }
         launch(c, "k_sample", [&] { k_sample<<<(unsigned)(nb * SAMPLE_PARTS), NTHREADS, 0, s>>>(g, in, SPART, fc, mask); });
         launch(c, "k_guess", [&] {
