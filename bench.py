@@ -40,6 +40,21 @@ sys.path.insert(0, ROOT)
 METRIC = 'Gvoxels/sec thresholded CCL end-to-end at 1/2/4/8 MI355X; % of HBM roofline'
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 B_ALG = 12.0                   # algorithmic bytes / voxel: f32 read + uint64 write (+1 with mask)
+
+
+def live_voxels(mask, block_shape):
+    """Voxels of the blocks that hold a mask voxel: the only blocks whose input the reference reads
+    (block_components.py:197-201 returns before reading the input of a block with an empty mask),
+    so a masked run's algorithmic bytes are 8 + 1 per voxel + 4 per voxel of these blocks."""
+    n = 0
+    Z, Y, X = mask.shape
+    for z in range(0, Z, block_shape[0]):
+        for y in range(0, Y, block_shape[1]):
+            for x in range(0, X, block_shape[2]):
+                b = mask[z:z + block_shape[0], y:y + block_shape[1], x:x + block_shape[2]]
+                if bool(b.any()):
+                    n += b.numel()
+    return n
 # algorithmic bytes per voxel of each kernel (DESIGN.md §3)
 KERNEL_BYTES = {'k_spec': 4.0, 'k_pass2': 8.0}
 
@@ -317,6 +332,13 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = nvox_all * args.steps / dt / 1e9
     b_alg = B_ALG + (1.0 if masked else 0.0)
+    if masked:
+        # input bytes only for the blocks holding a mask voxel (see live_voxels)
+        lv = torch.tensor([float(live_voxels(mask, block_shape))], dtype=torch.float64,
+                          device=dev if world > 1 and backend == 'nccl' else 'cpu')
+        if world > 1:
+            dist.all_reduce(lv)
+        b_alg = round(8.0 + 1.0 + 4.0 * float(lv.item()) / nvox_all, 4)
     # dominant kernel of this rank, timed by HIP events on the stream it runs on
     # host_* entries are the library's host-side accounting (allocations, stream synchronisations)
     host = {k: v for k, v in breakdown.items() if k.startswith('host_')}
