@@ -358,8 +358,9 @@ int cc_label_volume_sharded(cc_ctx* c, cc_comm* m, const float* slab_dev, const 
             CC_REQUIRE(z_offset % block_shape[0] == 0 && (slab_depth % block_shape[0] == 0 || z_offset + slab_depth == global_shape[0]),
                        "slabs must start and end on block faces");
             (void)to_mode(mode);
-            CC_REQUIRE((((uintptr_t)slab_dev | (uintptr_t)mask_dev | (uintptr_t)labels_dev) & 15) == 0,
-                       "slab / mask / labels not 16-byte aligned");
+            require_row_aligned(slab_dev, global_shape[2] * 4);
+            require_row_aligned(mask_dev, global_shape[2]);
+            require_row_aligned(labels_dev, global_shape[2] * 8);
             const int64_t nby = (global_shape[1] + block_shape[1] - 1) / block_shape[1];
             const int64_t nbx = (global_shape[2] + block_shape[2] - 1) / block_shape[2];
             cubes_ok = (nby == 1 || block_shape[1] % 2 == 0) && (nbx == 1 || block_shape[2] % 2 == 0);

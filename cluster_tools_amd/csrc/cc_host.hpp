@@ -1,6 +1,8 @@
 // cc_host.hpp -- host-side helpers shared by the library (cc_lib.hip) and the kernel
 // ablation harness (tools/ablate.hip): error type, block grid + tile tables.
 #pragma once
+#include <cstdint>
+#include <initializer_list>
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -25,6 +27,16 @@ struct CCError {
     do {                                                                                       \
         if (!(cond)) throw CCError{msg};                                                       \
     } while (0)
+
+// A device volume is read / written with vector accesses of up to 16 B wherever its rows allow
+// them, so its base must be aligned like its rows: to the largest power of two <= 16 dividing the
+// row's bytes (16 B for rows of a multiple of 16 bytes).  Any hipMalloc / torch allocation is, and
+// so is a z-slab view of one; a view at an odd element offset may not be.
+inline void require_row_aligned(const void* p, int64_t row_bytes) {
+    const int64_t need = row_bytes > 0 ? std::min<int64_t>(16, row_bytes & -row_bytes) : 16;
+    CC_REQUIRE(((uintptr_t)p % (uintptr_t)need) == 0,
+               "device buffer not " + std::to_string(need) + "-byte aligned (its rows are)");
+}
 
 // Block grid + tile tables (tiles tiled from each block's origin).
 struct HostGeom {

@@ -24,8 +24,8 @@
 static void phase_local(cc_ctx* c, const float* in, const uint8_t* mask, const int64_t shape[3],
                         const int64_t block_shape[3], double threshold, int mode, int64_t zoff,
                         bool local_only, bool fast = false, uint64_t* sum_out = nullptr) {
-    // the kernels' 16-B row loads assume 16-B aligned bases (any device allocation is)
-    CC_REQUIRE(((uintptr_t)in & 15) == 0 && ((uintptr_t)mask & 15) == 0, "input / mask not 16-byte aligned");
+    require_row_aligned(in, shape[2] * 4);
+    require_row_aligned(mask, shape[2]);
     RunState& st = state(c);
     st = RunState();
     st.fast = fast;
@@ -566,9 +566,9 @@ struct SeamDev {
 
 // LUT, final label per node, bit rows -> uint64 labels; small artefacts to host
 static void phase_final(cc_ctx* c, uint64_t* out, cc_result* res, const SeamDev* sd = nullptr) {
-    CC_REQUIRE(((uintptr_t)out & 15) == 0, "labels not 16-byte aligned");
     RunState& st = state(c);
     CC_REQUIRE(st.stage == 2, "phase order: call assign first");
+    require_row_aligned(out, st.hg.g.X * 8);
     Geom& g = st.hg.g;
     hipStream_t s = cstream(c);
     const int64_t nt = g.n_tiles, nb = g.n_blocks, nr = st.nr;
@@ -880,6 +880,7 @@ int cc_threshold(cc_ctx* c, const float* in, const int64_t shape[3], const int64
                  double threshold, int mode, uint8_t* out) {
     CC_TRY({
         CC_REQUIRE(c && in && out && shape && block_shape, "NULL argument");
+        require_row_aligned(in, shape[2] * 4);
         HIP_OK(hipSetDevice(c->device));
         const int md = to_mode(mode);
         RunState& st = state(c);
@@ -948,6 +949,8 @@ int cc_resize_mask_nearest(cc_ctx* c, const uint8_t* mask, const int64_t mshape[
                            int64_t z0, int64_t nz, uint8_t* out) {
     CC_TRY({
         CC_REQUIRE(c && mask && mshape && shape && out, "NULL argument");
+        require_row_aligned(mask, mshape[2]);
+        require_row_aligned(out, shape[2]);
         for (int a = 0; a < 3; ++a) CC_REQUIRE(mshape[a] > 0 && shape[a] > 0, "empty mask or volume");
         CC_REQUIRE(z0 >= 0 && nz >= 0 && z0 + nz <= shape[0], "z range outside the volume");
         CC_REQUIRE(shape[1] * shape[2] < (1LL << 40) && (2 * shape[2] + 1) * mshape[2] < (1LL << 62) &&

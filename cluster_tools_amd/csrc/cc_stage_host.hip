@@ -7,6 +7,7 @@ int64_t cc_block_faces(cc_ctx* c, const uint64_t* labels, const int64_t shape[3]
                        const uint64_t* offsets_host, uint64_t* pairs_host, int64_t cap, uint8_t* block_has_pairs_host) {
     try {
         CC_REQUIRE(c && labels && shape && block_shape && offsets_host, "NULL argument");
+        require_row_aligned(labels, shape[2] * 8);
         HIP_OK(hipSetDevice(c->device));
         hipStream_t s = cstream(c);
         int64_t nb[3], n_face = 0;
@@ -114,6 +115,7 @@ int cc_write(cc_ctx* c, uint64_t* labels, const int64_t shape[3], const int64_t 
              const uint64_t* offsets_host, const uint64_t* lut_host, uint64_t n_labels) {
     CC_TRY({
         CC_REQUIRE(c && labels && shape && block_shape && offsets_host && lut_host && n_labels >= 1, "bad arguments");
+        require_row_aligned(labels, shape[2] * 8);
         HIP_OK(hipSetDevice(c->device));
         hipStream_t s = cstream(c);
         int64_t nb[3];
@@ -145,6 +147,7 @@ int cc_generate_boundary_map(cc_ctx* c, float* out, const int64_t shape[3], cons
                              uint64_t seed, int dither) {
     CC_TRY({
         CC_REQUIRE(c && out && shape, "NULL argument");
+        require_row_aligned(out, shape[2] * 4);
         HIP_OK(hipSetDevice(c->device));
         int64_t o[3] = {0, 0, 0};
         if (origin) { o[0] = origin[0]; o[1] = origin[1]; o[2] = origin[2]; }
@@ -302,6 +305,7 @@ int64_t cc_seam_pairs_cubes32(cc_ctx* c, const uint32_t* upper_cubes, uint64_t u
 int cc_shard_top_cubes32(cc_ctx* c, uint32_t* cubes) {
     CC_TRY({
         CC_REQUIRE(c && cubes, "NULL argument");
+        require_row_aligned(cubes, 4);
         HIP_OK(hipSetDevice(c->device));
         RunState& st = state(c);
         CC_REQUIRE(st.stage == 2, "phase order: call cc_shard_assign first");
@@ -321,6 +325,7 @@ int cc_shard_top_cubes32(cc_ctx* c, uint32_t* cubes) {
 int cc_shard_top_plane32(cc_ctx* c, uint32_t* top32) {
     CC_TRY({
         CC_REQUIRE(c && top32, "NULL argument");
+        require_row_aligned(top32, 4);
         HIP_OK(hipSetDevice(c->device));
         RunState& st = state(c);
         CC_REQUIRE(st.stage == 2, "phase order: call cc_shard_assign first");
@@ -381,6 +386,7 @@ int cc_shard_dev_assign(cc_ctx* c, const uint64_t* sums_dev, int rank, int world
 int cc_shard_dev_top_cubes(cc_ctx* c, uint32_t* cubes_dev) {
     CC_TRY({
         CC_REQUIRE(c && cubes_dev, "NULL argument");
+        require_row_aligned(cubes_dev, 4);
         HIP_OK(hipSetDevice(c->device));
         RunState& st = state(c);
         CC_REQUIRE(st.stage == 2 && st.base_dev, "phase order: call cc_shard_dev_assign first");

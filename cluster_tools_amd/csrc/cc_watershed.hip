@@ -362,6 +362,8 @@ extern "C" int cc_normalize_channels(cc_ctx* c, const float* in, int64_t n_chann
                                      const int64_t block_shape[3], int agg, float* out) {
     CC_TRY({
         CC_REQUIRE(c && in && out && shape && block_shape, "NULL argument");
+        require_row_aligned(in, shape[2] * 4);
+        require_row_aligned(out, shape[2] * 4);
         CC_REQUIRE(n_channels >= 1 && n_channels < (1 << 20), "need at least one channel");
         CC_REQUIRE(agg >= 0 && agg <= 2, "agg must be 0 (mean), 1 (max) or 2 (min)");
         HIP_OK(hipSetDevice(c->device));
@@ -413,6 +415,10 @@ extern "C" int cc_watershed_from_seeds(cc_ctx* c, const float* in, const uint64_
                                        int64_t* rounds) {
     CC_TRY({
         CC_REQUIRE(c && in && seeds && out && shape && block_shape, "NULL argument");
+        require_row_aligned(in, shape[2] * 4);
+        require_row_aligned(seeds, shape[2] * 8);
+        require_row_aligned(mask, shape[2]);
+        require_row_aligned(out, shape[2] * 8);
         HIP_OK(hipSetDevice(c->device));
         hipStream_t s = cstream(c);
         // block statistics (normalize), the labelling path's tiles

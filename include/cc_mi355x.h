@@ -76,8 +76,11 @@ const char* cc_version(void);
  * mask_dev   uint8 [Z*Y*X] or NULL (nonzero = inside, block_components.py:194,225)
  * labels_dev uint64 [Z*Y*X] final labels (0 = background)
  * res        may be NULL
- * The three device pointers must be 16-byte aligned (any hipMalloc / torch allocation is; a
- * view at an odd element offset is refused with an error, as is the same in the sharded entry).
+ * Device volumes (here and in every entry below) are read / written with vector accesses of up to
+ * 16 B wherever their rows allow, so each base must be aligned like its rows: to the largest power
+ * of two <= 16 dividing the row's bytes (X * element size).  Any hipMalloc / torch allocation and
+ * any z-slab view of one is; a view at an odd element offset may not be, and is refused with an
+ * error (-1, cc_last_error) instead of being read.
  */
 int cc_label_volume(cc_ctx* ctx, const float* in_dev, const uint8_t* mask_dev,
                     const int64_t shape[3], const int64_t block_shape[3],

@@ -89,3 +89,21 @@ def test_misaligned_device_pointers_refused(ctx):
     ref = O.label_volume(np.zeros(shape, np.float32), bs, 0.5, 'less', np.ones(shape, np.uint8), n_threads=1)
     np.testing.assert_array_equal(lab.cpu().numpy().view(np.uint64), ref['labels'])
     assert res['n_labels'] == ref['n_labels']
+
+
+def test_slab_views_with_unaligned_rows_accepted(ctx):
+    """A z-slab view keeps its rows' alignment (the rule the entries check, include/cc_mi355x.h):
+    rows of 10 voxels need only 8-B (input), 2-B (mask) and 16-B (labels) bases, so views one
+    plane into their storage are labelled, bit-exact against the oracle."""
+    import torch
+    full = (9, 6, 10)
+    x = O.boundary_map(full, origin=(1, 2, 3))
+    m = (np.random.default_rng(5).random(full) < 0.8).astype(np.uint8)
+    xd, md = torch.from_numpy(x).cuda(), torch.from_numpy(m).cuda()
+    od = torch.empty(full, dtype=torch.int64, device='cuda')
+    for mode in ('greater', 'less'):
+        lab, res = ctx.label_volume(xd[1:], (4, 6, 10), 0.5, mode, mask=md[1:], out=od[1:])
+        ref = O.label_volume(np.ascontiguousarray(x[1:]), (4, 6, 10), 0.5, mode, np.ascontiguousarray(m[1:]),
+                             n_threads=1)
+        np.testing.assert_array_equal(lab.cpu().numpy().view(np.uint64), ref['labels'])
+        assert res['n_labels'] == ref['n_labels']
