@@ -352,9 +352,10 @@ class Context:
         """This rank's z-slab [z_offset, z_offset + len(slab)) of a volume sharded over comm's ranks
         (cc_label_volume_sharded: the schedule with RCCL inside the library).  `slab` / `mask`:
         CUDA tensors of the slab.  Returns (labels of the slab, result dict with the global
-        n_labels).  The call is collective (every rank of comm calls it); it is ordered on torch's
-        current stream: on the default (null) stream the library fences its own stream against it,
-        another current stream is bound to the context for the call."""
+        n_labels).  The call is collective (every rank of comm calls it).  It runs on the stream
+        bound with set_stream if there is one; else it is ordered on torch's current stream: on the
+        default (null) stream the library fences its own stream against it, another current stream
+        is bound to the context for the call."""
         import torch
         assert slab.is_cuda and slab.dtype == torch.float32 and slab.is_contiguous() and slab.dim() == 3
         if mask is not None:
