@@ -65,3 +65,39 @@ def test_fuzz_vs_oracle(ctx, monkeypatch, i, fast):
     assert res['n_labels'] == ref['n_labels'] and res['max_id'] == ref['max_id']
     np.testing.assert_array_equal(ctx.block_values(len(ref['values'])), ref['values'])
     np.testing.assert_array_equal(ctx.lut(res['n_labels']), ref['lut'])
+
+
+@pytest.mark.parametrize('i', range(0, N_CASES, 3))
+def test_fuzz_threshold_task_vs_oracle(ctx, i):
+    """The Threshold task's entry (cc_threshold) on the same cases (no mask: the task has none)."""
+    import torch
+    x, bs, thr, mode, _ = _case(i)
+    ref = O.threshold_volume(x, bs, thr, mode)
+    out = ctx.threshold(torch.from_numpy(x).cuda(), bs, thr, mode)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize('schedule', [None, 'sync'])
+@pytest.mark.parametrize('i', range(1, N_CASES, 4))
+def test_fuzz_sharded_vs_oracle(i, schedule):
+    """The z-slab schedule in one process over 2-4 slabs of the same cases (as many as the block
+    rows allow), against the oracle on the whole volume."""
+    import torch
+    from cluster_tools_amd import _lib
+    from cluster_tools_amd.distributed import label_slabs_single_process, assemble_lut
+    x, bs, thr, mode, m = _case(i)
+    nbz = -(-x.shape[0] // bs[0])
+    n = min(nbz, 2 + i % 3)
+    if n < 2:
+        pytest.skip('one block row: nothing to shard')
+    ref = O.label_volume(x, bs, thr, mode, m, n_threads=4)
+    ctxs = [_lib.Context(0) for _ in range(n)]
+    try:
+        lab, res, sums, luts = label_slabs_single_process(
+            ctxs, torch.from_numpy(x).cuda(), bs, thr, mode,
+            mask=None if m is None else torch.from_numpy(m).cuda(), schedule=schedule)
+        np.testing.assert_array_equal(lab.cpu().numpy().view(np.uint64), ref['labels'])
+        np.testing.assert_array_equal(assemble_lut(luts, sums), ref['lut'])
+    finally:
+        for c in ctxs:
+            c.close()
