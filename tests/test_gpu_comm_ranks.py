@@ -198,3 +198,24 @@ def test_ranks_world8_c3_full_size(tmp_path, masked):
         assert (z0, zs) == (128 * r, 128)
         assert e['xxh64'] == xxhash.xxh64(labels[z0:z0 + zs].data).hexdigest(), 'rank %d labels differ' % r
     print("world 8 C3 label seconds per rank:", [round(logs[r][0]["label_seconds"], 3) for r in range(8)])
+
+
+@pytest.mark.parametrize('shape,bs,world,mode,schedule', [
+    ((33, 65, 129), (11, 13, 43), 3, 'greater', 'synchronised'),   # odd block y / x: no cube form
+    ((20, 1, 300), (4, 1, 64), 2, 'less', 'one-read-back'),         # rows of one voxel in y
+    ((45, 130, 170), (15, 45, 63), 3, 'less', 'synchronised'),
+    ((9, 40, 2), (3, 40, 2), 3, 'greater', 'one-read-back'),        # slabs of 3 planes, 2-voxel rows
+])
+def test_ranks_geometries(tmp_path, shape, bs, world, mode, schedule):
+    """Odd and degenerate geometries through the library's entry at world 2 / 3: each slab's labels
+    against the oracle on the whole volume, the agreed schedule as the block shapes dictate."""
+    origin = (2, 3, 5)
+    logs = _run(tmp_path, world, [{'block_shape': list(bs)}], mode=mode, shape=shape, origin=origin)
+    ref = O.label_volume(O.boundary_map(shape, origin=origin), bs, 0.5, mode, None, n_threads=8)
+    for r in range(world):
+        e = logs[r][0]
+        assert e['ok'], 'rank %d: %s' % (r, e.get('error'))
+        assert e['res']['n_labels'] == ref['n_labels']
+        assert e['info']['schedule'] == schedule, (r, e['info'])
+    got = np.concatenate([np.load(str(tmp_path / ('rank%d_call0.npy' % r))) for r in range(world)])
+    np.testing.assert_array_equal(got.view(np.uint64), ref['labels'])
