@@ -157,6 +157,33 @@ __global__ __launch_bounds__(512) void wr_tile_s(unsigned long long* __restrict_
     }
 }
 
+// wr_tile_s plus k_pass2's per-tile bit-row read first (4 KB at bits + t * 512 in TILE-INDEX
+// order, whatever order the workgroups walk the tiles in): is a z-ordered walk slow because of
+// that read?  (BITSZ: the bit rows laid out in the walk's order instead)
+template <bool ZORD, bool BITSZ>
+__global__ __launch_bounds__(512) void wr_tile_bits(unsigned long long* __restrict__ out, const unsigned long long* __restrict__ bits,
+                                                    int64_t Y, int64_t X, int ntx, int nty, int ntz) {
+    const int t = blockIdx.x;
+    int tx, ty, tz;
+    if (ZORD) { tz = t % ntz; ty = (t / ntz) % nty; tx = t / (ntz * nty); }
+    else { tx = t % ntx; ty = (t / ntx) % nty; tz = t / (ntx * nty); }
+    const int64_t tile = BITSZ ? (int64_t)t : ((int64_t)tz * nty + ty) * ntx + tx;
+    const unsigned long long b = bits[tile * 512 + threadIdx.x];
+    __shared__ unsigned long long sb[512];
+    sb[threadIdx.x] = b;
+    __syncthreads();
+    for (int c = threadIdx.x; c < 4096; c += 512) {
+        const int cz = c / 512, cy = (c / 32) % 16, cx = c % 32;
+        const unsigned long long v = sb[(c * 7) & 511];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const int z = 2 * cz + (d >> 1), y = 2 * cy + (d & 1);
+            const int64_t idx = (((int64_t)tz * 16 + z) * Y + ty * 32 + y) * X + tx * 64 + 2 * cx;
+            *reinterpret_cast<ulonglong2*>(out + idx) = make_ulonglong2(v ^ (unsigned long long)c, (unsigned long long)d);
+        }
+    }
+}
+
 // read-side sweep: float4 lanes over TZ x TY x 64 tiles (k_spec's load shape)
 template <int TZ, int TY>
 __global__ __launch_bounds__(512) void rd_tile4_s(const float* __restrict__ in, int64_t Y, int64_t X, int ntx, int nty,
@@ -442,6 +469,15 @@ int main(int argc, char** argv) {
     WS(4, 128, false, "wr_s4x128")
     WS(2, 256, false, "wr_s2x256")
     WS(1, 512, false, "wr_s1x512")
+    {
+        unsigned long long* bits;
+        CHK(hipMalloc(&bits, (size_t)nt * 512 * 8));
+        CHK(hipMemset(bits, 0, (size_t)nt * 512 * 8));
+        r.push_back({"wr_bits_lin", time_ms(s, iters, [&] { wr_tile_bits<false, false><<<nt, 512, 0, s>>>(out, bits, Y, X, ntx, nty, (int)(Z / 16)); })});
+        r.push_back({"wr_bits_zord", time_ms(s, iters, [&] { wr_tile_bits<true, false><<<nt, 512, 0, s>>>(out, bits, Y, X, ntx, nty, (int)(Z / 16)); })});
+        r.push_back({"wr_bits_zord_zbits", time_ms(s, iters, [&] { wr_tile_bits<true, true><<<nt, 512, 0, s>>>(out, bits, Y, X, ntx, nty, (int)(Z / 16)); })});
+        CHK(hipFree(bits));
+    }
 #define RS(TZ, TY, NAME)                                                                                            \
     r.push_back({NAME, time_ms(s, iters, [&] { rd_tile4_s<TZ, TY><<<nt, 512, 0, s>>>(in, Y, X, ntx, (int)(Y / TY), dummy); })});
     RS(16, 32, "rd_s16x32")
